@@ -1,0 +1,121 @@
+"""Pin the oracle (oracle/) to golden vectors produced by the reference itself (tools/gen_golden.py)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import closed_form, cse_ref, sbm_ref
+
+SBM_CASES = ["sbm_n37", "sbm_n1", "sbm_n7_d96_k16", "sbm_n64_noncontig", "sbm_n150", "sbm_n33_d96"]
+
+
+def t(x, grad=False):
+    return torch.from_numpy(np.ascontiguousarray(x)).requires_grad_(grad)
+
+
+def sbm_params(z, grad=True):
+    return {k[2:]: t(v, grad) for k, v in z.items() if k.startswith("p:")}
+
+
+def test_bernoulli_equivalence_recorded(golden):
+    assert bool(golden("bernoulli_equivalence")["ok"][0])
+
+
+@pytest.mark.parametrize("case", SBM_CASES)
+def test_sbm_oracle_matches_reference(golden, case):
+    z = golden(case)
+    B, H, N, d, k = z["meta"]
+    Q, K, V = t(z["Q"], True), t(z["K"], True), t(z["V"], True)
+    params = sbm_params(z)
+    X, sp, graph, attn = sbm_ref.sbm_attention(Q, K, V, t(z["mask"]), params, t(z["u"]), int(k))
+    assert np.array_equal(graph.detach().numpy().astype(np.uint8), z["graph"])
+    np.testing.assert_allclose(X.detach().numpy(), z["X"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(attn.detach().numpy(), z["attn"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(sp.detach().numpy(), z["sparsity"], rtol=0, atol=0)
+    ((X * t(z["dX"])).sum() + (sp * t(z["dsparsity"])).sum()).backward()
+    for name, g in (("dQ", Q.grad), ("dK", K.grad), ("dV", V.grad)):
+        np.testing.assert_allclose(g.numpy(), z[name], rtol=1e-4, atol=1e-5, err_msg=name)
+    for pk, p in params.items():
+        np.testing.assert_allclose(p.grad.numpy(), z["g:" + pk], rtol=1e-4, atol=1e-5, err_msg=pk)
+
+
+@pytest.mark.parametrize("case", SBM_CASES)
+def test_sampler_bit_exact_on_reference_expA(golden, case):
+    """STE.py:10-15: A = u < clamp(expA, .01, .99) — bit-exact given the reference's own expA."""
+    z = golden(case)
+    A = sbm_ref.STESample.apply(t(z["expA"]), t(z["u"]))
+    assert np.array_equal(A.numpy().astype(np.uint8), z["graph"])
+
+
+@pytest.mark.parametrize("case", SBM_CASES)
+def test_closed_form_matches_reference(golden, case):
+    """The fp64 closed form (the kernels' spec) vs the reference autograd, at the kernel tolerance."""
+    z = golden(case)
+    B, H, N, d, k = z["meta"]
+    params = {k_[2:]: t(v) for k_, v in z.items() if k_.startswith("p:")}
+    out, g = closed_form.sbm_fwd_bwd(t(z["Q"]), t(z["K"]), t(z["V"]), t(z["mask"]), params, t(z["u"]), int(k),
+                                     t(z["dX"]), t(z["dsparsity"]), graph_override=t(z["graph"].astype(np.float32)))
+    np.testing.assert_allclose(out["X"].numpy(), z["X"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(out["attn"].numpy(), z["attn"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(out["expA"].numpy(), z["expA"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(g["Q"].numpy(), z["dQ"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(g["K"].numpy(), z["dK"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(g["V"].numpy(), z["dV"], rtol=1e-4, atol=1e-5)
+    for pk in params:
+        np.testing.assert_allclose(g[pk].numpy(), z["g:" + pk], rtol=1e-4, atol=1e-5, err_msg=pk)
+
+
+@pytest.mark.parametrize("case", ["full_n37", "full_n150"])
+def test_full_attention_oracle(golden, case):
+    z = golden(case)
+    Q, K, V = t(z["Q"], True), t(z["K"], True), t(z["V"], True)
+    X, sp, graph, attn = sbm_ref.full_attention(Q, K, V, t(z["mask"]))
+    np.testing.assert_allclose(X.detach().numpy(), z["X"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(attn.detach().numpy(), z["attn"], rtol=1e-5, atol=1e-6)
+    (X * t(z["dX"])).sum().backward()
+    for name, gg in (("dQ", Q.grad), ("dK", K.grad), ("dV", V.grad)):
+        np.testing.assert_allclose(gg.numpy(), z[name], rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("case", ["attn_layer_n29", "attn_layer_full_n29"])
+def test_attention_layer_oracle(golden, case):
+    z = golden(case)
+    B, N, dim, H, k, full = z["meta"]
+    params = {k_[2:]: t(v, True) for k_, v in z.items() if k_.startswith("p:")}
+    X = t(z["X"], True)
+    out, sp, graph, attn = sbm_ref.attention_layer(X, t(z["mask"]), params, t(z["u"]), int(H), int(dim // H), int(k),
+                                                   full_att=bool(full))
+    np.testing.assert_allclose(out.detach().numpy(), z["out"], rtol=1e-5, atol=1e-6)
+    loss = (out * t(z["dout"])).sum()
+    if sp is not None:
+        loss = loss + (sp * t(z["dsparsity"])).sum()
+    loss.backward()
+    np.testing.assert_allclose(X.grad.numpy(), z["dX"], rtol=1e-4, atol=1e-5)
+    for pk, p in params.items():
+        np.testing.assert_allclose(p.grad.numpy(), z["g:" + pk], rtol=1e-4, atol=1e-5, err_msg=pk)
+
+
+@pytest.mark.parametrize("case", ["rel_attn_n37", "rel_attn_n150", "rel_attn_n20_dk64"])
+def test_rel_attn_oracle(golden, case):
+    z = golden(case)
+    rel, mask = cse_ref.build_rel_mask(t(z["L"]), t(z["T"]), t(z["L_mask"]), t(z["T_mask"]))
+    q, k, v, lq, lk = (t(z[n], True) for n in ("q", "k", "v", "lq", "lk"))
+    o = cse_ref.rel_attn(q, k, v, lq, lk, rel, mask)
+    np.testing.assert_allclose(o.detach().numpy(), z["out"], rtol=1e-5, atol=1e-6)
+    (o * t(z["dO"])).sum().backward()
+    for n, x in (("dq", q), ("dk", k), ("dv", v), ("dlq", lq), ("dlk", lk)):
+        np.testing.assert_allclose(x.grad.numpy(), z[n], rtol=1e-4, atol=1e-5, err_msg=n)
+
+
+def test_disentangled_oracle(golden):
+    z = golden("disentangled_n23")
+    rel, mask = cse_ref.build_rel_mask(t(z["L"]), t(z["T"]), t(z["L_mask"]), t(z["T_mask"]))
+    params = {k_[2:]: t(v, True) for k_, v in z.items() if k_.startswith("p:")}
+    x, rq = t(z["x"], True), t(z["rel_q"], True)
+    out, none = cse_ref.disentangled_attn(x, params, rq, rel, mask)
+    assert none is None
+    np.testing.assert_allclose(out.detach().numpy(), z["out"], rtol=1e-5, atol=1e-6)
+    (out * t(z["dout"])).sum().backward()
+    np.testing.assert_allclose(x.grad.numpy(), z["dx"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(rq.grad.numpy(), z["drel_q"], rtol=1e-4, atol=1e-5)
+    for pk, p in params.items():
+        np.testing.assert_allclose(p.grad.numpy(), z["g:" + pk], rtol=1e-4, atol=1e-5, err_msg=pk)

@@ -1,0 +1,253 @@
+"""Generate golden vectors by running the REFERENCE itself (this container only).
+
+Imports /root/reference/module/{components,STE,sbm_attn,disentangled_attn}.py standalone
+(SURVEY.md Appendix A recipe: a synthetic ``module`` package, no shims needed), drives the
+reference's own ``torch.bernoulli`` with host-supplied uniforms (``u < p``; this script first
+re-verifies that this is bit-identical to the real CPU draw), runs forward + backward on
+seeded inputs, and writes small ``.npz`` fixtures to tests/golden/. The reference never
+travels to the GPU box; only these fixtures do.
+
+Run:  PYTHONDONTWRITEBYTECODE=1 python tools/gen_golden.py
+"""
+import importlib.util
+import math
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+REF = "/root/reference"
+OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tests", "golden")
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "code-structure-aware-transformer_amd"))
+from csa_amd.data import synthetic_batch  # noqa: E402
+
+
+def load_reference():
+    pkg = types.ModuleType("module")
+    pkg.__path__ = [f"{REF}/module"]
+    sys.modules["module"] = pkg
+
+    def load(n):
+        s = importlib.util.spec_from_file_location(f"module.{n}", f"{REF}/module/{n}.py")
+        m = importlib.util.module_from_spec(s)
+        sys.modules[f"module.{n}"] = m
+        s.loader.exec_module(m)
+        return m
+
+    comp = load("components")
+    pkg._get_clones, pkg.transpose_for_scores = comp._get_clones, comp.transpose_for_scores
+    return load("STE"), load("sbm_attn"), load("disentangled_attn")
+
+
+STE, SA, DA = load_reference()
+_real_bernoulli = torch.bernoulli
+
+
+def verify_bernoulli_equivalence():
+    """torch.bernoulli(p) == (torch.rand(p.shape) < p) under the same seed (CPU)."""
+    ok = True
+    for shape in [(1, 8, 150, 150), (7, 8, 150, 150), (3, 2, 37, 37)]:
+        p = torch.rand(shape, generator=torch.Generator().manual_seed(5)).clamp(0.01, 0.99)
+        torch.manual_seed(123)
+        a = _real_bernoulli(p)
+        torch.manual_seed(123)
+        b = (torch.rand(p.shape) < p).float()
+        ok &= bool(torch.equal(a, b))
+    return ok
+
+
+class HostUniforms:
+    """Context manager: make the reference's torch.bernoulli consume the given uniforms."""
+
+    def __init__(self, u):
+        self.u = u
+
+    def __enter__(self):
+        torch.bernoulli = lambda p: (self.u < p).to(p.dtype)
+
+    def __exit__(self, *a):
+        torch.bernoulli = _real_bernoulli
+
+
+def np32(t):
+    return t.detach().cpu().numpy().astype(np.float32)
+
+
+def sbm_case(name, B, H, N, d, k, pad_counts, seed, zero_row=None, noncontig=False):
+    g = torch.Generator().manual_seed(seed)
+    torch.manual_seed(seed)
+    mod = SA.SBMAttention({"attention_dropout": 0.2, "head_dim": d, "num_head": H, "num_clusters": [k]}, 0)
+    for n_, p in mod.named_parameters():  # CSATrans init: xavier for dim>1, orthogonal clusters
+        if p.dim() > 1:
+            torch.nn.init.xavier_uniform_(p)
+    torch.nn.init.orthogonal_(mod.layer.weight)
+    mod.eval()
+    if noncontig:  # (B,N,H*d) -> split_heads view, as Attention.forward produces
+        base = lambda: torch.randn(B, N, H * d, generator=g).reshape(B, N, H, d).transpose(1, 2)
+        Q, K, V = base(), base(), base()
+    else:
+        Q, K, V = (torch.randn(B, H, N, d, generator=g) for _ in range(3))
+    Q.requires_grad_(True); K.requires_grad_(True); V.requires_grad_(True)
+    mask = torch.zeros(B, N)
+    for b, pc in enumerate(pad_counts):
+        if pc:
+            mask[b, N - pc:] = 1.0
+    u = torch.rand(B, H, N, N, generator=g)
+    if zero_row is not None:
+        b, h, i = zero_row
+        u[b, h, i, :] = 0.995  # > clamp ceiling 0.99 -> sampled graph row all-zero
+    dX = torch.randn(B, H, N, d, generator=g)
+    dsp = torch.full((H,), 3.125e-4) + 1e-4 * torch.randn(H, generator=g)
+    with HostUniforms(u):
+        X, sparsity, graph, attn = mod(Q, K, V, mask)
+    # expA exactly as the reference computes it (sbm_attn.py:37-55), for the bit-exact sampler test
+    with torch.no_grad():
+        c = mod.layer.weight.reshape(H, k, -1)
+        S = torch.softmax(torch.matmul(c, c.transpose(-1, -2)).reshape(H, k * k), -1).reshape(H, k, k).unsqueeze(0).repeat((B, 1, 1, 1))
+        Qh = torch.sigmoid(torch.matmul(mod.proj(Q), c.transpose(-1, -2)))
+        Kh = torch.sigmoid(torch.matmul(mod.proj(K), c.transpose(-1, -2)))
+        expA = torch.matmul(Qh, torch.matmul(S, Kh.transpose(-1, -2)))
+    loss = (X * dX).sum() + (sparsity * dsp).sum()
+    loss.backward()
+    out = dict(Q=np32(Q), K=np32(K), V=np32(V), mask=np32(mask), u=np32(u), dX=np32(dX), dsparsity=np32(dsp),
+               X=np32(X), sparsity=np32(sparsity), graph=graph.detach().numpy().astype(np.uint8), attn=np32(attn),
+               expA=np32(expA), dQ=np32(Q.grad), dK=np32(K.grad), dV=np32(V.grad),
+               meta=np.array([B, H, N, d, k], np.int64))
+    for n_, p in mod.named_parameters():
+        out["p:" + n_] = np32(p)
+        out["g:" + n_] = np32(p.grad)
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **out)
+    print(f"{name}: sparsity={sparsity.detach().numpy()} |X|={X.abs().max().item():.3g}")
+
+
+def full_case(name, B, H, N, d, pad_counts, seed):
+    g = torch.Generator().manual_seed(seed)
+    mod = SA.FullAttention({"attention_dropout": 0.2, "head_dim": d, "num_head": H}, 0).eval()
+    Q, K, V = (torch.randn(B, H, N, d, generator=g).requires_grad_(True) for _ in range(3))
+    mask = torch.zeros(B, N)
+    for b, pc in enumerate(pad_counts):
+        if pc:
+            mask[b, N - pc:] = 1.0
+    dX = torch.randn(B, H, N, d, generator=g)
+    X, sp, graph, attn = mod(Q, K, V, mask)
+    assert sp is None and graph is mask
+    (X * dX).sum().backward()
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), Q=np32(Q), K=np32(K), V=np32(V), mask=np32(mask),
+                        dX=np32(dX), X=np32(X), attn=np32(attn), dQ=np32(Q.grad), dK=np32(K.grad),
+                        dV=np32(V.grad), meta=np.array([B, H, N, d], np.int64))
+    print(f"{name}: ok")
+
+
+def attention_layer_case(name, B, N, dim, H, k, pad_counts, seed, full_att=False):
+    g = torch.Generator().manual_seed(seed)
+    torch.manual_seed(seed)
+    cfg = {"attention_grad_checkpointing": False, "transformer_dim": dim, "head_dim": dim // H, "num_head": H,
+           "attn_type": "sbm", "attention_dropout": 0.2, "num_clusters": [k]}
+    mod = SA.Attention(cfg, 0, full_att=full_att)
+    for n_, p in mod.named_parameters():
+        if p.dim() > 1:
+            torch.nn.init.xavier_uniform_(p)
+    if not full_att:
+        torch.nn.init.orthogonal_(mod.attn.layer.weight)
+    mod.eval()
+    X = torch.randn(B, N, dim, generator=g).requires_grad_(True)
+    mask = torch.zeros(B, N, dtype=torch.bool)
+    for b, pc in enumerate(pad_counts):
+        if pc:
+            mask[b, N - pc:] = True
+    u = torch.rand(B, H, N, N, generator=g)
+    dout = torch.randn(B, N, dim, generator=g)
+    dsp = torch.full((H,), 3.125e-4)
+    with HostUniforms(u):
+        out, sparsity, graph, attn = mod([X, mask, []])
+    loss = (out * dout).sum() + ((sparsity * dsp).sum() if sparsity is not None else 0)
+    loss.backward()
+    res = dict(X=np32(X), mask=mask.numpy(), u=np32(u), dout=np32(dout), dsparsity=np32(dsp), out=np32(out),
+               attn=np32(attn), dX=np32(X.grad), meta=np.array([B, N, dim, H, k, int(full_att)], np.int64))
+    if sparsity is not None:
+        res["sparsity"] = np32(sparsity)
+        res["graph"] = graph.detach().numpy().astype(np.uint8)
+    for n_, p in mod.named_parameters():
+        res["p:" + n_] = np32(p)
+        res["g:" + n_] = np32(p.grad)
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **res)
+    print(f"{name}: ok")
+
+
+def relations(B, N, seed, min_nodes=None):
+    sb = synthetic_batch(B, max_size=N, seed=seed, min_nodes=min_nodes or max(1, N // 2), max_nodes=N)
+    rel = np.concatenate([np.repeat(sb["L"][:, None], 4, 1), np.repeat(sb["T"][:, None], 4, 1)], 1).astype(np.int64)
+    msk = np.concatenate([np.repeat(sb["L_mask"][:, None], 4, 1), np.repeat(sb["T_mask"][:, None], 4, 1)], 1)
+    return sb, torch.from_numpy(rel), torch.from_numpy(msk)
+
+
+def rel_attn_case(name, B, N, dk, L, seed):
+    g = torch.Generator().manual_seed(seed)
+    H = 8
+    sb, rel, msk = relations(B, N, seed)
+    q, k, v = (torch.randn(B, H, N, dk, generator=g).requires_grad_(True) for _ in range(3))
+    lq, lk = (torch.randn(1, H, L, dk, generator=g).requires_grad_(True) for _ in range(2))
+    dO = torch.randn(B, H, N, dk, generator=g)
+    o = DA.DisentangledAttn.rel_attn(q, k, v, lq, lk, rel, msk)
+    (o * dO).sum().backward()
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), q=np32(q), k=np32(k), v=np32(v), lq=np32(lq), lk=np32(lk),
+                        L=sb["L"], T=sb["T"], L_mask=sb["L_mask"], T_mask=sb["T_mask"], dO=np32(dO), out=np32(o),
+                        dq=np32(q.grad), dk=np32(k.grad), dv=np32(v.grad), dlq=np32(lq.grad), dlk=np32(lk.grad),
+                        meta=np.array([B, H, N, dk, L], np.int64))
+    print(f"{name}: ok")
+
+
+def disentangled_case(name, B, N, d_model, L, seed):
+    g = torch.Generator().manual_seed(seed)
+    torch.manual_seed(seed)
+    H = 8
+    mod = DA.DisentangledAttn(H, d_model, 0.2)
+    for n_, p in mod.named_parameters():
+        if p.dim() > 1:
+            torch.nn.init.xavier_uniform_(p)
+    mod.eval()
+    sb, rel, msk = relations(B, N, seed)
+    x = torch.randn(B, N, d_model, generator=g).requires_grad_(True)
+    rel_q = torch.randn(2, L, d_model, generator=g).requires_grad_(True)
+    dout = torch.randn(B, N, d_model, generator=g)
+    out, none = mod(x, x, x, [rel_q], rel, msk)
+    assert none is None
+    (out * dout).sum().backward()
+    res = dict(x=np32(x), rel_q=np32(rel_q), L=sb["L"], T=sb["T"], L_mask=sb["L_mask"], T_mask=sb["T_mask"],
+               dout=np32(dout), out=np32(out), dx=np32(x.grad), drel_q=np32(rel_q.grad),
+               meta=np.array([B, N, d_model, L], np.int64))
+    for n_, p in mod.named_parameters():
+        res["p:" + n_] = np32(p)
+        res["g:" + n_] = np32(p.grad)
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **res)
+    print(f"{name}: ok")
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    torch.set_num_threads(8)
+    eq = verify_bernoulli_equivalence()
+    print("bernoulli == rand<p (CPU):", eq)
+    assert eq, "host-uniform recipe does not reproduce torch.bernoulli"
+    np.savez(os.path.join(OUT, "bernoulli_equivalence.npz"), ok=np.array([eq]))
+    sbm_case("sbm_n37", B=2, H=2, N=37, d=64, k=10, pad_counts=[0, 7], seed=11)
+    sbm_case("sbm_n1", B=2, H=2, N=1, d=64, k=10, pad_counts=[0, 0], seed=12)
+    sbm_case("sbm_n7_d96_k16", B=2, H=2, N=7, d=96, k=16, pad_counts=[2, 0], seed=13)
+    sbm_case("sbm_n64_noncontig", B=2, H=2, N=64, d=64, k=10, pad_counts=[13, 0], seed=14, noncontig=True)
+    sbm_case("sbm_n150", B=1, H=2, N=150, d=64, k=10, pad_counts=[30], seed=15, zero_row=(0, 1, 5))
+    sbm_case("sbm_n33_d96", B=1, H=2, N=33, d=96, k=10, pad_counts=[1], seed=16)
+    full_case("full_n37", B=2, H=2, N=37, d=64, pad_counts=[0, 5], seed=21)
+    full_case("full_n150", B=1, H=2, N=150, d=64, pad_counts=[40], seed=22)
+    attention_layer_case("attn_layer_n29", B=2, N=29, dim=128, H=2, k=10, pad_counts=[0, 4], seed=31)
+    attention_layer_case("attn_layer_full_n29", B=2, N=29, dim=128, H=2, k=10, pad_counts=[3, 0], seed=32,
+                         full_att=True)
+    rel_attn_case("rel_attn_n37", B=2, N=37, dk=16, L=150, seed=41)
+    rel_attn_case("rel_attn_n150", B=1, N=150, dk=16, L=150, seed=42)
+    rel_attn_case("rel_attn_n20_dk64", B=1, N=20, dk=64, L=150, seed=43)
+    disentangled_case("disentangled_n23", B=2, N=23, d_model=128, L=150, seed=51)
+
+
+if __name__ == "__main__":
+    main()
