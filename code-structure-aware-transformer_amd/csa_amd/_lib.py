@@ -1,0 +1,129 @@
+"""ctypes binding of libcsa_hip.so (include/csa_hip.h). No torch types cross this boundary.
+
+The shared library is built in-tree (csa_amd/build.py -> csa_amd/lib/libcsa_hip.so) and loaded
+after torch so that it binds to the HIP runtime torch already loaded (same SONAME
+libamdhip64.so.7). There is deliberately no fallback: if the library is missing, every op
+raises.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("CSA_HIP_LIB", os.path.join(_HERE, "lib", "libcsa_hip.so"))
+
+CSA_ABI_VERSION = 1
+CSA_FLAG_DENSE = 1
+STATUS = {0: "CSA_OK", 1: "CSA_INVALID_ARG", 2: "CSA_UNSUPPORTED_SHAPE", 3: "CSA_LAUNCH_FAILED"}
+
+i64, u64, u32, f32, vp = ctypes.c_int64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_float, ctypes.c_void_p
+
+
+class SbmFwdArgs(ctypes.Structure):
+    _fields_ = [
+        ("B", i64), ("H", i64), ("N", i64), ("M", i64), ("d", i64), ("k", i64),
+        ("Q", vp), ("q_sb", i64), ("q_sh", i64), ("q_sn", i64),
+        ("K", vp), ("k_sb", i64), ("k_sh", i64), ("k_sn", i64),
+        ("V", vp), ("v_sb", i64), ("v_sh", i64), ("v_sn", i64),
+        ("key_mask", vp), ("mask_sb", i64),
+        ("cluster_w", vp),
+        ("proj_w", vp * 3), ("proj_b", vp * 3),
+        ("uniforms", vp),
+        ("seed", u64), ("offset", u64),
+        ("attn_dropout", f32), ("proj_dropout", f32),
+        ("flags", u32),
+        ("X", vp), ("sparsity", vp), ("state", vp),
+    ]
+
+
+class SbmBwdArgs(ctypes.Structure):
+    _fields_ = [
+        ("fwd", ctypes.POINTER(SbmFwdArgs)),
+        ("dX", vp), ("dsparsity", vp), ("dgraph", vp),
+        ("dQ", vp), ("dK", vp), ("dV", vp),
+        ("dcluster_w", vp), ("dproj_w", vp * 3), ("dproj_b", vp * 3),
+        ("workspace", vp),
+    ]
+
+
+class RelAttnArgs(ctypes.Structure):
+    _fields_ = [
+        ("B", i64), ("H", i64), ("N", i64), ("L", i64), ("d", i64),
+        ("q", vp), ("q_sb", i64), ("q_sh", i64), ("q_sn", i64),
+        ("k", vp), ("k_sb", i64), ("k_sh", i64), ("k_sn", i64),
+        ("v", vp), ("v_sb", i64), ("v_sh", i64), ("v_sn", i64),
+        ("lq", vp), ("lk", vp),
+        ("rel", vp), ("rel_sb", i64), ("rel_sh", i64),
+        ("mask", vp), ("mask_sb", i64), ("mask_sh", i64),
+        ("rel_head_group", i64),
+        ("out", vp), ("lse", vp),
+    ]
+
+
+class RelAttnBwdArgs(ctypes.Structure):
+    _fields_ = [
+        ("fwd", ctypes.POINTER(RelAttnArgs)),
+        ("dout", vp),
+        ("dq", vp), ("dk", vp), ("dv", vp),
+        ("dlq", vp), ("dlk", vp),
+        ("workspace", vp),
+    ]
+
+
+class CsaError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib():
+    """Load (once) and return the library; raises CsaError when it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise CsaError(f"libcsa_hip.so not found at {LIB_PATH}: run `python __graft_entry__.py build` "
+                       "(there is no CPU fallback for the hot path)")
+    L = ctypes.CDLL(LIB_PATH)
+    L.csa_abi_version.restype = ctypes.c_int
+    L.csa_status_str.restype = ctypes.c_char_p
+    L.csa_status_str.argtypes = [ctypes.c_int]
+    L.csa_last_error_str.restype = ctypes.c_char_p
+    L.csa_sbm_supported.restype = ctypes.c_int
+    L.csa_sbm_supported.argtypes = [i64, i64, u32]
+    for fn in ("csa_sbm_state_bytes", "csa_sbm_bwd_workspace_bytes"):
+        getattr(L, fn).restype = ctypes.c_size_t
+        getattr(L, fn).argtypes = [i64] * 6 + [u32]
+    L.csa_rel_attn_bwd_workspace_bytes.restype = ctypes.c_size_t
+    L.csa_rel_attn_bwd_workspace_bytes.argtypes = [i64] * 5
+    L.csa_sbm_fwd.restype = ctypes.c_int
+    L.csa_sbm_fwd.argtypes = [ctypes.POINTER(SbmFwdArgs), vp]
+    L.csa_sbm_maps.restype = ctypes.c_int
+    L.csa_sbm_maps.argtypes = [ctypes.POINTER(SbmFwdArgs), vp, vp, vp]
+    L.csa_sbm_bwd.restype = ctypes.c_int
+    L.csa_sbm_bwd.argtypes = [ctypes.POINTER(SbmBwdArgs), vp]
+    L.csa_ste_sample.restype = ctypes.c_int
+    L.csa_ste_sample.argtypes = [vp, vp, vp, i64, f32, f32, vp]
+    L.csa_ste_backward.restype = ctypes.c_int
+    L.csa_ste_backward.argtypes = [vp, vp, vp, i64, vp]
+    L.csa_rel_attn_fwd.restype = ctypes.c_int
+    L.csa_rel_attn_fwd.argtypes = [ctypes.POINTER(RelAttnArgs), vp]
+    L.csa_rel_attn_bwd.restype = ctypes.c_int
+    L.csa_rel_attn_bwd.argtypes = [ctypes.POINTER(RelAttnBwdArgs), vp]
+    if L.csa_abi_version() != CSA_ABI_VERSION:
+        raise CsaError(f"ABI mismatch: library {L.csa_abi_version()} != binding {CSA_ABI_VERSION}")
+    _lib = L
+    return L
+
+
+def check(status, what):
+    if status != 0:
+        L = lib()
+        raise CsaError(f"{what} failed: {STATUS.get(status, status)}: {L.csa_last_error_str().decode()}")
+
+
+EXPORTED_SYMBOLS = (
+    "csa_abi_version", "csa_status_str", "csa_last_error_str", "csa_sbm_supported", "csa_sbm_state_bytes",
+    "csa_sbm_bwd_workspace_bytes", "csa_sbm_fwd", "csa_sbm_maps", "csa_sbm_bwd", "csa_ste_sample",
+    "csa_ste_backward", "csa_rel_attn_bwd_workspace_bytes", "csa_rel_attn_fwd", "csa_rel_attn_bwd",
+)

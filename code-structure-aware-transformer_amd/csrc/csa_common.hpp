@@ -1,0 +1,101 @@
+// Device-side building blocks shared by the CSA-Trans attention kernels (gfx950 / CDNA4 only).
+//
+// Everything here is built around ONE matrix instruction, the exact-fp32 MFMA
+// v_mfma_f32_32x32x2_f32 (64 cycles/SIMD, result == k-ordered fmaf chain): the reference
+// computes the whole hot path in fp32 (module/sbm_attn.py:120-126 disables autocast and
+// casts to .float()), and parity is judged at rtol 1e-4 / atol 1e-5, so the contractions
+// run on fp32 MFMA.
+//
+// Lane conventions for one wave64 (c = lane & 31, h = lane >> 5):
+//   D[i][j] += sum_{k in step} A[i][k] B[k][j]
+//   A operand: lane holds A[i = c][k = kperm(s, h)]       (one float per K-step s)
+//   B operand: lane holds B[k = kperm(s, h)][j = c]
+//   C/D      : lane holds D[crow(r, h)][c] in register r (r = 0..15)
+// Any bijection kperm(s, h) is valid as long as both operands use the same one; we use
+//   "lin"  : k = s + (K/2) h          (operand loaded from a row-major row: each lane reads a
+//                                       contiguous run of K/2 floats -> dwordx4 loads)
+//   "acc"  : k = 32 t + crow(r, h)    (operand that IS a previous accumulator tile: the
+//                                       16 registers of tile t feed K-steps 16t .. 16t+15)
+// so an accumulator tile can feed the next product with no data movement whenever that
+// product sums over the tile's ROW index.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace csa {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+__device__ __forceinline__ int crow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+__device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 acc) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+}
+
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) z[r] = 0.f;
+  return z;
+}
+
+// Sum of a value over the two 32-lane halves (lane l <-> l ^ 32).
+__device__ __forceinline__ float xhalf_sum(float v) { return v + __shfl_xor(v, 32, 64); }
+__device__ __forceinline__ float xhalf_max(float v) { return fmaxf(v, __shfl_xor(v, 32, 64)); }
+
+// Reduce over the 32 lanes of each half (result replicated in every lane of the half).
+__device__ __forceinline__ float half_sum32(float v) {
+#pragma unroll
+  for (int o = 16; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Load `n` consecutive floats starting at p into dst[0..n) (n multiple of 4, p 16-B aligned when vec).
+template <int NV>
+__device__ __forceinline__ void load_run(float* dst, const float* __restrict__ p, bool valid) {
+  if (valid) {
+#pragma unroll
+    for (int i = 0; i < NV; i += 4) {
+      f32x4 v = *reinterpret_cast<const f32x4*>(p + i);
+      dst[i] = v[0]; dst[i + 1] = v[1]; dst[i + 2] = v[2]; dst[i + 3] = v[3];
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) dst[i] = 0.f;
+  }
+}
+
+// Scalar-load variant (no alignment requirement).
+template <int NV>
+__device__ __forceinline__ void load_run_s(float* dst, const float* __restrict__ p, int n_avail, bool valid) {
+#pragma unroll
+  for (int i = 0; i < NV; ++i) dst[i] = (valid && i < n_avail) ? p[i] : 0.f;
+}
+
+// ---------------------------------------------------------------------------------------
+// Philox4x32-10 counter-based RNG (Salmon et al., SC'11): stateless, so forward sampling
+// is reproducible from (seed, offset, element coordinates) on any launch geometry.
+// ---------------------------------------------------------------------------------------
+struct u32x4 { uint32_t x, y, z, w; };
+
+__device__ __forceinline__ u32x4 philox4x32_10(u32x4 ctr, uint32_t k0, uint32_t k1) {
+  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    uint32_t hi0 = __umulhi(M0, ctr.x), lo0 = M0 * ctr.x;
+    uint32_t hi1 = __umulhi(M1, ctr.z), lo1 = M1 * ctr.z;
+    ctr = u32x4{hi1 ^ ctr.y ^ k0, lo1, hi0 ^ ctr.w ^ k1, lo0};
+    k0 += W0; k1 += W1;
+  }
+  return ctr;
+}
+
+// 24-bit uniform in [0,1) (same resolution as torch's fp32 uniform).
+__device__ __forceinline__ float u01(uint32_t x) { return (float)(x >> 8) * (1.0f / 16777216.0f); }
+
+// Stream ids (Philox counter word 3 high bits) so independent draws never share counters.
+enum : uint32_t { RNG_STE = 1u, RNG_ATTN_DROP = 2u, RNG_PROJ_DROP = 3u };
+
+}  // namespace csa

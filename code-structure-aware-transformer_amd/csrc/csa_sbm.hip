@@ -1,0 +1,1345 @@
+// SBM attention (module/sbm_attn.py:11-87 + module/STE.py) as gfx950 HIP kernels.
+//
+// Pipeline (one forward + one backward = 9 launches, all stream-ordered, no host sync):
+//   fwd: k_cluster_softmax   S_h = softmax_{k^2}(C_h C_h^T)                      sbm_attn.py:37-39
+//        k_frag_prep         weights -> MFMA-operand-major fragments (L2-resident)
+//        k_proj_fwd          Qh = sigmoid(MLP(Q) C^T), Kh likewise, T = Kh S^T    sbm_attn.py:41-53
+//        k_attn_fwd          expA tile, u < clamp(expA) sampling, online softmax
+//                            with graph-masked L1 renormalisation, dropout, PV    sbm_attn.py:55-64, STE.py:10-15
+//        k_sparsity_finish   integer edge counts -> head-wise sparsity            sbm_attn.py:64
+//   bwd: k_attn_bwd_q        dQ (attention path), dQh, gamma = rowsum(dX*X)
+//        k_attn_bwd_kv       dK (attention path), dV, dT
+//        k_proj_bwd          STE/sigmoid/cluster/MLP backward (+dQ, +dK second path),
+//                            per-workgroup fixed-order partial slabs for dW, db, dC, dS
+//        k_param_reduce      fixed-order slab reduction, softmax_{k^2} backward -> dC
+// The N x N intermediates of the reference (expA, graph, dot, softmax, attn: ~11 fp32
+// (B,H,N,M) tensors) are never materialised: the sampled graph and the dropout keep-mask
+// are kept as 1 bit per edge for the backward, and the optional attn/graph maps are
+// produced by k_maps only when the caller asks for them.
+#include "csa_common.hpp"
+#include "../../include/csa_hip.h"
+
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+using namespace csa;
+
+namespace {
+
+constexpr float NEG_INF = -__builtin_inff();
+constexpr float NORM_EPS = 1e-12f;  // F.normalize default eps (sbm_attn.py:62)
+
+// ------------------------------------------------------------------------------------
+// Layout of the saved forward state (caller-allocated, csa_sbm_state_bytes)
+// ------------------------------------------------------------------------------------
+struct Layout {
+  int64_t B, H, N, M, D, k, kp, KT, NQB, NKB, Mpad;
+  size_t S, Qh, Kh, T, stats, Abits, Rbits, cnt, Wf[3], WfT[3], Cf, CfT, Sf, SfT, total;
+  // bwd workspace
+  size_t w_dQh, w_dT, w_slab, w_dS, w_dC, w_total;
+  int64_t G, slab_floats;
+};
+
+inline size_t al(size_t x) { return (x + 255) & ~size_t(255); }
+
+Layout make_layout(int64_t B, int64_t H, int64_t N, int64_t M, int64_t D, int64_t k, bool dense) {
+  Layout L;
+  L.B = B; L.H = H; L.N = N; L.M = M; L.D = D; L.k = dense ? 0 : k;
+  L.kp = dense ? 0 : ((k + 7) / 8) * 8;
+  L.KT = dense ? 0 : (k + 31) / 32;
+  L.NQB = (N + 31) / 32; L.NKB = (M + 31) / 32; L.Mpad = L.NKB * 32;
+  size_t o = 0;
+  auto take = [&](size_t bytes) { size_t r = o; o += al(bytes); return r; };
+  const int64_t KP32 = 32 * L.KT;
+  L.S = take(sizeof(float) * H * KP32 * KP32);
+  L.Qh = take(sizeof(float) * B * H * N * L.kp);
+  L.Kh = take(sizeof(float) * B * H * M * L.kp);
+  L.T = take(sizeof(float) * B * H * M * L.kp);
+  L.stats = take(sizeof(float) * B * H * N * 4);
+  L.Abits = take(sizeof(uint32_t) * B * H * L.NQB * L.Mpad);
+  L.Rbits = take(sizeof(uint32_t) * B * H * L.NQB * L.Mpad);
+  L.cnt = take(sizeof(unsigned long long) * H);
+  for (int l = 0; l < 3; ++l) L.Wf[l] = take(sizeof(float) * (dense ? 0 : D * D));
+  for (int l = 0; l < 3; ++l) L.WfT[l] = take(sizeof(float) * (dense ? 0 : D * D));
+  L.Cf = take(sizeof(float) * H * KP32 * D);
+  L.CfT = take(sizeof(float) * H * KP32 * D);
+  L.Sf = take(sizeof(float) * H * KP32 * KP32);
+  L.SfT = take(sizeof(float) * H * KP32 * KP32);
+  L.total = o;
+  // backward workspace
+  L.G = dense ? 0 : (B < 64 ? B : 64);
+  L.slab_floats = dense ? 0 : (3 * D * D + 3 * D + KP32 * D + KP32 * KP32);
+  o = 0;
+  L.w_dQh = take(sizeof(float) * B * H * N * L.kp);
+  L.w_dT = take(sizeof(float) * B * H * M * L.kp);
+  L.w_slab = take(sizeof(float) * H * L.G * L.slab_floats);
+  L.w_dS = take(sizeof(float) * H * KP32 * KP32);
+  L.w_dC = take(sizeof(float) * H * KP32 * D);
+  L.w_total = o;
+  return L;
+}
+
+template <typename T> __device__ __forceinline__ T* at(void* base, size_t off) {
+  return reinterpret_cast<T*>(reinterpret_cast<char*>(base) + off);
+}
+
+// Fragment of an MFMA A operand, stored operand-major: ((it * nsteps/4 + s/4) * 64 + lane) * 4 + s%4
+__device__ __forceinline__ f32x4 frag4(const float* __restrict__ f, int it, int nsteps, int s4) {
+  return *reinterpret_cast<const f32x4*>(f + ((size_t)(it * (nsteps >> 2) + s4) * 64 + lane_id()) * 4);
+}
+
+// ------------------------------------------------------------------------------------
+// F1: S_h = softmax over all k^2 entries of C_h C_h^T, zero-padded to (32KT x 32KT)
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_cluster_softmax(const float* __restrict__ C, float* __restrict__ S,
+                                                         int k, int D, int KP32) {
+  const int hd = blockIdx.x, tid = threadIdx.x;
+  __shared__ float dist[64 * 64];  // k <= 64
+  __shared__ float red[256];
+  const float* Ch = C + (size_t)hd * k * D;
+  const int kk = k * k;
+  for (int e = tid; e < kk; e += 256) {
+    const int a = e / k, b = e % k;
+    float acc = 0.f;
+    for (int t = 0; t < D; ++t) acc = fmaf(Ch[a * D + t], Ch[b * D + t], acc);
+    dist[e] = acc;
+  }
+  __syncthreads();
+  float mx = NEG_INF;
+  for (int e = tid; e < kk; e += 256) mx = fmaxf(mx, dist[e]);
+  red[tid] = mx;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (tid < s) red[tid] = fmaxf(red[tid], red[tid + s]);
+    __syncthreads();
+  }
+  mx = red[0];
+  __syncthreads();
+  float sm = 0.f;
+  for (int e = tid; e < kk; e += 256) sm += expf(dist[e] - mx);
+  red[tid] = sm;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (tid < s) red[tid] += red[tid + s];
+    __syncthreads();
+  }
+  sm = red[0];
+  float* Sh = S + (size_t)hd * KP32 * KP32;
+  for (int e = tid; e < KP32 * KP32; e += 256) {
+    const int a = e / KP32, b = e % KP32;
+    Sh[e] = (a < k && b < k) ? expf(dist[a * k + b] - mx) / sm : 0.f;
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Fragment prep: dst(it, s, lane) = Mat[32 it + c][kperm(s, h)] (or Mat^T), 0 outside.
+// ------------------------------------------------------------------------------------
+struct FragJob {
+  const float* src; float* dst;
+  int rows, cols, ld;         // source matrix (rows x cols, row stride ld)
+  int transpose;              // value = src[kk][r] instead of src[r][kk]
+  int acc_perm;               // kperm: 0 = lin (k = s + nsteps*h), 1 = acc (k = 32(s/16)+crow(s%16,h))
+  int nit, nsteps;            // output tiles x K-steps
+  int batch; int64_t src_bstride, dst_bstride;  // repeated per head
+};
+struct FragJobs { FragJob j[12]; int n; };
+
+__global__ __launch_bounds__(256) void k_frag_prep(const FragJobs jobs) {
+  const FragJob J = jobs.j[blockIdx.y];
+  const int64_t per = (int64_t)J.nit * J.nsteps * 64;
+  const int64_t total = per * J.batch;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int64_t bidx = e / per, rem = e % per;
+    const int s4 = (int)(rem / 256) % (J.nsteps / 4);
+    const int it = (int)(rem / 256) / (J.nsteps / 4);
+    const int lane = (int)(rem / 4) % 64, s = s4 * 4 + (int)(rem % 4);
+    const int c = lane & 31, h = lane >> 5;
+    const int r = 32 * it + c;
+    const int kk = J.acc_perm ? 32 * (s / 16) + crow(s % 16, h) : s + J.nsteps * h;
+    const float* src = J.src + bidx * J.src_bstride;
+    float v = 0.f;
+    if (r < J.rows && kk < J.cols) v = J.transpose ? src[(int64_t)kk * J.ld + r] : src[(int64_t)r * J.ld + kk];
+    J.dst[bidx * J.dst_bstride + rem] = v;
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Shared kernel arguments
+// ------------------------------------------------------------------------------------
+struct KArgs {
+  int B, H, N, M, k, kp, NQB, NKB, Mpad;
+  const float *Q, *K, *V; int64_t q_sb, q_sh, q_sn, k_sb, k_sh, k_sn, v_sb, v_sh, v_sn;
+  const float* mask; int64_t mask_sb;
+  const float* pb[3];  // proj biases
+  const float *Wf[3], *WfT[3], *Cf, *CfT, *Sf, *SfT, *S;
+  float *Qh, *Kh, *T, *stats;
+  uint32_t *Abits, *Rbits;
+  unsigned long long* cnt;
+  const float* U;
+  uint32_t seed_lo, seed_hi, off;
+  float attn_p, proj_p, scale;
+  // outputs
+  float* X;
+  // backward
+  const float *dX, *dsp, *dgraph;
+  float *dQ, *dK, *dV, *dQh, *dT, *slab;
+  int G; int64_t slab_floats;
+};
+
+__device__ __forceinline__ f32x4 philox_u4(uint32_t a, uint32_t b, uint32_t c, uint32_t stream, const KArgs& p) {
+  u32x4 r = philox4x32_10(u32x4{a, b, c, (stream << 28) ^ p.off}, p.seed_lo, p.seed_hi);
+  f32x4 o; o[0] = u01(r.x); o[1] = u01(r.y); o[2] = u01(r.z); o[3] = u01(r.w);
+  return o;
+}
+
+// MLP forward of one 32-row block held as lin-perm rows x[D/2] (see csa_common.hpp).
+// Produces the post-ReLU hidden activations h1, h2 and the output p as accumulator tiles
+// (feature rows in registers, data rows on lanes). Proj dropout p>0 applies
+// Linear -> Dropout -> ReLU (sbm_attn.py:22-30) with a stateless Philox mask.
+template <int D>
+__device__ __forceinline__ void mlp_fwd(const KArgs& p, const float (&x)[D / 2], f32x16 (&h1)[D / 32],
+                                        f32x16 (&h2)[D / 32], f32x16 (&po)[D / 32], int row, int bh, int isK) {
+  constexpr int DT = D / 32, NS = D / 2;
+  const int h = lane_id() >> 5;
+  const bool drop = p.proj_p > 0.f;
+  const float ks = drop ? 1.f / (1.f - p.proj_p) : 1.f;
+  // layer 0: lin-perm input
+#pragma unroll
+  for (int ot = 0; ot < DT; ++ot)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) h1[ot][r] = p.pb[0][32 * ot + crow(r, h)];
+#pragma unroll
+  for (int s4 = 0; s4 < NS / 4; ++s4)
+#pragma unroll
+    for (int ot = 0; ot < DT; ++ot) {
+      const f32x4 w = frag4(p.Wf[0], ot, NS, s4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) h1[ot] = mfma(w[j], x[4 * s4 + j], h1[ot]);
+    }
+  auto act = [&](f32x16(&a)[DT], int layer) {
+#pragma unroll
+    for (int ot = 0; ot < DT; ++ot)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        f32x4 u;
+        if (drop) u = philox_u4((uint32_t)row, (uint32_t)(8 * ot + 2 * g + h) | (layer << 16) | (isK << 20),
+                                (uint32_t)bh, RNG_PROJ_DROP, p);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float v = a[ot][4 * g + e];
+          if (drop) v = (u[e] >= p.proj_p) ? v * ks : 0.f;
+          a[ot][4 * g + e] = fmaxf(v, 0.f);
+        }
+      }
+  };
+  act(h1, 0);
+  // layers 1, 2: acc-perm input
+  auto dense_layer = [&](const f32x16(&in)[DT], f32x16(&out)[DT], int l) {
+#pragma unroll
+    for (int ot = 0; ot < DT; ++ot)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) out[ot][r] = p.pb[l][32 * ot + crow(r, h)];
+#pragma unroll
+    for (int t = 0; t < DT; ++t)
+#pragma unroll
+      for (int r4 = 0; r4 < 4; ++r4)
+#pragma unroll
+        for (int ot = 0; ot < DT; ++ot) {
+          const f32x4 w = frag4(p.Wf[l], ot, NS, 4 * t + r4);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) out[ot] = mfma(w[j], in[t][4 * r4 + j], out[ot]);
+        }
+  };
+  dense_layer(h1, h2, 1);
+  act(h2, 1);
+  dense_layer(h2, po, 2);
+}
+
+// hat^T = sigmoid(C_h p^T), rows (clusters) >= k zeroed.
+template <int D, int KT>
+__device__ __forceinline__ void cluster_hat(const KArgs& p, const f32x16 (&po)[D / 32], f32x16 (&hat)[KT], int hd) {
+  constexpr int NS = D / 2;
+  const int h = lane_id() >> 5;
+  const float* Cf = p.Cf + (size_t)hd * 32 * KT * D;
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt) {
+    hat[kt] = zero16();
+#pragma unroll
+    for (int s4 = 0; s4 < NS / 4; ++s4) {
+      const f32x4 w = frag4(Cf, kt, NS, s4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int s = 4 * s4 + j;
+        hat[kt] = mfma(w[j], po[s / 16][s % 16], hat[kt]);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int a = 32 * kt + crow(r, h);
+      hat[kt][r] = (a < p.k) ? 1.f / (1.f + expf(-hat[kt][r])) : 0.f;
+    }
+  }
+}
+
+// out^T = Sfrag * in^T (K = 32 KT clusters, acc-perm input)
+template <int KT>
+__device__ __forceinline__ void small_mm(const float* __restrict__ frag, const f32x16 (&in)[KT], f32x16 (&out)[KT]) {
+#pragma unroll
+  for (int at = 0; at < KT; ++at) {
+    out[at] = zero16();
+#pragma unroll
+    for (int s4 = 0; s4 < 4 * KT; ++s4) {
+      const f32x4 w = frag4(frag, at, 16 * KT, s4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int s = 4 * s4 + j;
+        out[at] = mfma(w[j], in[s / 16][s % 16], out[at]);
+      }
+    }
+  }
+}
+
+// Store an accumulator tile set (feature rows, data row = lane) to out[row][0..ncols) (row-major, ld)
+template <int NT>
+__device__ __forceinline__ void store_rows(float* __restrict__ out, int64_t ld, int ncols, const f32x16 (&a)[NT], bool valid) {
+  if (!valid) return;
+  const int h = lane_id() >> 5;
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int c0 = 32 * t + 8 * g + 4 * h;
+      if (c0 < ncols) {
+        f32x4 v; v[0] = a[t][4 * g]; v[1] = a[t][4 * g + 1]; v[2] = a[t][4 * g + 2]; v[3] = a[t][4 * g + 3];
+        *reinterpret_cast<f32x4*>(out + c0) = v;
+      }
+    }
+  (void)ld;
+}
+
+template <int NT>
+__device__ __forceinline__ void load_rows(f32x16 (&a)[NT], const float* __restrict__ in, int ncols, bool valid) {
+  const int h = lane_id() >> 5;
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int c0 = 32 * t + 8 * g + 4 * h;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (valid && c0 < ncols) v = *reinterpret_cast<const f32x4*>(in + c0);
+      a[t][4 * g] = v[0]; a[t][4 * g + 1] = v[1]; a[t][4 * g + 2] = v[2]; a[t][4 * g + 3] = v[3];
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// F2: per 32-row block of Q or K: Qh = sigmoid(MLP(Q) C^T); Kh likewise and T = Kh S^T.
+// grid (NQB + NKB, B*H), one wave per block.
+// ------------------------------------------------------------------------------------
+template <int D, int KT>
+__global__ __launch_bounds__(64) void k_proj_fwd(const KArgs p) {
+  const int lane = lane_id(), c = lane & 31, h = lane >> 5;
+  const int bh = blockIdx.y, b = bh / p.H, hd = bh % p.H;
+  const int isK = blockIdx.x >= p.NQB;
+  const int rb = isK ? blockIdx.x - p.NQB : blockIdx.x;
+  const int nrows = isK ? p.M : p.N;
+  const int row = rb * 32 + c;
+  const bool rv = row < nrows;
+  const float* X = isK ? p.K + b * p.k_sb + hd * p.k_sh + (int64_t)row * p.k_sn
+                       : p.Q + b * p.q_sb + hd * p.q_sh + (int64_t)row * p.q_sn;
+  float x[D / 2];
+  load_run<D / 2>(x, X + h * (D / 2), rv);
+  f32x16 h1[D / 32], h2[D / 32], po[D / 32], hat[KT];
+  mlp_fwd<D>(p, x, h1, h2, po, row, bh, isK);
+  cluster_hat<D, KT>(p, po, hat, hd);
+  if (!isK) {
+    store_rows<KT>(p.Qh + ((int64_t)bh * p.N + row) * p.kp, p.kp, p.kp, hat, rv);
+  } else {
+    store_rows<KT>(p.Kh + ((int64_t)bh * p.M + row) * p.kp, p.kp, p.kp, hat, rv);
+    f32x16 t[KT];
+    small_mm<KT>(p.Sf + (size_t)hd * 1024 * KT * KT, hat, t);
+    store_rows<KT>(p.T + ((int64_t)bh * p.M + row) * p.kp, p.kp, p.kp, t, rv);
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// F3: attention forward, one wave per (b, h, 32-query block), S^T orientation
+// (keys = accumulator rows, queries = lanes). Online softmax with two running sums:
+//   Z = sum e, Zg = sum e*A; X = (sum e*A*r V) / (Z * max(Zg/Z, 1e-12))
+// which equals F.normalize(softmax(s) * graph, p=1) @ dropout (sbm_attn.py:59-63).
+// ------------------------------------------------------------------------------------
+template <int D, int KPH, bool DENSE>
+__global__ __launch_bounds__(64) void k_attn_fwd(const KArgs p) {
+  constexpr int DT = D / 32, NS = D / 2;
+  const int lane = lane_id(), c = lane & 31, h = lane >> 5;
+  const int qb = blockIdx.x, bh = blockIdx.y, b = bh / p.H, hd = bh % p.H;
+  const int i = qb * 32 + c;
+  const bool iv = i < p.N;
+  float q[NS];
+  load_run<NS>(q, p.Q + b * p.q_sb + hd * p.q_sh + (int64_t)i * p.q_sn + h * NS, iv);
+  float qh[KPH > 0 ? KPH : 1];
+  if (!DENSE) load_run<KPH>(qh, p.Qh + ((int64_t)bh * p.N + i) * p.kp + h * KPH, iv);
+  const float* kb = p.K + b * p.k_sb + hd * p.k_sh;
+  const float* vb = p.V + b * p.v_sb + hd * p.v_sh;
+  const float* mk = p.mask ? p.mask + b * p.mask_sb : nullptr;
+  const bool drop = p.attn_p > 0.f;
+  const float dscale = drop ? 1.f / (1.f - p.attn_p) : 1.f;
+  float m_run = NEG_INF, zp = 0.f, zgp = 0.f;
+  f32x16 o[DT];
+#pragma unroll
+  for (int t = 0; t < DT; ++t) o[t] = zero16();
+  unsigned long long cnt = 0;
+
+  for (int kt = 0; kt < p.NKB; ++kt) {
+    const int j0 = kt * 32, jl = j0 + c;
+    const bool jv = jl < p.M;
+    float kr[NS];
+    load_run<NS>(kr, kb + (int64_t)jl * p.k_sn + h * NS, jv);
+    f32x16 sacc = zero16();
+#pragma unroll
+    for (int s = 0; s < NS; ++s) sacc = mfma(kr[s], q[s], sacc);
+    const bool kval = jv && (mk == nullptr || mk[jl] == 0.f);
+    const uint32_t vw = (uint32_t)__ballot(kval);
+    f32x16 eacc;
+    if (!DENSE) {
+      float tr[KPH > 0 ? KPH : 1];
+      load_run<KPH>(tr, p.T + ((int64_t)bh * p.M + jl) * p.kp + h * KPH, jv);
+      eacc = zero16();
+#pragma unroll
+      for (int s = 0; s < KPH; ++s) eacc = mfma(tr[s], qh[s], eacc);
+    }
+    float sv[16], w[16];
+    bool av[16], keep[16];
+    float tmax = NEG_INF;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const bool valid = (vw >> crow(r, h)) & 1u;
+      sv[r] = valid ? sacc[r] * p.scale : NEG_INF;
+      tmax = fmaxf(tmax, sv[r]);
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int jg = j0 + 8 * g + 4 * h;  // keys jg..jg+3 held in registers 4g..4g+3
+      if (!DENSE) {
+        f32x4 uu;
+        if (p.U) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            uu[e] = (iv && jg + e < p.M) ? p.U[((int64_t)bh * p.N + i) * p.M + jg + e] : 2.f;
+        } else {
+          uu = philox_u4((uint32_t)i, (uint32_t)(jg >> 2), (uint32_t)bh, RNG_STE, p);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float pr = fminf(fmaxf(eacc[4 * g + e], 0.01f), 0.99f);  // STE.py:11
+          av[4 * g + e] = iv && (jg + e < p.M) && (uu[e] < pr);          // STE.py:13
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) av[4 * g + e] = iv && (jg + e < p.M);
+      }
+      if (drop) {
+        const f32x4 ud = philox_u4((uint32_t)i, (uint32_t)(jg >> 2), (uint32_t)bh, RNG_ATTN_DROP, p);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) keep[4 * g + e] = ud[e] >= p.attn_p;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) keep[4 * g + e] = true;
+      }
+    }
+    // bit-pack the sampled graph / dropout keep mask: word [qb][key] holds 32 query bits
+    if (!DENSE || drop) {
+      uint32_t myA = 0, myR = 0;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if (!DENSE) {
+          const unsigned long long bal = __ballot(av[r]);
+          cnt += __popcll(bal);
+          myA |= (c == crow(r, 0)) ? (uint32_t)bal : 0u;
+          myA |= (c == crow(r, 1)) ? (uint32_t)(bal >> 32) : 0u;
+        }
+        if (drop) {
+          const unsigned long long bal = __ballot(keep[r]);
+          myR |= (c == crow(r, 0)) ? (uint32_t)bal : 0u;
+          myR |= (c == crow(r, 1)) ? (uint32_t)(bal >> 32) : 0u;
+        }
+      }
+      const int64_t widx = ((int64_t)bh * p.NQB + qb) * p.Mpad + j0 + c;
+      if (!DENSE && h == 0) p.Abits[widx] = myA;
+      if (drop && h == 1) p.Rbits[widx] = myR;
+    }
+    // online softmax update
+    tmax = xhalf_max(tmax);
+    const float m_new = fmaxf(m_run, tmax);
+    const float alpha = (m_new == NEG_INF) ? 1.f : expf(m_run - m_new);
+    zp *= alpha;
+    zgp *= alpha;
+#pragma unroll
+    for (int t = 0; t < DT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float e = (sv[r] == NEG_INF) ? 0.f : expf(sv[r] - m_new);
+      zp += e;
+      const float wa = av[r] ? e : 0.f;
+      zgp += wa;
+      w[r] = keep[r] ? wa * dscale : 0.f;
+    }
+    m_run = m_new;
+    // O^T += V^T W^T   (A = V^T: lane d holds V[key crow(r,h)][d])
+#pragma unroll
+    for (int t = 0; t < DT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int j = j0 + crow(r, h);
+        const float vt = (j < p.M) ? vb[(int64_t)j * p.v_sn + 32 * t + c] : 0.f;
+        o[t] = mfma(vt, w[r], o[t]);
+      }
+  }
+  const float Z = xhalf_sum(zp), Zg = xhalf_sum(zgp);
+  const float n = Zg / Z;
+  const float Dn = fmaxf(n, NORM_EPS);
+  const float inv = 1.f / (Z * Dn);
+  if (iv) {
+    float* xo = p.X + ((int64_t)bh * p.N + i) * D;
+#pragma unroll
+    for (int t = 0; t < DT; ++t) {
+      f32x16 v = o[t];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] *= inv;
+      o[t] = v;
+    }
+    store_rows<DT>(xo, D, D, o, true);
+    if (h == 0) {
+      f32x4 st;
+      st[0] = m_run + logf(Z);   // lse: P = exp(s - lse)
+      st[1] = 1.f / Dn;          // 1 / max(n, eps)
+      st[2] = (n >= NORM_EPS) ? 1.f : 0.f;
+      st[3] = 0.f;               // gamma, filled by the backward
+      *reinterpret_cast<f32x4*>(p.stats + ((int64_t)bh * p.N + i) * 4) = st;
+    }
+  }
+  if (!DENSE && lane == 0 && cnt) atomicAdd(p.cnt + hd, cnt);
+}
+
+__global__ void k_sparsity_finish(const unsigned long long* __restrict__ cnt, float* __restrict__ sp, int H, float bnm) {
+  const int t = threadIdx.x;
+  if (t < H) sp[t] = (float)cnt[t] / bnm;  // torch.sum(graph)/(b*n*m), exact integer count (sbm_attn.py:64)
+}
+
+// ------------------------------------------------------------------------------------
+// F4: optional maps: attn (B,H,N,M) and graph (B,H,N,M) fp32, S orientation (key = lane)
+// ------------------------------------------------------------------------------------
+template <int D, bool DENSE>
+__global__ __launch_bounds__(64) void k_maps(const KArgs p, float* __restrict__ graph, float* __restrict__ attn) {
+  constexpr int NS = D / 2;
+  const int lane = lane_id(), c = lane & 31, h = lane >> 5;
+  const int qb = blockIdx.x, bh = blockIdx.y, b = bh / p.H, hd = bh % p.H;
+  const int i0 = qb * 32;
+  float q[NS];
+  load_run<NS>(q, p.Q + b * p.q_sb + hd * p.q_sh + (int64_t)(i0 + c) * p.q_sn + h * NS, i0 + c < p.N);
+  float lse[16], invD[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int ii = i0 + crow(r, h);
+    lse[r] = (ii < p.N) ? p.stats[((int64_t)bh * p.N + ii) * 4 + 0] : 0.f;
+    invD[r] = (ii < p.N) ? p.stats[((int64_t)bh * p.N + ii) * 4 + 1] : 0.f;
+  }
+  const float* kb = p.K + b * p.k_sb + hd * p.k_sh;
+  const float* mk = p.mask ? p.mask + b * p.mask_sb : nullptr;
+  for (int kt = 0; kt < p.NKB; ++kt) {
+    const int j = kt * 32 + c;
+    const bool jv = j < p.M;
+    float kr[NS];
+    load_run<NS>(kr, kb + (int64_t)j * p.k_sn + h * NS, jv);
+    f32x16 sacc = zero16();
+#pragma unroll
+    for (int s = 0; s < NS; ++s) sacc = mfma(q[s], kr[s], sacc);
+    const bool kval = jv && (mk == nullptr || mk[j] == 0.f);
+    const uint32_t word = DENSE ? 0xffffffffu : (jv ? p.Abits[((int64_t)bh * p.NQB + qb) * p.Mpad + j] : 0u);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int ii = i0 + crow(r, h);
+      if (ii < p.N && jv) {
+        const bool a = (word >> crow(r, h)) & 1u;
+        const float pv = kval ? expf(sacc[r] * p.scale - lse[r]) : 0.f;
+        const int64_t o = ((int64_t)bh * p.N + ii) * p.M + j;
+        if (attn) attn[o] = a ? pv * invD[r] : 0.f;
+        if (graph) graph[o] = a ? 1.f : 0.f;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Backward elementwise core for one (query i, key j) element (see oracle/closed_form.py)
+// ------------------------------------------------------------------------------------
+struct Elem { float ds, g, attw; };
+
+__device__ __forceinline__ Elem bwd_elem(float s_raw, float dpp, bool kval, bool a, bool keep, bool inside,
+                                         float lse, float invD, float big, float gamma, float scale, float dscale,
+                                         float csp, float dgr) {
+  Elem r;
+  if (!inside) { r.ds = 0.f; r.g = 0.f; r.attw = 0.f; return r; }
+  const float P = kval ? expf(s_raw * scale - lse) : 0.f;
+  const float rm = keep ? dscale : 0.f;
+  const float dattn = dpp * rm;
+  const bool mpos = a && (P > 0.f);
+  const float dM = (dattn - ((big != 0.f && mpos) ? gamma : 0.f)) * invD;
+  const float dPm = a ? dM : 0.f;
+  const float rho = (big != 0.f) ? 0.f : gamma;
+  r.ds = P * (dPm - rho) * scale;
+  const float dA = dM * P + csp + dgr;
+  r.g = a ? fminf(fmaxf(dA, -1.f), 1.f) : 0.f;  // STE.py:19 hardtanh(A * grad)
+  r.attw = a ? P * invD * rm : 0.f;              // dropout(attn) weight for dV
+  return r;
+}
+
+// ------------------------------------------------------------------------------------
+// B2: per (b,h, query block), S^T orientation: dQ (attention path), dQh, gamma
+// ------------------------------------------------------------------------------------
+template <int D, int KT, bool DENSE>
+__global__ __launch_bounds__(64) void k_attn_bwd_q(const KArgs p) {
+  constexpr int DT = D / 32, NS = D / 2;
+  const int lane = lane_id(), c = lane & 31, h = lane >> 5;
+  const int qb = blockIdx.x, bh = blockIdx.y, b = bh / p.H, hd = bh % p.H;
+  const int i = qb * 32 + c;
+  const bool iv = i < p.N;
+  float q[NS], dx[NS];
+  load_run<NS>(q, p.Q + b * p.q_sb + hd * p.q_sh + (int64_t)i * p.q_sn + h * NS, iv);
+  load_run<NS>(dx, p.dX + ((int64_t)bh * p.N + i) * D + h * NS, iv);
+  float gp = 0.f;
+  {
+    float xr[NS];
+    load_run<NS>(xr, p.X + ((int64_t)bh * p.N + i) * D + h * NS, iv);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) gp = fmaf(dx[s], xr[s], gp);
+  }
+  const float gamma = xhalf_sum(gp);
+  f32x4 st = {0.f, 0.f, 0.f, 0.f};
+  if (iv) st = *reinterpret_cast<const f32x4*>(p.stats + ((int64_t)bh * p.N + i) * 4);
+  if (iv && h == 0) p.stats[((int64_t)bh * p.N + i) * 4 + 3] = gamma;
+  const float lse = st[0], invD = st[1], big = st[2];
+  const bool drop = p.attn_p > 0.f;
+  const float dscale = drop ? 1.f / (1.f - p.attn_p) : 1.f;
+  const float csp = (!DENSE && p.dsp) ? p.dsp[hd] / ((float)p.B * (float)p.N * (float)p.M) : 0.f;
+  const float* kb = p.K + b * p.k_sb + hd * p.k_sh;
+  const float* vb = p.V + b * p.v_sb + hd * p.v_sh;
+  const float* mk = p.mask ? p.mask + b * p.mask_sb : nullptr;
+  constexpr int KTA = KT > 0 ? KT : 1;
+  f32x16 dq[DT], dqh[KTA];
+#pragma unroll
+  for (int t = 0; t < DT; ++t) dq[t] = zero16();
+#pragma unroll
+  for (int t = 0; t < KTA; ++t) dqh[t] = zero16();
+  for (int kt = 0; kt < p.NKB; ++kt) {
+    const int j0 = kt * 32, jl = j0 + c;
+    const bool jv = jl < p.M;
+    f32x16 sacc = zero16(), dpacc = zero16();
+    {
+      float kr[NS];
+      load_run<NS>(kr, kb + (int64_t)jl * p.k_sn + h * NS, jv);
+#pragma unroll
+      for (int s = 0; s < NS; ++s) sacc = mfma(kr[s], q[s], sacc);
+    }
+    {
+      float vr[NS];
+      load_run<NS>(vr, vb + (int64_t)jl * p.v_sn + h * NS, jv);
+#pragma unroll
+      for (int s = 0; s < NS; ++s) dpacc = mfma(vr[s], dx[s], dpacc);
+    }
+    const bool kval = jv && (mk == nullptr || mk[jl] == 0.f);
+    const uint32_t vw = (uint32_t)__ballot(kval);
+    const int64_t widx = ((int64_t)bh * p.NQB + qb) * p.Mpad + jl;
+    const uint32_t wA = DENSE ? 0xffffffffu : p.Abits[widx];
+    const uint32_t wR = drop ? p.Rbits[widx] : 0xffffffffu;
+    float dsv[16], gv[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int jj = crow(r, h), j = j0 + jj;
+      const uint32_t a_w = DENSE ? 0xffffffffu : (uint32_t)__shfl((int)wA, jj, 64);
+      const uint32_t r_w = drop ? (uint32_t)__shfl((int)wR, jj, 64) : 0xffffffffu;
+      const bool a = (a_w >> c) & 1u;
+      const bool keep = (r_w >> c) & 1u;
+      const bool inside = iv && (j < p.M);
+      const float dgr = (p.dgraph && inside) ? p.dgraph[((int64_t)bh * p.N + i) * p.M + j] : 0.f;
+      const Elem e = bwd_elem(sacc[r], dpacc[r], (vw >> jj) & 1u, DENSE ? inside : a, keep, inside, lse, invD, big,
+                              gamma, p.scale, dscale, csp, dgr);
+      dsv[r] = e.ds;
+      gv[r] = e.g;
+    }
+    // dQ^T += K^T ds^T   (A = K^T: lane d holds K[key crow(r,h)][d])
+#pragma unroll
+    for (int t = 0; t < DT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int j = j0 + crow(r, h);
+        const float kv = (j < p.M) ? kb[(int64_t)j * p.k_sn + 32 * t + c] : 0.f;
+        dq[t] = mfma(kv, dsv[r], dq[t]);
+      }
+    if constexpr (!DENSE) {
+      // dQh^T += T^T G^T
+#pragma unroll
+      for (int at = 0; at < KTA; ++at)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int j = j0 + crow(r, h), a = 32 * at + c;
+          const float tv = (j < p.M && a < p.kp) ? p.T[((int64_t)bh * p.M + j) * p.kp + a] : 0.f;
+          dqh[at] = mfma(tv, gv[r], dqh[at]);
+        }
+    }
+  }
+  store_rows<DT>(p.dQ + ((int64_t)bh * p.N + i) * D, D, D, dq, iv);
+  if constexpr (!DENSE) store_rows<KTA>(p.dQh + ((int64_t)bh * p.N + i) * p.kp, p.kp, p.kp, dqh, iv);
+}
+
+// ------------------------------------------------------------------------------------
+// B1: per (b,h, key block), S orientation (queries = acc rows, keys = lanes): dK, dV, dT
+// ------------------------------------------------------------------------------------
+template <int D, int KT, bool DENSE>
+__global__ __launch_bounds__(64) void k_attn_bwd_kv(const KArgs p) {
+  constexpr int DT = D / 32, NS = D / 2;
+  const int lane = lane_id(), c = lane & 31, h = lane >> 5;
+  const int kbi = blockIdx.x, bh = blockIdx.y, b = bh / p.H, hd = bh % p.H;
+  const int j = kbi * 32 + c;
+  const bool jv = j < p.M;
+  const float* qbase = p.Q + b * p.q_sb + hd * p.q_sh;
+  const float* mk = p.mask ? p.mask + b * p.mask_sb : nullptr;
+  const bool kval = jv && (mk == nullptr || mk[j] == 0.f);
+  float kr[NS], vr[NS];
+  load_run<NS>(kr, p.K + b * p.k_sb + hd * p.k_sh + (int64_t)j * p.k_sn + h * NS, jv);
+  load_run<NS>(vr, p.V + b * p.v_sb + hd * p.v_sh + (int64_t)j * p.v_sn + h * NS, jv);
+  const bool drop = p.attn_p > 0.f;
+  const float dscale = drop ? 1.f / (1.f - p.attn_p) : 1.f;
+  const float csp = (!DENSE && p.dsp) ? p.dsp[hd] / ((float)p.B * (float)p.N * (float)p.M) : 0.f;
+  constexpr int KTA = KT > 0 ? KT : 1;
+  f32x16 dv[DT], dk[DT], dtt[KTA];
+#pragma unroll
+  for (int t = 0; t < DT; ++t) { dv[t] = zero16(); dk[t] = zero16(); }
+#pragma unroll
+  for (int t = 0; t < KTA; ++t) dtt[t] = zero16();
+  for (int qb = 0; qb < p.NQB; ++qb) {
+    const int i0 = qb * 32, il = i0 + c;
+    const bool ilv = il < p.N;
+    f32x16 sacc = zero16(), dpacc = zero16();
+    {
+      float qr[NS];
+      load_run<NS>(qr, qbase + (int64_t)il * p.q_sn + h * NS, ilv);
+#pragma unroll
+      for (int s = 0; s < NS; ++s) sacc = mfma(qr[s], kr[s], sacc);
+    }
+    {
+      float dxr[NS];
+      load_run<NS>(dxr, p.dX + ((int64_t)bh * p.N + il) * D + h * NS, ilv);
+#pragma unroll
+      for (int s = 0; s < NS; ++s) dpacc = mfma(dxr[s], vr[s], dpacc);
+    }
+    const int64_t widx = ((int64_t)bh * p.NQB + qb) * p.Mpad + j;
+    const uint32_t wA = DENSE ? 0xffffffffu : p.Abits[widx];
+    const uint32_t wR = drop ? p.Rbits[widx] : 0xffffffffu;
+    float dsv[16], gv[16], awv[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int ii = i0 + crow(r, h);
+      const bool inside = (ii < p.N) && jv;
+      f32x4 st = {0.f, 0.f, 0.f, 0.f};
+      if (ii < p.N) st = *reinterpret_cast<const f32x4*>(p.stats + ((int64_t)bh * p.N + ii) * 4);
+      const bool a = DENSE ? inside : ((wA >> crow(r, h)) & 1u);
+      const bool keep = (wR >> crow(r, h)) & 1u;
+      const float dgr = (p.dgraph && inside) ? p.dgraph[((int64_t)bh * p.N + ii) * p.M + j] : 0.f;
+      const Elem e = bwd_elem(sacc[r], dpacc[r], kval, a, keep, inside, st[0], st[1], st[2], st[3], p.scale, dscale,
+                              csp, dgr);
+      dsv[r] = e.ds;
+      gv[r] = e.g;
+      awv[r] = e.attw;
+    }
+    // dV^T += dX^T attw ; dK^T += Q^T ds   (A: lane d holds X[query crow(r,h)][d])
+#pragma unroll
+    for (int t = 0; t < DT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ii = i0 + crow(r, h);
+        const bool v = ii < p.N;
+        const float dxv = v ? p.dX[((int64_t)bh * p.N + ii) * D + 32 * t + c] : 0.f;
+        const float qv = v ? qbase[(int64_t)ii * p.q_sn + 32 * t + c] : 0.f;
+        dv[t] = mfma(dxv, awv[r], dv[t]);
+        dk[t] = mfma(qv, dsv[r], dk[t]);
+      }
+    if constexpr (!DENSE) {
+#pragma unroll
+      for (int at = 0; at < KTA; ++at)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int ii = i0 + crow(r, h), a = 32 * at + c;
+          const float qhv = (ii < p.N && a < p.kp) ? p.Qh[((int64_t)bh * p.N + ii) * p.kp + a] : 0.f;
+          dtt[at] = mfma(qhv, gv[r], dtt[at]);
+        }
+    }
+  }
+  store_rows<DT>(p.dK + ((int64_t)bh * p.M + j) * D, D, D, dk, jv);
+  store_rows<DT>(p.dV + ((int64_t)bh * p.M + j) * D, D, D, dv, jv);
+  if constexpr (!DENSE) store_rows<KTA>(p.dT + ((int64_t)bh * p.M + j) * p.kp, p.kp, p.kp, dtt, jv);
+}
+
+// ------------------------------------------------------------------------------------
+// B3: projection backward. Workgroup = 4 waves, grid (G, H): head hd, batch chunk g.
+// Each wave takes one 32-row item (Q or K block) at a time; the per-row weight gradients
+// dW = sum_rows dout (x) in are reduced over the WG's 128 rows through an LDS transpose
+// ([feature][row] staging) and an MFMA whose K dimension is the row index; each wave owns
+// a fixed subset of the output tiles and accumulates them into the WG's private slab
+// (plain read-modify-write, no atomics -> deterministic).
+// ------------------------------------------------------------------------------------
+constexpr int RW = 128 + 4;  // staging row stride (floats)
+
+template <int D, int KT>
+struct ProjBwdShape {
+  static constexpr int DT = D / 32, NS = D / 2, KP32 = 32 * KT;
+  static constexpr int ROWS = (D > KP32 ? D : KP32);
+  static constexpr size_t LDS_BYTES = sizeof(float) * 2 * ROWS * RW;
+};
+
+// Stage an accumulator tile set (feature rows, data rows on lanes) into LDS[f][wave*32 + c].
+template <int NT>
+__device__ __forceinline__ void stage_acc(float* __restrict__ buf, const f32x16 (&a)[NT], int nrows_valid) {
+  const int lane = lane_id(), c = lane & 31, h = lane >> 5, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int f = 32 * t + crow(r, h);
+      buf[f * RW + w * 32 + c] = (f < nrows_valid) ? a[t][r] : 0.f;
+    }
+}
+
+// C[32ot.., 32it..] (+)= sum over the 128 staged rows of DS[o][row] * IN[i][row]
+// -> RMW into slab (row-major ldo). Tiles (ot, it) for ot < nto, it < nti assigned round-robin to waves.
+__device__ __forceinline__ void wg_outer(const float* __restrict__ ds, const float* __restrict__ in, int nto, int nti,
+                                         float* __restrict__ slab, int ldo, int orows, int icols) {
+  const int lane = lane_id(), c = lane & 31, h = lane >> 5, w = threadIdx.x >> 6;
+  for (int tile = w; tile < nto * nti; tile += 4) {
+    const int ot = tile / nti, it = tile % nti;
+    f32x16 acc = zero16();
+    const float* a = ds + (32 * ot + c) * RW + 64 * h;
+    const float* bb = in + (32 * it + c) * RW + 64 * h;
+#pragma unroll 4
+    for (int s4 = 0; s4 < 16; ++s4) {
+      const f32x4 av = *reinterpret_cast<const f32x4*>(a + 4 * s4);
+      const f32x4 bv = *reinterpret_cast<const f32x4*>(bb + 4 * s4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc = mfma(av[e], bv[e], acc);
+    }
+    const int col = 32 * it + c;
+    if (col < icols) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = 32 * ot + crow(r, h);
+        if (row < orows) slab[row * ldo + col] += acc[r];
+      }
+    }
+  }
+}
+
+// db[f] += sum over the 128 staged rows of DS[f][row]   (threads f < nf)
+__device__ __forceinline__ void wg_rowsum(const float* __restrict__ ds, int nf, float* __restrict__ slab) {
+  const int t = threadIdx.x;
+  if (t < nf) {
+    float s = 0.f;
+    const float* a = ds + t * RW;
+#pragma unroll 8
+    for (int r4 = 0; r4 < 32; ++r4) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(a + 4 * r4);
+      s += (v[0] + v[1]) + (v[2] + v[3]);
+    }
+    slab[t] += s;
+  }
+}
+
+// out^T = Wfrag^T-style product: out[it] = sum_s frag[it][s] * in[s/16][s%16] (acc-perm input)
+template <int NTO, int NTI>
+__device__ __forceinline__ void mm_acc(const float* __restrict__ frag, const f32x16 (&in)[NTI], f32x16 (&out)[NTO]) {
+  constexpr int NSTEP = 16 * NTI;
+#pragma unroll
+  for (int t = 0; t < NTO; ++t) out[t] = zero16();
+#pragma unroll
+  for (int s4 = 0; s4 < NSTEP / 4; ++s4)
+#pragma unroll
+    for (int t = 0; t < NTO; ++t) {
+      const f32x4 w = frag4(frag, t, NSTEP, s4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int s = 4 * s4 + e;
+        out[t] = mfma(w[e], in[s / 16][s % 16], out[t]);
+      }
+    }
+}
+
+template <int D, int KT>
+__global__ __launch_bounds__(256) void k_proj_bwd(const KArgs p) {
+  using Sh = ProjBwdShape<D, KT>;
+  constexpr int DT = Sh::DT, NS = Sh::NS, KP32 = Sh::KP32, ROWS = Sh::ROWS;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* DS = lds;
+  float* IN = lds + ROWS * RW;
+  const int lane = lane_id(), c = lane & 31, h = lane >> 5, w = threadIdx.x >> 6;
+  const int hd = blockIdx.y, g = blockIdx.x, G = gridDim.x;
+  const int b_lo = (int)((int64_t)g * p.B / G), b_hi = (int)((int64_t)(g + 1) * p.B / G);
+  const int per_b = p.NQB + p.NKB;
+  const int n_items = (b_hi - b_lo) * per_b;
+  float* slab = p.slab + ((int64_t)hd * G + g) * p.slab_floats;
+  float* sW[3] = {slab, slab + D * D, slab + 2 * D * D};
+  float* sb[3] = {slab + 3 * D * D, slab + 3 * D * D + D, slab + 3 * D * D + 2 * D};
+  float* sC = slab + 3 * D * D + 3 * D;
+  float* sS = sC + KP32 * D;
+  const float ks = p.proj_p > 0.f ? 1.f / (1.f - p.proj_p) : 1.f;
+  const float* CfT = p.CfT + (size_t)hd * KP32 * D;
+  const float* SfT = p.SfT + (size_t)hd * KP32 * KP32;
+
+  for (int grp = 0; grp * 4 < n_items; ++grp) {
+    const int item = grp * 4 + w;
+    const bool has = item < n_items;
+    const int b = b_lo + (has ? item / per_b : 0);
+    const int r_ = has ? item % per_b : 0;
+    const int isK = r_ >= p.NQB;
+    const int rb = isK ? r_ - p.NQB : r_;
+    const int nrows = isK ? p.M : p.N;
+    const int row = rb * 32 + c;
+    const bool rv = has && row < nrows;
+    const int bh = b * p.H + hd;
+    const float* X = isK ? p.K + b * p.k_sb + hd * p.k_sh + (int64_t)row * p.k_sn
+                         : p.Q + b * p.q_sb + hd * p.q_sh + (int64_t)row * p.q_sn;
+    float x[NS];
+    load_run<NS>(x, X + h * NS, rv);
+    f32x16 h1[DT], h2[DT], po[DT], hat[KT];
+    mlp_fwd<D>(p, x, h1, h2, po, row, bh, isK);
+    cluster_hat<D, KT>(p, po, hat, hd);
+    // gradient w.r.t. the sigmoid output
+    f32x16 dhat[KT], gin[KT];
+    load_rows<KT>(gin, (isK ? p.dT + ((int64_t)bh * p.M + row) * p.kp : p.dQh + ((int64_t)bh * p.N + row) * p.kp),
+                  p.kp, rv);
+    // ---- dS_h += sum_rows dT^T Kh^T  (T_j = S Kh_j) ; K items only
+    stage_acc<KT>(DS, gin, isK ? KP32 : 0);
+    stage_acc<KT>(IN, hat, isK ? KP32 : 0);
+    __syncthreads();
+    wg_outer(DS, IN, KT, KT, sS, KP32, KP32, KP32);
+    __syncthreads();
+    if (isK) {
+      mm_acc<KT, KT>(SfT, gin, dhat);  // dKh^T = S^T dT^T
+    } else {
+#pragma unroll
+      for (int t = 0; t < KT; ++t) dhat[t] = gin[t];
+    }
+    // dZ = dhat * sigmoid'
+#pragma unroll
+    for (int t = 0; t < KT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dhat[t][r] = dhat[t][r] * hat[t][r] * (1.f - hat[t][r]);
+    // ---- dC_h += sum_rows dZ^T p^T
+    stage_acc<KT>(DS, dhat, KP32);
+    stage_acc<DT>(IN, po, D);
+    __syncthreads();
+    wg_outer(DS, IN, KT, DT, sC, D, KP32, D);
+    __syncthreads();
+    // dp^T = C^T dZ^T
+    f32x16 dcur[DT];
+    mm_acc<DT, KT>(CfT, dhat, dcur);
+    // ---- layer 2 (proj.6): dW2 += dp^T h2 ; db2 ; dh2 = W2^T dp
+    stage_acc<DT>(DS, dcur, D);
+    stage_acc<DT>(IN, h2, D);
+    __syncthreads();
+    wg_outer(DS, IN, DT, DT, sW[2], D, D, D);
+    wg_rowsum(DS, D, sb[2]);
+    __syncthreads();
+    {
+      f32x16 dh[DT];
+      mm_acc<DT, DT>(p.WfT[2], dcur, dh);
+#pragma unroll
+      for (int t = 0; t < DT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dcur[t][r] = (h2[t][r] > 0.f) ? dh[t][r] * ks : 0.f;
+    }
+    // ---- layer 1 (proj.3)
+    stage_acc<DT>(DS, dcur, D);
+    stage_acc<DT>(IN, h1, D);
+    __syncthreads();
+    wg_outer(DS, IN, DT, DT, sW[1], D, D, D);
+    wg_rowsum(DS, D, sb[1]);
+    __syncthreads();
+    {
+      f32x16 dh[DT];
+      mm_acc<DT, DT>(p.WfT[1], dcur, dh);
+#pragma unroll
+      for (int t = 0; t < DT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dcur[t][r] = (h1[t][r] > 0.f) ? dh[t][r] * ks : 0.f;
+    }
+    // ---- layer 0 (proj.0): input x is lin-perm: IN[s + NS*h][row] = x[s]
+    stage_acc<DT>(DS, dcur, D);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) IN[(s + NS * h) * RW + w * 32 + c] = x[s];
+    __syncthreads();
+    wg_outer(DS, IN, DT, DT, sW[0], D, D, D);
+    wg_rowsum(DS, D, sb[0]);
+    __syncthreads();
+    {
+      f32x16 dxm[DT];
+      mm_acc<DT, DT>(p.WfT[0], dcur, dxm);
+      if (rv) {  // second-path gradient: dQ/dK += MLP backward
+        float* dst = isK ? p.dK + ((int64_t)bh * p.M + row) * D : p.dQ + ((int64_t)bh * p.N + row) * D;
+#pragma unroll
+        for (int t = 0; t < DT; ++t)
+#pragma unroll
+          for (int g4 = 0; g4 < 4; ++g4) {
+            const int c0 = 32 * t + 8 * g4 + 4 * h;
+            f32x4 v = *reinterpret_cast<f32x4*>(dst + c0);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += dxm[t][4 * g4 + e];
+            *reinterpret_cast<f32x4*>(dst + c0) = v;
+          }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// B4: fixed-order reduction of the partial slabs
+//   out dW, db (sum over H x G slabs); dS_h (sum over G) -> workspace
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_reduce_slabs(const KArgs p, int D, int KP32, float* __restrict__ dW0,
+                                                      float* __restrict__ dW1, float* __restrict__ dW2,
+                                                      float* __restrict__ db0, float* __restrict__ db1,
+                                                      float* __restrict__ db2, float* __restrict__ dS_ws,
+                                                      float* __restrict__ dC_ws) {
+  const int64_t nW = 3LL * D * D + 3LL * D;
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int G = p.G;
+  if (e < nW) {
+    float s = 0.f;
+    for (int hg = 0; hg < p.H * G; ++hg) s += p.slab[(int64_t)hg * p.slab_floats + e];
+    const int64_t DD = (int64_t)D * D;
+    if (e < DD) dW0[e] = s;
+    else if (e < 2 * DD) dW1[e - DD] = s;
+    else if (e < 3 * DD) dW2[e - 2 * DD] = s;
+    else if (e < 3 * DD + D) db0[e - 3 * DD] = s;
+    else if (e < 3 * DD + 2 * D) db1[e - 3 * DD - D] = s;
+    else db2[e - 3 * DD - 2 * D] = s;
+    return;
+  }
+  const int64_t nC = (int64_t)p.H * KP32 * D, nS = (int64_t)p.H * KP32 * KP32;
+  int64_t f = e - nW;
+  if (f < nC) {
+    const int hd = (int)(f / (KP32 * D));
+    const int64_t off = 3LL * D * D + 3LL * D + f % (KP32 * D);
+    float s = 0.f;
+    for (int gg = 0; gg < G; ++gg) s += p.slab[((int64_t)hd * G + gg) * p.slab_floats + off];
+    dC_ws[f] = s;
+    return;
+  }
+  f -= nC;
+  if (f < nS) {
+    const int hd = (int)(f / (KP32 * KP32));
+    const int64_t off = 3LL * D * D + 3LL * D + (int64_t)KP32 * D + f % (KP32 * KP32);
+    float s = 0.f;
+    for (int gg = 0; gg < G; ++gg) s += p.slab[((int64_t)hd * G + gg) * p.slab_floats + off];
+    dS_ws[f] = s;
+  }
+}
+
+// dC_h = dC_ws[h] + (dD + dD^T) C_h, dD = S o (dS - <S, dS>)   (softmax over k^2, sbm_attn.py:39)
+__global__ __launch_bounds__(256) void k_cluster_grad(const float* __restrict__ S, const float* __restrict__ dS_ws,
+                                                      const float* __restrict__ dC_ws, const float* __restrict__ C,
+                                                      float* __restrict__ dC, int k, int D, int KP32) {
+  const int hd = blockIdx.x, tid = threadIdx.x;
+  __shared__ float dD[32 * 32 * 4];
+  __shared__ float red[256];
+  const float* Sh = S + (size_t)hd * KP32 * KP32;
+  const float* dSh = dS_ws + (size_t)hd * KP32 * KP32;
+  float acc = 0.f;
+  for (int e = tid; e < k * k; e += 256) {
+    const int a = e / k, b = e % k;
+    acc += Sh[a * KP32 + b] * dSh[a * KP32 + b];
+  }
+  red[tid] = acc;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (tid < s) red[tid] += red[tid + s];
+    __syncthreads();
+  }
+  const float dot = red[0];
+  for (int e = tid; e < k * k; e += 256) {
+    const int a = e / k, b = e % k;
+    dD[e] = Sh[a * KP32 + b] * (dSh[a * KP32 + b] - dot);
+  }
+  __syncthreads();
+  const float* Ch = C + (size_t)hd * k * D;
+  for (int e = tid; e < k * D; e += 256) {
+    const int a = e / D, t = e % D;
+    float s = dC_ws[((size_t)hd * KP32 + a) * D + t];
+    for (int b = 0; b < k; ++b) s = fmaf(dD[a * k + b] + dD[b * k + a], Ch[b * D + t], s);
+    dC[(size_t)hd * k * D + e] = s;
+  }
+}
+
+__global__ void k_ste_sample(const float* __restrict__ pr, const float* __restrict__ u, float* __restrict__ A,
+                             int64_t n, float lo, float hi) {
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256)
+    A[e] = (u[e] < fminf(fmaxf(pr[e], lo), hi)) ? 1.f : 0.f;
+}
+
+__global__ void k_ste_backward(const float* __restrict__ A, const float* __restrict__ g, float* __restrict__ out,
+                               int64_t n) {
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256)
+    out[e] = fminf(fmaxf(A[e] * g[e], -1.f), 1.f);
+}
+
+// ------------------------------------------------------------------------------------
+// Host side
+// ------------------------------------------------------------------------------------
+thread_local char g_err[512] = "";
+
+csa_status fail(csa_status s, const char* msg) {
+  snprintf(g_err, sizeof(g_err), "%s", msg);
+  return s;
+}
+
+csa_status check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    snprintf(g_err, sizeof(g_err), "%s: %s", what, hipGetErrorString(e));
+    return CSA_LAUNCH_FAILED;
+  }
+  return CSA_OK;
+}
+
+bool supported(int64_t d, int64_t k, uint32_t flags) {
+  if (d != 64 && d != 96) return false;
+  if (flags & CSA_FLAG_DENSE) return true;
+  return k >= 1 && k <= 32;
+}
+
+KArgs make_kargs(const csa_sbm_fwd_args* a, const Layout& L) {
+  KArgs p;
+  memset(&p, 0, sizeof(p));
+  p.B = (int)a->B; p.H = (int)a->H; p.N = (int)a->N; p.M = (int)a->M; p.k = (int)L.k; p.kp = (int)L.kp;
+  p.NQB = (int)L.NQB; p.NKB = (int)L.NKB; p.Mpad = (int)L.Mpad;
+  p.Q = a->Q; p.K = a->K; p.V = a->V;
+  p.q_sb = a->q_sb; p.q_sh = a->q_sh; p.q_sn = a->q_sn;
+  p.k_sb = a->k_sb; p.k_sh = a->k_sh; p.k_sn = a->k_sn;
+  p.v_sb = a->v_sb; p.v_sh = a->v_sh; p.v_sn = a->v_sn;
+  p.mask = a->key_mask; p.mask_sb = a->mask_sb;
+  for (int l = 0; l < 3; ++l) p.pb[l] = a->proj_b[l];
+  void* st = a->state;
+  for (int l = 0; l < 3; ++l) {
+    p.Wf[l] = (const float*)((char*)st + L.Wf[l]);
+    p.WfT[l] = (const float*)((char*)st + L.WfT[l]);
+  }
+  p.Cf = (const float*)((char*)st + L.Cf); p.CfT = (const float*)((char*)st + L.CfT);
+  p.Sf = (const float*)((char*)st + L.Sf); p.SfT = (const float*)((char*)st + L.SfT);
+  p.S = (const float*)((char*)st + L.S);
+  p.Qh = (float*)((char*)st + L.Qh); p.Kh = (float*)((char*)st + L.Kh); p.T = (float*)((char*)st + L.T);
+  p.stats = (float*)((char*)st + L.stats);
+  p.Abits = (uint32_t*)((char*)st + L.Abits); p.Rbits = (uint32_t*)((char*)st + L.Rbits);
+  p.cnt = (unsigned long long*)((char*)st + L.cnt);
+  p.U = a->uniforms;
+  p.seed_lo = (uint32_t)a->seed; p.seed_hi = (uint32_t)(a->seed >> 32); p.off = (uint32_t)a->offset;
+  p.attn_p = a->attn_dropout; p.proj_p = a->proj_dropout;
+  p.scale = 1.f / sqrtf((float)a->d);
+  p.X = a->X;
+  return p;
+}
+
+csa_status validate_fwd(const csa_sbm_fwd_args* a) {
+  if (!a) return fail(CSA_INVALID_ARG, "null args");
+  const bool dense = a->flags & CSA_FLAG_DENSE;
+  if (a->B < 1 || a->H < 1 || a->N < 1 || a->M < 1) return fail(CSA_INVALID_ARG, "B, H, N, M must be >= 1");
+  if (!a->Q || !a->K || !a->V || !a->X || !a->state) return fail(CSA_INVALID_ARG, "null Q/K/V/X/state");
+  if (!supported(a->d, a->k, a->flags)) return fail(CSA_UNSUPPORTED_SHAPE, "unsupported (d, k): d in {64,96}, k in [1,32]");
+  if (!dense) {
+    if (!a->cluster_w || !a->sparsity) return fail(CSA_INVALID_ARG, "null cluster_w/sparsity");
+    for (int l = 0; l < 3; ++l)
+      if (!a->proj_w[l] || !a->proj_b[l]) return fail(CSA_INVALID_ARG, "null proj weight/bias");
+  }
+  if (a->attn_dropout < 0.f || a->attn_dropout >= 1.f || a->proj_dropout < 0.f || a->proj_dropout >= 1.f)
+    return fail(CSA_INVALID_ARG, "dropout p must be in [0,1)");
+  auto al16 = [](const void* ptr, int64_t sb, int64_t sh, int64_t sn) {
+    return (((uintptr_t)ptr) % 16 == 0) && sb % 4 == 0 && sh % 4 == 0 && sn % 4 == 0;
+  };
+  if (!al16(a->Q, a->q_sb, a->q_sh, a->q_sn) || !al16(a->K, a->k_sb, a->k_sh, a->k_sn) ||
+      !al16(a->V, a->v_sb, a->v_sh, a->v_sn))
+    return fail(CSA_INVALID_ARG, "Q/K/V must be 16-byte aligned with strides multiple of 4 elements");
+  if (((uintptr_t)a->X) % 16) return fail(CSA_INVALID_ARG, "X must be 16-byte aligned");
+  return CSA_OK;
+}
+
+template <int D, int KPH, int KT>
+csa_status launch_fwd(const csa_sbm_fwd_args* a, const Layout& L, hipStream_t st) {
+  KArgs p = make_kargs(a, L);
+  const int BH = (int)(a->B * a->H);
+  if constexpr (KPH > 0) {
+    const int KP32 = 32 * KT;
+    float* S = (float*)((char*)a->state + L.S);
+    hipLaunchKernelGGL(k_cluster_softmax, dim3(a->H), dim3(256), 0, st, a->cluster_w, S, (int)a->k, D, KP32);
+    FragJobs J;
+    memset(&J, 0, sizeof(J));
+    int n = 0;
+    for (int l = 0; l < 3; ++l) {  // forward weights: A[o][i] = W[o][i]; l=0 lin-perm, else acc-perm
+      J.j[n++] = FragJob{a->proj_w[l], (float*)p.Wf[l], D, D, D, 0, l == 0 ? 0 : 1, D / 32, D / 2, 1, 0, 0};
+    }
+    for (int l = 0; l < 3; ++l) {  // transposed (backward): A[i][o] = W[o][i], acc-perm over o
+      J.j[n++] = FragJob{a->proj_w[l], (float*)p.WfT[l], D, D, D, 1, 1, D / 32, D / 2, 1, 0, 0};
+    }
+    J.j[n++] = FragJob{a->cluster_w, (float*)p.Cf, (int)a->k, D, D, 0, 1, KT, D / 2, (int)a->H, a->k * D,
+                       (int64_t)KP32 * D};
+    J.j[n++] = FragJob{a->cluster_w, (float*)p.CfT, D, (int)a->k, D, 1, 1, D / 32, 16 * KT, (int)a->H, a->k * D,
+                       (int64_t)KP32 * D};
+    J.j[n++] = FragJob{S, (float*)p.Sf, KP32, KP32, KP32, 0, 1, KT, 16 * KT, (int)a->H, (int64_t)KP32 * KP32,
+                       (int64_t)KP32 * KP32};
+    J.j[n++] = FragJob{S, (float*)p.SfT, KP32, KP32, KP32, 1, 1, KT, 16 * KT, (int)a->H, (int64_t)KP32 * KP32,
+                       (int64_t)KP32 * KP32};
+    J.n = n;
+    hipLaunchKernelGGL(k_frag_prep, dim3(16, n), dim3(256), 0, st, J);
+    if (hipMemsetAsync(p.cnt, 0, sizeof(unsigned long long) * a->H, st) != hipSuccess)
+      return check_launch("memset counters");
+    hipLaunchKernelGGL((k_proj_fwd<D, KT>), dim3(L.NQB + L.NKB, BH), dim3(64), 0, st, p);
+    hipLaunchKernelGGL((k_attn_fwd<D, KPH, false>), dim3(L.NQB, BH), dim3(64), 0, st, p);
+    hipLaunchKernelGGL(k_sparsity_finish, dim3(1), dim3(64), 0, st, (const unsigned long long*)p.cnt, a->sparsity,
+                       (int)a->H, (float)a->B * (float)a->N * (float)a->M);
+  } else {
+    hipLaunchKernelGGL((k_attn_fwd<D, 0, true>), dim3(L.NQB, BH), dim3(64), 0, st, p);
+  }
+  return check_launch("csa_sbm_fwd");
+}
+
+template <int D, int KT>
+csa_status launch_bwd(const csa_sbm_bwd_args* b, const Layout& L, hipStream_t st) {
+  const csa_sbm_fwd_args* a = b->fwd;
+  KArgs p = make_kargs(a, L);
+  const bool dense = a->flags & CSA_FLAG_DENSE;
+  p.dX = b->dX; p.dsp = b->dsparsity; p.dgraph = b->dgraph;
+  p.dQ = b->dQ; p.dK = b->dK; p.dV = b->dV;
+  p.dQh = (float*)((char*)b->workspace + L.w_dQh);
+  p.dT = (float*)((char*)b->workspace + L.w_dT);
+  p.slab = (float*)((char*)b->workspace + L.w_slab);
+  p.G = (int)L.G; p.slab_floats = L.slab_floats;
+  const int BH = (int)(a->B * a->H);
+  (void)dense;
+  if constexpr (KT > 0) {
+    hipLaunchKernelGGL((k_attn_bwd_q<D, KT, false>), dim3(L.NQB, BH), dim3(64), 0, st, p);
+    hipLaunchKernelGGL((k_attn_bwd_kv<D, KT, false>), dim3(L.NKB, BH), dim3(64), 0, st, p);
+    if (hipMemsetAsync(p.slab, 0, sizeof(float) * a->H * L.G * L.slab_floats, st) != hipSuccess)
+      return check_launch("memset slabs");
+    using Sh = ProjBwdShape<D, KT>;
+    (void)hipFuncSetAttribute((const void*)k_proj_bwd<D, KT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)Sh::LDS_BYTES);
+    hipLaunchKernelGGL((k_proj_bwd<D, KT>), dim3(L.G, a->H), dim3(256), Sh::LDS_BYTES, st, p);
+    const int KP32 = 32 * KT;
+    float* dS_ws = (float*)((char*)b->workspace + L.w_dS);
+    float* dC_ws = (float*)((char*)b->workspace + L.w_dC);
+    const int64_t total = 3LL * D * D + 3LL * D + (int64_t)a->H * KP32 * D + (int64_t)a->H * KP32 * KP32;
+    hipLaunchKernelGGL(k_reduce_slabs, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, p, D, KP32,
+                       b->dproj_w[0], b->dproj_w[1], b->dproj_w[2], b->dproj_b[0], b->dproj_b[1], b->dproj_b[2],
+                       dS_ws, dC_ws);
+    hipLaunchKernelGGL(k_cluster_grad, dim3(a->H), dim3(256), 0, st, p.S, (const float*)dS_ws,
+                       (const float*)dC_ws, a->cluster_w, b->dcluster_w, (int)a->k, D, KP32);
+  } else {
+    hipLaunchKernelGGL((k_attn_bwd_q<D, 0, true>), dim3(L.NQB, BH), dim3(64), 0, st, p);
+    hipLaunchKernelGGL((k_attn_bwd_kv<D, 0, true>), dim3(L.NKB, BH), dim3(64), 0, st, p);
+  }
+  return check_launch("csa_sbm_bwd");
+}
+
+}  // namespace
+
+extern "C" {
+
+int csa_abi_version(void) { return CSA_ABI_VERSION; }
+
+const char* csa_status_str(csa_status s) {
+  switch (s) {
+    case CSA_OK: return "CSA_OK";
+    case CSA_INVALID_ARG: return "CSA_INVALID_ARG";
+    case CSA_UNSUPPORTED_SHAPE: return "CSA_UNSUPPORTED_SHAPE";
+    case CSA_LAUNCH_FAILED: return "CSA_LAUNCH_FAILED";
+  }
+  return "CSA_UNKNOWN";
+}
+
+const char* csa_last_error_str(void) { return g_err; }
+
+int csa_sbm_supported(int64_t d, int64_t k, uint32_t flags) { return supported(d, k, flags) ? 1 : 0; }
+
+size_t csa_sbm_state_bytes(int64_t B, int64_t H, int64_t N, int64_t M, int64_t d, int64_t k, uint32_t flags) {
+  return make_layout(B, H, N, M, d, k, flags & CSA_FLAG_DENSE).total;
+}
+
+size_t csa_sbm_bwd_workspace_bytes(int64_t B, int64_t H, int64_t N, int64_t M, int64_t d, int64_t k, uint32_t flags) {
+  return make_layout(B, H, N, M, d, k, flags & CSA_FLAG_DENSE).w_total;
+}
+
+csa_status csa_sbm_fwd(const csa_sbm_fwd_args* a, void* stream) {
+  csa_status s = validate_fwd(a);
+  if (s != CSA_OK) return s;
+  const Layout L = make_layout(a->B, a->H, a->N, a->M, a->d, a->k, a->flags & CSA_FLAG_DENSE);
+  hipStream_t st = (hipStream_t)stream;
+  const bool dense = a->flags & CSA_FLAG_DENSE;
+  if (a->d == 64) {
+    if (dense) return launch_fwd<64, 0, 1>(a, L, st);
+    return L.kp <= 16 ? launch_fwd<64, 8, 1>(a, L, st) : launch_fwd<64, 16, 1>(a, L, st);
+  }
+  if (dense) return launch_fwd<96, 0, 1>(a, L, st);
+  return L.kp <= 16 ? launch_fwd<96, 8, 1>(a, L, st) : launch_fwd<96, 16, 1>(a, L, st);
+}
+
+csa_status csa_sbm_maps(const csa_sbm_fwd_args* a, float* graph, float* attn, void* stream) {
+  csa_status s = validate_fwd(a);
+  if (s != CSA_OK) return s;
+  if (!graph && !attn) return CSA_OK;
+  const bool dense = a->flags & CSA_FLAG_DENSE;
+  const Layout L = make_layout(a->B, a->H, a->N, a->M, a->d, a->k, dense);
+  KArgs p = make_kargs(a, L);
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 grid((unsigned)L.NQB, (unsigned)(a->B * a->H));
+  if (a->d == 64) {
+    if (dense) hipLaunchKernelGGL((k_maps<64, true>), grid, dim3(64), 0, st, p, graph, attn);
+    else hipLaunchKernelGGL((k_maps<64, false>), grid, dim3(64), 0, st, p, graph, attn);
+  } else {
+    if (dense) hipLaunchKernelGGL((k_maps<96, true>), grid, dim3(64), 0, st, p, graph, attn);
+    else hipLaunchKernelGGL((k_maps<96, false>), grid, dim3(64), 0, st, p, graph, attn);
+  }
+  return check_launch("csa_sbm_maps");
+}
+
+csa_status csa_sbm_bwd(const csa_sbm_bwd_args* b, void* stream) {
+  if (!b || !b->fwd) return fail(CSA_INVALID_ARG, "null args");
+  csa_status s = validate_fwd(b->fwd);
+  if (s != CSA_OK) return s;
+  const csa_sbm_fwd_args* a = b->fwd;
+  const bool dense = a->flags & CSA_FLAG_DENSE;
+  if (!b->dX || !b->dQ || !b->dK || !b->dV || (!dense && !b->workspace))
+    return fail(CSA_INVALID_ARG, "null dX/dQ/dK/dV/workspace");
+  if (!dense && (!b->dcluster_w || !b->dproj_w[0] || !b->dproj_w[1] || !b->dproj_w[2] || !b->dproj_b[0] ||
+                 !b->dproj_b[1] || !b->dproj_b[2]))
+    return fail(CSA_INVALID_ARG, "null parameter-gradient output");
+  const Layout L = make_layout(a->B, a->H, a->N, a->M, a->d, a->k, dense);
+  hipStream_t st = (hipStream_t)stream;
+  if (a->d == 64) return dense ? launch_bwd<64, 0>(b, L, st) : launch_bwd<64, 1>(b, L, st);
+  return dense ? launch_bwd<96, 0>(b, L, st) : launch_bwd<96, 1>(b, L, st);
+}
+
+csa_status csa_ste_sample(const float* pr, const float* u, float* A, int64_t n, float lo, float hi, void* stream) {
+  if (!pr || !u || !A || n < 0) return fail(CSA_INVALID_ARG, "null pointer or negative n");
+  if (n == 0) return CSA_OK;
+  const unsigned grid = (unsigned)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
+  hipLaunchKernelGGL(k_ste_sample, dim3(grid), dim3(256), 0, (hipStream_t)stream, pr, u, A, n, lo, hi);
+  return check_launch("csa_ste_sample");
+}
+
+csa_status csa_ste_backward(const float* A, const float* g, float* out, int64_t n, void* stream) {
+  if (!A || !g || !out || n < 0) return fail(CSA_INVALID_ARG, "null pointer or negative n");
+  if (n == 0) return CSA_OK;
+  const unsigned grid = (unsigned)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
+  hipLaunchKernelGGL(k_ste_backward, dim3(grid), dim3(256), 0, (hipStream_t)stream, A, g, out, n);
+  return check_launch("csa_ste_backward");
+}
+
+}  // extern "C"

@@ -1,0 +1,124 @@
+/* C ABI of libcsa_hip.so — MI355X (gfx950) kernels for the CSA-Trans attention hot path.
+ *
+ * Every entry point replaces one piece of the reference's PyTorch-eager hot path
+ * (paths relative to the reference repo saeyoon17/Code-Structure-Aware-Transformer):
+ *
+ *   csa_sbm_fwd        module/sbm_attn.py:32-66   SBMAttention.forward (+ STE.py:10-15 sampling)
+ *                      module/sbm_attn.py:77-87   FullAttention.forward   (flags & CSA_FLAG_DENSE)
+ *   csa_sbm_maps       module/sbm_attn.py:62,57   the returned `attn` / `graph` maps (optional)
+ *   csa_sbm_bwd        autograd of the above incl. STE.py:17-19 (hardtanh straight-through)
+ *   csa_ste_sample     module/STE.py:10-15        standalone sampler (bit-exact test surface)
+ *   csa_rel_attn_fwd   module/disentangled_attn.py:44-65 DisentangledAttn.rel_attn
+ *   csa_rel_attn_bwd   autograd of rel_attn (gather backward = deterministic scatter-add)
+ *
+ * Conventions (all entry points):
+ *   - fp32 data; device pointers; sizes and strides are int64 ELEMENT counts; the last
+ *     (feature) dimension is always contiguous, so a (B,H,N,d) operand is described by its
+ *     b/h/n strides (the non-contiguous split_heads view of sbm_attn.py:137-140 is accepted).
+ *   - The caller allocates every output, the saved state and the workspace (sizes from the
+ *     *_bytes() queries). The library never allocates, never synchronises the host, never
+ *     throws, keeps no mutable globals, and enqueues everything on `stream` (stream-ordered,
+ *     graph-capturable, re-entrant). Results are deterministic for fixed inputs (integer
+ *     atomics only; float reductions use fixed-order partial slabs).
+ *   - Errors: CSA_INVALID_ARG (null/inconsistent arguments), CSA_UNSUPPORTED_SHAPE (outside
+ *     the compiled instantiations, see csa_sbm_supported), CSA_LAUNCH_FAILED (HIP error; text
+ *     via csa_last_error_str on the calling thread).
+ */
+#ifndef CSA_HIP_H
+#define CSA_HIP_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CSA_ABI_VERSION 1
+
+typedef enum csa_status {
+  CSA_OK = 0,
+  CSA_INVALID_ARG = 1,
+  CSA_UNSUPPORTED_SHAPE = 2,
+  CSA_LAUNCH_FAILED = 3
+} csa_status;
+
+/* flags */
+#define CSA_FLAG_DENSE 1u /* FullAttention (graph == 1, no cluster projection, no sampling) */
+
+typedef struct csa_sbm_fwd_args {
+  int64_t B, H, N, M, d, k; /* batch, heads, queries, keys, head_dim, clusters (k ignored if DENSE) */
+  const float* Q; int64_t q_sb, q_sh, q_sn; /* (B,H,N,d) */
+  const float* K; int64_t k_sb, k_sh, k_sn; /* (B,H,M,d) */
+  const float* V; int64_t v_sb, v_sh, v_sn; /* (B,H,M,d) */
+  const float* key_mask; int64_t mask_sb;   /* (B,M) 1.0 = padded key (sbm_attn.py:61); may be NULL */
+  const float* cluster_w;                   /* layer.weight (H*k, d) contiguous (sbm_attn.py:19) */
+  const float* proj_w[3]; const float* proj_b[3]; /* proj.0/.3/.6 weight (d,d) and bias (d) */
+  const float* uniforms;      /* (B,H,N,M) contiguous host-supplied draws, or NULL = Philox */
+  uint64_t seed, offset;      /* Philox key / counter offset (sampling + dropout) */
+  float attn_dropout;         /* drop_attn p (0 in eval) — sbm_attn.py:14,63 */
+  float proj_dropout;         /* proj Dropout p (0 in eval) — sbm_attn.py:24,27 */
+  uint32_t flags;
+  float* X;                   /* out (B,H,N,d) contiguous */
+  float* sparsity;            /* out (H,) head-wise sparsity (sbm_attn.py:64); NULL if DENSE */
+  void* state;                /* csa_sbm_state_bytes(): saved for backward and csa_sbm_maps */
+} csa_sbm_fwd_args;
+
+typedef struct csa_sbm_bwd_args {
+  const csa_sbm_fwd_args* fwd; /* the forward's arguments (same inputs and the filled state) */
+  const float* dX;             /* (B,H,N,d) contiguous */
+  const float* dsparsity;      /* (H,) or NULL */
+  const float* dgraph;         /* (B,H,N,M) grad of the returned graph map, or NULL */
+  float* dQ; float* dK; float* dV; /* out (B,H,N|M,d) contiguous */
+  float* dcluster_w;           /* out (H*k, d); NULL if DENSE */
+  float* dproj_w[3]; float* dproj_b[3]; /* out; NULL if DENSE */
+  void* workspace;             /* csa_sbm_bwd_workspace_bytes() */
+} csa_sbm_bwd_args;
+
+int csa_abi_version(void);
+const char* csa_status_str(csa_status s);
+const char* csa_last_error_str(void);
+/* 1 if (d, k, flags) is a compiled instantiation */
+int csa_sbm_supported(int64_t d, int64_t k, uint32_t flags);
+size_t csa_sbm_state_bytes(int64_t B, int64_t H, int64_t N, int64_t M, int64_t d, int64_t k, uint32_t flags);
+size_t csa_sbm_bwd_workspace_bytes(int64_t B, int64_t H, int64_t N, int64_t M, int64_t d, int64_t k, uint32_t flags);
+
+csa_status csa_sbm_fwd(const csa_sbm_fwd_args* a, void* stream);
+/* Materialise attn (B,H,N,M) and/or graph (B,H,N,M) fp32 maps from a completed forward. */
+csa_status csa_sbm_maps(const csa_sbm_fwd_args* a, float* graph, float* attn, void* stream);
+csa_status csa_sbm_bwd(const csa_sbm_bwd_args* a, void* stream);
+
+/* STE.py:10-15 as A = (u < clamp(p, lo, hi)); n elements, contiguous. */
+csa_status csa_ste_sample(const float* p, const float* u, float* A, int64_t n, float lo, float hi, void* stream);
+/* STE.py:17-19: gin = hardtanh(A * gout). */
+csa_status csa_ste_backward(const float* A, const float* gout, float* gin, int64_t n, void* stream);
+
+/* ---- CSE disentangled relation attention (module/disentangled_attn.py:44-65) ---- */
+typedef struct csa_rel_attn_args {
+  int64_t B, H, N, L, d; /* H must be 8 (4 parent + 4 sibling heads, disentangled_attn.py:29-33) */
+  const float* q; int64_t q_sb, q_sh, q_sn;
+  const float* k; int64_t k_sb, k_sh, k_sn;
+  const float* v; int64_t v_sb, v_sh, v_sn;
+  const float* lq; const float* lk; /* (H, L, d) contiguous (batch dim 1 dropped) */
+  const uint8_t* rel;  int64_t rel_sb, rel_sh;  /* (B,*,N,N) relation index < L; head stride may be 0 */
+  const uint8_t* mask; int64_t mask_sb, mask_sh;/* (B,*,N,N) 1 = masked (-1e9); head stride may be 0 */
+  int64_t rel_head_group; /* heads [0,g) read plane 0, heads [g,H) plane 1 (CSE: 4); 0 = use rel_sh */
+  float* out;          /* (B,H,N,d) contiguous */
+  float* lse;          /* (B,H,N) saved row log-sum-exp for backward */
+} csa_rel_attn_args;
+
+typedef struct csa_rel_attn_bwd_args {
+  const csa_rel_attn_args* fwd;
+  const float* dout;   /* (B,H,N,d) contiguous */
+  float* dq; float* dk; float* dv; /* (B,H,N,d) contiguous */
+  float* dlq; float* dlk;          /* (H,L,d) */
+  void* workspace;
+} csa_rel_attn_bwd_args;
+
+size_t csa_rel_attn_bwd_workspace_bytes(int64_t B, int64_t H, int64_t N, int64_t L, int64_t d);
+csa_status csa_rel_attn_fwd(const csa_rel_attn_args* a, void* stream);
+csa_status csa_rel_attn_bwd(const csa_rel_attn_bwd_args* a, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CSA_HIP_H */
