@@ -1,0 +1,249 @@
+#!/usr/bin/env python
+"""bench.py — SBM-attention fwd+bwd ASTs/s at L=150 (BASELINE.json configs[1]) on MI355X.
+
+One "step" = one SBMAttention training pass (module/sbm_attn.py:32-66 forward + backward, train
+mode: attention + proj dropout on, Bernoulli edge sampling from in-kernel Philox) over a batch of
+256 synthetic 150-node ASTs with config/python.py dims (H=8, head_dim=64, k=10), inputs resident
+in HBM. The upstream gradients are X's (dX ~ N(0,1)) and sparsity's (sw/32 per head), exactly
+what the reference's train step feeds the layer (script/train.py:109).
+
+Multi-GPU (torchrun, one process per GPU): each rank processes its own 256 ASTs (weak scaling)
+and the layer's parameter gradients are all-reduced by DDP over RCCL, the one exchange of
+script/train.py:83,109. value = ASTs processed by all ranks / max-over-ranks wall time.
+
+Printed JSON line (rank 0): contract fields + "roofline" for the dominant kernel (HIP events
+recorded around that kernel's launch on its stream, every timed step) + "cpu_baseline" (the
+oracle restatement of the reference op sequence on the host CPU, rank 0 at N=1).
+"""
+import argparse
+import ctypes
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "code-structure-aware-transformer_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "SBM-attn fwd+bwd ASTs/sec (L=150) + train samples/sec @1/2/4/8 GPU"
+PEAK_F32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32-input MFMA dense peak
+PEAK_HBM_GBS = 8000.0
+
+
+def stage_flops_per_ast(H, N, M, D, k):
+    """Algorithmic FLOPs per AST (one batch element, all heads) per kernel stage."""
+    return {
+        "proj_fwd": H * ((N + M) * (6 * D * D + 2 * k * D) + M * 2 * k * k),
+        "attn_fwd": H * (4 * N * M * D + 2 * N * M * k),
+        "attn_bwd_q": H * (4 * N * M * D + 2 * N * M * k),
+        "attn_bwd_kv": H * (4 * N * M * D + 2 * N * M * k),
+        "proj_bwd": H * ((N + M) * (12 * D * D + 4 * k * D) + M * 4 * k * k),
+    }
+
+
+class HipEvents:
+    """hipEvent_t handles created through the HIP runtime torch already loaded."""
+
+    def __init__(self):
+        self.hip = ctypes.CDLL("libamdhip64.so.7")
+        self.hip.hipEventCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+        self.hip.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p, ctypes.c_void_p]
+        self.hip.hipEventDestroy.argtypes = [ctypes.c_void_p]
+        self.made = []
+
+    def create(self):
+        e = ctypes.c_void_p()
+        if self.hip.hipEventCreate(ctypes.byref(e)) != 0:
+            raise RuntimeError("hipEventCreate failed")
+        self.made.append(e)
+        return e
+
+    def elapsed_ms(self, a, b):
+        ms = ctypes.c_float()
+        if self.hip.hipEventElapsedTime(ctypes.byref(ms), a, b) != 0:
+            return float("nan")
+        return ms.value
+
+    def destroy(self):
+        for e in self.made:
+            self.hip.hipEventDestroy(e)
+
+
+def cpu_baseline(seconds, B=16, H=8, N=150, d=64, k=10):
+    """Oracle (torch-CPU restatement of sbm_attn.py:32-66 + STE.py) fwd+bwd, train mode, timed on host cores."""
+    from oracle import sbm_ref
+    threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+    torch.set_num_threads(threads)
+    g = torch.Generator().manual_seed(0)
+    Q, K, V = (torch.randn(B, H, N, d, generator=g).requires_grad_(True) for _ in range(3))
+    params = {"layer.weight": torch.nn.init.orthogonal_(torch.empty(H * k, d)).requires_grad_(True)}
+    for i in (0, 3, 6):
+        params[f"proj.{i}.weight"] = torch.nn.init.xavier_uniform_(torch.empty(d, d)).requires_grad_(True)
+        params[f"proj.{i}.bias"] = torch.zeros(d).requires_grad_(True)
+    mask = torch.zeros(B, N)
+    dX = torch.randn(B, H, N, d, generator=g)
+    dsp = torch.full((H,), 3.125e-4)
+
+    def step():
+        u = torch.rand(B, H, N, N)  # == torch.bernoulli's draws
+        keep = (torch.rand(B, H, N, N) >= 0.2).float() / 0.8
+        pk = {n: (torch.rand(B, H, N, d) >= 0.2).float() / 0.8 for n in ("q0", "q1", "k0", "k1")}
+        X, sp, graph, attn = sbm_ref.sbm_attention(Q, K, V, mask, params, u, k, attn_keep=keep, proj_keep=pk)
+        torch.autograd.backward([X, sp], [dX, dsp])
+
+    step()
+    n, t0 = 0, time.perf_counter()
+    while True:
+        step()
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds and n >= 2:
+            break
+    return {"value": round(n * B / el, 2), "unit": "ASTs/s", "cores": threads, "kind": "port",
+            "sample": f"{n} oracle fwd+bwd steps of B={B} (H=8,N=150,d=64,k=10, train mode) in {el:.1f}s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--dense", action="store_true", help="FullAttention ablation (config/python_full_att.py)")
+    ap.add_argument("--eval", action="store_true", help="eval mode (no dropout)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    from csa_amd import ops
+    from csa_amd._lib import STAGES, CsaProf, KERNEL_OF_STAGE
+    from csa_amd.module.sbm_attn import FullAttention, SBMAttention
+
+    B, H, N, d, k = args.batch, 8, 150, 64, 10
+    torch.manual_seed(1234 + rank)
+    cfg = {"attention_dropout": 0.2, "head_dim": d, "num_head": H, "num_clusters": [k], "return_maps": False}
+    mod = (FullAttention(cfg, 0) if args.dense else SBMAttention(cfg, 0)).to(dev)
+    for p in mod.parameters():
+        if p.dim() > 1:
+            torch.nn.init.xavier_uniform_(p)
+    if not args.dense:
+        torch.nn.init.orthogonal_(mod.layer.weight)
+    mod.train(not args.eval)
+    model = mod
+    if world > 1 and not args.dense:
+        model = torch.nn.parallel.DistributedDataParallel(mod, device_ids=[local])
+    Q, K, V = (torch.randn(B, H, N, d, device=dev).requires_grad_(True) for _ in range(3))
+    mask = torch.zeros(B, N, device=dev)
+    dX = torch.randn(B, H, N, d, device=dev)
+    dsp = torch.full((H,), 3.125e-4, device=dev)
+
+    def step():
+        for t in (Q, K, V):
+            t.grad = None
+        for p in mod.parameters():
+            p.grad = None
+        X, sp, _, _ = model(Q, K, V, mask)
+        if sp is None:
+            torch.autograd.backward([X], [dX])
+        else:
+            torch.autograd.backward([X, sp], [dX, dsp])
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    ev = HipEvents()
+    profs = []
+    for _ in range(args.steps):
+        pf, pb = CsaProf(), CsaProf()
+        for name, s in STAGES.items():
+            tgt = pf if name in ("prep", "proj_fwd", "attn_fwd") else pb
+            tgt.start[s], tgt.stop[s] = ev.create().value, ev.create().value
+        profs.append((pf, pb))
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ops.set_stage_profiler(*profs[i])
+        step()
+    ops.set_stage_profiler(None, None)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # per-stage kernel time (HIP events around each launch, every timed step)
+    stage_ms = {}
+    for name, s in STAGES.items():
+        vals = []
+        for pf, pb in profs:
+            tgt = pf if name in ("prep", "proj_fwd", "attn_fwd") else pb
+            if tgt.start[s] and tgt.stop[s]:
+                vals.append(ev.elapsed_ms(ctypes.c_void_p(tgt.start[s]), ctypes.c_void_p(tgt.stop[s])))
+        vals = [v for v in vals if v == v and v > 0]
+        if vals:
+            stage_ms[name] = sum(vals) / len(vals)
+    ev.destroy()
+
+    ms_per_step = elapsed * 1000.0 / args.steps
+    value = world * B * args.steps / elapsed
+    flops = stage_flops_per_ast(H, N, N, d, 0 if args.dense else k)
+    if args.dense:
+        flops = {"attn_fwd": H * 4 * N * N * d, "attn_bwd_q": H * 4 * N * N * d, "attn_bwd_kv": H * 4 * N * N * d}
+    timed = {s: v for s, v in stage_ms.items() if s in flops}
+    dom = max(timed, key=timed.get) if timed else None
+    roofline = None
+    if dom:
+        ach = flops[dom] * B / (timed[dom] * 1e-3) / 1e12
+        roofline = {"bound": "mfma", "kernel": KERNEL_OF_STAGE[dom], "achieved": round(ach, 2),
+                    "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / PEAK_F32_MFMA_TFLOPS, 4),
+                    "traffic": None, "avg_launch_ms": round(timed[dom], 4)}
+        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc):
+            with open(pmc) as f:
+                tr = json.load(f).get(KERNEL_OF_STAGE[dom])
+            if tr:
+                roofline["traffic"] = tr
+    total_flops = sum(flops.values()) * B
+    out = {
+        "metric": METRIC, "value": round(value, 1), "unit": "ASTs/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32", "data": "synthetic (N(0,1) Q/K/V, 150-node ASTs, no padding)",
+        "config": {"workload": "SBMAttention fwd+bwd (config/python.py dims) " + ("dense FullAttention" if args.dense
+                   else "SBM"), "global_batch": B * world, "per_gpu_batch": B, "seq_len": N, "heads": H,
+                   "head_dim": d, "clusters": 0 if args.dense else k, "mode": "eval" if args.eval else "train",
+                   "parallelism": f"dp{world}"},
+        "roofline": roofline,
+        "step_tflops": round(total_flops / (ms_per_step * 1e-3) / 1e12, 2),
+        "step_frac_of_f32_mfma_peak": round(total_flops / (ms_per_step * 1e-3) / 1e12 / PEAK_F32_MFMA_TFLOPS, 4),
+        "stage_ms": {s: round(v, 4) for s, v in stage_ms.items()},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -18,6 +18,16 @@ STATUS = {0: "CSA_OK", 1: "CSA_INVALID_ARG", 2: "CSA_UNSUPPORTED_SHAPE", 3: "CSA
 i64, u64, u32, f32, vp = ctypes.c_int64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_float, ctypes.c_void_p
 
 
+CSA_STAGE_COUNT = 8
+STAGES = {"prep": 0, "proj_fwd": 1, "attn_fwd": 2, "attn_bwd_q": 3, "attn_bwd_kv": 4, "proj_bwd": 5, "reduce": 6}
+KERNEL_OF_STAGE = {"proj_fwd": "k_proj_fwd", "attn_fwd": "k_attn_fwd", "attn_bwd_q": "k_attn_bwd_q",
+                   "attn_bwd_kv": "k_attn_bwd_kv", "proj_bwd": "k_proj_bwd"}
+
+
+class CsaProf(ctypes.Structure):
+    _fields_ = [("start", vp * CSA_STAGE_COUNT), ("stop", vp * CSA_STAGE_COUNT)]
+
+
 class SbmFwdArgs(ctypes.Structure):
     _fields_ = [
         ("B", i64), ("H", i64), ("N", i64), ("M", i64), ("d", i64), ("k", i64),
@@ -32,6 +42,7 @@ class SbmFwdArgs(ctypes.Structure):
         ("attn_dropout", f32), ("proj_dropout", f32),
         ("flags", u32),
         ("X", vp), ("sparsity", vp), ("state", vp),
+        ("prof", ctypes.POINTER(CsaProf)),
     ]
 
 
@@ -42,6 +53,7 @@ class SbmBwdArgs(ctypes.Structure):
         ("dQ", vp), ("dK", vp), ("dV", vp),
         ("dcluster_w", vp), ("dproj_w", vp * 3), ("dproj_b", vp * 3),
         ("workspace", vp),
+        ("prof", ctypes.POINTER(CsaProf)),
     ]
 
 

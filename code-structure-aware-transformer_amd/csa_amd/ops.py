@@ -22,6 +22,15 @@ from ._lib import CSA_FLAG_DENSE, SbmBwdArgs, SbmFwdArgs, check, lib
 __all__ = ["sbm_attention", "dense_attention", "ste_sample", "ste_backward", "rel_attn", "SBMAttentionFunction"]
 
 
+# Optional per-stage event profiling (bench.py): csa_prof structs owned by the caller.
+_PROF = {"fwd": None, "bwd": None}
+
+
+def set_stage_profiler(fwd_prof=None, bwd_prof=None):
+    """Install caller-owned csa_prof structs (ctypes) that the next sbm fwd/bwd calls record into."""
+    _PROF["fwd"], _PROF["bwd"] = fwd_prof, bwd_prof
+
+
 def _ptr(t: Optional[torch.Tensor]):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
@@ -105,6 +114,8 @@ def sbm_fwd_op(Q: torch.Tensor, K: torch.Tensor, V: torch.Tensor, mask: Optional
     sp = torch.empty(0 if dense else H, device=Q.device, dtype=torch.float32)
     state = torch.empty(L.csa_sbm_state_bytes(B, H, N, M, d, k, flags), device=Q.device, dtype=torch.uint8)
     a = _fwd_struct(Q, K, V, mask, cw, pw, pb, u, seed, offset, attn_p, proj_p, dense, X, sp, state, k)
+    if _PROF["fwd"] is not None:
+        a.prof = ctypes.pointer(_PROF["fwd"])
     check(L.csa_sbm_fwd(ctypes.byref(a), _stream(Q.device)), "csa_sbm_fwd")
     return X, sp, state
 
@@ -187,6 +198,8 @@ def sbm_bwd_op(Q: torch.Tensor, K: torch.Tensor, V: torch.Tensor, mask: Optional
         ws = torch.empty(L.csa_sbm_bwd_workspace_bytes(B, H, N, M, d, k, flags), device=Q.device, dtype=torch.uint8)
         b.workspace = ws.data_ptr()
         keep.append(ws)
+    if _PROF["bwd"] is not None:
+        b.prof = ctypes.pointer(_PROF["bwd"])
     check(L.csa_sbm_bwd(ctypes.byref(b), _stream(Q.device)), "csa_sbm_bwd")
     return outs
 

@@ -1097,6 +1097,16 @@ __global__ void k_ste_backward(const float* __restrict__ A, const float* __restr
 // ------------------------------------------------------------------------------------
 thread_local char g_err[512] = "";
 
+struct Stage {  // records caller-owned events around one stage (no-op when prof is NULL)
+  const csa_prof* pf; int s; hipStream_t st;
+  Stage(const csa_prof* pf_, int s_, hipStream_t st_) : pf(pf_), s(s_), st(st_) {
+    if (pf && pf->start[s]) (void)hipEventRecord((hipEvent_t)pf->start[s], st);
+  }
+  ~Stage() {
+    if (pf && pf->stop[s]) (void)hipEventRecord((hipEvent_t)pf->stop[s], st);
+  }
+};
+
 csa_status fail(csa_status s, const char* msg) {
   snprintf(g_err, sizeof(g_err), "%s", msg);
   return s;
@@ -1178,6 +1188,8 @@ csa_status launch_fwd(const csa_sbm_fwd_args* a, const Layout& L, hipStream_t st
   if constexpr (KPH > 0) {
     const int KP32 = 32 * KT;
     float* S = (float*)((char*)a->state + L.S);
+    {
+    Stage sg(a->prof, CSA_STAGE_PREP, st);
     hipLaunchKernelGGL(k_cluster_softmax, dim3(a->H), dim3(256), 0, st, a->cluster_w, S, (int)a->k, D, KP32);
     FragJobs J;
     memset(&J, 0, sizeof(J));
@@ -1200,11 +1212,19 @@ csa_status launch_fwd(const csa_sbm_fwd_args* a, const Layout& L, hipStream_t st
     hipLaunchKernelGGL(k_frag_prep, dim3(16, n), dim3(256), 0, st, J);
     if (hipMemsetAsync(p.cnt, 0, sizeof(unsigned long long) * a->H, st) != hipSuccess)
       return check_launch("memset counters");
-    hipLaunchKernelGGL((k_proj_fwd<D, KT>), dim3(L.NQB + L.NKB, BH), dim3(64), 0, st, p);
-    hipLaunchKernelGGL((k_attn_fwd<D, KPH, false>), dim3(L.NQB, BH), dim3(64), 0, st, p);
+    }
+    {
+      Stage sg(a->prof, CSA_STAGE_PROJ_FWD, st);
+      hipLaunchKernelGGL((k_proj_fwd<D, KT>), dim3(L.NQB + L.NKB, BH), dim3(64), 0, st, p);
+    }
+    {
+      Stage sg(a->prof, CSA_STAGE_ATTN_FWD, st);
+      hipLaunchKernelGGL((k_attn_fwd<D, KPH, false>), dim3(L.NQB, BH), dim3(64), 0, st, p);
+    }
     hipLaunchKernelGGL(k_sparsity_finish, dim3(1), dim3(64), 0, st, (const unsigned long long*)p.cnt, a->sparsity,
                        (int)a->H, (float)a->B * (float)a->N * (float)a->M);
   } else {
+    Stage sg(a->prof, CSA_STAGE_ATTN_FWD, st);
     hipLaunchKernelGGL((k_attn_fwd<D, 0, true>), dim3(L.NQB, BH), dim3(64), 0, st, p);
   }
   return check_launch("csa_sbm_fwd");
@@ -1223,15 +1243,26 @@ csa_status launch_bwd(const csa_sbm_bwd_args* b, const Layout& L, hipStream_t st
   p.G = (int)L.G; p.slab_floats = L.slab_floats;
   const int BH = (int)(a->B * a->H);
   (void)dense;
+  const csa_prof* pf = b->prof;
   if constexpr (KT > 0) {
-    hipLaunchKernelGGL((k_attn_bwd_q<D, KT, false>), dim3(L.NQB, BH), dim3(64), 0, st, p);
-    hipLaunchKernelGGL((k_attn_bwd_kv<D, KT, false>), dim3(L.NKB, BH), dim3(64), 0, st, p);
+    {
+      Stage sg(pf, CSA_STAGE_ATTN_BWD_Q, st);
+      hipLaunchKernelGGL((k_attn_bwd_q<D, KT, false>), dim3(L.NQB, BH), dim3(64), 0, st, p);
+    }
+    {
+      Stage sg(pf, CSA_STAGE_ATTN_BWD_KV, st);
+      hipLaunchKernelGGL((k_attn_bwd_kv<D, KT, false>), dim3(L.NKB, BH), dim3(64), 0, st, p);
+    }
     if (hipMemsetAsync(p.slab, 0, sizeof(float) * a->H * L.G * L.slab_floats, st) != hipSuccess)
       return check_launch("memset slabs");
     using Sh = ProjBwdShape<D, KT>;
     (void)hipFuncSetAttribute((const void*)k_proj_bwd<D, KT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)Sh::LDS_BYTES);
-    hipLaunchKernelGGL((k_proj_bwd<D, KT>), dim3(L.G, a->H), dim3(256), Sh::LDS_BYTES, st, p);
+    {
+      Stage sg(pf, CSA_STAGE_PROJ_BWD, st);
+      hipLaunchKernelGGL((k_proj_bwd<D, KT>), dim3(L.G, a->H), dim3(256), Sh::LDS_BYTES, st, p);
+    }
+    Stage sr(pf, CSA_STAGE_REDUCE, st);
     const int KP32 = 32 * KT;
     float* dS_ws = (float*)((char*)b->workspace + L.w_dS);
     float* dC_ws = (float*)((char*)b->workspace + L.w_dC);
@@ -1242,7 +1273,11 @@ csa_status launch_bwd(const csa_sbm_bwd_args* b, const Layout& L, hipStream_t st
     hipLaunchKernelGGL(k_cluster_grad, dim3(a->H), dim3(256), 0, st, p.S, (const float*)dS_ws,
                        (const float*)dC_ws, a->cluster_w, b->dcluster_w, (int)a->k, D, KP32);
   } else {
-    hipLaunchKernelGGL((k_attn_bwd_q<D, 0, true>), dim3(L.NQB, BH), dim3(64), 0, st, p);
+    {
+      Stage sg(pf, CSA_STAGE_ATTN_BWD_Q, st);
+      hipLaunchKernelGGL((k_attn_bwd_q<D, 0, true>), dim3(L.NQB, BH), dim3(64), 0, st, p);
+    }
+    Stage sg(pf, CSA_STAGE_ATTN_BWD_KV, st);
     hipLaunchKernelGGL((k_attn_bwd_kv<D, 0, true>), dim3(L.NKB, BH), dim3(64), 0, st, p);
   }
   return check_launch("csa_sbm_bwd");

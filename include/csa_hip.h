@@ -45,6 +45,23 @@ typedef enum csa_status {
 /* flags */
 #define CSA_FLAG_DENSE 1u /* FullAttention (graph == 1, no cluster projection, no sampling) */
 
+/* Optional per-stage timing: caller-created hipEvent_t handles; when start[s] and stop[s] are
+ * non-NULL the library records them on `stream` around stage s (no library-side state). */
+enum {
+  CSA_STAGE_PREP = 0,       /* cluster softmax + fragment prep */
+  CSA_STAGE_PROJ_FWD = 1,   /* k_proj_fwd */
+  CSA_STAGE_ATTN_FWD = 2,   /* k_attn_fwd */
+  CSA_STAGE_ATTN_BWD_Q = 3, /* k_attn_bwd_q */
+  CSA_STAGE_ATTN_BWD_KV = 4,/* k_attn_bwd_kv */
+  CSA_STAGE_PROJ_BWD = 5,   /* k_proj_bwd */
+  CSA_STAGE_REDUCE = 6,     /* slab reduction + cluster grad */
+  CSA_STAGE_COUNT = 8
+};
+typedef struct csa_prof {
+  void* start[CSA_STAGE_COUNT];
+  void* stop[CSA_STAGE_COUNT];
+} csa_prof;
+
 typedef struct csa_sbm_fwd_args {
   int64_t B, H, N, M, d, k; /* batch, heads, queries, keys, head_dim, clusters (k ignored if DENSE) */
   const float* Q; int64_t q_sb, q_sh, q_sn; /* (B,H,N,d) */
@@ -61,6 +78,7 @@ typedef struct csa_sbm_fwd_args {
   float* X;                   /* out (B,H,N,d) contiguous */
   float* sparsity;            /* out (H,) head-wise sparsity (sbm_attn.py:64); NULL if DENSE */
   void* state;                /* csa_sbm_state_bytes(): saved for backward and csa_sbm_maps */
+  const csa_prof* prof;       /* optional stage timing (NULL = off) */
 } csa_sbm_fwd_args;
 
 typedef struct csa_sbm_bwd_args {
@@ -72,6 +90,7 @@ typedef struct csa_sbm_bwd_args {
   float* dcluster_w;           /* out (H*k, d); NULL if DENSE */
   float* dproj_w[3]; float* dproj_b[3]; /* out; NULL if DENSE */
   void* workspace;             /* csa_sbm_bwd_workspace_bytes() */
+  const csa_prof* prof;        /* optional stage timing (NULL = off) */
 } csa_sbm_bwd_args;
 
 int csa_abi_version(void);

@@ -1,0 +1,68 @@
+"""CPU-side checks of the C-ABI library: it loads, exports every symbol include/csa_hip.h declares,
+and its host-side queries/validation behave (no GPU compute is launched)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+
+def declared_symbols():
+    src = open(os.path.join(ROOT, "include", "csa_hip.h")).read()
+    return sorted(set(re.findall(r"\b(csa_[a-z_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    from csa_amd import _lib
+    L = _lib.lib()
+    syms = declared_symbols()
+    assert len(syms) >= 14
+    for s in syms:
+        assert hasattr(L, s), s
+    assert set(syms) == set(_lib.EXPORTED_SYMBOLS)
+
+
+def test_abi_version_and_status_strings():
+    from csa_amd import _lib
+    L = _lib.lib()
+    assert L.csa_abi_version() == _lib.CSA_ABI_VERSION
+    assert L.csa_status_str(0) == b"CSA_OK"
+    assert L.csa_status_str(2) == b"CSA_UNSUPPORTED_SHAPE"
+
+
+def test_supported_shapes():
+    from csa_amd import _lib
+    L = _lib.lib()
+    assert L.csa_sbm_supported(64, 10, 0) and L.csa_sbm_supported(96, 10, 0)
+    assert L.csa_sbm_supported(64, 0, _lib.CSA_FLAG_DENSE)
+    assert not L.csa_sbm_supported(48, 10, 0)
+    assert not L.csa_sbm_supported(64, 33, 0)
+
+
+def test_state_and_workspace_sizes_monotone():
+    from csa_amd import _lib
+    L = _lib.lib()
+    a = L.csa_sbm_state_bytes(2, 8, 150, 150, 64, 10, 0)
+    b = L.csa_sbm_state_bytes(4, 8, 150, 150, 64, 10, 0)
+    assert 0 < a < b
+    assert L.csa_sbm_bwd_workspace_bytes(256, 8, 150, 150, 64, 10, 0) > 0
+
+
+def test_invalid_args_rejected_without_gpu():
+    from csa_amd import _lib
+    L = _lib.lib()
+    a = _lib.SbmFwdArgs()  # all zero -> INVALID_ARG before any HIP call
+    assert L.csa_sbm_fwd(ctypes.byref(a), None) == 1
+    assert b"B, H, N, M" in L.csa_last_error_str()
+    assert L.csa_sbm_fwd(None, None) == 1
+    assert L.csa_ste_sample(None, None, None, 4, 0.01, 0.99, None) == 1
+
+
+def test_ops_refuse_cpu_tensors():
+    import torch
+    import csa_amd.ops  # noqa: F401
+    x = torch.zeros(4)
+    with pytest.raises(RuntimeError):
+        torch.ops.csa.ste_sample(x, x, 0.01, 0.99)
