@@ -67,7 +67,8 @@ class RelAttnArgs(ctypes.Structure):
         ("rel", vp), ("rel_sb", i64), ("rel_sh", i64),
         ("mask", vp), ("mask_sb", i64), ("mask_sh", i64),
         ("rel_head_group", i64),
-        ("out", vp), ("lse", vp),
+        ("out", vp), ("row_stats", vp),
+        ("state", vp),
     ]
 
 
@@ -106,8 +107,9 @@ def lib():
     for fn in ("csa_sbm_state_bytes", "csa_sbm_bwd_workspace_bytes"):
         getattr(L, fn).restype = ctypes.c_size_t
         getattr(L, fn).argtypes = [i64] * 6 + [u32]
-    L.csa_rel_attn_bwd_workspace_bytes.restype = ctypes.c_size_t
-    L.csa_rel_attn_bwd_workspace_bytes.argtypes = [i64] * 5
+    for fn in ("csa_rel_attn_state_bytes", "csa_rel_attn_bwd_workspace_bytes"):
+        getattr(L, fn).restype = ctypes.c_size_t
+        getattr(L, fn).argtypes = [i64] * 5
     L.csa_sbm_fwd.restype = ctypes.c_int
     L.csa_sbm_fwd.argtypes = [ctypes.POINTER(SbmFwdArgs), vp]
     L.csa_sbm_maps.restype = ctypes.c_int
@@ -137,5 +139,5 @@ def check(status, what):
 EXPORTED_SYMBOLS = (
     "csa_abi_version", "csa_status_str", "csa_last_error_str", "csa_sbm_supported", "csa_sbm_state_bytes",
     "csa_sbm_bwd_workspace_bytes", "csa_sbm_fwd", "csa_sbm_maps", "csa_sbm_bwd", "csa_ste_sample",
-    "csa_ste_backward", "csa_rel_attn_bwd_workspace_bytes", "csa_rel_attn_fwd", "csa_rel_attn_bwd",
+    "csa_ste_backward", "csa_rel_attn_state_bytes", "csa_rel_attn_bwd_workspace_bytes", "csa_rel_attn_fwd", "csa_rel_attn_bwd",
 )

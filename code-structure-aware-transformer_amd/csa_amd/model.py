@@ -1,0 +1,324 @@
+"""CSATrans assembled around the MI355X attention kernels (the caller side of the hot path).
+
+Mirrors module/csa_trans.py:67-236, module/sbm_model.py, module/base_seq2seq.py:40-114 and
+module/components.py with the SAME module attribute names, so the state_dict keys match the
+reference's and reference checkpoints load. What changes:
+
+* SBM encoder attention = csa_amd.module.sbm_attn.Attention (fused HIP SBM/dense kernels); the
+  per-layer (B,H,N,N) graph/attn maps are not materialised unless ``return_maps=True``
+  (the train step discards them, script/train.py:107).
+* CSE relation attention = csa_amd.module.disentangled_attn.DisentangledAttn fed the compact
+  (B,2,N,N) uint8 relation planes (parent L, sibling T) directly, instead of the reference's
+  repeat(4)+cat int64 (B,8,N,N) copies (module/csa_trans.py:206-211).
+* Everything else (embeddings, LayerNorm, FFN, nn.MultiheadAttention decoder, generator) is
+  stock PyTorch-ROCm, exactly as in the reference.
+"""
+import copy
+import math
+from types import SimpleNamespace
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .module.disentangled_attn import DisentangledAttn
+from .module.sbm_attn import Attention
+
+PAD = 0
+
+
+def _clones(m, n):
+    return nn.ModuleList([copy.deepcopy(m) for _ in range(n)])
+
+
+class PositionalEncoding(nn.Module):
+    """components.py:PositionalEncoding (sinusoidal, buffer `pe`)."""
+
+    def __init__(self, emb_size, max_len=5000):
+        super().__init__()
+        position = torch.arange(0, max_len).unsqueeze(1)
+        div = torch.exp(torch.arange(0, emb_size, 2) * -(math.log(10000.0) / emb_size))
+        pe = torch.zeros(max_len, emb_size)
+        pe[:, 0::2] = torch.sin(position * div)
+        pe[:, 1::2] = torch.cos(position * div)
+        self.register_buffer("pe", pe.unsqueeze(0))
+
+    def forward(self, x):
+        return x + self.pe[:, : x.size(1)]
+
+
+class Embeddings(nn.Module):
+    """components.py:Embeddings: word embedding (+ positional) -> LayerNorm -> dropout."""
+
+    def __init__(self, hidden_size, vocab_size, dropout=0.1, with_pos=False):
+        super().__init__()
+        self.word_embeddings = nn.Embedding(vocab_size, hidden_size, padding_idx=0)
+        self.pos_emb = PositionalEncoding(hidden_size) if with_pos else None
+        self.norm = nn.LayerNorm(hidden_size)
+        self.dropout = nn.Dropout(dropout)
+
+    def forward(self, x):
+        e = self.word_embeddings(x)
+        if self.pos_emb is not None:
+            e = self.pos_emb(e)
+        return self.dropout(self.norm(e))
+
+
+class FeedForward(nn.Module):
+    def __init__(self, d_model, dim_feed_forward, dropout=0.1):
+        super().__init__()
+        self.linear1 = nn.Linear(d_model, dim_feed_forward)
+        self.linear2 = nn.Linear(dim_feed_forward, d_model)
+        self.dropout = nn.Dropout(dropout)
+
+    def forward(self, x):
+        return self.linear2(self.dropout(F.gelu(self.linear1(x)))), None
+
+
+class SublayerConnection(nn.Module):
+    """Pre-LN residual: x + dropout(sublayer(norm(x)))."""
+
+    def __init__(self, size, dropout):
+        super().__init__()
+        self.norm = nn.LayerNorm(size)
+        self.dropout = nn.Dropout(dropout)
+
+    def forward(self, x, sublayer):
+        out, w = sublayer(self.norm(x))
+        return x + self.dropout(out), w
+
+
+class CSE_layer(nn.Module):  # noqa: N801 (reference name)
+    def __init__(self, hidden_size, num_heads, dim_feed_forward, dropout):
+        super().__init__()
+        self.num_heads = num_heads
+        self.hidden_size = hidden_size
+        self.self_attn = DisentangledAttn(num_heads, hidden_size, dropout)
+        self.feed_forward = FeedForward(hidden_size, dim_feed_forward, dropout=dropout)
+        self.dropout = nn.Dropout(dropout)
+        self.sublayer = _clones(SublayerConnection(hidden_size, dropout), 2)
+
+    def forward(self, src, rel_emb, rel, mask):
+        src, _ = self.sublayer[0](src, lambda x: self.self_attn(x, x, x, rel_emb, rel, mask))
+        src, _ = self.sublayer[1](src, self.feed_forward)
+        return src
+
+
+class CSE(nn.Module):
+    """module/csa_trans.py:180-217 with zero-copy relation planes."""
+
+    def __init__(self, encoder_layer, num_layers, num_heads, hidden_size, dropout=0.2, max_src_len=150):
+        super().__init__()
+        self.layers = _clones(encoder_layer, num_layers)
+        self.num_heads = num_heads
+        self.hidden_size = hidden_size
+        self.d_k = hidden_size // num_heads
+        self.max_src_len = max_src_len
+        self.edge_dim = self.d_k
+        self.L_q = nn.Embedding(max_src_len, hidden_size)
+        self.T_q = nn.Embedding(max_src_len, hidden_size)
+        self.f = nn.ReLU()
+        self.dropout = nn.Dropout(dropout)
+        self.norm = nn.LayerNorm(hidden_size)
+
+    def build_rel_emb(self):
+        return [torch.stack([self.L_q.weight, self.T_q.weight])]
+
+    def forward(self, data):
+        out = data.src_pe_emb
+        rel = torch.stack([data.L, data.T], 1)          # (B,2,N,N) uint8: heads 0-3 read L, 4-7 read T
+        mask = torch.stack([data.L_mask, data.T_mask], 1)
+        rel_emb = self.build_rel_emb()
+        for layer in self.layers:
+            out = layer(out, rel_emb, rel, mask)
+        return self.norm(out)
+
+
+class Transformer(nn.Module):
+    """module/sbm_model.py:10-31 pre-LN block around the fused Attention."""
+
+    def __init__(self, config, idx):
+        super().__init__()
+        self.norm1 = nn.LayerNorm(config["transformer_dim"])
+        self.mha = Attention(config, idx, config["full_att"])
+        self.dropout1 = nn.Dropout(p=config["dropout_prob"])
+        self.norm2 = nn.LayerNorm(config["transformer_dim"])
+        self.mlpblock = nn.Sequential(
+            nn.Linear(config["transformer_dim"], config["transformer_hidden_dim"]), nn.GELU(),
+            nn.Dropout(p=config["dropout_prob"]),
+            nn.Linear(config["transformer_hidden_dim"], config["transformer_dim"]), nn.Dropout(p=config["dropout_prob"]))
+
+    def forward(self, X, mask, deliver):
+        out, sparsity, graph, attn = self.mha([self.norm1(X), mask, deliver])
+        X = self.dropout1(out) + X
+        X = self.mlpblock(self.norm2(X)) + X
+        return X, sparsity, graph, attn
+
+
+class SBM(nn.Module):
+    """module/sbm_model.py:34-70."""
+
+    def __init__(self, config, sbm_enc_dim, pe_dim, pegen_dim, use_pegen):
+        super().__init__()
+        self.num_layers = config["sbm_layers"]
+        for idx in range(self.num_layers):
+            setattr(self, f"transformer_{idx}", Transformer(config, idx))
+        self.norm = nn.LayerNorm(sbm_enc_dim)
+        self.out = nn.Linear(sbm_enc_dim, config["out_dim"])
+        if use_pegen == "sequential":
+            self.pe = PositionalEncoding(sbm_enc_dim, config["max_src_len"])
+        else:
+            self.pe_expand = nn.Linear(pegen_dim, pe_dim)
+        self.use_pegen = use_pegen
+
+    def forward(self, data, src_pe, use_pe):
+        mask = data.src_mask
+        if use_pe != "sequential":
+            pe = self.pe_expand(src_pe)
+            X = torch.cat([data.src_emb, pe], dim=-1)
+        else:
+            pe = None
+            X = self.pe(data.src_emb)
+        sparsities, graphs, attns = (), [], []
+        for idx in range(self.num_layers):
+            X, sp, g, a = getattr(self, f"transformer_{idx}")(X, mask, [])
+            sparsities += (sp,)
+            graphs.append(g)
+            attns.append(a)
+        X = self.norm(X) * ~mask[:, :, None]
+        return self.out(X), sparsities, graphs, attns, pe
+
+
+class DecoderLayer(nn.Module):
+    def __init__(self, d_model, nhead, dim_feedforward=2048, dropout=0.1, activation="gelu"):
+        super().__init__()
+        self.self_attn = nn.MultiheadAttention(d_model, nhead, dropout=dropout)
+        self.multihead_attn = nn.MultiheadAttention(d_model, nhead, dropout=dropout)
+        self.feed_forward = FeedForward(d_model, dim_feedforward, dropout=dropout)
+        self.sublayer = _clones(SublayerConnection(d_model, dropout), 3)
+        self.dropout3 = nn.Dropout(dropout)
+
+    def forward(self, tgt, memory, tgt_mask=None, memory_key_padding_mask=None):
+        tgt, _ = self.sublayer[0](tgt, lambda x: self.self_attn(x, x, x, attn_mask=tgt_mask, need_weights=False))
+        tgt, w = self.sublayer[1](tgt, lambda x: self.multihead_attn(
+            x, memory, memory, key_padding_mask=memory_key_padding_mask, need_weights=False))
+        tgt, _ = self.sublayer[2](tgt, self.feed_forward)
+        return tgt, w
+
+
+class BaseDecoder(nn.Module):
+    def __init__(self, decoder_layer, num_layers, norm=None):
+        super().__init__()
+        self.layers = _clones(decoder_layer, num_layers)
+        self.num_layers = num_layers
+        self.norm = norm
+
+    def forward(self, tgt, memory, tgt_mask, memory_key_padding_mask=None):
+        out, w = tgt, None
+        for mod in self.layers:
+            out, w = mod(out, memory, tgt_mask=tgt_mask, memory_key_padding_mask=memory_key_padding_mask)
+        return (self.norm(out) if self.norm is not None else out), w
+
+
+class Generator(nn.Module):
+    """components.py:Generator: log(softmax(dropout(linear)))  (log of softmax, not log_softmax)."""
+
+    def __init__(self, tgt_vocab_size, hidden_size, dropout):
+        super().__init__()
+        self.soft_max = nn.Softmax(-1)
+        self.dropout = nn.Dropout(dropout)
+        self.linear = nn.Linear(hidden_size, tgt_vocab_size)
+
+    def forward(self, x):
+        return torch.log(self.soft_max(self.dropout(self.linear(x))))
+
+
+def make_std_mask(tgt, pad=PAD):
+    """dataset/base_data_set.py:125-135: pad | future mask, (B,T,T) bool."""
+    T = tgt.size(-1)
+    future = torch.triu(torch.ones(T, T, dtype=torch.bool, device=tgt.device), diagonal=1)
+    return (tgt == pad).unsqueeze(-2) | future.unsqueeze(0)
+
+
+class CSATrans(nn.Module):
+    """module/csa_trans.py:67-177 (+ BaseTrans.forward/encode/decode, base_seq2seq.py:40-114)."""
+
+    def __init__(self, src_vocab_size, tgt_vocab_size, hidden_size, num_heads, num_layers, sbm_layers, use_pegen,
+                 dim_feed_forward, dropout, pe_dim, pegen_dim, sbm_enc_dim, clusters, full_att, state_dict=None,
+                 max_src_len=150, return_maps=False):
+        super().__init__()
+        if use_pegen != "pegen":
+            raise NotImplementedError("only the pegen (CSE) structure encoding is on the accelerated path")
+        self.num_heads = num_heads
+        self.pe_dim, self.pegen_dim = pe_dim, pegen_dim
+        self.use_pegen = use_pegen
+        self.src_embedding = Embeddings(sbm_enc_dim - pe_dim, src_vocab_size, dropout, with_pos=False)
+        self.tgt_embedding = Embeddings(hidden_size, tgt_vocab_size, dropout, with_pos=True)
+        self.src_pe_embedding = Embeddings(pegen_dim, src_vocab_size, dropout, with_pos=False)
+        self.pegen = CSE(CSE_layer(pegen_dim, num_heads, pegen_dim, dropout), num_layers, num_heads, pegen_dim,
+                         dropout=dropout, max_src_len=max_src_len)
+        config = {"sbm_layers": sbm_layers, "transformer_dim": sbm_enc_dim, "transformer_hidden_dim": sbm_enc_dim,
+                  "head_dim": sbm_enc_dim // num_heads, "num_head": num_heads, "attn_type": "sbm",
+                  "attention_grad_checkpointing": False, "attention_dropout": 0.2, "num_clusters": clusters,
+                  "dropout_prob": 0.2, "out_dim": hidden_size, "max_src_len": max_src_len, "full_att": full_att,
+                  "return_maps": return_maps}
+        self.SBM = SBM(config, sbm_enc_dim, pe_dim, pegen_dim, use_pegen)
+        self.decoder = BaseDecoder(DecoderLayer(hidden_size, num_heads, dim_feed_forward, dropout, "gelu"), 4,
+                                   norm=nn.LayerNorm(hidden_size))
+        self.generator = Generator(tgt_vocab_size, hidden_size, dropout)
+        if state_dict is None:
+            for p in self.parameters():
+                if p.dim() > 1:
+                    nn.init.xavier_uniform_(p)
+            if not full_att:
+                for i in range(sbm_layers):
+                    nn.init.orthogonal_(getattr(self.SBM, f"transformer_{i}").mha.attn.layer.weight)
+        else:
+            self.load_state_dict(state_dict)
+
+    def forward(self, data):
+        data.src_mask = data.src_seq.eq(PAD)
+        data.src_emb = self.src_embedding(data.src_seq)
+        data.src_pe_emb = self.src_pe_embedding(data.src_seq)
+        data.tgt_mask = make_std_mask(data.tgt_seq, PAD)
+        data.tgt_emb = self.tgt_embedding(data.tgt_seq)
+        src_pe = self.pegen(data)
+        enc, sparsity, graphs, attns, pe = self.SBM(data, src_pe, self.use_pegen)
+        sparsity = 1 if sparsity[0] is None else torch.mean(torch.stack(sparsity))  # base_seq2seq.py:92-95
+        tgt_mask = data.tgt_mask.repeat(self.num_heads, 1, 1)
+        dec, _ = self.decoder(data.tgt_emb.permute(1, 0, 2), enc.permute(1, 0, 2), tgt_mask=tgt_mask,
+                              memory_key_padding_mask=data.src_mask)
+        out = self.generator(dec.permute(1, 0, 2))
+        return out, sparsity, pe, graphs, attns
+
+
+def label_smoothing_loss(logp, target, padding_idx=PAD):
+    """utils/label_smooth.py:15-40 at smoothing=0 (all configs): KLDiv(sum) against the one-hot
+    true_dist with padded rows zeroed, divided by the non-pad token count — computed without
+    materialising the (B*T, V) true_dist: sum over non-pad rows of -logp[target]."""
+    x = logp.reshape(-1, logp.size(-1))
+    t = target.reshape(-1)
+    ntokens = (t != padding_idx).sum()
+    picked = x.gather(1, t.unsqueeze(1)).squeeze(1)
+    return -(picked * (t != padding_idx)).sum() / ntokens
+
+
+def batch_to_device(sb, device):
+    """Synthetic batch dict (csa_amd.data.synthetic_batch) -> device-resident namespace."""
+    g = lambda k, dt=None: torch.as_tensor(sb[k], dtype=dt).to(device, non_blocking=True)
+    return SimpleNamespace(src_seq=g("src_seq", torch.int64), tgt_seq=g("tgt_seq", torch.int64),
+                           L=g("L", torch.uint8), T=g("T", torch.uint8), L_mask=g("L_mask", torch.uint8),
+                           T_mask=g("T_mask", torch.uint8)), g("target", torch.int64)
+
+
+CONFIGS = {  # config/python.py, config/java.py, config/python_full_att.py (vocab sizes: create_vocab caps)
+    "python": dict(src_vocab_size=10000, tgt_vocab_size=20000, hidden_size=512, num_heads=8, num_layers=4,
+                   sbm_layers=4, use_pegen="pegen", dim_feed_forward=2048, dropout=0.2, pe_dim=256,
+                   pegen_dim=512, sbm_enc_dim=512, clusters=[10, 10, 10, 10], full_att=False),
+    "java": dict(src_vocab_size=10000, tgt_vocab_size=20000, hidden_size=512, num_heads=8, num_layers=4,
+                 sbm_layers=4, use_pegen="pegen", dim_feed_forward=2048, dropout=0.2, pe_dim=128, pegen_dim=512,
+                 sbm_enc_dim=768, clusters=[10, 10, 10, 10], full_att=False),
+    "python_full_att": dict(src_vocab_size=10000, tgt_vocab_size=20000, hidden_size=512, num_heads=8,
+                            num_layers=4, sbm_layers=4, use_pegen="pegen", dim_feed_forward=2048, dropout=0.2,
+                            pe_dim=256, pegen_dim=512, sbm_enc_dim=512, clusters=[10, 10, 10, 10], full_att=True),
+}

@@ -1,13 +1,23 @@
-"""Drop-in DisentangledAttn (module/disentangled_attn.py:11-65) — see rel_ops for the kernels."""
-import torch
+"""Drop-in DisentangledAttn (module/disentangled_attn.py:11-65): same constructor, forward signature,
+return tuple and state_dict keys; the relation attention runs in torch.ops.csa.rel_attn_*."""
+import copy
+
 import torch.nn as nn
 
-__all__ = ["DisentangledAttn"]
+from .. import rel_ops
+
+__all__ = ["DisentangledAttn", "transpose_for_scores", "_get_clones"]
 
 
 def _get_clones(module, N):
-    import copy
+    """module/components.py:_get_clones."""
     return nn.ModuleList([copy.deepcopy(module) for _ in range(N)])
+
+
+def transpose_for_scores(x, num_heads):
+    """module/components.py:transpose_for_scores (a strided view; the kernels consume it in place)."""
+    x = x.view(*(x.size()[:-1] + (num_heads, -1)))
+    return x.permute(0, 2, 1, 3)
 
 
 class DisentangledAttn(nn.Module):
@@ -23,4 +33,21 @@ class DisentangledAttn(nn.Module):
         self.t_linear = _get_clones(nn.Linear(d_model, self.d_k * 4), 2)
 
     def forward(self, query, key, value, rel_emb, rel, mask):
-        raise NotImplementedError("rel_attn kernels not built yet")
+        query, key, value = [transpose_for_scores(l(x), self.h) for l, x in zip(self.linear_layers, (query, key, value))]
+        lq = rel_emb[0]
+        l = lq[0].unsqueeze(0)  # 1, L, d
+        t = lq[1].unsqueeze(0)
+        lq, lk = [transpose_for_scores(lin(x), 4) for lin, x in zip(self.l_linear, (l, l))]
+        tq, tk = [transpose_for_scores(lin(x), 4) for lin, x in zip(self.t_linear, (t, t))]
+        import torch
+        lq = torch.cat([lq, tq], dim=1)  # 1, 8, L, d
+        lk = torch.cat([lk, tk], dim=1)
+        output = self.rel_attn(query, key, value, lq, lk, rel, mask)
+        output = output.permute(0, 2, 1, 3).contiguous()
+        output = output.view(*(output.size()[:-2] + (-1,)))
+        output = self.linear_layers[-1](output)
+        return output, None
+
+    @staticmethod
+    def rel_attn(q, k, v, lq, lk, rel, mask):
+        return rel_ops.rel_attn(q, k, v, lq, lk, rel, mask)

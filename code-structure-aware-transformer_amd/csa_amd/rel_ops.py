@@ -1,0 +1,121 @@
+"""torch.ops.csa.rel_attn_{fwd,bwd} + autograd for DisentangledAttn.rel_attn
+(module/disentangled_attn.py:44-65) over the C ABI."""
+import ctypes
+from typing import List
+
+import torch
+
+from ._lib import RelAttnArgs, RelAttnBwdArgs, check, lib
+from .ops import _bhnd, _require_gpu, _stream
+
+
+def _planes(rel: torch.Tensor, mask: torch.Tensor, H: int):
+    """Relation/mask planes as uint8 + (batch stride, head stride, head group).
+
+    Accepts the reference layout (B,H,N,N) int64 / bool (module/csa_trans.py:206-211) or the compact
+    CSE layout (B,2,N,N) uint8 planes (parent L, sibling T) shared by heads [0,H/2) and [H/2,H)."""
+    if rel.dim() != 4:
+        raise ValueError("rel must be (B,H,N,N) or (B,2,N,N)")
+    rel = rel if rel.dtype == torch.uint8 else rel.to(torch.uint8)
+    mask = mask if mask.dtype == torch.uint8 else mask.to(torch.uint8)
+    rel, mask = rel.contiguous(), mask.contiguous()
+    if rel.shape[1] == 2 and H != 2:
+        group = H // 2
+    elif rel.shape[1] == H:
+        group = 0
+    else:
+        raise ValueError(f"rel has {rel.shape[1]} planes for {H} heads")
+    return rel, mask, group
+
+
+def _fwd_args(q, k, v, lq, lk, rel, mask, group, out, lse, state):
+    B, H, N, d = q.shape
+    a = RelAttnArgs()
+    a.B, a.H, a.N, a.L, a.d = B, H, N, lq.shape[1], d
+    a.q, (a.q_sb, a.q_sh, a.q_sn) = q.data_ptr(), q.stride()[:3]
+    a.k, (a.k_sb, a.k_sh, a.k_sn) = k.data_ptr(), k.stride()[:3]
+    a.v, (a.v_sb, a.v_sh, a.v_sn) = v.data_ptr(), v.stride()[:3]
+    a.lq, a.lk = lq.data_ptr(), lk.data_ptr()
+    a.rel, a.rel_sb, a.rel_sh = rel.data_ptr(), rel.stride(0), rel.stride(1)
+    a.mask, a.mask_sb, a.mask_sh = mask.data_ptr(), mask.stride(0), mask.stride(1)
+    a.rel_head_group = group
+    a.out, a.row_stats, a.state = out.data_ptr(), lse.data_ptr(), state.data_ptr()
+    return a
+
+
+@torch.library.custom_op("csa::rel_attn_fwd", mutates_args=())
+def rel_attn_fwd_op(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, lq: torch.Tensor, lk: torch.Tensor,
+                    rel: torch.Tensor, mask: torch.Tensor, group: int) -> List[torch.Tensor]:
+    """Returns [out (B,H,N,d), row_stats (B,H,N,2), state (uint8)]."""
+    _require_gpu(q, k, v, lq, lk, rel, mask)
+    q, k, v = _bhnd(q), _bhnd(k), _bhnd(v)
+    lq, lk = lq.float().contiguous(), lk.float().contiguous()
+    B, H, N, d = q.shape
+    L = lq.shape[1]
+    out = torch.empty(B, H, N, d, device=q.device, dtype=torch.float32)
+    lse = torch.empty(B, H, N, 2, device=q.device, dtype=torch.float32)  # (row max, 1/row sum)
+    state = torch.empty(lib().csa_rel_attn_state_bytes(B, H, N, L, d), device=q.device, dtype=torch.uint8)
+    a = _fwd_args(q, k, v, lq, lk, rel, mask, group, out, lse, state)
+    check(lib().csa_rel_attn_fwd(ctypes.byref(a), _stream(q.device)), "csa_rel_attn_fwd")
+    return [out, lse, state]
+
+
+@rel_attn_fwd_op.register_fake
+def _(q, k, v, lq, lk, rel, mask, group):
+    B, H, N, d = q.shape
+    return [q.new_empty(B, H, N, d), q.new_empty(B, H, N, 2),
+            q.new_empty(lib().csa_rel_attn_state_bytes(B, H, N, lq.shape[1], d), dtype=torch.uint8)]
+
+
+@torch.library.custom_op("csa::rel_attn_bwd", mutates_args=())
+def rel_attn_bwd_op(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, lq: torch.Tensor, lk: torch.Tensor,
+                    rel: torch.Tensor, mask: torch.Tensor, group: int, out: torch.Tensor, lse: torch.Tensor,
+                    state: torch.Tensor, dout: torch.Tensor) -> List[torch.Tensor]:
+    """Returns [dq, dk, dv, dlq (H,L,d), dlk (H,L,d)]."""
+    q, k, v = _bhnd(q), _bhnd(k), _bhnd(v)
+    lq, lk = lq.float().contiguous(), lk.float().contiguous()
+    dout = dout.float().contiguous()
+    B, H, N, d = q.shape
+    L = lq.shape[1]
+    a = _fwd_args(q, k, v, lq, lk, rel, mask, group, out, lse, state)
+    dq, dk, dv = (torch.empty(B, H, N, d, device=q.device, dtype=torch.float32) for _ in range(3))
+    dlq, dlk = torch.empty_like(lq), torch.empty_like(lk)
+    ws = torch.empty(lib().csa_rel_attn_bwd_workspace_bytes(B, H, N, L, d), device=q.device, dtype=torch.uint8)
+    b = RelAttnBwdArgs()
+    b.fwd = ctypes.pointer(a)
+    b.dout, b.dq, b.dk, b.dv = dout.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr()
+    b.dlq, b.dlk, b.workspace = dlq.data_ptr(), dlk.data_ptr(), ws.data_ptr()
+    check(lib().csa_rel_attn_bwd(ctypes.byref(b), _stream(q.device)), "csa_rel_attn_bwd")
+    return [dq, dk, dv, dlq, dlk]
+
+
+@rel_attn_bwd_op.register_fake
+def _(q, k, v, lq, lk, rel, mask, group, out, lse, state, dout):
+    return [torch.empty_like(q), torch.empty_like(k), torch.empty_like(v), torch.empty_like(lq), torch.empty_like(lk)]
+
+
+class RelAttnFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, lq, lk, rel, mask, group):
+        out, lse, state = torch.ops.csa.rel_attn_fwd(q, k, v, lq, lk, rel, mask, group)
+        ctx.save_for_backward(q, k, v, lq, lk, rel, mask, out, lse, state)
+        ctx.group = group
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        q, k, v, lq, lk, rel, mask, out, lse, state = ctx.saved_tensors
+        dq, dk, dv, dlq, dlk = torch.ops.csa.rel_attn_bwd(q, k, v, lq, lk, rel, mask, ctx.group, out, lse, state, dout)
+        return dq, dk, dv, dlq, dlk, None, None, None
+
+
+def rel_attn(q, k, v, lq, lk, rel, mask):
+    """DisentangledAttn.rel_attn (module/disentangled_attn.py:44-65) on the GPU.
+
+    q,k,v (B,H,N,d) (strided views fine); lq,lk (1,H,L,d) or (H,L,d); rel/mask (B,H,N,N) (reference
+    int64/bool layout) or (B,2,N,N) uint8 planes shared by head halves (compact CSE layout)."""
+    H = q.shape[1]
+    rel, mask, group = _planes(rel, mask, H)
+    if lq.dim() == 4:
+        lq, lk = lq[0], lk[0]
+    return RelAttnFunction.apply(q, k, v, lq, lk, rel, mask, group)

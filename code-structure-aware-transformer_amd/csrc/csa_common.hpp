@@ -98,4 +98,8 @@ __device__ __forceinline__ float u01(uint32_t x) { return (float)(x >> 8) * (1.0
 // Stream ids (Philox counter word 3 high bits) so independent draws never share counters.
 enum : uint32_t { RNG_STE = 1u, RNG_ATTN_DROP = 2u, RNG_PROJ_DROP = 3u };
 
+// Per-thread last-error text shared by every translation unit (csa_last_error_str).
+void set_error(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
+const char* get_error();
+
 }  // namespace csa

@@ -1,8 +1,502 @@
-// placeholder (replaced below in this round)
+// CSE disentangled AST-relation attention (module/disentangled_attn.py:44-65) on gfx950.
+//
+//   s[x,y] = (q_x.k_y + lq[rel[y,x]].k_y + q_x.lk[rel[x,y]]) / sqrt(3 d);  s[mask] = -1e9;
+//   out = softmax(s) v
+//
+// Forward:  k_bgemm   C2P  = Q LK^T   (B,H,N,Lp)   p2c/c2p relation logits, as the reference's
+//           k_bgemm   P2CT = K LQ^T   (B,H,M,Lp)   lq @ k^T / q @ lk^T (disentangled_attn.py:53-58)
+//           k_rel_fwd one wave per (b,h,32 queries): c2c by MFMA + per-element gathers of the two
+//                     relation logits, -1e9 masking, online softmax, PV; saves (row max, 1/row sum).
+// Backward: k_rel_bwd_q    recompute P, dP = dO V^T (MFMA), g = P (dP - dO.O)/sqrt(3d) (0 where masked);
+//                          dq += g K (MFMA); materialises g and P (B,H,N,N) once.
+//           k_bgemm        dv = P^T dO, dk = g^T Q
+//           k_rel_scatter  G_c2p[x][r] = sum_{y: rel[x,y]=r} g[x,y];  G_p2cT[y][r] = sum_{x: rel[y,x]=r} g[x,y]
+//                          (the gather backward; one thread per row/column, fixed order => deterministic)
+//           k_bgemm        dq += G_c2p LK ; dk += G_p2cT LQ ; dlk = sum_b G_c2p^T Q ; dlq = sum_b G_p2cT^T K
+// Relation planes are uint8 (B,P,N,N) with a head->plane map (heads 0-3 parent plane L, 4-7 sibling
+// plane T; module/csa_trans.py:206-211), replacing the reference's repeated int64 (B,8,N,N) copies.
+#include "csa_common.hpp"
 #include "../../include/csa_hip.h"
-#include <hip/hip_runtime.h>
-extern "C" {
-size_t csa_rel_attn_bwd_workspace_bytes(int64_t, int64_t, int64_t, int64_t, int64_t) { return 0; }
-csa_status csa_rel_attn_fwd(const csa_rel_attn_args*, void*) { return CSA_UNSUPPORTED_SHAPE; }
-csa_status csa_rel_attn_bwd(const csa_rel_attn_bwd_args*, void*) { return CSA_UNSUPPORTED_SHAPE; }
+
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+using namespace csa;
+
+namespace {
+
+constexpr float NEG_INF = -__builtin_inff();
+
+// ------------------------------------------------------------------------------------
+// Generic batched fp32 MFMA GEMM:  C[bat](m,n) (+)= alpha * sum_{r<R} sum_{k<K} A(r,bat,m,k) * B(r,bat,n,k)
+// element addresses: X[(bat / H2) * x_b1 + (bat % H2) * x_b2 + r * x_r + m * x_m + k * x_k]
+// One wave per 32x32 C tile; K consumed in chunks of 32 (16 MFMA K-steps, lin perm).
+// ------------------------------------------------------------------------------------
+struct GemmArgs {
+  const float* A; int64_t a_m, a_k, a_b1, a_b2, a_r;
+  const float* B; int64_t b_n, b_k, b_b1, b_b2, b_r;
+  float* C; int64_t c_m, c_n, c_b1, c_b2;
+  int M, N, K, H2, R;
+  float alpha; int accumulate;
+};
+
+__global__ __launch_bounds__(64) void k_bgemm(const GemmArgs g) {
+  const int lane = lane_id(), c = lane & 31, h = lane >> 5;
+  const int n0 = blockIdx.x * 32, m0 = blockIdx.y * 32, bat = blockIdx.z;
+  const int b1 = bat / g.H2, b2 = bat % g.H2;
+  const float* A = g.A + b1 * g.a_b1 + b2 * g.a_b2;
+  const float* Bp = g.B + b1 * g.b_b1 + b2 * g.b_b2;
+  const int m = m0 + c, n = n0 + c;
+  const bool mv = m < g.M, nv = n < g.N;
+  f32x16 acc = zero16();
+  for (int r = 0; r < g.R; ++r) {
+    const float* Ar = A + r * g.a_r + (int64_t)m * g.a_m;
+    const float* Br = Bp + r * g.b_r + (int64_t)n * g.b_n;
+    for (int k0 = 0; k0 < g.K; k0 += 32) {
+      float av[16], bv[16];
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const int kk = k0 + 16 * h + s;
+        av[s] = (mv && kk < g.K) ? Ar[(int64_t)kk * g.a_k] : 0.f;
+        bv[s] = (nv && kk < g.K) ? Br[(int64_t)kk * g.b_k] : 0.f;
+      }
+#pragma unroll
+      for (int s = 0; s < 16; ++s) acc = mfma(av[s], bv[s], acc);
+    }
+  }
+  float* C = g.C + b1 * g.c_b1 + b2 * g.c_b2;
+  if (nv) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int mm = m0 + crow(r, h);
+      if (mm < g.M) {
+        float* p = C + (int64_t)mm * g.c_m + (int64_t)n * g.c_n;
+        *p = g.accumulate ? *p + g.alpha * acc[r] : g.alpha * acc[r];
+      }
+    }
+  }
 }
+
+struct RelArgs {
+  int B, H, N, L, Lp, NQB, NKB, group;
+  const float *q, *k, *v; int64_t q_sb, q_sh, q_sn, k_sb, k_sh, k_sn, v_sb, v_sh, v_sn;
+  const uint8_t *rel, *mask; int64_t rel_sb, rel_sh, mask_sb, mask_sh;
+  const float *c2p, *p2ct;  // (B,H,N,Lp), (B,H,N,Lp)
+  float *out, *stats;
+  float inv_scale;
+  // backward
+  const float* dout;
+  float *dq, *G, *P;
+};
+
+__device__ __forceinline__ int64_t plane_off(const RelArgs& p, int b, int hd, int64_t sb, int64_t sh) {
+  if (p.group > 0) return b * sb + (hd >= p.group ? 1 : 0) * sh;
+  return b * sb + hd * sh;
+}
+
+// Score of one (x, y) element; returns NEG_INF outside the matrix.
+__device__ __forceinline__ float rel_score(const RelArgs& p, float c2c, int x, int y, const uint8_t* rp,
+                                           const uint8_t* mp, const float* c2p, const float* p2ct) {
+  if (x >= p.N || y >= p.N) return NEG_INF;
+  int rxy = rp[(int64_t)x * p.N + y], ryx = rp[(int64_t)y * p.N + x];
+  rxy = rxy < p.L ? rxy : p.L - 1;  // memory safety; the reference requires rel < L
+  ryx = ryx < p.L ? ryx : p.L - 1;
+  if (mp[(int64_t)x * p.N + y]) return -1e9f;  // masked_fill(mask == 1, -1e9) (disentangled_attn.py:62)
+  return (c2c + c2p[(int64_t)x * p.Lp + rxy] + p2ct[(int64_t)y * p.Lp + ryx]) * p.inv_scale;
+}
+
+// ------------------------------------------------------------------------------------
+// Forward: one wave per (b,h, 32-query block); S^T orientation (keys = acc rows, queries = lanes)
+// ------------------------------------------------------------------------------------
+template <int D>
+__global__ __launch_bounds__(64) void k_rel_fwd(const RelArgs p) {
+  constexpr int DT = (D + 31) / 32, NS = D / 2;
+  const int lane = lane_id(), c = lane & 31, h = lane >> 5;
+  const int qb = blockIdx.x, bh = blockIdx.y, b = bh / p.H, hd = bh % p.H;
+  const int i = qb * 32 + c;
+  const bool iv = i < p.N;
+  float q[NS];
+  load_run<NS>(q, p.q + b * p.q_sb + hd * p.q_sh + (int64_t)i * p.q_sn + h * NS, iv);
+  const float* kb = p.k + b * p.k_sb + hd * p.k_sh;
+  const float* vb = p.v + b * p.v_sb + hd * p.v_sh;
+  const uint8_t* rp = p.rel + plane_off(p, b, hd, p.rel_sb, p.rel_sh);
+  const uint8_t* mp = p.mask + plane_off(p, b, hd, p.mask_sb, p.mask_sh);
+  const float* c2p = p.c2p + (int64_t)bh * p.N * p.Lp;
+  const float* p2ct = p.p2ct + (int64_t)bh * p.N * p.Lp;
+  float m_run = NEG_INF, zp = 0.f;
+  f32x16 o[DT];
+#pragma unroll
+  for (int t = 0; t < DT; ++t) o[t] = zero16();
+  for (int kt = 0; kt < p.NKB; ++kt) {
+    const int j0 = kt * 32, jl = j0 + c;
+    float kr[NS];
+    load_run<NS>(kr, kb + (int64_t)jl * p.k_sn + h * NS, jl < p.N);
+    f32x16 sacc = zero16();
+#pragma unroll
+    for (int s = 0; s < NS; ++s) sacc = mfma(kr[s], q[s], sacc);
+    float sv[16];
+    float tmax = NEG_INF;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      sv[r] = rel_score(p, sacc[r], i, j0 + crow(r, h), rp, mp, c2p, p2ct);
+      tmax = fmaxf(tmax, sv[r]);
+    }
+    tmax = xhalf_max(tmax);
+    const float m_new = fmaxf(m_run, tmax);
+    const float alpha = (m_new == NEG_INF) ? 1.f : expf(m_run - m_new);
+    zp *= alpha;
+#pragma unroll
+    for (int t = 0; t < DT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
+    float w[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      w[r] = (sv[r] == NEG_INF) ? 0.f : expf(sv[r] - m_new);
+      zp += w[r];
+    }
+    m_run = m_new;
+#pragma unroll
+    for (int t = 0; t < DT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int j = j0 + crow(r, h);
+        const float vt = (j < p.N && 32 * t + c < D) ? vb[(int64_t)j * p.v_sn + 32 * t + c] : 0.f;
+        o[t] = mfma(vt, w[r], o[t]);
+      }
+  }
+  const float Z = xhalf_sum(zp);
+  if (iv) {
+    const float inv = 1.f / Z;
+    float* xo = p.out + ((int64_t)bh * p.N + i) * D;
+#pragma unroll
+    for (int t = 0; t < DT; ++t)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = o[t][4 * g4 + e] * inv;
+        if (32 * t + 8 * g4 + 4 * h < D) *reinterpret_cast<f32x4*>(xo + 32 * t + 8 * g4 + 4 * h) = v;
+      }
+    if (h == 0) {
+      p.stats[((int64_t)bh * p.N + i) * 2] = m_run;
+      p.stats[((int64_t)bh * p.N + i) * 2 + 1] = inv;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Backward (query side): g, P materialised; dq (c2c part) by MFMA
+// ------------------------------------------------------------------------------------
+template <int D>
+__global__ __launch_bounds__(64) void k_rel_bwd_q(const RelArgs p) {
+  constexpr int DT = (D + 31) / 32, NS = D / 2;
+  const int lane = lane_id(), c = lane & 31, h = lane >> 5;
+  const int qb = blockIdx.x, bh = blockIdx.y, b = bh / p.H, hd = bh % p.H;
+  const int i = qb * 32 + c;
+  const bool iv = i < p.N;
+  float q[NS], dO[NS];
+  load_run<NS>(q, p.q + b * p.q_sb + hd * p.q_sh + (int64_t)i * p.q_sn + h * NS, iv);
+  load_run<NS>(dO, p.dout + ((int64_t)bh * p.N + i) * D + h * NS, iv);
+  float dp = 0.f;
+  {
+    float o[NS];
+    load_run<NS>(o, p.out + ((int64_t)bh * p.N + i) * D + h * NS, iv);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) dp = fmaf(dO[s], o[s], dp);
+  }
+  const float delta = xhalf_sum(dp);
+  const float rmax = iv ? p.stats[((int64_t)bh * p.N + i) * 2] : 0.f;
+  const float rinv = iv ? p.stats[((int64_t)bh * p.N + i) * 2 + 1] : 0.f;
+  const float* kb = p.k + b * p.k_sb + hd * p.k_sh;
+  const float* vb = p.v + b * p.v_sb + hd * p.v_sh;
+  const uint8_t* rp = p.rel + plane_off(p, b, hd, p.rel_sb, p.rel_sh);
+  const uint8_t* mp = p.mask + plane_off(p, b, hd, p.mask_sb, p.mask_sh);
+  const float* c2p = p.c2p + (int64_t)bh * p.N * p.Lp;
+  const float* p2ct = p.p2ct + (int64_t)bh * p.N * p.Lp;
+  float* Gb = p.G + (int64_t)bh * p.N * p.N;
+  float* Pb = p.P + (int64_t)bh * p.N * p.N;
+  f32x16 dq[DT];
+#pragma unroll
+  for (int t = 0; t < DT; ++t) dq[t] = zero16();
+  for (int kt = 0; kt < p.NKB; ++kt) {
+    const int j0 = kt * 32, jl = j0 + c;
+    const bool jv = jl < p.N;
+    f32x16 sacc = zero16(), dpacc = zero16();
+    {
+      float kr[NS];
+      load_run<NS>(kr, kb + (int64_t)jl * p.k_sn + h * NS, jv);
+#pragma unroll
+      for (int s = 0; s < NS; ++s) sacc = mfma(kr[s], q[s], sacc);
+    }
+    {
+      float vr[NS];
+      load_run<NS>(vr, vb + (int64_t)jl * p.v_sn + h * NS, jv);
+#pragma unroll
+      for (int s = 0; s < NS; ++s) dpacc = mfma(vr[s], dO[s], dpacc);
+    }
+    float gv[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int y = j0 + crow(r, h);
+      const float sc = rel_score(p, sacc[r], i, y, rp, mp, c2p, p2ct);
+      float P = 0.f, g = 0.f;
+      if (sc != NEG_INF) {
+        P = expf(sc - rmax) * rinv;
+        const bool masked = mp[(int64_t)i * p.N + y] != 0;
+        g = masked ? 0.f : P * (dpacc[r] - delta) * p.inv_scale;
+        Gb[(int64_t)i * p.N + y] = g;
+        Pb[(int64_t)i * p.N + y] = P;
+      }
+      gv[r] = g;
+    }
+#pragma unroll
+    for (int t = 0; t < DT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int j = j0 + crow(r, h);
+        const float kv = (j < p.N && 32 * t + c < D) ? kb[(int64_t)j * p.k_sn + 32 * t + c] : 0.f;
+        dq[t] = mfma(kv, gv[r], dq[t]);
+      }
+  }
+  if (iv) {
+    float* dst = p.dq + ((int64_t)bh * p.N + i) * D;
+#pragma unroll
+    for (int t = 0; t < DT; ++t)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = dq[t][4 * g4 + e];
+        if (32 * t + 8 * g4 + 4 * h < D) *reinterpret_cast<f32x4*>(dst + 32 * t + 8 * g4 + 4 * h) = v;
+      }
+  }
+}
+
+// Gather backward as a deterministic scatter: one thread owns one row (mode 0: G_c2p[x][.], bins
+// over rel[x,y] along y) or one column (mode 1: G_p2cT[y][.], bins over rel[y,x] along x).
+__global__ __launch_bounds__(64) void k_rel_scatter(const RelArgs p, float* __restrict__ out, int mode) {
+  extern __shared__ __attribute__((aligned(16))) float bins[];
+  const int t = threadIdx.x;
+  const int64_t rowid = (int64_t)blockIdx.x * 64 + t;  // over B*H*N
+  float* my = bins + t * p.Lp;
+  for (int r = 0; r < p.Lp; ++r) my[r] = 0.f;
+  if (rowid < (int64_t)p.B * p.H * p.N) {
+    const int bh = (int)(rowid / p.N), x = (int)(rowid % p.N);
+    const int b = bh / p.H, hd = bh % p.H;
+    const uint8_t* rp = p.rel + plane_off(p, b, hd, p.rel_sb, p.rel_sh);
+    const float* Gb = p.G + (int64_t)bh * p.N * p.N;
+    if (mode == 0) {
+      for (int y = 0; y < p.N; ++y) {
+        int r = rp[(int64_t)x * p.N + y];
+        r = r < p.L ? r : p.L - 1;
+        my[r] += Gb[(int64_t)x * p.N + y];
+      }
+    } else {
+      for (int xx = 0; xx < p.N; ++xx) {
+        int r = rp[(int64_t)x * p.N + xx];  // rel[y = x][xx]
+        r = r < p.L ? r : p.L - 1;
+        my[r] += Gb[(int64_t)xx * p.N + x];
+      }
+    }
+    float* o = out + rowid * p.Lp;
+    for (int r = 0; r < p.Lp; ++r) o[r] = my[r];
+  }
+}
+
+csa_status rfail(csa_status s, const char* m) {
+  csa::set_error("%s", m);
+  return s;
+}
+
+csa_status rcheck(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    csa::set_error("%s: %s", what, hipGetErrorString(e));
+    return CSA_LAUNCH_FAILED;
+  }
+  return CSA_OK;
+}
+
+void gemm(hipStream_t st, const GemmArgs& g, int nbat) {
+  dim3 grid((unsigned)((g.N + 31) / 32), (unsigned)((g.M + 31) / 32), (unsigned)nbat);
+  hipLaunchKernelGGL(k_bgemm, grid, dim3(64), 0, st, g);
+}
+
+struct RelLayout {
+  int64_t Lp;
+  size_t c2p, p2ct, state_total;       // forward state
+  size_t G, P, gc2p, gp2ct, ws_total;  // backward workspace
+};
+
+inline size_t ral(size_t x) { return (x + 255) & ~size_t(255); }
+
+RelLayout rel_layout(int64_t B, int64_t H, int64_t N, int64_t L) {
+  RelLayout R;
+  R.Lp = ((L + 3) / 4) * 4;
+  size_t o = 0;
+  auto take = [&](size_t bytes) { size_t r = o; o += ral(bytes); return r; };
+  R.c2p = take(sizeof(float) * B * H * N * R.Lp);
+  R.p2ct = take(sizeof(float) * B * H * N * R.Lp);
+  R.state_total = o;
+  o = 0;
+  R.G = take(sizeof(float) * B * H * N * N);
+  R.P = take(sizeof(float) * B * H * N * N);
+  R.gc2p = take(sizeof(float) * B * H * N * R.Lp);
+  R.gp2ct = take(sizeof(float) * B * H * N * R.Lp);
+  R.ws_total = o;
+  return R;
+}
+
+csa_status validate_rel(const csa_rel_attn_args* a) {
+  if (!a) return rfail(CSA_INVALID_ARG, "null args");
+  if (a->B < 1 || a->H < 1 || a->N < 1 || a->L < 1) return rfail(CSA_INVALID_ARG, "B, H, N, L must be >= 1");
+  if (a->d != 16 && a->d != 32 && a->d != 64 && a->d != 96)
+    return rfail(CSA_UNSUPPORTED_SHAPE, "d_k must be 16, 32, 64 or 96");
+  if (a->L > 256) return rfail(CSA_UNSUPPORTED_SHAPE, "relation vocabulary L must be <= 256 (uint8 indices)");
+  if (!a->q || !a->k || !a->v || !a->lq || !a->lk || !a->rel || !a->mask || !a->out || !a->row_stats || !a->state)
+    return rfail(CSA_INVALID_ARG, "null pointer");
+  if (a->rel_head_group < 0 || a->rel_head_group > a->H) return rfail(CSA_INVALID_ARG, "bad rel_head_group");
+  auto al16 = [](const void* ptr, int64_t sb, int64_t sh, int64_t sn) {
+    return (((uintptr_t)ptr) % 16 == 0) && sb % 4 == 0 && sh % 4 == 0 && sn % 4 == 0;
+  };
+  if (!al16(a->q, a->q_sb, a->q_sh, a->q_sn) || !al16(a->k, a->k_sb, a->k_sh, a->k_sn) ||
+      !al16(a->v, a->v_sb, a->v_sh, a->v_sn) || ((uintptr_t)a->out) % 16)
+    return rfail(CSA_INVALID_ARG, "q/k/v/out must be 16-byte aligned with strides multiple of 4 elements");
+  return CSA_OK;
+}
+
+RelArgs make_rel(const csa_rel_attn_args* a, const RelLayout& R) {
+  void* ws = a->state;
+  RelArgs p;
+  memset(&p, 0, sizeof(p));
+  p.B = (int)a->B; p.H = (int)a->H; p.N = (int)a->N; p.L = (int)a->L; p.Lp = (int)R.Lp;
+  p.NQB = (int)((a->N + 31) / 32); p.NKB = p.NQB; p.group = (int)a->rel_head_group;
+  p.q = a->q; p.k = a->k; p.v = a->v;
+  p.q_sb = a->q_sb; p.q_sh = a->q_sh; p.q_sn = a->q_sn;
+  p.k_sb = a->k_sb; p.k_sh = a->k_sh; p.k_sn = a->k_sn;
+  p.v_sb = a->v_sb; p.v_sh = a->v_sh; p.v_sn = a->v_sn;
+  p.rel = a->rel; p.mask = a->mask;
+  p.rel_sb = a->rel_sb; p.rel_sh = a->rel_sh; p.mask_sb = a->mask_sb; p.mask_sh = a->mask_sh;
+  p.c2p = (const float*)((char*)ws + R.c2p);
+  p.p2ct = (const float*)((char*)ws + R.p2ct);
+  p.out = a->out; p.stats = a->row_stats;
+  p.inv_scale = 1.f / sqrtf(3.f * (float)a->d);
+  return p;
+}
+
+// relation logits: C2P[b,h] = Q LK_h^T (N x L), P2CT[b,h] = K LQ_h^T (N x L)
+void rel_logits(const csa_rel_attn_args* a, const RelLayout& R, hipStream_t st) {
+  void* ws = a->state;
+  for (int which = 0; which < 2; ++which) {
+    GemmArgs g;
+    memset(&g, 0, sizeof(g));
+    const float* X = which == 0 ? a->q : a->k;
+    g.A = X; g.a_m = which == 0 ? a->q_sn : a->k_sn; g.a_k = 1;
+    g.a_b1 = which == 0 ? a->q_sb : a->k_sb; g.a_b2 = which == 0 ? a->q_sh : a->k_sh;
+    g.B = which == 0 ? a->lk : a->lq; g.b_n = a->d; g.b_k = 1; g.b_b1 = 0; g.b_b2 = a->L * a->d;
+    g.C = (float*)((char*)ws + (which == 0 ? R.c2p : R.p2ct));
+    g.c_m = R.Lp; g.c_n = 1; g.c_b1 = a->H * a->N * R.Lp; g.c_b2 = a->N * R.Lp;
+    g.M = (int)a->N; g.N = (int)a->L; g.K = (int)a->d; g.H2 = (int)a->H; g.R = 1; g.alpha = 1.f; g.accumulate = 0;
+    gemm(st, g, (int)(a->B * a->H));
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t csa_rel_attn_state_bytes(int64_t B, int64_t H, int64_t N, int64_t L, int64_t d) {
+  (void)d;
+  return rel_layout(B, H, N, L).state_total;
+}
+
+size_t csa_rel_attn_bwd_workspace_bytes(int64_t B, int64_t H, int64_t N, int64_t L, int64_t d) {
+  (void)d;
+  return rel_layout(B, H, N, L).ws_total;
+}
+
+csa_status csa_rel_attn_fwd(const csa_rel_attn_args* a, void* stream) {
+  csa_status s = validate_rel(a);
+  if (s != CSA_OK) return s;
+  const RelLayout R = rel_layout(a->B, a->H, a->N, a->L);
+  hipStream_t st = (hipStream_t)stream;
+  rel_logits(a, R, st);
+  RelArgs p = make_rel(a, R);
+  const dim3 grid((unsigned)p.NQB, (unsigned)(a->B * a->H));
+  if (a->d == 64) hipLaunchKernelGGL(k_rel_fwd<64>, grid, dim3(64), 0, st, p);
+  else if (a->d == 32) hipLaunchKernelGGL(k_rel_fwd<32>, grid, dim3(64), 0, st, p);
+  else if (a->d == 16) hipLaunchKernelGGL(k_rel_fwd<16>, grid, dim3(64), 0, st, p);
+  else hipLaunchKernelGGL(k_rel_fwd<96>, grid, dim3(64), 0, st, p);
+  return rcheck("csa_rel_attn_fwd");
+}
+
+csa_status csa_rel_attn_bwd(const csa_rel_attn_bwd_args* b, void* stream) {
+  if (!b || !b->fwd) return rfail(CSA_INVALID_ARG, "null args");
+  const csa_rel_attn_args* a = b->fwd;
+  csa_status s = validate_rel(a);
+  if (s != CSA_OK) return s;
+  if (!b->dout || !b->dq || !b->dk || !b->dv || !b->dlq || !b->dlk || !b->workspace)
+    return rfail(CSA_INVALID_ARG, "null gradient pointer / workspace");
+  const RelLayout R = rel_layout(a->B, a->H, a->N, a->L);
+  hipStream_t st = (hipStream_t)stream;
+  void* ws = b->workspace;
+  RelArgs p = make_rel(a, R);
+  p.dout = b->dout; p.dq = b->dq;
+  p.G = (float*)((char*)ws + R.G);
+  p.P = (float*)((char*)ws + R.P);
+  const int B = (int)a->B, H = (int)a->H, N = (int)a->N, L = (int)a->L, D = (int)a->d;
+  const int64_t Lp = R.Lp;
+  // zero G/P (entries beyond N are never written; the GEMMs read only [0,N))
+  const dim3 grid((unsigned)p.NQB, (unsigned)(B * H));
+  if (D == 64) hipLaunchKernelGGL(k_rel_bwd_q<64>, grid, dim3(64), 0, st, p);
+  else if (D == 32) hipLaunchKernelGGL(k_rel_bwd_q<32>, grid, dim3(64), 0, st, p);
+  else if (D == 16) hipLaunchKernelGGL(k_rel_bwd_q<16>, grid, dim3(64), 0, st, p);
+  else hipLaunchKernelGGL(k_rel_bwd_q<96>, grid, dim3(64), 0, st, p);
+  // dv = P^T dO ; dk = G^T Q    (per (b,h): C(m=y, n=dd) = sum_x X(x,y) Y(x,dd))
+  for (int which = 0; which < 2; ++which) {
+    GemmArgs g;
+    memset(&g, 0, sizeof(g));
+    g.A = which == 0 ? p.P : p.G; g.a_m = 1; g.a_k = N; g.a_b1 = (int64_t)H * N * N; g.a_b2 = (int64_t)N * N;
+    if (which == 0) { g.B = b->dout; g.b_n = 1; g.b_k = D; g.b_b1 = (int64_t)H * N * D; g.b_b2 = (int64_t)N * D; }
+    else { g.B = a->q; g.b_n = 1; g.b_k = a->q_sn; g.b_b1 = a->q_sb; g.b_b2 = a->q_sh; }
+    g.C = which == 0 ? b->dv : b->dk; g.c_m = D; g.c_n = 1; g.c_b1 = (int64_t)H * N * D; g.c_b2 = (int64_t)N * D;
+    g.M = N; g.N = D; g.K = N; g.H2 = H; g.R = 1; g.alpha = 1.f; g.accumulate = 0;
+    gemm(st, g, B * H);
+  }
+  // gather backward
+  float* gc2p = (float*)((char*)ws + R.gc2p);
+  float* gp2ct = (float*)((char*)ws + R.gp2ct);
+  const unsigned nrow = (unsigned)(((int64_t)B * H * N + 63) / 64);
+  const size_t lds = sizeof(float) * 64 * Lp;
+  (void)hipFuncSetAttribute((const void*)k_rel_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(k_rel_scatter, dim3(nrow), dim3(64), lds, st, p, gc2p, 0);
+  hipLaunchKernelGGL(k_rel_scatter, dim3(nrow), dim3(64), lds, st, p, gp2ct, 1);
+  // dq += G_c2p LK_h ; dk += G_p2cT LQ_h    (C(m=x, n=dd) = sum_r G(x,r) LK(r,dd))
+  for (int which = 0; which < 2; ++which) {
+    GemmArgs g;
+    memset(&g, 0, sizeof(g));
+    g.A = which == 0 ? gc2p : gp2ct; g.a_m = Lp; g.a_k = 1; g.a_b1 = (int64_t)H * N * Lp; g.a_b2 = (int64_t)N * Lp;
+    g.B = which == 0 ? a->lk : a->lq; g.b_n = 1; g.b_k = D; g.b_b1 = 0; g.b_b2 = (int64_t)L * D;
+    g.C = which == 0 ? b->dq : b->dk; g.c_m = D; g.c_n = 1; g.c_b1 = (int64_t)H * N * D; g.c_b2 = (int64_t)N * D;
+    g.M = N; g.N = D; g.K = L; g.H2 = H; g.R = 1; g.alpha = 1.f; g.accumulate = 1;
+    gemm(st, g, B * H);
+  }
+  // dlk_h = sum_b G_c2p^T Q ; dlq_h = sum_b G_p2cT^T K    (C(m=r, n=dd) = sum_b sum_x G(x,r) X(x,dd))
+  for (int which = 0; which < 2; ++which) {
+    GemmArgs g;
+    memset(&g, 0, sizeof(g));
+    g.A = which == 0 ? gc2p : gp2ct; g.a_m = 1; g.a_k = Lp; g.a_b1 = 0; g.a_b2 = (int64_t)N * Lp;
+    g.a_r = (int64_t)H * N * Lp;
+    const float* X = which == 0 ? a->q : a->k;
+    g.B = X; g.b_n = 1; g.b_k = which == 0 ? a->q_sn : a->k_sn; g.b_b1 = 0;
+    g.b_b2 = which == 0 ? a->q_sh : a->k_sh; g.b_r = which == 0 ? a->q_sb : a->k_sb;
+    g.C = which == 0 ? b->dlk : b->dlq; g.c_m = D; g.c_n = 1; g.c_b1 = 0; g.c_b2 = (int64_t)L * D;
+    g.M = L; g.N = D; g.K = N; g.H2 = H; g.R = B; g.alpha = 1.f; g.accumulate = 0;
+    gemm(st, g, H);
+  }
+  return rcheck("csa_rel_attn_bwd");
+}
+
+}  // extern "C"

@@ -20,10 +20,22 @@
 #include "../../include/csa_hip.h"
 
 #include <math.h>
+#include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
 
 using namespace csa;
+
+namespace csa {
+static thread_local char g_err[512] = "";
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+const char* get_error() { return g_err; }
+}  // namespace csa
 
 namespace {
 
@@ -1095,7 +1107,6 @@ __global__ void k_ste_backward(const float* __restrict__ A, const float* __restr
 // ------------------------------------------------------------------------------------
 // Host side
 // ------------------------------------------------------------------------------------
-thread_local char g_err[512] = "";
 
 struct Stage {  // records caller-owned events around one stage (no-op when prof is NULL)
   const csa_prof* pf; int s; hipStream_t st;
@@ -1108,14 +1119,14 @@ struct Stage {  // records caller-owned events around one stage (no-op when prof
 };
 
 csa_status fail(csa_status s, const char* msg) {
-  snprintf(g_err, sizeof(g_err), "%s", msg);
+  csa::set_error("%s", msg);
   return s;
 }
 
 csa_status check_launch(const char* what) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
-    snprintf(g_err, sizeof(g_err), "%s: %s", what, hipGetErrorString(e));
+    csa::set_error("%s: %s", what, hipGetErrorString(e));
     return CSA_LAUNCH_FAILED;
   }
   return CSA_OK;
@@ -1299,7 +1310,7 @@ const char* csa_status_str(csa_status s) {
   return "CSA_UNKNOWN";
 }
 
-const char* csa_last_error_str(void) { return g_err; }
+const char* csa_last_error_str(void) { return csa::get_error(); }
 
 int csa_sbm_supported(int64_t d, int64_t k, uint32_t flags) { return supported(d, k, flags) ? 1 : 0; }
 

@@ -122,7 +122,9 @@ typedef struct csa_rel_attn_args {
   const uint8_t* mask; int64_t mask_sb, mask_sh;/* (B,*,N,N) 1 = masked (-1e9); head stride may be 0 */
   int64_t rel_head_group; /* heads [0,g) read plane 0, heads [g,H) plane 1 (CSE: 4); 0 = use rel_sh */
   float* out;          /* (B,H,N,d) contiguous */
-  float* lse;          /* (B,H,N) saved row log-sum-exp for backward */
+  float* row_stats;    /* (B,H,N,2) saved (row max, 1/row sum) for backward; kept separate because
+                          fully masked rows sit at -1e9 where max + log(sum) is not representable */
+  void* state;         /* csa_rel_attn_state_bytes(): relation logits q.lk^T, k.lq^T, kept for backward */
 } csa_rel_attn_args;
 
 typedef struct csa_rel_attn_bwd_args {
@@ -133,6 +135,7 @@ typedef struct csa_rel_attn_bwd_args {
   void* workspace;
 } csa_rel_attn_bwd_args;
 
+size_t csa_rel_attn_state_bytes(int64_t B, int64_t H, int64_t N, int64_t L, int64_t d);
 size_t csa_rel_attn_bwd_workspace_bytes(int64_t B, int64_t H, int64_t N, int64_t L, int64_t d);
 csa_status csa_rel_attn_fwd(const csa_rel_attn_args* a, void* stream);
 csa_status csa_rel_attn_bwd(const csa_rel_attn_bwd_args* a, void* stream);

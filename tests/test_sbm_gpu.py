@@ -94,3 +94,33 @@ def test_full_attention_matches_reference(golden, case):
     (X * dev(z["dX"])).sum().backward()
     for name, t in (("dQ", Q), ("dK", K), ("dV", V)):
         np.testing.assert_allclose(t.grad.cpu().numpy(), z[name], rtol=RTOL, atol=ATOL, err_msg=name)
+
+
+@pytest.mark.skipif(not has_gpu(), reason="needs GPU")
+@pytest.mark.parametrize("case", ["attn_layer_n29", "attn_layer_full_n29"])
+def test_attention_layer_matches_reference(golden, case):
+    """module/sbm_attn.py:90-140 Attention (W_q/W_k/W_v, strided split_heads views, ff)."""
+    from csa_amd.module.sbm_attn import Attention
+    z = golden(case)
+    B, N, dim, H, k, full = (int(v) for v in z["meta"])
+    cfg = {"attention_grad_checkpointing": False, "transformer_dim": dim, "head_dim": dim // H, "num_head": H,
+           "attn_type": "sbm", "attention_dropout": 0.2, "num_clusters": [k]}
+    m = Attention(cfg, 0, full_att=bool(full))
+    m.load_state_dict({kk[2:]: torch.from_numpy(v) for kk, v in z.items() if kk.startswith("p:")}, strict=False)
+    m = m.cuda().eval()
+    if not full:
+        m.attn.uniforms = dev(z["u"])
+    X = dev(z["X"], True)
+    out, sp, graph, attn = m([X, dev(z["mask"]), []])
+    if not full:
+        np.testing.assert_array_equal(graph.detach().cpu().numpy().astype(np.uint8), z["graph"])
+    np.testing.assert_allclose(out.detach().cpu().numpy(), z["out"], rtol=RTOL, atol=ATOL)
+    loss = (out * dev(z["dout"])).sum()
+    if sp is not None:
+        np.testing.assert_array_equal(sp.detach().cpu().numpy(), z["sparsity"])
+        loss = loss + (sp * dev(z["dsparsity"])).sum()
+    loss.backward()
+    np.testing.assert_allclose(X.grad.cpu().numpy(), z["dX"], rtol=RTOL, atol=ATOL)
+    for pn, p in m.named_parameters():
+        np.testing.assert_allclose(p.grad.cpu().numpy(), z["g:" + pn], rtol=RTOL, atol=ATOL, err_msg=pn)
+
