@@ -108,6 +108,42 @@ def cpu_baseline(seconds, B=16, H=8, N=150, d=64, k=10):
             "sample": f"{n} oracle fwd+bwd steps of B={B} (H=8,N=150,d=64,k=10, train mode) in {el:.1f}s"}
 
 
+def train_step_bench(world, rank, dev, steps, warmup, config="java", per_gpu_batch=64, nbatches=3):
+    """script/train.py:_update (config/java.py dims) under DDP/RCCL; returns samples/s over all ranks."""
+    from csa_amd.data import synthetic_batch
+    from csa_amd.model import CONFIGS, CSATrans, batch_to_device, label_smoothing_loss
+    from csa_amd.train import AdamW, make_train_step, wrap_ddp
+    torch.manual_seed(2021 + rank)  # set_seed(seed + rank), script/train.py:158
+    model = CSATrans(**CONFIGS[config]).to(dev)
+    ddp = wrap_ddp(model, dev)
+    opt = AdamW(model.parameters(), lr=1e-4, correct_bias=False)
+    scaler = torch.amp.GradScaler("cuda")
+    step = make_train_step(ddp, opt, label_smoothing_loss, sw=1e-2, scaler=scaler)
+    batches = [batch_to_device(synthetic_batch(per_gpu_batch, 150, seed=1 + 1000 * rank + i), dev)
+               for i in range(nbatches)]
+    for i in range(warmup):
+        step(*batches[i % nbatches])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        loss = step(*batches[i % nbatches])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    nparam = sum(p.numel() for p in model.parameters())
+    return {"config": f"config/{config}.py CSATrans summary train step (DDP over RCCL)", "per_gpu_batch": per_gpu_batch,
+            "global_batch": per_gpu_batch * world, "steps": steps, "warmup": warmup,
+            "ms_per_step": round(el * 1000 / steps, 3), "samples_per_s": round(world * per_gpu_batch * steps / el, 1),
+            "params": nparam, "last_loss": round(float(loss), 4)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -118,6 +154,8 @@ def main():
     ap.add_argument("--eval", action="store_true", help="eval mode (no dropout)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-train", action="store_true", help="skip the full train-step measurement")
+    ap.add_argument("--train-steps", type=int, default=10)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -237,6 +275,8 @@ def main():
         "step_frac_of_f32_mfma_peak": round(total_flops / (ms_per_step * 1e-3) / 1e12 / PEAK_F32_MFMA_TFLOPS, 4),
         "stage_ms": {s: round(v, 4) for s, v in stage_ms.items()},
     }
+    if not args.no_train:
+        out["train"] = train_step_bench(world, rank, dev, args.train_steps, max(2, args.warmup))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     if rank == 0:

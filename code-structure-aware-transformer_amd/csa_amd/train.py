@@ -1,0 +1,112 @@
+"""The data-parallel training step of script/train.py:103-116, on PyTorch-ROCm + RCCL.
+
+    _update: model.train(); zero_grad; y_pred, sparsity, ... = model(x)
+             loss = LabelSmoothing(y_pred, y); GradScaler.scale(loss + sw*sparsity).backward()
+             scaler.step(AdamW); scaler.update()
+
+Multi-GPU: one process per GPU (torchrun), DistributedDataParallel over the "nccl" backend (= RCCL
+on ROCm, xGMI between the GPUs of a node) as idist.auto_model does (script/train.py:83,331); each
+rank draws its own batches (DistributedSampler semantics: per-rank shard) and seeds with
+seed + rank (script/train.py:158). DDP averages gradients, so the global step equals the mean of
+the per-rank losses, exactly the reference's semantics (LabelSmoothing divides by per-rank
+ntokens, utils/label_smooth.py:27,40).
+
+The optimizer is the reference's HF-style AdamW (script/optimizer.py:49-106) with
+correct_bias=False (script/train.py:80), implemented with multi-tensor foreach kernels instead of
+a per-parameter Python loop.
+"""
+import os
+
+import torch
+import torch.distributed as dist
+
+
+class AdamW(torch.optim.Optimizer):
+    """script/optimizer.py:10-106 (decoupled weight decay, optional bias correction), foreach-fused."""
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-6, weight_decay=0.0, correct_bias=True):
+        if lr < 0.0 or not 0.0 <= betas[0] < 1.0 or not 0.0 <= betas[1] < 1.0 or eps < 0.0:
+            raise ValueError("invalid AdamW hyper-parameters")
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
+                                      correct_bias=correct_bias))
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        for group in self.param_groups:
+            ps = [p for p in group["params"] if p.grad is not None]
+            if not ps:
+                continue
+            grads = [p.grad for p in ps]
+            m, v = [], []
+            for p in ps:
+                st = self.state[p]
+                if len(st) == 0:
+                    st["step"] = 0
+                    st["exp_avg"] = torch.zeros_like(p)
+                    st["exp_avg_sq"] = torch.zeros_like(p)
+                st["step"] += 1
+                m.append(st["exp_avg"])
+                v.append(st["exp_avg_sq"])
+            b1, b2 = group["betas"]
+            torch._foreach_mul_(m, b1)
+            torch._foreach_add_(m, grads, alpha=1.0 - b1)
+            torch._foreach_mul_(v, b2)
+            torch._foreach_addcmul_(v, grads, grads, value=1.0 - b2)
+            denom = torch._foreach_sqrt(v)
+            torch._foreach_add_(denom, group["eps"])
+            step_size = group["lr"]
+            if group["correct_bias"]:
+                t = self.state[ps[0]]["step"]
+                step_size = step_size * (1.0 - b2 ** t) ** 0.5 / (1.0 - b1 ** t)
+            torch._foreach_addcdiv_(ps, m, denom, value=-step_size)
+            if group["weight_decay"] > 0.0:
+                torch._foreach_add_(ps, ps, alpha=-group["lr"] * group["weight_decay"])
+        return loss
+
+
+def init_distributed():
+    """torchrun env -> (rank, world, local_rank, device); RCCL process group when world > 1."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
+    else:
+        device = torch.device("cpu")
+    if world > 1 and not dist.is_initialized():
+        if device.type == "cuda":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group("gloo")
+    return rank, world, local, device
+
+
+def wrap_ddp(model, device):
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        return torch.nn.parallel.DistributedDataParallel(
+            model, device_ids=[device.index] if device.type == "cuda" else None,
+            gradient_as_bucket_view=True, bucket_cap_mb=64)
+    return model
+
+
+def make_train_step(model, optimizer, loss_fn, sw=1e-2, scaler=None, sync_loss=False):
+    """Returns step(x, y) implementing script/train.py:_update (lines 103-116)."""
+
+    def step(x, y):
+        model.train()
+        optimizer.zero_grad(set_to_none=True)
+        y_pred, sparsity, src_pe, graphs, attns = model(x)
+        loss = loss_fn(y_pred, y)
+        total = loss + sw * sparsity
+        if scaler is not None:
+            scaler.scale(total).backward()
+            scaler.step(optimizer)
+            scaler.update()
+        else:
+            total.backward()
+            optimizer.step()
+        return loss.item() if sync_loss else loss.detach()
+
+    return step

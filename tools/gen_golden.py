@@ -225,6 +225,132 @@ def disentangled_case(name, B, N, d_model, L, seed):
     print(f"{name}: ok")
 
 
+def label_smoothing_case(name, seed):
+    """utils/label_smooth.py:15-40 (smoothing=0 as in every config) on log(softmax) outputs with padding."""
+    s = importlib.util.spec_from_file_location("ref_label_smooth", f"{REF}/utils/label_smooth.py")
+    m = importlib.util.module_from_spec(s)
+    s.loader.exec_module(m)
+    g = torch.Generator().manual_seed(seed)
+    B, T, V = 3, 7, 50
+    logits = torch.randn(B, T, V, generator=g).requires_grad_(True)
+    x = torch.log(torch.softmax(logits, -1))
+    target = torch.randint(4, V, (B, T), generator=g)
+    target[0, 5:] = 0
+    target[2, 3:] = 0
+    crit = m.LabelSmoothing(padding_idx=0, smoothing=0.0)
+    loss = crit(x, target)
+    loss.backward()
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), logits=np32(logits), target=target.numpy(),
+                        loss=np.array([loss.item()], np.float32), dlogits=np32(logits.grad))
+    print(f"{name}: loss={loss.item():.5f}")
+
+
+def adamw_case(name, seed):
+    """script/optimizer.py AdamW with correct_bias=False (script/train.py:80), 3 steps."""
+    s = importlib.util.spec_from_file_location("ref_optimizer", f"{REF}/script/optimizer.py")
+    m = importlib.util.module_from_spec(s)
+    s.loader.exec_module(m)
+    g = torch.Generator().manual_seed(seed)
+    p0 = torch.randn(5, 4, generator=g)
+    p1 = torch.randn(7, generator=g)
+    grads = [(torch.randn(5, 4, generator=g), torch.randn(7, generator=g)) for _ in range(3)]
+    a, b = torch.nn.Parameter(p0.clone()), torch.nn.Parameter(p1.clone())
+    opt = m.AdamW([a, b], lr=1e-2, correct_bias=False)
+    for ga, gb in grads:
+        a.grad, b.grad = ga.clone(), gb.clone()
+        opt.step()
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), p0=np32(p0), p1=np32(p1),
+                        g0=np.stack([np32(x[0]) for x in grads]), g1=np.stack([np32(x[1]) for x in grads]),
+                        out0=np32(a), out1=np32(b))
+    print(f"{name}: ok")
+
+
+def load_full_reference_package():
+    """SURVEY.md Appendix A, option 2: the whole `module` package with 3 in-process shims
+    (torch 2.10 dropped T_co; torch_geometric and ipdb are not installed)."""
+    import typing
+    import torch.utils.data.dataset as tds
+    if not hasattr(tds, "T_co"):
+        tds.T_co = typing.TypeVar("T_co", covariant=True)
+    tg = types.ModuleType("torch_geometric")
+    tgd = types.ModuleType("torch_geometric.data")
+
+    class Data:
+        def __init__(self, **kw):
+            self.__dict__.update(kw)
+
+        def to(self, device):
+            return self
+    tgd.Data = Data
+    tg.data = tgd
+    sys.modules.setdefault("torch_geometric", tg)
+    sys.modules.setdefault("torch_geometric.data", tgd)
+    sys.modules.setdefault("ipdb", types.ModuleType("ipdb"))
+    for k in [k for k in sys.modules if k == "module" or k.startswith("module.")]:
+        del sys.modules[k]
+    sys.path.insert(0, REF)
+    import module as refmod  # noqa
+    return refmod, Data
+
+
+GRAD_KEYS = ("mha.attn.", "self_attn.l_linear.0", "self_attn.t_linear.1", "pegen.L_q", "pegen.T_q",
+             "SBM.out.bias", "pe_expand.bias", "generator.linear.bias")
+
+
+def fill_params_deterministic(model, seed):
+    """Every parameter <- N(0,1) * 0.5/sqrt(fan_in) from numpy's PCG64 in sorted-key order (reproducible
+    anywhere, so the fixture need not carry the weights; tests/test_model_gpu.py applies the same fill)."""
+    rng = np.random.default_rng(seed)
+    named = dict(model.named_parameters())
+    with torch.no_grad():
+        for k in sorted(named):
+            p = named[k]
+            fan = p.shape[-1] if p.dim() > 1 else 1
+            p.copy_(torch.from_numpy((rng.standard_normal(p.shape) * (0.5 / np.sqrt(fan))).astype(np.float32)))
+
+
+def csatrans_case(name, seed):
+    """Tiny CSATrans (module/csa_trans.py) forward + loss + sw*sparsity backward, eval mode,
+    host-supplied uniforms per SBM layer; saves the state_dict (checks key compatibility)."""
+    refmod, Data = load_full_reference_package()
+    s = importlib.util.spec_from_file_location("ref_label_smooth", f"{REF}/utils/label_smooth.py")
+    ls = importlib.util.module_from_spec(s)
+    s.loader.exec_module(ls)
+    torch.manual_seed(seed)
+    kw = dict(src_vocab_size=50, tgt_vocab_size=60, hidden_size=64, num_heads=8, num_layers=1, sbm_layers=2,
+              use_pegen="pegen", dim_feed_forward=128, dropout=0.2, pe_dim=32, pegen_dim=128, sbm_enc_dim=512,
+              clusters=[10, 12], full_att=False)
+    model = refmod.CSATrans(**kw).eval()
+    fill_params_deterministic(model, seed)
+    B, N = 2, 20
+    sb = synthetic_batch(B, max_size=N, seed=seed, min_nodes=12, max_nodes=N, src_vocab=50, tgt_vocab=60,
+                         max_tgt_len=9)
+    f = lambda a: torch.from_numpy(np.asarray(a))
+    data = Data(src_seq=f(sb["src_seq"]), tgt_seq=f(sb["tgt_seq"]), L=f(sb["L"]).float(), T=f(sb["T"]).float(),
+                L_mask=f(sb["L_mask"]), T_mask=f(sb["T_mask"]))
+    g = torch.Generator().manual_seed(seed + 1)
+    us = [torch.rand(B, 8, N, N, generator=g) for _ in range(2)]
+    it = iter(us)
+    torch.bernoulli = lambda p: (next(it) < p).to(p.dtype)
+    try:
+        out, sparsity, src_pe, graphs, attns = model(data)
+    finally:
+        torch.bernoulli = _real_bernoulli
+    loss = ls.LabelSmoothing(padding_idx=0, smoothing=0.0)(out, f(sb["target"]))
+    total = loss + 1e-2 * sparsity
+    total.backward()
+    res = {"src_seq": sb["src_seq"], "tgt_seq": sb["tgt_seq"], "target": sb["target"], "L": sb["L"], "T": sb["T"],
+           "L_mask": sb["L_mask"], "T_mask": sb["T_mask"], "u0": np32(us[0]), "u1": np32(us[1]),
+           "out": np32(out), "sparsity": np.array([sparsity.item()], np.float32),
+           "loss": np.array([loss.item()], np.float32)}
+    res["state_keys"] = np.array(sorted(model.state_dict().keys()))
+    for k, p in model.named_parameters():
+        if any(t in k for t in GRAD_KEYS):
+            res["g:" + k] = np32(p.grad)
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **res)
+    print(f"{name}: loss={loss.item():.5f} sparsity={sparsity.item():.5f} keys={len(model.state_dict())}")
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     torch.set_num_threads(8)
@@ -247,6 +373,9 @@ def main():
     rel_attn_case("rel_attn_n150", B=1, N=150, dk=16, L=150, seed=42)
     rel_attn_case("rel_attn_n20_dk64", B=1, N=20, dk=64, L=150, seed=43)
     disentangled_case("disentangled_n23", B=2, N=23, d_model=128, L=150, seed=51)
+    label_smoothing_case("label_smoothing", seed=61)
+    adamw_case("adamw_nobias", seed=62)
+    csatrans_case("csatrans_tiny", seed=71)
 
 
 if __name__ == "__main__":
