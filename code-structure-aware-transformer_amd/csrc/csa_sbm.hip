@@ -96,9 +96,20 @@ template <typename T> __device__ __forceinline__ T* at(void* base, size_t off) {
   return reinterpret_cast<T*>(reinterpret_cast<char*>(base) + off);
 }
 
-// Fragment of an MFMA A operand, stored operand-major: ((it * nsteps/4 + s/4) * 64 + lane) * 4 + s%4
+// Scheduling fence: bounds how far the scheduler hoists the (L2-resident) fragment loads ahead of
+// their MFMAs, which otherwise inflates register pressure past two waves per SIMD.
+__device__ __forceinline__ void fence_sched() { __builtin_amdgcn_sched_barrier(0); }
+
+// Fragment of an MFMA A operand, stored operand-major: ((it * nsteps/4 + s/4) * 64 + lane) * 4 + s%4.
+// Loaded with a buffer load: one wave-uniform descriptor (SGPRs), the lane's byte offset as the only
+// VGPR and the fragment's offset as a scalar. A plain pointer load makes the compiler materialise a
+// 64-bit per-lane address for every one of the ~100 fragment loads of a layer chain and hoist them
+// all to kernel entry, which spilled k_proj_bwd to scratch (guide T8/T20).
 __device__ __forceinline__ f32x4 frag4(const float* __restrict__ f, int it, int nsteps, int s4) {
-  return *reinterpret_cast<const f32x4*>(f + ((size_t)(it * (nsteps >> 2) + s4) * 64 + lane_id()) * 4);
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(f), (short)0, 0x7fffffff, 0x00020000);
+  const int soff = (it * (nsteps >> 2) + s4) * 1024;
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, lane_id() * 16, soff, 0));
 }
 
 // ------------------------------------------------------------------------------------
@@ -205,67 +216,85 @@ __device__ __forceinline__ f32x4 philox_u4(uint32_t a, uint32_t b, uint32_t c, u
   return o;
 }
 
-// MLP forward of one 32-row block held as lin-perm rows x[D/2] (see csa_common.hpp).
-// Produces the post-ReLU hidden activations h1, h2 and the output p as accumulator tiles
-// (feature rows in registers, data rows on lanes). Proj dropout p>0 applies
-// Linear -> Dropout -> ReLU (sbm_attn.py:22-30) with a stateless Philox mask.
+// MLP forward pieces for one 32-row block held as lin-perm rows x[D/2] (see csa_common.hpp).
+// Hidden activations are accumulator tiles (feature rows in registers, data rows on lanes).
+// Proj dropout p>0 applies Linear -> Dropout -> ReLU (sbm_attn.py:22-30) with a stateless Philox
+// mask keyed by (row, feature, layer, Q/K), so the backward regenerates it bit-identically.
 template <int D>
-__device__ __forceinline__ void mlp_fwd(const KArgs& p, const float (&x)[D / 2], f32x16 (&h1)[D / 32],
-                                        f32x16 (&h2)[D / 32], f32x16 (&po)[D / 32], int row, int bh, int isK) {
-  constexpr int DT = D / 32, NS = D / 2;
+__device__ __forceinline__ void mlp_act(const KArgs& p, f32x16 (&a)[D / 32], int layer, int row, int bh, int isK) {
+  constexpr int DT = D / 32;
   const int h = lane_id() >> 5;
   const bool drop = p.proj_p > 0.f;
   const float ks = drop ? 1.f / (1.f - p.proj_p) : 1.f;
-  // layer 0: lin-perm input
+#pragma unroll
+  for (int ot = 0; ot < DT; ++ot)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      f32x4 u = {1.f, 1.f, 1.f, 1.f};
+      if (drop) u = philox_u4((uint32_t)row, (uint32_t)(8 * ot + 2 * g + h) | (layer << 16) | (isK << 20),
+                              (uint32_t)bh, RNG_PROJ_DROP, p);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float v = a[ot][4 * g + e];
+        if (drop) v = (u[e] >= p.proj_p) ? v * ks : 0.f;
+        a[ot][4 * g + e] = fmaxf(v, 0.f);
+      }
+    }
+}
+
+// h1 = relu(drop(W0 x + b0)) from lin-perm input rows
+template <int D>
+__device__ __forceinline__ void mlp_layer0(const KArgs& p, const float (&x)[D / 2], f32x16 (&h1)[D / 32], int row,
+                                           int bh, int isK) {
+  constexpr int DT = D / 32, NS = D / 2;
+  const int h = lane_id() >> 5;
 #pragma unroll
   for (int ot = 0; ot < DT; ++ot)
 #pragma unroll
     for (int r = 0; r < 16; ++r) h1[ot][r] = p.pb[0][32 * ot + crow(r, h)];
 #pragma unroll
-  for (int s4 = 0; s4 < NS / 4; ++s4)
+  for (int s4 = 0; s4 < NS / 4; ++s4) {
 #pragma unroll
     for (int ot = 0; ot < DT; ++ot) {
       const f32x4 w = frag4(p.Wf[0], ot, NS, s4);
 #pragma unroll
       for (int j = 0; j < 4; ++j) h1[ot] = mfma(w[j], x[4 * s4 + j], h1[ot]);
     }
-  auto act = [&](f32x16(&a)[DT], int layer) {
+    if ((s4 & 1) == 1) fence_sched();
+  }
+  mlp_act<D>(p, h1, 0, row, bh, isK);
+}
+
+// out = W_l in + b_l  (acc-perm input), l = 1, 2
+template <int D>
+__device__ __forceinline__ void mlp_layer(const KArgs& p, const f32x16 (&in)[D / 32], f32x16 (&out)[D / 32], int l) {
+  constexpr int DT = D / 32, NS = D / 2;
+  const int h = lane_id() >> 5;
 #pragma unroll
-    for (int ot = 0; ot < DT; ++ot)
+  for (int ot = 0; ot < DT; ++ot)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        f32x4 u;
-        if (drop) u = philox_u4((uint32_t)row, (uint32_t)(8 * ot + 2 * g + h) | (layer << 16) | (isK << 20),
-                                (uint32_t)bh, RNG_PROJ_DROP, p);
+    for (int r = 0; r < 16; ++r) out[ot][r] = p.pb[l][32 * ot + crow(r, h)];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float v = a[ot][4 * g + e];
-          if (drop) v = (u[e] >= p.proj_p) ? v * ks : 0.f;
-          a[ot][4 * g + e] = fmaxf(v, 0.f);
-        }
+  for (int t = 0; t < DT; ++t)
+#pragma unroll
+    for (int r4 = 0; r4 < 4; ++r4) {
+#pragma unroll
+      for (int ot = 0; ot < DT; ++ot) {
+        const f32x4 w = frag4(p.Wf[l], ot, NS, 4 * t + r4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) out[ot] = mfma(w[j], in[t][4 * r4 + j], out[ot]);
       }
-  };
-  act(h1, 0);
-  // layers 1, 2: acc-perm input
-  auto dense_layer = [&](const f32x16(&in)[DT], f32x16(&out)[DT], int l) {
-#pragma unroll
-    for (int ot = 0; ot < DT; ++ot)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) out[ot][r] = p.pb[l][32 * ot + crow(r, h)];
-#pragma unroll
-    for (int t = 0; t < DT; ++t)
-#pragma unroll
-      for (int r4 = 0; r4 < 4; ++r4)
-#pragma unroll
-        for (int ot = 0; ot < DT; ++ot) {
-          const f32x4 w = frag4(p.Wf[l], ot, NS, 4 * t + r4);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) out[ot] = mfma(w[j], in[t][4 * r4 + j], out[ot]);
-        }
-  };
-  dense_layer(h1, h2, 1);
-  act(h2, 1);
-  dense_layer(h2, po, 2);
+      if ((r4 & 1) == 1) fence_sched();
+    }
+}
+
+template <int D>
+__device__ __forceinline__ void mlp_fwd(const KArgs& p, const float (&x)[D / 2], f32x16 (&h1)[D / 32],
+                                        f32x16 (&h2)[D / 32], f32x16 (&po)[D / 32], int row, int bh, int isK) {
+  mlp_layer0<D>(p, x, h1, row, bh, isK);
+  mlp_layer<D>(p, h1, h2, 1);
+  mlp_act<D>(p, h2, 1, row, bh, isK);
+  mlp_layer<D>(p, h2, po, 2);
 }
 
 // hat^T = sigmoid(C_h p^T), rows (clusters) >= k zeroed.
@@ -612,7 +641,7 @@ __device__ __forceinline__ Elem bwd_elem(float s_raw, float dpp, bool kval, bool
 // B2: per (b,h, query block), S^T orientation: dQ (attention path), dQh, gamma
 // ------------------------------------------------------------------------------------
 template <int D, int KT, bool DENSE>
-__global__ __launch_bounds__(64) void k_attn_bwd_q(const KArgs p) {
+__global__ __launch_bounds__(64, (D <= 64 ? 2 : 1)) void k_attn_bwd_q(const KArgs p) {
   constexpr int DT = D / 32, NS = D / 2;
   const int lane = lane_id(), c = lane & 31, h = lane >> 5;
   const int qb = blockIdx.x, bh = blockIdx.y, b = bh / p.H, hd = bh % p.H;
@@ -646,6 +675,9 @@ __global__ __launch_bounds__(64) void k_attn_bwd_q(const KArgs p) {
 #pragma unroll
   for (int t = 0; t < KTA; ++t) dqh[t] = zero16();
   for (int kt = 0; kt < p.NKB; ++kt) {
+    int ln = threadIdx.x;  // opaque per iteration: keeps per-key addresses out of the prologue
+    asm volatile("" : "+v"(ln));
+    const int c = ln & 31, h = (ln >> 5) & 1;
     const int j0 = kt * 32, jl = j0 + c;
     const bool jv = jl < p.M;
     f32x16 sacc = zero16(), dpacc = zero16();
@@ -710,7 +742,7 @@ __global__ __launch_bounds__(64) void k_attn_bwd_q(const KArgs p) {
 // B1: per (b,h, key block), S orientation (queries = acc rows, keys = lanes): dK, dV, dT
 // ------------------------------------------------------------------------------------
 template <int D, int KT, bool DENSE>
-__global__ __launch_bounds__(64) void k_attn_bwd_kv(const KArgs p) {
+__global__ __launch_bounds__(64, (D <= 64 ? 2 : 1)) void k_attn_bwd_kv(const KArgs p) {
   constexpr int DT = D / 32, NS = D / 2;
   const int lane = lane_id(), c = lane & 31, h = lane >> 5;
   const int kbi = blockIdx.x, bh = blockIdx.y, b = bh / p.H, hd = bh % p.H;
@@ -732,6 +764,9 @@ __global__ __launch_bounds__(64) void k_attn_bwd_kv(const KArgs p) {
 #pragma unroll
   for (int t = 0; t < KTA; ++t) dtt[t] = zero16();
   for (int qb = 0; qb < p.NQB; ++qb) {
+    int ln = threadIdx.x;  // opaque per iteration: keeps per-row addresses out of the prologue
+    asm volatile("" : "+v"(ln));
+    const int c = ln & 31, h = (ln >> 5) & 1;
     const int i0 = qb * 32, il = i0 + c;
     const bool ilv = il < p.N;
     f32x16 sacc = zero16(), dpacc = zero16();
@@ -813,8 +848,8 @@ struct ProjBwdShape {
 
 // Stage an accumulator tile set (feature rows, data rows on lanes) into LDS[f][wave*32 + c].
 template <int NT>
-__device__ __forceinline__ void stage_acc(float* __restrict__ buf, const f32x16 (&a)[NT], int nrows_valid) {
-  const int lane = lane_id(), c = lane & 31, h = lane >> 5, w = threadIdx.x >> 6;
+__device__ __forceinline__ void stage_acc(float* __restrict__ buf, const f32x16 (&a)[NT], int nrows_valid, int tid) {
+  const int lane = tid & 63, c = lane & 31, h = lane >> 5, w = tid >> 6;
 #pragma unroll
   for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -827,8 +862,8 @@ __device__ __forceinline__ void stage_acc(float* __restrict__ buf, const f32x16 
 // C[32ot.., 32it..] (+)= sum over the 128 staged rows of DS[o][row] * IN[i][row]
 // -> RMW into slab (row-major ldo). Tiles (ot, it) for ot < nto, it < nti assigned round-robin to waves.
 __device__ __forceinline__ void wg_outer(const float* __restrict__ ds, const float* __restrict__ in, int nto, int nti,
-                                         float* __restrict__ slab, int ldo, int orows, int icols) {
-  const int lane = lane_id(), c = lane & 31, h = lane >> 5, w = threadIdx.x >> 6;
+                                         float* __restrict__ slab, int ldo, int orows, int icols, int tid) {
+  const int lane = tid & 63, c = lane & 31, h = lane >> 5, w = tid >> 6;
   for (int tile = w; tile < nto * nti; tile += 4) {
     const int ot = tile / nti, it = tile % nti;
     f32x16 acc = zero16();
@@ -853,8 +888,8 @@ __device__ __forceinline__ void wg_outer(const float* __restrict__ ds, const flo
 }
 
 // db[f] += sum over the 128 staged rows of DS[f][row]   (threads f < nf)
-__device__ __forceinline__ void wg_rowsum(const float* __restrict__ ds, int nf, float* __restrict__ slab) {
-  const int t = threadIdx.x;
+__device__ __forceinline__ void wg_rowsum(const float* __restrict__ ds, int nf, float* __restrict__ slab, int tid) {
+  const int t = tid;
   if (t < nf) {
     float s = 0.f;
     const float* a = ds + t * RW;
@@ -874,7 +909,7 @@ __device__ __forceinline__ void mm_acc(const float* __restrict__ frag, const f32
 #pragma unroll
   for (int t = 0; t < NTO; ++t) out[t] = zero16();
 #pragma unroll
-  for (int s4 = 0; s4 < NSTEP / 4; ++s4)
+  for (int s4 = 0; s4 < NSTEP / 4; ++s4) {
 #pragma unroll
     for (int t = 0; t < NTO; ++t) {
       const f32x4 w = frag4(frag, t, NSTEP, s4);
@@ -884,10 +919,12 @@ __device__ __forceinline__ void mm_acc(const float* __restrict__ frag, const f32
         out[t] = mfma(w[e], in[s / 16][s % 16], out[t]);
       }
     }
+    if ((s4 & 1) == 1) fence_sched();
+  }
 }
 
 template <int D, int KT>
-__global__ __launch_bounds__(256) void k_proj_bwd(const KArgs p) {
+__global__ __launch_bounds__(256, (D <= 64 ? 2 : 1)) void k_proj_bwd(const KArgs p) {
   using Sh = ProjBwdShape<D, KT>;
   constexpr int DT = Sh::DT, NS = Sh::NS, KP32 = Sh::KP32, ROWS = Sh::ROWS;
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -908,6 +945,10 @@ __global__ __launch_bounds__(256) void k_proj_bwd(const KArgs p) {
   const float* SfT = p.SfT + (size_t)hd * KP32 * KP32;
 
   for (int grp = 0; grp * 4 < n_items; ++grp) {
+    // Opaque copy of the thread id: addresses derived from it are recomputed in the loop instead of
+    // ~100 of them being hoisted to kernel entry and pinned in registers for the whole kernel.
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
     const int item = grp * 4 + w;
     const bool has = item < n_items;
     const int b = b_lo + (has ? item / per_b : 0);
@@ -922,18 +963,24 @@ __global__ __launch_bounds__(256) void k_proj_bwd(const KArgs p) {
                          : p.Q + b * p.q_sb + hd * p.q_sh + (int64_t)row * p.q_sn;
     float x[NS];
     load_run<NS>(x, X + h * NS, rv);
-    f32x16 h1[DT], h2[DT], po[DT], hat[KT];
-    mlp_fwd<D>(p, x, h1, h2, po, row, bh, isK);
+    f32x16 h2[DT], po[DT], hat[KT];
+    {
+      f32x16 h1[DT];
+      mlp_layer0<D>(p, x, h1, row, bh, isK);
+      mlp_layer<D>(p, h1, h2, 1);
+    }
+    mlp_act<D>(p, h2, 1, row, bh, isK);
+    mlp_layer<D>(p, h2, po, 2);
     cluster_hat<D, KT>(p, po, hat, hd);
     // gradient w.r.t. the sigmoid output
     f32x16 dhat[KT], gin[KT];
     load_rows<KT>(gin, (isK ? p.dT + ((int64_t)bh * p.M + row) * p.kp : p.dQh + ((int64_t)bh * p.N + row) * p.kp),
                   p.kp, rv);
     // ---- dS_h += sum_rows dT^T Kh^T  (T_j = S Kh_j) ; K items only
-    stage_acc<KT>(DS, gin, isK ? KP32 : 0);
-    stage_acc<KT>(IN, hat, isK ? KP32 : 0);
+    stage_acc<KT>(DS, gin, isK ? KP32 : 0, tid);
+    stage_acc<KT>(IN, hat, isK ? KP32 : 0, tid);
     __syncthreads();
-    wg_outer(DS, IN, KT, KT, sS, KP32, KP32, KP32);
+    wg_outer(DS, IN, KT, KT, sS, KP32, KP32, KP32, tid);
     __syncthreads();
     if (isK) {
       mm_acc<KT, KT>(SfT, gin, dhat);  // dKh^T = S^T dT^T
@@ -947,20 +994,20 @@ __global__ __launch_bounds__(256) void k_proj_bwd(const KArgs p) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) dhat[t][r] = dhat[t][r] * hat[t][r] * (1.f - hat[t][r]);
     // ---- dC_h += sum_rows dZ^T p^T
-    stage_acc<KT>(DS, dhat, KP32);
-    stage_acc<DT>(IN, po, D);
+    stage_acc<KT>(DS, dhat, KP32, tid);
+    stage_acc<DT>(IN, po, D, tid);
     __syncthreads();
-    wg_outer(DS, IN, KT, DT, sC, D, KP32, D);
+    wg_outer(DS, IN, KT, DT, sC, D, KP32, D, tid);
     __syncthreads();
     // dp^T = C^T dZ^T
     f32x16 dcur[DT];
     mm_acc<DT, KT>(CfT, dhat, dcur);
     // ---- layer 2 (proj.6): dW2 += dp^T h2 ; db2 ; dh2 = W2^T dp
-    stage_acc<DT>(DS, dcur, D);
-    stage_acc<DT>(IN, h2, D);
+    stage_acc<DT>(DS, dcur, D, tid);
+    stage_acc<DT>(IN, h2, D, tid);
     __syncthreads();
-    wg_outer(DS, IN, DT, DT, sW[2], D, D, D);
-    wg_rowsum(DS, D, sb[2]);
+    wg_outer(DS, IN, DT, DT, sW[2], D, D, D, tid);
+    wg_rowsum(DS, D, sb[2], tid);
     __syncthreads();
     {
       f32x16 dh[DT];
@@ -970,14 +1017,16 @@ __global__ __launch_bounds__(256) void k_proj_bwd(const KArgs p) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) dcur[t][r] = (h2[t][r] > 0.f) ? dh[t][r] * ks : 0.f;
     }
-    // ---- layer 1 (proj.3)
-    stage_acc<DT>(DS, dcur, D);
-    stage_acc<DT>(IN, h1, D);
-    __syncthreads();
-    wg_outer(DS, IN, DT, DT, sW[1], D, D, D);
-    wg_rowsum(DS, D, sb[1]);
-    __syncthreads();
+    // ---- layer 1 (proj.3): recompute h1 from x (cheaper than keeping it live across the backward)
     {
+      f32x16 h1[DT];
+      mlp_layer0<D>(p, x, h1, row, bh, isK);
+      stage_acc<DT>(DS, dcur, D, tid);
+      stage_acc<DT>(IN, h1, D, tid);
+      __syncthreads();
+      wg_outer(DS, IN, DT, DT, sW[1], D, D, D, tid);
+      wg_rowsum(DS, D, sb[1], tid);
+      __syncthreads();
       f32x16 dh[DT];
       mm_acc<DT, DT>(p.WfT[1], dcur, dh);
 #pragma unroll
@@ -986,12 +1035,12 @@ __global__ __launch_bounds__(256) void k_proj_bwd(const KArgs p) {
         for (int r = 0; r < 16; ++r) dcur[t][r] = (h1[t][r] > 0.f) ? dh[t][r] * ks : 0.f;
     }
     // ---- layer 0 (proj.0): input x is lin-perm: IN[s + NS*h][row] = x[s]
-    stage_acc<DT>(DS, dcur, D);
+    stage_acc<DT>(DS, dcur, D, tid);
 #pragma unroll
-    for (int s = 0; s < NS; ++s) IN[(s + NS * h) * RW + w * 32 + c] = x[s];
+    for (int s = 0; s < NS; ++s) IN[(s + NS * ((tid >> 5) & 1)) * RW + (tid >> 6) * 32 + (tid & 31)] = x[s];
     __syncthreads();
-    wg_outer(DS, IN, DT, DT, sW[0], D, D, D);
-    wg_rowsum(DS, D, sb[0]);
+    wg_outer(DS, IN, DT, DT, sW[0], D, D, D, tid);
+    wg_rowsum(DS, D, sb[0], tid);
     __syncthreads();
     {
       f32x16 dxm[DT];
