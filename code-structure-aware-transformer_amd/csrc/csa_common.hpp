@@ -75,15 +75,18 @@ __device__ __forceinline__ void load_run_s(float* dst, const float* __restrict__
 }
 
 // ---------------------------------------------------------------------------------------
-// Philox4x32-10 counter-based RNG (Salmon et al., SC'11): stateless, so forward sampling
-// is reproducible from (seed, offset, element coordinates) on any launch geometry.
+// Philox4x32 counter-based RNG (Salmon et al., SC'11): stateless, so forward sampling is
+// reproducible from (seed, offset, element coordinates) on any launch geometry. 7 rounds: the
+// Random123 paper reports Philox4x32-7 passing TestU01 BigCrush (10 is the conservative default).
 // ---------------------------------------------------------------------------------------
 struct u32x4 { uint32_t x, y, z, w; };
 
-__device__ __forceinline__ u32x4 philox4x32_10(u32x4 ctr, uint32_t k0, uint32_t k1) {
+constexpr int PHILOX_ROUNDS = 7;
+
+__device__ __forceinline__ u32x4 philox4x32(u32x4 ctr, uint32_t k0, uint32_t k1) {
   const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
 #pragma unroll
-  for (int i = 0; i < 10; ++i) {
+  for (int i = 0; i < PHILOX_ROUNDS; ++i) {
     uint32_t hi0 = __umulhi(M0, ctr.x), lo0 = M0 * ctr.x;
     uint32_t hi1 = __umulhi(M1, ctr.z), lo1 = M1 * ctr.z;
     ctr = u32x4{hi1 ^ ctr.y ^ k0, lo1, hi0 ^ ctr.w ^ k1, lo0};

@@ -58,8 +58,9 @@ inline size_t al(size_t x) { return (x + 255) & ~size_t(255); }
 Layout make_layout(int64_t B, int64_t H, int64_t N, int64_t M, int64_t D, int64_t k, bool dense) {
   Layout L;
   L.B = B; L.H = H; L.N = N; L.M = M; L.D = D; L.k = dense ? 0 : k;
-  L.kp = dense ? 0 : ((k + 7) / 8) * 8;
-  L.KT = dense ? 0 : (k + 31) / 32;
+  // kp (stored cluster width) is exactly 2*KPH of the instantiation used: 16, 32, 64 or 128
+  L.kp = dense ? 0 : (k <= 16 ? 16 : k <= 32 ? 32 : k <= 64 ? 64 : 128);
+  L.KT = dense ? 0 : (L.kp <= 32 ? 1 : L.kp / 32);
   L.NQB = (N + 31) / 32; L.NKB = (M + 31) / 32; L.Mpad = L.NKB * 32;
   size_t o = 0;
   auto take = [&](size_t bytes) { size_t r = o; o += al(bytes); return r; };
@@ -118,19 +119,17 @@ __device__ __forceinline__ f32x4 frag4(const float* __restrict__ f, int it, int 
 __global__ __launch_bounds__(256) void k_cluster_softmax(const float* __restrict__ C, float* __restrict__ S,
                                                          int k, int D, int KP32) {
   const int hd = blockIdx.x, tid = threadIdx.x;
-  __shared__ float dist[64 * 64];  // k <= 64
   __shared__ float red[256];
   const float* Ch = C + (size_t)hd * k * D;
   const int kk = k * k;
-  for (int e = tid; e < kk; e += 256) {
+  auto dist = [&](int e) {
     const int a = e / k, b = e % k;
     float acc = 0.f;
     for (int t = 0; t < D; ++t) acc = fmaf(Ch[a * D + t], Ch[b * D + t], acc);
-    dist[e] = acc;
-  }
-  __syncthreads();
+    return acc;
+  };
   float mx = NEG_INF;
-  for (int e = tid; e < kk; e += 256) mx = fmaxf(mx, dist[e]);
+  for (int e = tid; e < kk; e += 256) mx = fmaxf(mx, dist(e));
   red[tid] = mx;
   __syncthreads();
   for (int s = 128; s > 0; s >>= 1) {
@@ -140,7 +139,7 @@ __global__ __launch_bounds__(256) void k_cluster_softmax(const float* __restrict
   mx = red[0];
   __syncthreads();
   float sm = 0.f;
-  for (int e = tid; e < kk; e += 256) sm += expf(dist[e] - mx);
+  for (int e = tid; e < kk; e += 256) sm += expf(dist(e) - mx);
   red[tid] = sm;
   __syncthreads();
   for (int s = 128; s > 0; s >>= 1) {
@@ -151,7 +150,7 @@ __global__ __launch_bounds__(256) void k_cluster_softmax(const float* __restrict
   float* Sh = S + (size_t)hd * KP32 * KP32;
   for (int e = tid; e < KP32 * KP32; e += 256) {
     const int a = e / KP32, b = e % KP32;
-    Sh[e] = (a < k && b < k) ? expf(dist[a * k + b] - mx) / sm : 0.f;
+    Sh[e] = (a < k && b < k) ? expf(dist(a * k + b) - mx) / sm : 0.f;
   }
 }
 
@@ -211,7 +210,7 @@ struct KArgs {
 };
 
 __device__ __forceinline__ f32x4 philox_u4(uint32_t a, uint32_t b, uint32_t c, uint32_t stream, const KArgs& p) {
-  u32x4 r = philox4x32_10(u32x4{a, b, c, (stream << 28) ^ p.off}, p.seed_lo, p.seed_hi);
+  u32x4 r = philox4x32(u32x4{a, b, c, (stream << 28) ^ p.off}, p.seed_lo, p.seed_hi);
   f32x4 o; o[0] = u01(r.x); o[1] = u01(r.y); o[2] = u01(r.z); o[3] = u01(r.w);
   return o;
 }
@@ -641,7 +640,7 @@ __device__ __forceinline__ Elem bwd_elem(float s_raw, float dpp, bool kval, bool
 // B2: per (b,h, query block), S^T orientation: dQ (attention path), dQh, gamma
 // ------------------------------------------------------------------------------------
 template <int D, int KT, bool DENSE>
-__global__ __launch_bounds__(64, (D <= 64 ? 2 : 1)) void k_attn_bwd_q(const KArgs p) {
+__global__ __launch_bounds__(64, (D <= 64 && KT <= 1 ? 2 : 1)) void k_attn_bwd_q(const KArgs p) {
   constexpr int DT = D / 32, NS = D / 2;
   const int lane = lane_id(), c = lane & 31, h = lane >> 5;
   const int qb = blockIdx.x, bh = blockIdx.y, b = bh / p.H, hd = bh % p.H;
@@ -742,7 +741,7 @@ __global__ __launch_bounds__(64, (D <= 64 ? 2 : 1)) void k_attn_bwd_q(const KArg
 // B1: per (b,h, key block), S orientation (queries = acc rows, keys = lanes): dK, dV, dT
 // ------------------------------------------------------------------------------------
 template <int D, int KT, bool DENSE>
-__global__ __launch_bounds__(64, (D <= 64 ? 2 : 1)) void k_attn_bwd_kv(const KArgs p) {
+__global__ __launch_bounds__(64, (D <= 64 && KT <= 1 ? 2 : 1)) void k_attn_bwd_kv(const KArgs p) {
   constexpr int DT = D / 32, NS = D / 2;
   const int lane = lane_id(), c = lane & 31, h = lane >> 5;
   const int kbi = blockIdx.x, bh = blockIdx.y, b = bh / p.H, hd = bh % p.H;
@@ -924,7 +923,7 @@ __device__ __forceinline__ void mm_acc(const float* __restrict__ frag, const f32
 }
 
 template <int D, int KT>
-__global__ __launch_bounds__(256, (D <= 64 ? 2 : 1)) void k_proj_bwd(const KArgs p) {
+__global__ __launch_bounds__(256, (D <= 64 && KT <= 1 ? 2 : 1)) void k_proj_bwd(const KArgs p) {
   using Sh = ProjBwdShape<D, KT>;
   constexpr int DT = Sh::DT, NS = Sh::NS, KP32 = Sh::KP32, ROWS = Sh::ROWS;
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -1111,7 +1110,6 @@ __global__ __launch_bounds__(256) void k_cluster_grad(const float* __restrict__ 
                                                       const float* __restrict__ dC_ws, const float* __restrict__ C,
                                                       float* __restrict__ dC, int k, int D, int KP32) {
   const int hd = blockIdx.x, tid = threadIdx.x;
-  __shared__ float dD[32 * 32 * 4];
   __shared__ float red[256];
   const float* Sh = S + (size_t)hd * KP32 * KP32;
   const float* dSh = dS_ws + (size_t)hd * KP32 * KP32;
@@ -1127,16 +1125,12 @@ __global__ __launch_bounds__(256) void k_cluster_grad(const float* __restrict__ 
     __syncthreads();
   }
   const float dot = red[0];
-  for (int e = tid; e < k * k; e += 256) {
-    const int a = e / k, b = e % k;
-    dD[e] = Sh[a * KP32 + b] * (dSh[a * KP32 + b] - dot);
-  }
-  __syncthreads();
+  auto dD = [&](int a, int b) { return Sh[a * KP32 + b] * (dSh[a * KP32 + b] - dot); };
   const float* Ch = C + (size_t)hd * k * D;
   for (int e = tid; e < k * D; e += 256) {
     const int a = e / D, t = e % D;
     float s = dC_ws[((size_t)hd * KP32 + a) * D + t];
-    for (int b = 0; b < k; ++b) s = fmaf(dD[a * k + b] + dD[b * k + a], Ch[b * D + t], s);
+    for (int b = 0; b < k; ++b) s = fmaf(dD(a, b) + dD(b, a), Ch[b * D + t], s);
     dC[(size_t)hd * k * D + e] = s;
   }
 }
@@ -1184,7 +1178,7 @@ csa_status check_launch(const char* what) {
 bool supported(int64_t d, int64_t k, uint32_t flags) {
   if (d != 64 && d != 96) return false;
   if (flags & CSA_FLAG_DENSE) return true;
-  return k >= 1 && k <= 32;
+  return k >= 1 && k <= (d == 64 ? 128 : 32);  // d=64: cluster sweep up to 128 (BASELINE config 5)
 }
 
 KArgs make_kargs(const csa_sbm_fwd_args* a, const Layout& L) {
@@ -1223,7 +1217,7 @@ csa_status validate_fwd(const csa_sbm_fwd_args* a) {
   const bool dense = a->flags & CSA_FLAG_DENSE;
   if (a->B < 1 || a->H < 1 || a->N < 1 || a->M < 1) return fail(CSA_INVALID_ARG, "B, H, N, M must be >= 1");
   if (!a->Q || !a->K || !a->V || !a->X || !a->state) return fail(CSA_INVALID_ARG, "null Q/K/V/X/state");
-  if (!supported(a->d, a->k, a->flags)) return fail(CSA_UNSUPPORTED_SHAPE, "unsupported (d, k): d in {64,96}, k in [1,32]");
+  if (!supported(a->d, a->k, a->flags)) return fail(CSA_UNSUPPORTED_SHAPE, "unsupported (d, k): d=64 with k in [1,128], or d=96 with k in [1,32]");
   if (!dense) {
     if (!a->cluster_w || !a->sparsity) return fail(CSA_INVALID_ARG, "null cluster_w/sparsity");
     for (int l = 0; l < 3; ++l)
@@ -1379,7 +1373,12 @@ csa_status csa_sbm_fwd(const csa_sbm_fwd_args* a, void* stream) {
   const bool dense = a->flags & CSA_FLAG_DENSE;
   if (a->d == 64) {
     if (dense) return launch_fwd<64, 0, 1>(a, L, st);
-    return L.kp <= 16 ? launch_fwd<64, 8, 1>(a, L, st) : launch_fwd<64, 16, 1>(a, L, st);
+    switch (L.kp) {
+      case 16: return launch_fwd<64, 8, 1>(a, L, st);
+      case 32: return launch_fwd<64, 16, 1>(a, L, st);
+      case 64: return launch_fwd<64, 32, 2>(a, L, st);
+      default: return launch_fwd<64, 64, 4>(a, L, st);
+    }
   }
   if (dense) return launch_fwd<96, 0, 1>(a, L, st);
   return L.kp <= 16 ? launch_fwd<96, 8, 1>(a, L, st) : launch_fwd<96, 16, 1>(a, L, st);
@@ -1417,7 +1416,10 @@ csa_status csa_sbm_bwd(const csa_sbm_bwd_args* b, void* stream) {
     return fail(CSA_INVALID_ARG, "null parameter-gradient output");
   const Layout L = make_layout(a->B, a->H, a->N, a->M, a->d, a->k, dense);
   hipStream_t st = (hipStream_t)stream;
-  if (a->d == 64) return dense ? launch_bwd<64, 0>(b, L, st) : launch_bwd<64, 1>(b, L, st);
+  if (a->d == 64) {
+    if (dense) return launch_bwd<64, 0>(b, L, st);
+    return L.KT == 1 ? launch_bwd<64, 1>(b, L, st) : L.KT == 2 ? launch_bwd<64, 2>(b, L, st) : launch_bwd<64, 4>(b, L, st);
+  }
   return dense ? launch_bwd<96, 0>(b, L, st) : launch_bwd<96, 1>(b, L, st);
 }
 

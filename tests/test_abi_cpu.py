@@ -38,7 +38,8 @@ def test_supported_shapes():
     assert L.csa_sbm_supported(64, 10, 0) and L.csa_sbm_supported(96, 10, 0)
     assert L.csa_sbm_supported(64, 0, _lib.CSA_FLAG_DENSE)
     assert not L.csa_sbm_supported(48, 10, 0)
-    assert not L.csa_sbm_supported(64, 33, 0)
+    assert L.csa_sbm_supported(64, 128, 0) and not L.csa_sbm_supported(64, 129, 0)
+    assert not L.csa_sbm_supported(96, 33, 0)
 
 
 def test_state_and_workspace_sizes_monotone():
