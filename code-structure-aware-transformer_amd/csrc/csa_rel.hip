@@ -144,7 +144,7 @@ __global__ __launch_bounds__(64) void k_rel_fwd(const RelArgs p) {
     }
     tmax = xhalf_max(tmax);
     const float m_new = fmaxf(m_run, tmax);
-    const float alpha = (m_new == NEG_INF) ? 1.f : expf(m_run - m_new);
+    const float alpha = (m_new == NEG_INF) ? 1.f : __expf(m_run - m_new);
     zp *= alpha;
 #pragma unroll
     for (int t = 0; t < DT; ++t)
@@ -153,7 +153,7 @@ __global__ __launch_bounds__(64) void k_rel_fwd(const RelArgs p) {
     float w[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      w[r] = (sv[r] == NEG_INF) ? 0.f : expf(sv[r] - m_new);
+      w[r] = (sv[r] == NEG_INF) ? 0.f : __expf(sv[r] - m_new);
       zp += w[r];
     }
     m_run = m_new;
@@ -243,7 +243,7 @@ __global__ __launch_bounds__(64) void k_rel_bwd_q(const RelArgs p) {
       const float sc = rel_score(p, sacc[r], i, y, rp, mp, c2p, p2ct);
       float P = 0.f, g = 0.f;
       if (sc != NEG_INF) {
-        P = expf(sc - rmax) * rinv;
+        P = __expf(sc - rmax) * rinv;
         const bool masked = mp[(int64_t)i * p.N + y] != 0;
         g = masked ? 0.f : P * (dpacc[r] - delta) * p.inv_scale;
         Gb[(int64_t)i * p.N + y] = g;

@@ -511,7 +511,7 @@ __global__ __launch_bounds__(64) void k_attn_fwd(const KArgs p) {
     // online softmax update
     tmax = xhalf_max(tmax);
     const float m_new = fmaxf(m_run, tmax);
-    const float alpha = (m_new == NEG_INF) ? 1.f : expf(m_run - m_new);
+    const float alpha = (m_new == NEG_INF) ? 1.f : __expf(m_run - m_new);
     zp *= alpha;
     zgp *= alpha;
 #pragma unroll
@@ -520,7 +520,7 @@ __global__ __launch_bounds__(64) void k_attn_fwd(const KArgs p) {
       for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const float e = (sv[r] == NEG_INF) ? 0.f : expf(sv[r] - m_new);
+      const float e = (sv[r] == NEG_INF) ? 0.f : __expf(sv[r] - m_new);
       zp += e;
       const float wa = av[r] ? e : 0.f;
       zgp += wa;
@@ -603,7 +603,7 @@ __global__ __launch_bounds__(64) void k_maps(const KArgs p, float* __restrict__ 
       const int ii = i0 + crow(r, h);
       if (ii < p.N && jv) {
         const bool a = (word >> crow(r, h)) & 1u;
-        const float pv = kval ? expf(sacc[r] * p.scale - lse[r]) : 0.f;
+        const float pv = kval ? __expf(sacc[r] * p.scale - lse[r]) : 0.f;
         const int64_t o = ((int64_t)bh * p.N + ii) * p.M + j;
         if (attn) attn[o] = a ? pv * invD[r] : 0.f;
         if (graph) graph[o] = a ? 1.f : 0.f;
@@ -622,7 +622,7 @@ __device__ __forceinline__ Elem bwd_elem(float s_raw, float dpp, bool kval, bool
                                          float csp, float dgr) {
   Elem r;
   if (!inside) { r.ds = 0.f; r.g = 0.f; r.attw = 0.f; return r; }
-  const float P = kval ? expf(s_raw * scale - lse) : 0.f;
+  const float P = kval ? __expf(s_raw * scale - lse) : 0.f;
   const float rm = keep ? dscale : 0.f;
   const float dattn = dpp * rm;
   const bool mpos = a && (P > 0.f);
