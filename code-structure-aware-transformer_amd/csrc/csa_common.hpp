@@ -101,6 +101,22 @@ __device__ __forceinline__ float u01(uint32_t x) { return (float)(x >> 8) * (1.0
 // Stream ids (Philox counter word 3 high bits) so independent draws never share counters.
 enum : uint32_t { RNG_STE = 1u, RNG_ATTN_DROP = 2u, RNG_PROJ_DROP = 3u };
 
+// XCD-aware block mapping. MI355X dispatches consecutive workgroups round-robin over its 8 XCDs,
+// each with a private L2; the NB blocks of one (b,h) re-read the same K/V (or Q/dX) tiles, so they
+// should share an XCD. Grid = 8 * ceil(BH/8) * NB one-dimensional blocks; block id -> (bh, blk) with
+// bh = 8*(slot / NB) + id % 8, blk = slot % NB, slot = id / 8 (bh >= BH: idle block). Placement only
+// affects speed (guide §1), never results.
+struct BhBlock { int bh, blk; bool valid; };
+__device__ __forceinline__ BhBlock xcd_block(int nb, int BH) {
+  const int id = blockIdx.x, x = id & 7, slot = id >> 3;
+  BhBlock r;
+  r.bh = 8 * (slot / nb) + x;
+  r.blk = slot % nb;
+  r.valid = r.bh < BH;
+  return r;
+}
+inline unsigned xcd_grid(int nb, int BH) { return (unsigned)(8 * ((BH + 7) / 8) * nb); }
+
 // Per-thread last-error text shared by every translation unit (csa_last_error_str).
 void set_error(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
 const char* get_error();

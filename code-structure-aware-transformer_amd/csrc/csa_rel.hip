@@ -113,7 +113,9 @@ template <int D>
 __global__ __launch_bounds__(64) void k_rel_fwd(const RelArgs p) {
   constexpr int DT = (D + 31) / 32, NS = D / 2;
   const int lane = lane_id(), c = lane & 31, h = lane >> 5;
-  const int qb = blockIdx.x, bh = blockIdx.y, b = bh / p.H, hd = bh % p.H;
+  const BhBlock xb = xcd_block(p.NQB, p.B * p.H);
+  if (!xb.valid) return;
+  const int qb = xb.blk, bh = xb.bh, b = bh / p.H, hd = bh % p.H;
   const int i = qb * 32 + c;
   const bool iv = i < p.N;
   float q[NS];
@@ -193,7 +195,9 @@ template <int D>
 __global__ __launch_bounds__(64) void k_rel_bwd_q(const RelArgs p) {
   constexpr int DT = (D + 31) / 32, NS = D / 2;
   const int lane = lane_id(), c = lane & 31, h = lane >> 5;
-  const int qb = blockIdx.x, bh = blockIdx.y, b = bh / p.H, hd = bh % p.H;
+  const BhBlock xb = xcd_block(p.NQB, p.B * p.H);
+  if (!xb.valid) return;
+  const int qb = xb.blk, bh = xb.bh, b = bh / p.H, hd = bh % p.H;
   const int i = qb * 32 + c;
   const bool iv = i < p.N;
   float q[NS], dO[NS];
@@ -424,7 +428,7 @@ csa_status csa_rel_attn_fwd(const csa_rel_attn_args* a, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   rel_logits(a, R, st);
   RelArgs p = make_rel(a, R);
-  const dim3 grid((unsigned)p.NQB, (unsigned)(a->B * a->H));
+  const dim3 grid(xcd_grid(p.NQB, (int)(a->B * a->H)));
   if (a->d == 64) hipLaunchKernelGGL(k_rel_fwd<64>, grid, dim3(64), 0, st, p);
   else if (a->d == 32) hipLaunchKernelGGL(k_rel_fwd<32>, grid, dim3(64), 0, st, p);
   else if (a->d == 16) hipLaunchKernelGGL(k_rel_fwd<16>, grid, dim3(64), 0, st, p);
@@ -449,7 +453,7 @@ csa_status csa_rel_attn_bwd(const csa_rel_attn_bwd_args* b, void* stream) {
   const int B = (int)a->B, H = (int)a->H, N = (int)a->N, L = (int)a->L, D = (int)a->d;
   const int64_t Lp = R.Lp;
   // zero G/P (entries beyond N are never written; the GEMMs read only [0,N))
-  const dim3 grid((unsigned)p.NQB, (unsigned)(B * H));
+  const dim3 grid(xcd_grid(p.NQB, B * H));
   if (D == 64) hipLaunchKernelGGL(k_rel_bwd_q<64>, grid, dim3(64), 0, st, p);
   else if (D == 32) hipLaunchKernelGGL(k_rel_bwd_q<32>, grid, dim3(64), 0, st, p);
   else if (D == 16) hipLaunchKernelGGL(k_rel_bwd_q<16>, grid, dim3(64), 0, st, p);

@@ -412,7 +412,9 @@ template <int D, int KPH, bool DENSE>
 __global__ __launch_bounds__(64) void k_attn_fwd(const KArgs p) {
   constexpr int DT = D / 32, NS = D / 2;
   const int lane = lane_id(), c = lane & 31, h = lane >> 5;
-  const int qb = blockIdx.x, bh = blockIdx.y, b = bh / p.H, hd = bh % p.H;
+  const BhBlock xb = xcd_block(p.NQB, p.B * p.H);
+  if (!xb.valid) return;
+  const int qb = xb.blk, bh = xb.bh, b = bh / p.H, hd = bh % p.H;
   const int i = qb * 32 + c;
   const bool iv = i < p.N;
   float q[NS];
@@ -575,7 +577,9 @@ template <int D, bool DENSE>
 __global__ __launch_bounds__(64) void k_maps(const KArgs p, float* __restrict__ graph, float* __restrict__ attn) {
   constexpr int NS = D / 2;
   const int lane = lane_id(), c = lane & 31, h = lane >> 5;
-  const int qb = blockIdx.x, bh = blockIdx.y, b = bh / p.H, hd = bh % p.H;
+  const BhBlock xb = xcd_block(p.NQB, p.B * p.H);
+  if (!xb.valid) return;
+  const int qb = xb.blk, bh = xb.bh, b = bh / p.H, hd = bh % p.H;
   const int i0 = qb * 32;
   float q[NS];
   load_run<NS>(q, p.Q + b * p.q_sb + hd * p.q_sh + (int64_t)(i0 + c) * p.q_sn + h * NS, i0 + c < p.N);
@@ -643,7 +647,9 @@ template <int D, int KT, bool DENSE>
 __global__ __launch_bounds__(64, (D <= 64 && KT <= 1 ? 2 : 1)) void k_attn_bwd_q(const KArgs p) {
   constexpr int DT = D / 32, NS = D / 2;
   const int lane = lane_id(), c = lane & 31, h = lane >> 5;
-  const int qb = blockIdx.x, bh = blockIdx.y, b = bh / p.H, hd = bh % p.H;
+  const BhBlock xb = xcd_block(p.NQB, p.B * p.H);
+  if (!xb.valid) return;
+  const int qb = xb.blk, bh = xb.bh, b = bh / p.H, hd = bh % p.H;
   const int i = qb * 32 + c;
   const bool iv = i < p.N;
   float q[NS], dx[NS];
@@ -744,7 +750,9 @@ template <int D, int KT, bool DENSE>
 __global__ __launch_bounds__(64, (D <= 64 && KT <= 1 ? 2 : 1)) void k_attn_bwd_kv(const KArgs p) {
   constexpr int DT = D / 32, NS = D / 2;
   const int lane = lane_id(), c = lane & 31, h = lane >> 5;
-  const int kbi = blockIdx.x, bh = blockIdx.y, b = bh / p.H, hd = bh % p.H;
+  const BhBlock xb = xcd_block(p.NKB, p.B * p.H);
+  if (!xb.valid) return;
+  const int kbi = xb.blk, bh = xb.bh, b = bh / p.H, hd = bh % p.H;
   const int j = kbi * 32 + c;
   const bool jv = j < p.M;
   const float* qbase = p.Q + b * p.q_sb + hd * p.q_sh;
@@ -865,6 +873,16 @@ __device__ __forceinline__ void wg_outer(const float* __restrict__ ds, const flo
   const int lane = tid & 63, c = lane & 31, h = lane >> 5, w = tid >> 6;
   for (int tile = w; tile < nto * nti; tile += 4) {
     const int ot = tile / nti, it = tile % nti;
+    const int col = 32 * it + c;
+    // issue the slab reads first: their L2 latency hides under the tile's 64 MFMAs
+    f32x16 old = zero16();
+    if (col < icols) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = 32 * ot + crow(r, h);
+        if (row < orows) old[r] = slab[row * ldo + col];
+      }
+    }
     f32x16 acc = zero16();
     const float* a = ds + (32 * ot + c) * RW + 64 * h;
     const float* bb = in + (32 * it + c) * RW + 64 * h;
@@ -875,12 +893,11 @@ __device__ __forceinline__ void wg_outer(const float* __restrict__ ds, const flo
 #pragma unroll
       for (int e = 0; e < 4; ++e) acc = mfma(av[e], bv[e], acc);
     }
-    const int col = 32 * it + c;
     if (col < icols) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = 32 * ot + crow(r, h);
-        if (row < orows) slab[row * ldo + col] += acc[r];
+        if (row < orows) slab[row * ldo + col] = old[r] + acc[r];
       }
     }
   }
@@ -1273,13 +1290,13 @@ csa_status launch_fwd(const csa_sbm_fwd_args* a, const Layout& L, hipStream_t st
     }
     {
       Stage sg(a->prof, CSA_STAGE_ATTN_FWD, st);
-      hipLaunchKernelGGL((k_attn_fwd<D, KPH, false>), dim3(L.NQB, BH), dim3(64), 0, st, p);
+      hipLaunchKernelGGL((k_attn_fwd<D, KPH, false>), dim3(xcd_grid((int)L.NQB, BH)), dim3(64), 0, st, p);
     }
     hipLaunchKernelGGL(k_sparsity_finish, dim3(1), dim3(64), 0, st, (const unsigned long long*)p.cnt, a->sparsity,
                        (int)a->H, (float)a->B * (float)a->N * (float)a->M);
   } else {
     Stage sg(a->prof, CSA_STAGE_ATTN_FWD, st);
-    hipLaunchKernelGGL((k_attn_fwd<D, 0, true>), dim3(L.NQB, BH), dim3(64), 0, st, p);
+    hipLaunchKernelGGL((k_attn_fwd<D, 0, true>), dim3(xcd_grid((int)L.NQB, BH)), dim3(64), 0, st, p);
   }
   return check_launch("csa_sbm_fwd");
 }
@@ -1301,11 +1318,11 @@ csa_status launch_bwd(const csa_sbm_bwd_args* b, const Layout& L, hipStream_t st
   if constexpr (KT > 0) {
     {
       Stage sg(pf, CSA_STAGE_ATTN_BWD_Q, st);
-      hipLaunchKernelGGL((k_attn_bwd_q<D, KT, false>), dim3(L.NQB, BH), dim3(64), 0, st, p);
+      hipLaunchKernelGGL((k_attn_bwd_q<D, KT, false>), dim3(xcd_grid((int)L.NQB, BH)), dim3(64), 0, st, p);
     }
     {
       Stage sg(pf, CSA_STAGE_ATTN_BWD_KV, st);
-      hipLaunchKernelGGL((k_attn_bwd_kv<D, KT, false>), dim3(L.NKB, BH), dim3(64), 0, st, p);
+      hipLaunchKernelGGL((k_attn_bwd_kv<D, KT, false>), dim3(xcd_grid((int)L.NKB, BH)), dim3(64), 0, st, p);
     }
     if (hipMemsetAsync(p.slab, 0, sizeof(float) * a->H * L.G * L.slab_floats, st) != hipSuccess)
       return check_launch("memset slabs");
@@ -1329,10 +1346,10 @@ csa_status launch_bwd(const csa_sbm_bwd_args* b, const Layout& L, hipStream_t st
   } else {
     {
       Stage sg(pf, CSA_STAGE_ATTN_BWD_Q, st);
-      hipLaunchKernelGGL((k_attn_bwd_q<D, 0, true>), dim3(L.NQB, BH), dim3(64), 0, st, p);
+      hipLaunchKernelGGL((k_attn_bwd_q<D, 0, true>), dim3(xcd_grid((int)L.NQB, BH)), dim3(64), 0, st, p);
     }
     Stage sg(pf, CSA_STAGE_ATTN_BWD_KV, st);
-    hipLaunchKernelGGL((k_attn_bwd_kv<D, 0, true>), dim3(L.NKB, BH), dim3(64), 0, st, p);
+    hipLaunchKernelGGL((k_attn_bwd_kv<D, 0, true>), dim3(xcd_grid((int)L.NKB, BH)), dim3(64), 0, st, p);
   }
   return check_launch("csa_sbm_bwd");
 }
@@ -1392,7 +1409,7 @@ csa_status csa_sbm_maps(const csa_sbm_fwd_args* a, float* graph, float* attn, vo
   const Layout L = make_layout(a->B, a->H, a->N, a->M, a->d, a->k, dense);
   KArgs p = make_kargs(a, L);
   hipStream_t st = (hipStream_t)stream;
-  const dim3 grid((unsigned)L.NQB, (unsigned)(a->B * a->H));
+  const dim3 grid(xcd_grid((int)L.NQB, (int)(a->B * a->H)));
   if (a->d == 64) {
     if (dense) hipLaunchKernelGGL((k_maps<64, true>), grid, dim3(64), 0, st, p, graph, attn);
     else hipLaunchKernelGGL((k_maps<64, false>), grid, dim3(64), 0, st, p, graph, attn);
