@@ -52,20 +52,26 @@ __device__ __forceinline__ float half_sum32(float v) {
   return v;
 }
 
-// Load `n` consecutive floats starting at p into dst[0..n) (n multiple of 4, p 16-B aligned when vec).
+// Load `NV` consecutive floats from p (16-B aligned) into dst, zeroed when !valid.
+// p must ALWAYS be a dereferenceable address (callers clamp the row index): the load is issued
+// unconditionally and only the value is selected. A branch around a load makes hipcc wait
+// vmcnt(0) inside it, serialising every load of a tile (guide §5, trap (c)).
 template <int NV>
 __device__ __forceinline__ void load_run(float* dst, const float* __restrict__ p, bool valid) {
-  if (valid) {
 #pragma unroll
-    for (int i = 0; i < NV; i += 4) {
-      f32x4 v = *reinterpret_cast<const f32x4*>(p + i);
-      dst[i] = v[0]; dst[i + 1] = v[1]; dst[i + 2] = v[2]; dst[i + 3] = v[3];
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < NV; ++i) dst[i] = 0.f;
+  for (int i = 0; i < NV; i += 4) {
+    f32x4 v = *reinterpret_cast<const f32x4*>(p + i);
+    dst[i] = valid ? v[0] : 0.f; dst[i + 1] = valid ? v[1] : 0.f;
+    dst[i + 2] = valid ? v[2] : 0.f; dst[i + 3] = valid ? v[3] : 0.f;
   }
 }
+
+// Unconditional scalar load of p[min(idx, hi)], zeroed when !valid (see load_run).
+__device__ __forceinline__ float ldz(const float* __restrict__ p, int64_t idx, int64_t hi, bool valid) {
+  const float v = p[idx < hi ? idx : hi];
+  return valid ? v : 0.f;
+}
+__device__ __forceinline__ int imin(int a, int b) { return a < b ? a : b; }
 
 // Scalar-load variant (no alignment requirement).
 template <int NV>

@@ -96,14 +96,18 @@ __device__ __forceinline__ int64_t plane_off(const RelArgs& p, int b, int hd, in
 }
 
 // Score of one (x, y) element; returns NEG_INF outside the matrix.
+// All loads are unconditional on clamped indices (a branch around a load serialises the tile's
+// loads behind vmcnt(0), see csa_common.hpp load_run); validity is applied to the value.
 __device__ __forceinline__ float rel_score(const RelArgs& p, float c2c, int x, int y, const uint8_t* rp,
                                            const uint8_t* mp, const float* c2p, const float* p2ct) {
-  if (x >= p.N || y >= p.N) return NEG_INF;
-  int rxy = rp[(int64_t)x * p.N + y], ryx = rp[(int64_t)y * p.N + x];
+  const bool inside = x < p.N && y < p.N;
+  const int xc = imin(x, p.N - 1), yc = imin(y, p.N - 1);
+  int rxy = rp[(int64_t)xc * p.N + yc], ryx = rp[(int64_t)yc * p.N + xc];
   rxy = rxy < p.L ? rxy : p.L - 1;  // memory safety; the reference requires rel < L
   ryx = ryx < p.L ? ryx : p.L - 1;
-  if (mp[(int64_t)x * p.N + y]) return -1e9f;  // masked_fill(mask == 1, -1e9) (disentangled_attn.py:62)
-  return (c2c + c2p[(int64_t)x * p.Lp + rxy] + p2ct[(int64_t)y * p.Lp + ryx]) * p.inv_scale;
+  const bool masked = mp[(int64_t)xc * p.N + yc] != 0;
+  const float v = (c2c + c2p[(int64_t)xc * p.Lp + rxy] + p2ct[(int64_t)yc * p.Lp + ryx]) * p.inv_scale;
+  return !inside ? NEG_INF : masked ? -1e9f : v;  // masked_fill(mask == 1, -1e9) (disentangled_attn.py:62)
 }
 
 // ------------------------------------------------------------------------------------
@@ -118,8 +122,9 @@ __global__ __launch_bounds__(64) void k_rel_fwd(const RelArgs p) {
   const int qb = xb.blk, bh = xb.bh, b = bh / p.H, hd = bh % p.H;
   const int i = qb * 32 + c;
   const bool iv = i < p.N;
+  const int ic = imin(i, p.N - 1);
   float q[NS];
-  load_run<NS>(q, p.q + b * p.q_sb + hd * p.q_sh + (int64_t)i * p.q_sn + h * NS, iv);
+  load_run<NS>(q, p.q + b * p.q_sb + hd * p.q_sh + (int64_t)ic * p.q_sn + h * NS, iv);
   const float* kb = p.k + b * p.k_sb + hd * p.k_sh;
   const float* vb = p.v + b * p.v_sb + hd * p.v_sh;
   const uint8_t* rp = p.rel + plane_off(p, b, hd, p.rel_sb, p.rel_sh);
@@ -133,7 +138,7 @@ __global__ __launch_bounds__(64) void k_rel_fwd(const RelArgs p) {
   for (int kt = 0; kt < p.NKB; ++kt) {
     const int j0 = kt * 32, jl = j0 + c;
     float kr[NS];
-    load_run<NS>(kr, kb + (int64_t)jl * p.k_sn + h * NS, jl < p.N);
+    load_run<NS>(kr, kb + (int64_t)imin(jl, p.N - 1) * p.k_sn + h * NS, jl < p.N);
     f32x16 sacc = zero16();
 #pragma unroll
     for (int s = 0; s < NS; ++s) sacc = mfma(kr[s], q[s], sacc);
@@ -164,7 +169,8 @@ __global__ __launch_bounds__(64) void k_rel_fwd(const RelArgs p) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int j = j0 + crow(r, h);
-        const float vt = (j < p.N && 32 * t + c < D) ? vb[(int64_t)j * p.v_sn + 32 * t + c] : 0.f;
+        const float vt = ldz(vb, (int64_t)imin(j, p.N - 1) * p.v_sn + imin(32 * t + c, D - 1), INT64_MAX,
+                             j < p.N && 32 * t + c < D);
         o[t] = mfma(vt, w[r], o[t]);
       }
   }
@@ -200,19 +206,20 @@ __global__ __launch_bounds__(64) void k_rel_bwd_q(const RelArgs p) {
   const int qb = xb.blk, bh = xb.bh, b = bh / p.H, hd = bh % p.H;
   const int i = qb * 32 + c;
   const bool iv = i < p.N;
+  const int ic = imin(i, p.N - 1);
   float q[NS], dO[NS];
-  load_run<NS>(q, p.q + b * p.q_sb + hd * p.q_sh + (int64_t)i * p.q_sn + h * NS, iv);
-  load_run<NS>(dO, p.dout + ((int64_t)bh * p.N + i) * D + h * NS, iv);
+  load_run<NS>(q, p.q + b * p.q_sb + hd * p.q_sh + (int64_t)ic * p.q_sn + h * NS, iv);
+  load_run<NS>(dO, p.dout + ((int64_t)bh * p.N + ic) * D + h * NS, iv);
   float dp = 0.f;
   {
     float o[NS];
-    load_run<NS>(o, p.out + ((int64_t)bh * p.N + i) * D + h * NS, iv);
+    load_run<NS>(o, p.out + ((int64_t)bh * p.N + ic) * D + h * NS, iv);
 #pragma unroll
     for (int s = 0; s < NS; ++s) dp = fmaf(dO[s], o[s], dp);
   }
   const float delta = xhalf_sum(dp);
-  const float rmax = iv ? p.stats[((int64_t)bh * p.N + i) * 2] : 0.f;
-  const float rinv = iv ? p.stats[((int64_t)bh * p.N + i) * 2 + 1] : 0.f;
+  const float rmax = p.stats[((int64_t)bh * p.N + ic) * 2];
+  const float rinv = p.stats[((int64_t)bh * p.N + ic) * 2 + 1];
   const float* kb = p.k + b * p.k_sb + hd * p.k_sh;
   const float* vb = p.v + b * p.v_sb + hd * p.v_sh;
   const uint8_t* rp = p.rel + plane_off(p, b, hd, p.rel_sb, p.rel_sh);
@@ -227,16 +234,17 @@ __global__ __launch_bounds__(64) void k_rel_bwd_q(const RelArgs p) {
   for (int kt = 0; kt < p.NKB; ++kt) {
     const int j0 = kt * 32, jl = j0 + c;
     const bool jv = jl < p.N;
+    const int jc = imin(jl, p.N - 1);
     f32x16 sacc = zero16(), dpacc = zero16();
     {
       float kr[NS];
-      load_run<NS>(kr, kb + (int64_t)jl * p.k_sn + h * NS, jv);
+      load_run<NS>(kr, kb + (int64_t)jc * p.k_sn + h * NS, jv);
 #pragma unroll
       for (int s = 0; s < NS; ++s) sacc = mfma(kr[s], q[s], sacc);
     }
     {
       float vr[NS];
-      load_run<NS>(vr, vb + (int64_t)jl * p.v_sn + h * NS, jv);
+      load_run<NS>(vr, vb + (int64_t)jc * p.v_sn + h * NS, jv);
 #pragma unroll
       for (int s = 0; s < NS; ++s) dpacc = mfma(vr[s], dO[s], dpacc);
     }
@@ -245,11 +253,11 @@ __global__ __launch_bounds__(64) void k_rel_bwd_q(const RelArgs p) {
     for (int r = 0; r < 16; ++r) {
       const int y = j0 + crow(r, h);
       const float sc = rel_score(p, sacc[r], i, y, rp, mp, c2p, p2ct);
-      float P = 0.f, g = 0.f;
-      if (sc != NEG_INF) {
-        P = __expf(sc - rmax) * rinv;
-        const bool masked = mp[(int64_t)i * p.N + y] != 0;
-        g = masked ? 0.f : P * (dpacc[r] - delta) * p.inv_scale;
+      const bool inside = sc != NEG_INF;
+      const bool masked = mp[(int64_t)ic * p.N + imin(y, p.N - 1)] != 0;
+      const float P = inside ? __expf(sc - rmax) * rinv : 0.f;
+      const float g = (inside && !masked) ? P * (dpacc[r] - delta) * p.inv_scale : 0.f;
+      if (inside) {
         Gb[(int64_t)i * p.N + y] = g;
         Pb[(int64_t)i * p.N + y] = P;
       }
@@ -260,7 +268,8 @@ __global__ __launch_bounds__(64) void k_rel_bwd_q(const RelArgs p) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int j = j0 + crow(r, h);
-        const float kv = (j < p.N && 32 * t + c < D) ? kb[(int64_t)j * p.k_sn + 32 * t + c] : 0.f;
+        const float kv = ldz(kb, (int64_t)imin(j, p.N - 1) * p.k_sn + imin(32 * t + c, D - 1), INT64_MAX,
+                             j < p.N && 32 * t + c < D);
         dq[t] = mfma(kv, gv[r], dq[t]);
       }
   }

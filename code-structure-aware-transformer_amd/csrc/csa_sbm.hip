@@ -366,9 +366,10 @@ __device__ __forceinline__ void load_rows(f32x16 (&a)[NT], const float* __restri
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int c0 = 32 * t + 8 * g + 4 * h;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (valid && c0 < ncols) v = *reinterpret_cast<const f32x4*>(in + c0);
-      a[t][4 * g] = v[0]; a[t][4 * g + 1] = v[1]; a[t][4 * g + 2] = v[2]; a[t][4 * g + 3] = v[3];
+      const bool ok = valid && c0 < ncols;
+      const f32x4 v = *reinterpret_cast<const f32x4*>(in + (c0 < ncols ? c0 : ncols - 4));
+      a[t][4 * g] = ok ? v[0] : 0.f; a[t][4 * g + 1] = ok ? v[1] : 0.f;
+      a[t][4 * g + 2] = ok ? v[2] : 0.f; a[t][4 * g + 3] = ok ? v[3] : 0.f;
     }
 }
 
@@ -385,8 +386,9 @@ __global__ __launch_bounds__(64) void k_proj_fwd(const KArgs p) {
   const int nrows = isK ? p.M : p.N;
   const int row = rb * 32 + c;
   const bool rv = row < nrows;
-  const float* X = isK ? p.K + b * p.k_sb + hd * p.k_sh + (int64_t)row * p.k_sn
-                       : p.Q + b * p.q_sb + hd * p.q_sh + (int64_t)row * p.q_sn;
+  const int rowc = imin(row, nrows - 1);
+  const float* X = isK ? p.K + b * p.k_sb + hd * p.k_sh + (int64_t)rowc * p.k_sn
+                       : p.Q + b * p.q_sb + hd * p.q_sh + (int64_t)rowc * p.q_sn;
   float x[D / 2];
   load_run<D / 2>(x, X + h * (D / 2), rv);
   f32x16 h1[D / 32], h2[D / 32], po[D / 32], hat[KT];
@@ -417,10 +419,11 @@ __global__ __launch_bounds__(64) void k_attn_fwd(const KArgs p) {
   const int qb = xb.blk, bh = xb.bh, b = bh / p.H, hd = bh % p.H;
   const int i = qb * 32 + c;
   const bool iv = i < p.N;
+  const int ic = imin(i, p.N - 1);
   float q[NS];
-  load_run<NS>(q, p.Q + b * p.q_sb + hd * p.q_sh + (int64_t)i * p.q_sn + h * NS, iv);
+  load_run<NS>(q, p.Q + b * p.q_sb + hd * p.q_sh + (int64_t)ic * p.q_sn + h * NS, iv);
   float qh[KPH > 0 ? KPH : 1];
-  if (!DENSE) load_run<KPH>(qh, p.Qh + ((int64_t)bh * p.N + i) * p.kp + h * KPH, iv);
+  if (!DENSE) load_run<KPH>(qh, p.Qh + ((int64_t)bh * p.N + ic) * p.kp + h * KPH, iv);
   const float* kb = p.K + b * p.k_sb + hd * p.k_sh;
   const float* vb = p.V + b * p.v_sb + hd * p.v_sh;
   const float* mk = p.mask ? p.mask + b * p.mask_sb : nullptr;
@@ -435,17 +438,19 @@ __global__ __launch_bounds__(64) void k_attn_fwd(const KArgs p) {
   for (int kt = 0; kt < p.NKB; ++kt) {
     const int j0 = kt * 32, jl = j0 + c;
     const bool jv = jl < p.M;
+    const int jc = imin(jl, p.M - 1);
     float kr[NS];
-    load_run<NS>(kr, kb + (int64_t)jl * p.k_sn + h * NS, jv);
+    load_run<NS>(kr, kb + (int64_t)jc * p.k_sn + h * NS, jv);
     f32x16 sacc = zero16();
 #pragma unroll
     for (int s = 0; s < NS; ++s) sacc = mfma(kr[s], q[s], sacc);
-    const bool kval = jv && (mk == nullptr || mk[jl] == 0.f);
+    const float mval = mk ? mk[jc] : 0.f;
+    const bool kval = jv && mval == 0.f;
     const uint32_t vw = (uint32_t)__ballot(kval);
     f32x16 eacc;
     if (!DENSE) {
       float tr[KPH > 0 ? KPH : 1];
-      load_run<KPH>(tr, p.T + ((int64_t)bh * p.M + jl) * p.kp + h * KPH, jv);
+      load_run<KPH>(tr, p.T + ((int64_t)bh * p.M + jc) * p.kp + h * KPH, jv);
       eacc = zero16();
 #pragma unroll
       for (int s = 0; s < KPH; ++s) eacc = mfma(tr[s], qh[s], eacc);
@@ -466,8 +471,10 @@ __global__ __launch_bounds__(64) void k_attn_fwd(const KArgs p) {
         f32x4 uu;
         if (p.U) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
-            uu[e] = (iv && jg + e < p.M) ? p.U[((int64_t)bh * p.N + i) * p.M + jg + e] : 2.f;
+          for (int e = 0; e < 4; ++e) {
+            const float v = p.U[((int64_t)bh * p.N + ic) * p.M + imin(jg + e, p.M - 1)];
+            uu[e] = (iv && jg + e < p.M) ? v : 2.f;
+          }
         } else {
           uu = philox_u4((uint32_t)i, (uint32_t)(jg >> 2), (uint32_t)bh, RNG_STE, p);
         }
@@ -535,7 +542,7 @@ __global__ __launch_bounds__(64) void k_attn_fwd(const KArgs p) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int j = j0 + crow(r, h);
-        const float vt = (j < p.M) ? vb[(int64_t)j * p.v_sn + 32 * t + c] : 0.f;
+        const float vt = ldz(vb, (int64_t)imin(j, p.M - 1) * p.v_sn + 32 * t + c, INT64_MAX, j < p.M);
         o[t] = mfma(vt, w[r], o[t]);
       }
   }
@@ -582,26 +589,28 @@ __global__ __launch_bounds__(64) void k_maps(const KArgs p, float* __restrict__ 
   const int qb = xb.blk, bh = xb.bh, b = bh / p.H, hd = bh % p.H;
   const int i0 = qb * 32;
   float q[NS];
-  load_run<NS>(q, p.Q + b * p.q_sb + hd * p.q_sh + (int64_t)(i0 + c) * p.q_sn + h * NS, i0 + c < p.N);
+  load_run<NS>(q, p.Q + b * p.q_sb + hd * p.q_sh + (int64_t)imin(i0 + c, p.N - 1) * p.q_sn + h * NS, i0 + c < p.N);
   float lse[16], invD[16];
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
-    const int ii = i0 + crow(r, h);
-    lse[r] = (ii < p.N) ? p.stats[((int64_t)bh * p.N + ii) * 4 + 0] : 0.f;
-    invD[r] = (ii < p.N) ? p.stats[((int64_t)bh * p.N + ii) * 4 + 1] : 0.f;
+    const int ii = imin(i0 + crow(r, h), p.N - 1);
+    lse[r] = p.stats[((int64_t)bh * p.N + ii) * 4 + 0];
+    invD[r] = p.stats[((int64_t)bh * p.N + ii) * 4 + 1];
   }
   const float* kb = p.K + b * p.k_sb + hd * p.k_sh;
   const float* mk = p.mask ? p.mask + b * p.mask_sb : nullptr;
   for (int kt = 0; kt < p.NKB; ++kt) {
     const int j = kt * 32 + c;
     const bool jv = j < p.M;
+    const int jc = imin(j, p.M - 1);
     float kr[NS];
-    load_run<NS>(kr, kb + (int64_t)j * p.k_sn + h * NS, jv);
+    load_run<NS>(kr, kb + (int64_t)jc * p.k_sn + h * NS, jv);
     f32x16 sacc = zero16();
 #pragma unroll
     for (int s = 0; s < NS; ++s) sacc = mfma(q[s], kr[s], sacc);
-    const bool kval = jv && (mk == nullptr || mk[j] == 0.f);
-    const uint32_t word = DENSE ? 0xffffffffu : (jv ? p.Abits[((int64_t)bh * p.NQB + qb) * p.Mpad + j] : 0u);
+    const float mval = mk ? mk[jc] : 0.f;
+    const bool kval = jv && mval == 0.f;
+    const uint32_t word = DENSE ? 0xffffffffu : p.Abits[((int64_t)bh * p.NQB + qb) * p.Mpad + j];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int ii = i0 + crow(r, h);
@@ -652,19 +661,19 @@ __global__ __launch_bounds__(64, (D <= 64 && KT <= 1 ? 2 : 1)) void k_attn_bwd_q
   const int qb = xb.blk, bh = xb.bh, b = bh / p.H, hd = bh % p.H;
   const int i = qb * 32 + c;
   const bool iv = i < p.N;
+  const int ic = imin(i, p.N - 1);
   float q[NS], dx[NS];
-  load_run<NS>(q, p.Q + b * p.q_sb + hd * p.q_sh + (int64_t)i * p.q_sn + h * NS, iv);
-  load_run<NS>(dx, p.dX + ((int64_t)bh * p.N + i) * D + h * NS, iv);
+  load_run<NS>(q, p.Q + b * p.q_sb + hd * p.q_sh + (int64_t)ic * p.q_sn + h * NS, iv);
+  load_run<NS>(dx, p.dX + ((int64_t)bh * p.N + ic) * D + h * NS, iv);
   float gp = 0.f;
   {
     float xr[NS];
-    load_run<NS>(xr, p.X + ((int64_t)bh * p.N + i) * D + h * NS, iv);
+    load_run<NS>(xr, p.X + ((int64_t)bh * p.N + ic) * D + h * NS, iv);
 #pragma unroll
     for (int s = 0; s < NS; ++s) gp = fmaf(dx[s], xr[s], gp);
   }
   const float gamma = xhalf_sum(gp);
-  f32x4 st = {0.f, 0.f, 0.f, 0.f};
-  if (iv) st = *reinterpret_cast<const f32x4*>(p.stats + ((int64_t)bh * p.N + i) * 4);
+  f32x4 st = *reinterpret_cast<const f32x4*>(p.stats + ((int64_t)bh * p.N + ic) * 4);
   if (iv && h == 0) p.stats[((int64_t)bh * p.N + i) * 4 + 3] = gamma;
   const float lse = st[0], invD = st[1], big = st[2];
   const bool drop = p.attn_p > 0.f;
@@ -685,20 +694,22 @@ __global__ __launch_bounds__(64, (D <= 64 && KT <= 1 ? 2 : 1)) void k_attn_bwd_q
     const int c = ln & 31, h = (ln >> 5) & 1;
     const int j0 = kt * 32, jl = j0 + c;
     const bool jv = jl < p.M;
+    const int jc = imin(jl, p.M - 1);
     f32x16 sacc = zero16(), dpacc = zero16();
     {
       float kr[NS];
-      load_run<NS>(kr, kb + (int64_t)jl * p.k_sn + h * NS, jv);
+      load_run<NS>(kr, kb + (int64_t)jc * p.k_sn + h * NS, jv);
 #pragma unroll
       for (int s = 0; s < NS; ++s) sacc = mfma(kr[s], q[s], sacc);
     }
     {
       float vr[NS];
-      load_run<NS>(vr, vb + (int64_t)jl * p.v_sn + h * NS, jv);
+      load_run<NS>(vr, vb + (int64_t)jc * p.v_sn + h * NS, jv);
 #pragma unroll
       for (int s = 0; s < NS; ++s) dpacc = mfma(vr[s], dx[s], dpacc);
     }
-    const bool kval = jv && (mk == nullptr || mk[jl] == 0.f);
+    const float mval = mk ? mk[jc] : 0.f;
+    const bool kval = jv && mval == 0.f;
     const uint32_t vw = (uint32_t)__ballot(kval);
     const int64_t widx = ((int64_t)bh * p.NQB + qb) * p.Mpad + jl;
     const uint32_t wA = DENSE ? 0xffffffffu : p.Abits[widx];
@@ -712,7 +723,7 @@ __global__ __launch_bounds__(64, (D <= 64 && KT <= 1 ? 2 : 1)) void k_attn_bwd_q
       const bool a = (a_w >> c) & 1u;
       const bool keep = (r_w >> c) & 1u;
       const bool inside = iv && (j < p.M);
-      const float dgr = (p.dgraph && inside) ? p.dgraph[((int64_t)bh * p.N + i) * p.M + j] : 0.f;
+      const float dgr = p.dgraph ? ldz(p.dgraph, ((int64_t)bh * p.N + ic) * p.M + imin(j, p.M - 1), INT64_MAX, inside) : 0.f;
       const Elem e = bwd_elem(sacc[r], dpacc[r], (vw >> jj) & 1u, DENSE ? inside : a, keep, inside, lse, invD, big,
                               gamma, p.scale, dscale, csp, dgr);
       dsv[r] = e.ds;
@@ -724,7 +735,7 @@ __global__ __launch_bounds__(64, (D <= 64 && KT <= 1 ? 2 : 1)) void k_attn_bwd_q
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int j = j0 + crow(r, h);
-        const float kv = (j < p.M) ? kb[(int64_t)j * p.k_sn + 32 * t + c] : 0.f;
+        const float kv = ldz(kb, (int64_t)imin(j, p.M - 1) * p.k_sn + 32 * t + c, INT64_MAX, j < p.M);
         dq[t] = mfma(kv, dsv[r], dq[t]);
       }
     if constexpr (!DENSE) {
@@ -734,7 +745,8 @@ __global__ __launch_bounds__(64, (D <= 64 && KT <= 1 ? 2 : 1)) void k_attn_bwd_q
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int j = j0 + crow(r, h), a = 32 * at + c;
-          const float tv = (j < p.M && a < p.kp) ? p.T[((int64_t)bh * p.M + j) * p.kp + a] : 0.f;
+          const float tv = ldz(p.T, ((int64_t)bh * p.M + imin(j, p.M - 1)) * p.kp + imin(a, p.kp - 1), INT64_MAX,
+                               j < p.M && a < p.kp);
           dqh[at] = mfma(tv, gv[r], dqh[at]);
         }
     }
@@ -755,12 +767,14 @@ __global__ __launch_bounds__(64, (D <= 64 && KT <= 1 ? 2 : 1)) void k_attn_bwd_k
   const int kbi = xb.blk, bh = xb.bh, b = bh / p.H, hd = bh % p.H;
   const int j = kbi * 32 + c;
   const bool jv = j < p.M;
+  const int jc = imin(j, p.M - 1);
   const float* qbase = p.Q + b * p.q_sb + hd * p.q_sh;
   const float* mk = p.mask ? p.mask + b * p.mask_sb : nullptr;
-  const bool kval = jv && (mk == nullptr || mk[j] == 0.f);
+  const float mval = mk ? mk[jc] : 0.f;
+  const bool kval = jv && mval == 0.f;
   float kr[NS], vr[NS];
-  load_run<NS>(kr, p.K + b * p.k_sb + hd * p.k_sh + (int64_t)j * p.k_sn + h * NS, jv);
-  load_run<NS>(vr, p.V + b * p.v_sb + hd * p.v_sh + (int64_t)j * p.v_sn + h * NS, jv);
+  load_run<NS>(kr, p.K + b * p.k_sb + hd * p.k_sh + (int64_t)jc * p.k_sn + h * NS, jv);
+  load_run<NS>(vr, p.V + b * p.v_sb + hd * p.v_sh + (int64_t)jc * p.v_sn + h * NS, jv);
   const bool drop = p.attn_p > 0.f;
   const float dscale = drop ? 1.f / (1.f - p.attn_p) : 1.f;
   const float csp = (!DENSE && p.dsp) ? p.dsp[hd] / ((float)p.B * (float)p.N * (float)p.M) : 0.f;
@@ -776,16 +790,17 @@ __global__ __launch_bounds__(64, (D <= 64 && KT <= 1 ? 2 : 1)) void k_attn_bwd_k
     const int c = ln & 31, h = (ln >> 5) & 1;
     const int i0 = qb * 32, il = i0 + c;
     const bool ilv = il < p.N;
+    const int ilc = imin(il, p.N - 1);
     f32x16 sacc = zero16(), dpacc = zero16();
     {
       float qr[NS];
-      load_run<NS>(qr, qbase + (int64_t)il * p.q_sn + h * NS, ilv);
+      load_run<NS>(qr, qbase + (int64_t)ilc * p.q_sn + h * NS, ilv);
 #pragma unroll
       for (int s = 0; s < NS; ++s) sacc = mfma(qr[s], kr[s], sacc);
     }
     {
       float dxr[NS];
-      load_run<NS>(dxr, p.dX + ((int64_t)bh * p.N + il) * D + h * NS, ilv);
+      load_run<NS>(dxr, p.dX + ((int64_t)bh * p.N + ilc) * D + h * NS, ilv);
 #pragma unroll
       for (int s = 0; s < NS; ++s) dpacc = mfma(dxr[s], vr[s], dpacc);
     }
@@ -797,11 +812,11 @@ __global__ __launch_bounds__(64, (D <= 64 && KT <= 1 ? 2 : 1)) void k_attn_bwd_k
     for (int r = 0; r < 16; ++r) {
       const int ii = i0 + crow(r, h);
       const bool inside = (ii < p.N) && jv;
-      f32x4 st = {0.f, 0.f, 0.f, 0.f};
-      if (ii < p.N) st = *reinterpret_cast<const f32x4*>(p.stats + ((int64_t)bh * p.N + ii) * 4);
+      const int iic = imin(ii, p.N - 1);
+      const f32x4 st = *reinterpret_cast<const f32x4*>(p.stats + ((int64_t)bh * p.N + iic) * 4);
       const bool a = DENSE ? inside : ((wA >> crow(r, h)) & 1u);
       const bool keep = (wR >> crow(r, h)) & 1u;
-      const float dgr = (p.dgraph && inside) ? p.dgraph[((int64_t)bh * p.N + ii) * p.M + j] : 0.f;
+      const float dgr = p.dgraph ? ldz(p.dgraph, ((int64_t)bh * p.N + iic) * p.M + jc, INT64_MAX, inside) : 0.f;
       const Elem e = bwd_elem(sacc[r], dpacc[r], kval, a, keep, inside, st[0], st[1], st[2], st[3], p.scale, dscale,
                               csp, dgr);
       dsv[r] = e.ds;
@@ -815,8 +830,9 @@ __global__ __launch_bounds__(64, (D <= 64 && KT <= 1 ? 2 : 1)) void k_attn_bwd_k
       for (int r = 0; r < 16; ++r) {
         const int ii = i0 + crow(r, h);
         const bool v = ii < p.N;
-        const float dxv = v ? p.dX[((int64_t)bh * p.N + ii) * D + 32 * t + c] : 0.f;
-        const float qv = v ? qbase[(int64_t)ii * p.q_sn + 32 * t + c] : 0.f;
+        const int iic = imin(ii, p.N - 1);
+        const float dxv = ldz(p.dX, ((int64_t)bh * p.N + iic) * D + 32 * t + c, INT64_MAX, v);
+        const float qv = ldz(qbase, (int64_t)iic * p.q_sn + 32 * t + c, INT64_MAX, v);
         dv[t] = mfma(dxv, awv[r], dv[t]);
         dk[t] = mfma(qv, dsv[r], dk[t]);
       }
@@ -826,7 +842,8 @@ __global__ __launch_bounds__(64, (D <= 64 && KT <= 1 ? 2 : 1)) void k_attn_bwd_k
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int ii = i0 + crow(r, h), a = 32 * at + c;
-          const float qhv = (ii < p.N && a < p.kp) ? p.Qh[((int64_t)bh * p.N + ii) * p.kp + a] : 0.f;
+          const float qhv = ldz(p.Qh, ((int64_t)bh * p.N + imin(ii, p.N - 1)) * p.kp + imin(a, p.kp - 1), INT64_MAX,
+                                ii < p.N && a < p.kp);
           dtt[at] = mfma(qhv, gv[r], dtt[at]);
         }
     }
@@ -974,9 +991,10 @@ __global__ __launch_bounds__(256, (D <= 64 && KT <= 1 ? 2 : 1)) void k_proj_bwd(
     const int nrows = isK ? p.M : p.N;
     const int row = rb * 32 + c;
     const bool rv = has && row < nrows;
+    const int rowc = imin(row, nrows - 1);
     const int bh = b * p.H + hd;
-    const float* X = isK ? p.K + b * p.k_sb + hd * p.k_sh + (int64_t)row * p.k_sn
-                         : p.Q + b * p.q_sb + hd * p.q_sh + (int64_t)row * p.q_sn;
+    const float* X = isK ? p.K + b * p.k_sb + hd * p.k_sh + (int64_t)rowc * p.k_sn
+                         : p.Q + b * p.q_sb + hd * p.q_sh + (int64_t)rowc * p.q_sn;
     float x[NS];
     load_run<NS>(x, X + h * NS, rv);
     f32x16 h2[DT], po[DT], hat[KT];
@@ -990,7 +1008,7 @@ __global__ __launch_bounds__(256, (D <= 64 && KT <= 1 ? 2 : 1)) void k_proj_bwd(
     cluster_hat<D, KT>(p, po, hat, hd);
     // gradient w.r.t. the sigmoid output
     f32x16 dhat[KT], gin[KT];
-    load_rows<KT>(gin, (isK ? p.dT + ((int64_t)bh * p.M + row) * p.kp : p.dQh + ((int64_t)bh * p.N + row) * p.kp),
+    load_rows<KT>(gin, (isK ? p.dT + ((int64_t)bh * p.M + rowc) * p.kp : p.dQh + ((int64_t)bh * p.N + rowc) * p.kp),
                   p.kp, rv);
     // ---- dS_h += sum_rows dT^T Kh^T  (T_j = S Kh_j) ; K items only
     stage_acc<KT>(DS, gin, isK ? KP32 : 0, tid);
