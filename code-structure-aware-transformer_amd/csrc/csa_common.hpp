@@ -107,6 +107,68 @@ __device__ __forceinline__ float u01(uint32_t x) { return (float)(x >> 8) * (1.0
 // Stream ids (Philox counter word 3 high bits) so independent draws never share counters.
 enum : uint32_t { RNG_STE = 1u, RNG_ATTN_DROP = 2u, RNG_PROJ_DROP = 3u };
 
+// ---------------------------------------------------------------------------------------
+// Wave-private LDS tile images filled by LDS-DMA (buffer_load_dword ... lds: 64 lanes x 4 B per
+// instruction straight into LDS, no VGPR round trip, completion tracked by vmcnt).
+// K/V tiles are stored with a padded row stride of D+4 floats. Both operand read patterns are
+// then conflict-free and reduce to one lane base plus a compile-time offset, so no per-read
+// address registers are needed:
+//   row segments (MFMA A operand, ds_read_b128: 16 lanes = 16 rows) -> 4-bank row skew;
+//   transposed reads (ds_read_b32: 32 lanes = 32 consecutive columns of one row).
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+// Byte offset of a dynamic-LDS pointer (taken once, outside hot loops: the generic->LDS cast
+// carries a null check).
+__device__ __forceinline__ uint32_t lds_offset(const float* p) {
+  return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const float*)p;
+}
+__device__ __forceinline__ lds_ptr_t lds_at(uint32_t off) { return (lds_ptr_t)(uintptr_t)off; }
+
+// Raw buffer resource over [base, base + nbytes).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float* base, int nbytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, nbytes, 0x00020000);
+}
+
+// Rows r0..r0+31 of a row-major fp32 matrix (row stride ld_bytes; rows >= M repeat row M-1,
+// so the image only ever holds real, finite data) into an LDS image at byte offset img with
+// row stride (D+4) floats. One 64-lane dword DMA per 64 columns of a row; the clamped row
+// offset goes in soffset (SGPR), the lane's column in voffset (one VGPR for the whole tile).
+template <int D>
+__device__ __forceinline__ void dma_rows(uint32_t img, __amdgpu_buffer_rsrc_t src, int ld_bytes, int r0, int M) {
+  // opaque per call: otherwise hipcc hoists all 32 (img + const) M0 values out of the caller's
+  // loop and spills them to VGPR lanes
+  asm volatile("" : "+s"(img));
+  const int voff = lane_id() * 4;
+#pragma unroll
+  for (int r = 0; r < 32; ++r) {
+    const int soff = imin(r0 + r, M - 1) * ld_bytes;
+#pragma unroll
+    for (int piece = 0; piece < (D + 63) / 64; ++piece) {
+      const uint32_t dst = img + 4 * (r * (D + 4) + 64 * piece);
+      if (D - 64 * piece >= 64) {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(src, lds_at(dst), 4, voff + 256 * piece, soff, 0, 0);
+      } else if (lane_id() < D - 64 * piece) {  // exec-masked tail piece (D = 96)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(src, lds_at(dst), 4, voff + 256 * piece, soff, 0, 0);
+      }
+    }
+  }
+}
+
+// Rows r0..r0+31 of a contiguous (M, W) row-major matrix into an unpadded image (32*W floats).
+// src must span exactly M rows: rows >= M fall outside the buffer and are not real data.
+template <int W>
+__device__ __forceinline__ void dma_tile_contig(uint32_t img, __amdgpu_buffer_rsrc_t src, int r0) {
+  asm volatile("" : "+s"(img));
+  const int voff = lane_id() * 4 + r0 * W * 4;
+#pragma unroll
+  for (int i = 0; i < W / 2; ++i)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(src, lds_at(img + 256 * i), 4, voff + 256 * i, 0, 0, 0);
+}
+
+// Wait for every outstanding vector-memory op of this wave (incl. LDS-DMA) before reading LDS.
+__device__ __forceinline__ void wait_vm_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 // XCD-aware block mapping. MI355X dispatches consecutive workgroups round-robin over its 8 XCDs,
 // each with a private L2; the NB blocks of one (b,h) re-read the same K/V (or Q/dX) tiles, so they
 // should share an XCD. Grid = 8 * ceil(BH/8) * NB one-dimensional blocks; block id -> (bh, blk) with

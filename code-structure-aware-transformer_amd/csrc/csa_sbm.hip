@@ -411,8 +411,21 @@ __global__ __launch_bounds__(64) void k_proj_fwd(const KArgs p) {
 // which equals F.normalize(softmax(s) * graph, p=1) @ dropout (sbm_attn.py:59-63).
 // ------------------------------------------------------------------------------------
 template <int D, int KPH, bool DENSE>
-__global__ __launch_bounds__(64) void k_attn_fwd(const KArgs p) {
-  constexpr int DT = D / 32, NS = D / 2;
+struct AttnFwdLds {
+  static constexpr int DP = D + 4, KP = 2 * KPH;                  // padded K/V row, T row
+  static constexpr int FLOATS = 2 * 32 * DP + 32 * KP;            // K image, V image, T image
+  static constexpr size_t BYTES = sizeof(float) * FLOATS;
+};
+
+template <int D, int KPH, bool DENSE>
+__global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd(const KArgs p) {
+  using LY = AttnFwdLds<D, KPH, DENSE>;
+  constexpr int DT = D / 32, NS = D / 2, DP = LY::DP, KP = LY::KP;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const float* Kimg = lds;
+  const float* Vimg = lds + 32 * DP;
+  const float* Timg = lds + 64 * DP;
+  const uint32_t Kl = lds_offset(Kimg), Vl = Kl + 4 * 32 * DP, Tl = Kl + 8 * 32 * DP;
   const int lane = lane_id(), c = lane & 31, h = lane >> 5;
   const BhBlock xb = xcd_block(p.NQB, p.B * p.H);
   if (!xb.valid) return;
@@ -420,13 +433,20 @@ __global__ __launch_bounds__(64) void k_attn_fwd(const KArgs p) {
   const int i = qb * 32 + c;
   const bool iv = i < p.N;
   const int ic = imin(i, p.N - 1);
+  const __amdgpu_buffer_rsrc_t kr = make_rsrc(p.K + b * p.k_sb + hd * p.k_sh, 0x7fffffff);
+  const __amdgpu_buffer_rsrc_t vr = make_rsrc(p.V + b * p.v_sb + hd * p.v_sh, 0x7fffffff);
+  const __amdgpu_buffer_rsrc_t tr = make_rsrc(p.T + (int64_t)bh * p.M * p.kp, p.M * p.kp * 4);
+  const int kld = (int)p.k_sn * 4, vld = (int)p.v_sn * 4;
+  const float* mk = p.mask ? p.mask + b * p.mask_sb : nullptr;
+  // tile 0 in flight while the query-side operands load
+  dma_rows<D>(Kl, kr, kld, 0, p.M);
+  dma_rows<D>(Vl, vr, vld, 0, p.M);
+  if constexpr (!DENSE) dma_tile_contig<KP>(Tl, tr, 0);
+  float mnext = mk ? mk[imin(c, p.M - 1)] : 0.f;
   float q[NS];
   load_run<NS>(q, p.Q + b * p.q_sb + hd * p.q_sh + (int64_t)ic * p.q_sn + h * NS, iv);
   float qh[KPH > 0 ? KPH : 1];
   if (!DENSE) load_run<KPH>(qh, p.Qh + ((int64_t)bh * p.N + ic) * p.kp + h * KPH, iv);
-  const float* kb = p.K + b * p.k_sb + hd * p.k_sh;
-  const float* vb = p.V + b * p.v_sb + hd * p.v_sh;
-  const float* mk = p.mask ? p.mask + b * p.mask_sb : nullptr;
   const bool drop = p.attn_p > 0.f;
   const float dscale = drop ? 1.f / (1.f - p.attn_p) : 1.f;
   float m_run = NEG_INF, zp = 0.f, zgp = 0.f;
@@ -438,23 +458,42 @@ __global__ __launch_bounds__(64) void k_attn_fwd(const KArgs p) {
   for (int kt = 0; kt < p.NKB; ++kt) {
     const int j0 = kt * 32, jl = j0 + c;
     const bool jv = jl < p.M;
-    const int jc = imin(jl, p.M - 1);
-    float kr[NS];
-    load_run<NS>(kr, kb + (int64_t)jc * p.k_sn + h * NS, jv);
+    wait_vm_all();  // tile kt's K/V/T images and mask value have landed
+    const float mval = mnext;
+    // S^T = K Q^T : A operand = K rows from the image (row c, lin-perm chunks of half h)
     f32x16 sacc = zero16();
 #pragma unroll
-    for (int s = 0; s < NS; ++s) sacc = mfma(kr[s], q[s], sacc);
-    const float mval = mk ? mk[jc] : 0.f;
-    const bool kval = jv && mval == 0.f;
-    const uint32_t vw = (uint32_t)__ballot(kval);
+    for (int j = 0; j < NS / 4; ++j) {
+      const f32x4 kv = *reinterpret_cast<const f32x4*>(Kimg + c * DP + NS * h + 4 * j);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) sacc = mfma(kv[e], q[4 * j + e], sacc);
+    }
     f32x16 eacc;
-    if (!DENSE) {
-      float tr[KPH > 0 ? KPH : 1];
-      load_run<KPH>(tr, p.T + ((int64_t)bh * p.M + jc) * p.kp + h * KPH, jv);
+    if constexpr (!DENSE) {
       eacc = zero16();
 #pragma unroll
-      for (int s = 0; s < KPH; ++s) eacc = mfma(tr[s], qh[s], eacc);
+      for (int j = 0; j < KPH / 4; ++j) {
+        const f32x4 tv = *reinterpret_cast<const f32x4*>(Timg + c * KP + KPH * h + 4 * j);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) eacc = mfma(tv[e], qh[4 * j + e], eacc);
+      }
     }
+    // V^T operand values for this tile's PV: lane (d = 32t + c) reads V[key crow(r,h)][d]
+    float vt[DT][16];
+#pragma unroll
+    for (int t = 0; t < DT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) vt[t][r] = Vimg[crow(r, h) * DP + 32 * t + c];
+    // all of tile kt is in registers: start tile kt+1's DMA (overlaps the softmax and PV below)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (kt + 1 < p.NKB) {
+      dma_rows<D>(Kl, kr, kld, j0 + 32, p.M);
+      dma_rows<D>(Vl, vr, vld, j0 + 32, p.M);
+      if constexpr (!DENSE) dma_tile_contig<KP>(Tl, tr, j0 + 32);
+      mnext = mk ? mk[imin(jl + 32, p.M - 1)] : 0.f;
+    }
+    const bool kval = jv && mval == 0.f;
+    const uint32_t vw = (uint32_t)__ballot(kval);
     float sv[16], w[16];
     bool av[16], keep[16];
     float tmax = NEG_INF;
@@ -536,15 +575,11 @@ __global__ __launch_bounds__(64) void k_attn_fwd(const KArgs p) {
       w[r] = keep[r] ? wa * dscale : 0.f;
     }
     m_run = m_new;
-    // O^T += V^T W^T   (A = V^T: lane d holds V[key crow(r,h)][d])
+    // O^T += V^T W^T (keys beyond M carry w = 0)
 #pragma unroll
     for (int t = 0; t < DT; ++t)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int j = j0 + crow(r, h);
-        const float vt = ldz(vb, (int64_t)imin(j, p.M - 1) * p.v_sn + 32 * t + c, INT64_MAX, j < p.M);
-        o[t] = mfma(vt, w[r], o[t]);
-      }
+      for (int r = 0; r < 16; ++r) o[t] = mfma(vt[t][r], w[r], o[t]);
   }
   const float Z = xhalf_sum(zp), Zg = xhalf_sum(zgp);
   const float n = Zg / Z;
@@ -1308,13 +1343,15 @@ csa_status launch_fwd(const csa_sbm_fwd_args* a, const Layout& L, hipStream_t st
     }
     {
       Stage sg(a->prof, CSA_STAGE_ATTN_FWD, st);
-      hipLaunchKernelGGL((k_attn_fwd<D, KPH, false>), dim3(xcd_grid((int)L.NQB, BH)), dim3(64), 0, st, p);
+      constexpr size_t lds_bytes = AttnFwdLds<D, KPH, false>::BYTES;
+      hipLaunchKernelGGL((k_attn_fwd<D, KPH, false>), dim3(xcd_grid((int)L.NQB, BH)), dim3(64), lds_bytes, st, p);
     }
     hipLaunchKernelGGL(k_sparsity_finish, dim3(1), dim3(64), 0, st, (const unsigned long long*)p.cnt, a->sparsity,
                        (int)a->H, (float)a->B * (float)a->N * (float)a->M);
   } else {
     Stage sg(a->prof, CSA_STAGE_ATTN_FWD, st);
-    hipLaunchKernelGGL((k_attn_fwd<D, 0, true>), dim3(xcd_grid((int)L.NQB, BH)), dim3(64), 0, st, p);
+    constexpr size_t lds_bytes = AttnFwdLds<D, 0, true>::BYTES;
+    hipLaunchKernelGGL((k_attn_fwd<D, 0, true>), dim3(xcd_grid((int)L.NQB, BH)), dim3(64), lds_bytes, st, p);
   }
   return check_launch("csa_sbm_fwd");
 }
