@@ -166,6 +166,18 @@ __device__ __forceinline__ void dma_tile_contig(uint32_t img, __amdgpu_buffer_rs
     __builtin_amdgcn_raw_ptr_buffer_load_lds(src, lds_at(img + 256 * i), 4, voff + 256 * i, 0, 0, 0);
 }
 
+// Zero an LDS image of NF floats before its first DMA, so rows a DMA leaves
+// untouched (out-of-range rows of dma_tile_contig) hold zeros or earlier finite data, never garbage.
+template <int NF>
+__device__ __forceinline__ void lds_zero(float* img) {
+  static_assert(NF % 4 == 0, "whole f32x4 stores");
+  const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < (NF / 4 + 63) / 64; ++i)
+    if (64 * i + lane_id() < NF / 4) reinterpret_cast<f32x4*>(img)[64 * i + lane_id()] = z;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
 // Wait for every outstanding vector-memory op of this wave (incl. LDS-DMA) before reading LDS.
 __device__ __forceinline__ void wait_vm_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 

@@ -687,9 +687,24 @@ __device__ __forceinline__ Elem bwd_elem(float s_raw, float dpp, bool kval, bool
 // ------------------------------------------------------------------------------------
 // B2: per (b,h, query block), S^T orientation: dQ (attention path), dQh, gamma
 // ------------------------------------------------------------------------------------
-template <int D, int KT, bool DENSE>
-__global__ __launch_bounds__(64, (D <= 64 && KT <= 1 ? 2 : 1)) void k_attn_bwd_q(const KArgs p) {
-  constexpr int DT = D / 32, NS = D / 2;
+template <int D, int KPH>
+struct AttnBwdShape {
+  static constexpr int DP = D + 4, KP = 2 * KPH;
+  static constexpr int KT = KPH == 0 ? 0 : (KP <= 32 ? 1 : KP / 32), KTA = KT > 0 ? KT : 1;
+  // bwd_q images: K, V (padded rows), T; bwd_kv images: Q, dX (padded rows), Qh, stats
+  static constexpr size_t Q_BYTES = sizeof(float) * (2 * 32 * DP + 32 * KP);
+  static constexpr size_t KV_BYTES = sizeof(float) * (2 * 32 * DP + 32 * KP + 32 * 4);
+};
+
+template <int D, int KPH, bool DENSE>
+__global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd_q(const KArgs p) {
+  using SH = AttnBwdShape<D, KPH>;
+  constexpr int DT = D / 32, NS = D / 2, DP = SH::DP, KP = SH::KP, KTA = SH::KTA;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const float* Kimg = lds;
+  const float* Vimg = lds + 32 * DP;
+  const float* Timg = lds + 64 * DP;
+  const uint32_t Kl = lds_offset(Kimg), Vl = Kl + 4 * 32 * DP, Tl = Kl + 8 * 32 * DP;
   const int lane = lane_id(), c = lane & 31, h = lane >> 5;
   const BhBlock xb = xcd_block(p.NQB, p.B * p.H);
   if (!xb.valid) return;
@@ -697,6 +712,21 @@ __global__ __launch_bounds__(64, (D <= 64 && KT <= 1 ? 2 : 1)) void k_attn_bwd_q
   const int i = qb * 32 + c;
   const bool iv = i < p.N;
   const int ic = imin(i, p.N - 1);
+  const __amdgpu_buffer_rsrc_t kr = make_rsrc(p.K + b * p.k_sb + hd * p.k_sh, 0x7fffffff);
+  const __amdgpu_buffer_rsrc_t vr = make_rsrc(p.V + b * p.v_sb + hd * p.v_sh, 0x7fffffff);
+  const __amdgpu_buffer_rsrc_t tr = make_rsrc(DENSE ? p.K : p.T + (int64_t)bh * p.M * p.kp, p.M * p.kp * 4);
+  const int kld = (int)p.k_sn * 4, vld = (int)p.v_sn * 4;
+  // rows past M lie outside tr: zero the T image once so they never hold garbage (NaN * 0)
+  if constexpr (!DENSE) lds_zero<32 * KP>(const_cast<float*>(Timg));
+  dma_rows<D>(Kl, kr, kld, 0, p.M);
+  dma_rows<D>(Vl, vr, vld, 0, p.M);
+  if constexpr (!DENSE) dma_tile_contig<KP>(Tl, tr, 0);
+  const float* mk = p.mask ? p.mask + b * p.mask_sb : nullptr;
+  const bool drop = p.attn_p > 0.f;
+  const int64_t wrow = ((int64_t)bh * p.NQB + qb) * p.Mpad + c;
+  float mnext = mk ? mk[imin(c, p.M - 1)] : 0.f;
+  uint32_t wAn = DENSE ? 0xffffffffu : p.Abits[wrow];
+  uint32_t wRn = drop ? p.Rbits[wrow] : 0xffffffffu;
   float q[NS], dx[NS];
   load_run<NS>(q, p.Q + b * p.q_sb + hd * p.q_sh + (int64_t)ic * p.q_sn + h * NS, iv);
   load_run<NS>(dx, p.dX + ((int64_t)bh * p.N + ic) * D + h * NS, iv);
@@ -711,44 +741,61 @@ __global__ __launch_bounds__(64, (D <= 64 && KT <= 1 ? 2 : 1)) void k_attn_bwd_q
   f32x4 st = *reinterpret_cast<const f32x4*>(p.stats + ((int64_t)bh * p.N + ic) * 4);
   if (iv && h == 0) p.stats[((int64_t)bh * p.N + i) * 4 + 3] = gamma;
   const float lse = st[0], invD = st[1], big = st[2];
-  const bool drop = p.attn_p > 0.f;
   const float dscale = drop ? 1.f / (1.f - p.attn_p) : 1.f;
   const float csp = (!DENSE && p.dsp) ? p.dsp[hd] / ((float)p.B * (float)p.N * (float)p.M) : 0.f;
-  const float* kb = p.K + b * p.k_sb + hd * p.k_sh;
-  const float* vb = p.V + b * p.v_sb + hd * p.v_sh;
-  const float* mk = p.mask ? p.mask + b * p.mask_sb : nullptr;
-  constexpr int KTA = KT > 0 ? KT : 1;
+  const int tcol = imin(c, KP - 1);
   f32x16 dq[DT], dqh[KTA];
 #pragma unroll
   for (int t = 0; t < DT; ++t) dq[t] = zero16();
 #pragma unroll
   for (int t = 0; t < KTA; ++t) dqh[t] = zero16();
   for (int kt = 0; kt < p.NKB; ++kt) {
-    int ln = threadIdx.x;  // opaque per iteration: keeps per-key addresses out of the prologue
+    int ln = threadIdx.x;  // opaque per iteration: keeps the per-row LDS addresses out of the prologue
     asm volatile("" : "+v"(ln));
     const int c = ln & 31, h = (ln >> 5) & 1;
     const int j0 = kt * 32, jl = j0 + c;
-    const bool jv = jl < p.M;
-    const int jc = imin(jl, p.M - 1);
+    wait_vm_all();  // tile kt's K/V/T images and its mask / bit words have landed
+    const float mval = mnext;
+    const uint32_t wA = wAn, wR = wRn;
     f32x16 sacc = zero16(), dpacc = zero16();
-    {
-      float kr[NS];
-      load_run<NS>(kr, kb + (int64_t)jc * p.k_sn + h * NS, jv);
 #pragma unroll
-      for (int s = 0; s < NS; ++s) sacc = mfma(kr[s], q[s], sacc);
-    }
-    {
-      float vr[NS];
-      load_run<NS>(vr, vb + (int64_t)jc * p.v_sn + h * NS, jv);
+    for (int j = 0; j < NS / 4; ++j) {
+      const f32x4 kv = *reinterpret_cast<const f32x4*>(Kimg + c * DP + NS * h + 4 * j);
 #pragma unroll
-      for (int s = 0; s < NS; ++s) dpacc = mfma(vr[s], dx[s], dpacc);
+      for (int e = 0; e < 4; ++e) sacc = mfma(kv[e], q[4 * j + e], sacc);
     }
-    const float mval = mk ? mk[jc] : 0.f;
-    const bool kval = jv && mval == 0.f;
+#pragma unroll
+    for (int j = 0; j < NS / 4; ++j) {
+      const f32x4 vv = *reinterpret_cast<const f32x4*>(Vimg + c * DP + NS * h + 4 * j);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dpacc = mfma(vv[e], dx[4 * j + e], dpacc);
+    }
+    // transposed operands of this tile's dQ / dQh products (lane d holds K[key crow(r,h)][d])
+    float kT[DT][16], tT[KTA][16];
+#pragma unroll
+    for (int t = 0; t < DT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) kT[t][r] = Kimg[crow(r, h) * DP + 32 * t + c];
+    if constexpr (!DENSE) {
+#pragma unroll
+      for (int at = 0; at < KTA; ++at)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float v = Timg[crow(r, h) * KP + (KP >= 32 ? 32 * at + c : tcol)];
+          tT[at][r] = (KP >= 32 || c < KP) ? v : 0.f;
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (kt + 1 < p.NKB) {  // tile kt+1 streams in under the elementwise work and the products below
+      dma_rows<D>(Kl, kr, kld, j0 + 32, p.M);
+      dma_rows<D>(Vl, vr, vld, j0 + 32, p.M);
+      if constexpr (!DENSE) dma_tile_contig<KP>(Tl, tr, j0 + 32);
+      mnext = mk ? mk[imin(jl + 32, p.M - 1)] : 0.f;
+      if constexpr (!DENSE) wAn = p.Abits[wrow + j0 + 32];
+      if (drop) wRn = p.Rbits[wrow + j0 + 32];
+    }
+    const bool kval = jl < p.M && mval == 0.f;
     const uint32_t vw = (uint32_t)__ballot(kval);
-    const int64_t widx = ((int64_t)bh * p.NQB + qb) * p.Mpad + jl;
-    const uint32_t wA = DENSE ? 0xffffffffu : p.Abits[widx];
-    const uint32_t wR = drop ? p.Rbits[widx] : 0xffffffffu;
     float dsv[16], gv[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -764,26 +811,16 @@ __global__ __launch_bounds__(64, (D <= 64 && KT <= 1 ? 2 : 1)) void k_attn_bwd_q
       dsv[r] = e.ds;
       gv[r] = e.g;
     }
-    // dQ^T += K^T ds^T   (A = K^T: lane d holds K[key crow(r,h)][d])
+    // dQ^T += K^T ds^T ; dQh^T += T^T G^T  (keys beyond M carry ds = G = 0)
 #pragma unroll
     for (int t = 0; t < DT; ++t)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int j = j0 + crow(r, h);
-        const float kv = ldz(kb, (int64_t)imin(j, p.M - 1) * p.k_sn + 32 * t + c, INT64_MAX, j < p.M);
-        dq[t] = mfma(kv, dsv[r], dq[t]);
-      }
+      for (int r = 0; r < 16; ++r) dq[t] = mfma(kT[t][r], dsv[r], dq[t]);
     if constexpr (!DENSE) {
-      // dQh^T += T^T G^T
 #pragma unroll
       for (int at = 0; at < KTA; ++at)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int j = j0 + crow(r, h), a = 32 * at + c;
-          const float tv = ldz(p.T, ((int64_t)bh * p.M + imin(j, p.M - 1)) * p.kp + imin(a, p.kp - 1), INT64_MAX,
-                               j < p.M && a < p.kp);
-          dqh[at] = mfma(tv, gv[r], dqh[at]);
-        }
+        for (int r = 0; r < 16; ++r) dqh[at] = mfma(tT[at][r], gv[r], dqh[at]);
     }
   }
   store_rows<DT>(p.dQ + ((int64_t)bh * p.N + i) * D, D, D, dq, iv);
@@ -793,9 +830,16 @@ __global__ __launch_bounds__(64, (D <= 64 && KT <= 1 ? 2 : 1)) void k_attn_bwd_q
 // ------------------------------------------------------------------------------------
 // B1: per (b,h, key block), S orientation (queries = acc rows, keys = lanes): dK, dV, dT
 // ------------------------------------------------------------------------------------
-template <int D, int KT, bool DENSE>
-__global__ __launch_bounds__(64, (D <= 64 && KT <= 1 ? 2 : 1)) void k_attn_bwd_kv(const KArgs p) {
-  constexpr int DT = D / 32, NS = D / 2;
+template <int D, int KPH, bool DENSE>
+__global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd_kv(const KArgs p) {
+  using SH = AttnBwdShape<D, KPH>;
+  constexpr int DT = D / 32, NS = D / 2, DP = SH::DP, KP = SH::KP, KTA = SH::KTA;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const float* Qimg = lds;
+  const float* Ximg = lds + 32 * DP;   // dX rows
+  const float* Himg = lds + 64 * DP;   // Qh rows
+  const float* Simg = lds + 64 * DP + 32 * KP;  // stats rows (lse, 1/D, big, gamma)
+  const uint32_t Ql = lds_offset(Qimg), Xl = Ql + 4 * 32 * DP, Hl = Ql + 8 * 32 * DP, Sl = Hl + 4 * 32 * KP;
   const int lane = lane_id(), c = lane & 31, h = lane >> 5;
   const BhBlock xb = xcd_block(p.NKB, p.B * p.H);
   if (!xb.valid) return;
@@ -803,84 +847,103 @@ __global__ __launch_bounds__(64, (D <= 64 && KT <= 1 ? 2 : 1)) void k_attn_bwd_k
   const int j = kbi * 32 + c;
   const bool jv = j < p.M;
   const int jc = imin(j, p.M - 1);
-  const float* qbase = p.Q + b * p.q_sb + hd * p.q_sh;
+  const __amdgpu_buffer_rsrc_t qr_ = make_rsrc(p.Q + b * p.q_sb + hd * p.q_sh, 0x7fffffff);
+  const __amdgpu_buffer_rsrc_t xr_ = make_rsrc(p.dX + (int64_t)bh * p.N * D, 0x7fffffff);
+  const __amdgpu_buffer_rsrc_t hr_ = make_rsrc(DENSE ? p.dX : p.Qh + (int64_t)bh * p.N * p.kp, p.N * p.kp * 4);
+  const __amdgpu_buffer_rsrc_t sr_ = make_rsrc(p.stats + (int64_t)bh * p.N * 4, p.N * 16);
+  const int qld = (int)p.q_sn * 4;
+  // rows past N lie outside hr_/sr_: zero those images once so they never hold garbage
+  lds_zero<32 * KP + 128>(const_cast<float*>(Himg));
+  dma_rows<D>(Ql, qr_, qld, 0, p.N);
+  dma_rows<D>(Xl, xr_, 4 * D, 0, p.N);
+  if constexpr (!DENSE) dma_tile_contig<KP>(Hl, hr_, 0);
+  dma_tile_contig<4>(Sl, sr_, 0);
+  const bool drop = p.attn_p > 0.f;
+  const int64_t wcol = (int64_t)bh * p.NQB * p.Mpad + j;
+  uint32_t wAn = DENSE ? 0xffffffffu : p.Abits[wcol];
+  uint32_t wRn = drop ? p.Rbits[wcol] : 0xffffffffu;
   const float* mk = p.mask ? p.mask + b * p.mask_sb : nullptr;
   const float mval = mk ? mk[jc] : 0.f;
   const bool kval = jv && mval == 0.f;
   float kr[NS], vr[NS];
   load_run<NS>(kr, p.K + b * p.k_sb + hd * p.k_sh + (int64_t)jc * p.k_sn + h * NS, jv);
   load_run<NS>(vr, p.V + b * p.v_sb + hd * p.v_sh + (int64_t)jc * p.v_sn + h * NS, jv);
-  const bool drop = p.attn_p > 0.f;
   const float dscale = drop ? 1.f / (1.f - p.attn_p) : 1.f;
   const float csp = (!DENSE && p.dsp) ? p.dsp[hd] / ((float)p.B * (float)p.N * (float)p.M) : 0.f;
-  constexpr int KTA = KT > 0 ? KT : 1;
+  const int hcol = imin(c, KP - 1);
   f32x16 dv[DT], dk[DT], dtt[KTA];
 #pragma unroll
   for (int t = 0; t < DT; ++t) { dv[t] = zero16(); dk[t] = zero16(); }
 #pragma unroll
   for (int t = 0; t < KTA; ++t) dtt[t] = zero16();
   for (int qb = 0; qb < p.NQB; ++qb) {
-    int ln = threadIdx.x;  // opaque per iteration: keeps per-row addresses out of the prologue
+    int ln = threadIdx.x;  // opaque per iteration: keeps the per-row LDS addresses out of the prologue
     asm volatile("" : "+v"(ln));
     const int c = ln & 31, h = (ln >> 5) & 1;
-    const int i0 = qb * 32, il = i0 + c;
-    const bool ilv = il < p.N;
-    const int ilc = imin(il, p.N - 1);
+    const int i0 = qb * 32;
+    const bool more = qb + 1 < p.NQB;
+    wait_vm_all();  // query block qb's Q / dX / Qh / stats images and bit words have landed
+    const uint32_t wA = wAn, wR = wRn;
+    if (more) {
+      if constexpr (!DENSE) wAn = p.Abits[wcol + (int64_t)(qb + 1) * p.Mpad];
+      if (drop) wRn = p.Rbits[wcol + (int64_t)(qb + 1) * p.Mpad];
+    }
     f32x16 sacc = zero16(), dpacc = zero16();
-    {
-      float qr[NS];
-      load_run<NS>(qr, qbase + (int64_t)ilc * p.q_sn + h * NS, ilv);
 #pragma unroll
-      for (int s = 0; s < NS; ++s) sacc = mfma(qr[s], kr[s], sacc);
-    }
-    {
-      float dxr[NS];
-      load_run<NS>(dxr, p.dX + ((int64_t)bh * p.N + ilc) * D + h * NS, ilv);
+    for (int s4 = 0; s4 < NS / 4; ++s4) {
+      const f32x4 qv = *reinterpret_cast<const f32x4*>(Qimg + c * DP + NS * h + 4 * s4);
 #pragma unroll
-      for (int s = 0; s < NS; ++s) dpacc = mfma(dxr[s], vr[s], dpacc);
+      for (int e = 0; e < 4; ++e) sacc = mfma(qv[e], kr[4 * s4 + e], sacc);
     }
-    const int64_t widx = ((int64_t)bh * p.NQB + qb) * p.Mpad + j;
-    const uint32_t wA = DENSE ? 0xffffffffu : p.Abits[widx];
-    const uint32_t wR = drop ? p.Rbits[widx] : 0xffffffffu;
+#pragma unroll
+    for (int s4 = 0; s4 < NS / 4; ++s4) {
+      const f32x4 xv = *reinterpret_cast<const f32x4*>(Ximg + c * DP + NS * h + 4 * s4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dpacc = mfma(xv[e], vr[4 * s4 + e], dpacc);
+    }
     float dsv[16], gv[16], awv[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int ii = i0 + crow(r, h);
       const bool inside = (ii < p.N) && jv;
-      const int iic = imin(ii, p.N - 1);
-      const f32x4 st = *reinterpret_cast<const f32x4*>(p.stats + ((int64_t)bh * p.N + iic) * 4);
+      const f32x4 st = *reinterpret_cast<const f32x4*>(Simg + 4 * crow(r, h));
       const bool a = DENSE ? inside : ((wA >> crow(r, h)) & 1u);
       const bool keep = (wR >> crow(r, h)) & 1u;
-      const float dgr = p.dgraph ? ldz(p.dgraph, ((int64_t)bh * p.N + iic) * p.M + jc, INT64_MAX, inside) : 0.f;
+      const float dgr = p.dgraph ? ldz(p.dgraph, ((int64_t)bh * p.N + imin(ii, p.N - 1)) * p.M + jc, INT64_MAX, inside) : 0.f;
       const Elem e = bwd_elem(sacc[r], dpacc[r], kval, a, keep, inside, st[0], st[1], st[2], st[3], p.scale, dscale,
                               csp, dgr);
       dsv[r] = e.ds;
       gv[r] = e.g;
       awv[r] = e.attw;
     }
-    // dV^T += dX^T attw ; dK^T += Q^T ds   (A: lane d holds X[query crow(r,h)][d])
+    // dV^T += dX^T attw  (A: lane d holds dX[query crow(r,h)][d]; queries beyond N carry attw = 0)
 #pragma unroll
     for (int t = 0; t < DT; ++t)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int ii = i0 + crow(r, h);
-        const bool v = ii < p.N;
-        const int iic = imin(ii, p.N - 1);
-        const float dxv = ldz(p.dX, ((int64_t)bh * p.N + iic) * D + 32 * t + c, INT64_MAX, v);
-        const float qv = ldz(qbase, (int64_t)iic * p.q_sn + 32 * t + c, INT64_MAX, v);
-        dv[t] = mfma(dxv, awv[r], dv[t]);
-        dk[t] = mfma(qv, dsv[r], dk[t]);
-      }
+      for (int r = 0; r < 16; ++r) dv[t] = mfma(Ximg[crow(r, h) * DP + 32 * t + c], awv[r], dv[t]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (more) dma_rows<D>(Xl, xr_, 4 * D, i0 + 32, p.N);
+    // dK^T += Q^T ds
+#pragma unroll
+    for (int t = 0; t < DT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dk[t] = mfma(Qimg[crow(r, h) * DP + 32 * t + c], dsv[r], dk[t]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (more) dma_rows<D>(Ql, qr_, qld, i0 + 32, p.N);
+    // dT^T += Qh^T G
     if constexpr (!DENSE) {
 #pragma unroll
       for (int at = 0; at < KTA; ++at)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int ii = i0 + crow(r, h), a = 32 * at + c;
-          const float qhv = ldz(p.Qh, ((int64_t)bh * p.N + imin(ii, p.N - 1)) * p.kp + imin(a, p.kp - 1), INT64_MAX,
-                                ii < p.N && a < p.kp);
-          dtt[at] = mfma(qhv, gv[r], dtt[at]);
+          const float v = Himg[crow(r, h) * KP + (KP >= 32 ? 32 * at + c : hcol)];
+          dtt[at] = mfma((KP >= 32 || c < KP) ? v : 0.f, gv[r], dtt[at]);
         }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (more) {
+      if constexpr (!DENSE) dma_tile_contig<KP>(Hl, hr_, i0 + 32);
+      dma_tile_contig<4>(Sl, sr_, i0 + 32);
     }
   }
   store_rows<DT>(p.dK + ((int64_t)bh * p.M + j) * D, D, D, dk, jv);
@@ -1356,7 +1419,7 @@ csa_status launch_fwd(const csa_sbm_fwd_args* a, const Layout& L, hipStream_t st
   return check_launch("csa_sbm_fwd");
 }
 
-template <int D, int KT>
+template <int D, int KPH, int KT>
 csa_status launch_bwd(const csa_sbm_bwd_args* b, const Layout& L, hipStream_t st) {
   const csa_sbm_fwd_args* a = b->fwd;
   KArgs p = make_kargs(a, L);
@@ -1373,11 +1436,13 @@ csa_status launch_bwd(const csa_sbm_bwd_args* b, const Layout& L, hipStream_t st
   if constexpr (KT > 0) {
     {
       Stage sg(pf, CSA_STAGE_ATTN_BWD_Q, st);
-      hipLaunchKernelGGL((k_attn_bwd_q<D, KT, false>), dim3(xcd_grid((int)L.NQB, BH)), dim3(64), 0, st, p);
+      constexpr size_t lds_bytes = AttnBwdShape<D, KPH>::Q_BYTES;
+      hipLaunchKernelGGL((k_attn_bwd_q<D, KPH, false>), dim3(xcd_grid((int)L.NQB, BH)), dim3(64), lds_bytes, st, p);
     }
     {
       Stage sg(pf, CSA_STAGE_ATTN_BWD_KV, st);
-      hipLaunchKernelGGL((k_attn_bwd_kv<D, KT, false>), dim3(xcd_grid((int)L.NKB, BH)), dim3(64), 0, st, p);
+      constexpr size_t lds_bytes = AttnBwdShape<D, KPH>::KV_BYTES;
+      hipLaunchKernelGGL((k_attn_bwd_kv<D, KPH, false>), dim3(xcd_grid((int)L.NKB, BH)), dim3(64), lds_bytes, st, p);
     }
     if (hipMemsetAsync(p.slab, 0, sizeof(float) * a->H * L.G * L.slab_floats, st) != hipSuccess)
       return check_launch("memset slabs");
@@ -1401,10 +1466,12 @@ csa_status launch_bwd(const csa_sbm_bwd_args* b, const Layout& L, hipStream_t st
   } else {
     {
       Stage sg(pf, CSA_STAGE_ATTN_BWD_Q, st);
-      hipLaunchKernelGGL((k_attn_bwd_q<D, 0, true>), dim3(xcd_grid((int)L.NQB, BH)), dim3(64), 0, st, p);
+      constexpr size_t lds_bytes = AttnBwdShape<D, 0>::Q_BYTES;
+      hipLaunchKernelGGL((k_attn_bwd_q<D, 0, true>), dim3(xcd_grid((int)L.NQB, BH)), dim3(64), lds_bytes, st, p);
     }
     Stage sg(pf, CSA_STAGE_ATTN_BWD_KV, st);
-    hipLaunchKernelGGL((k_attn_bwd_kv<D, 0, true>), dim3(xcd_grid((int)L.NKB, BH)), dim3(64), 0, st, p);
+    constexpr size_t lds_bytes = AttnBwdShape<D, 0>::KV_BYTES;
+    hipLaunchKernelGGL((k_attn_bwd_kv<D, 0, true>), dim3(xcd_grid((int)L.NKB, BH)), dim3(64), lds_bytes, st, p);
   }
   return check_launch("csa_sbm_bwd");
 }
@@ -1489,10 +1556,16 @@ csa_status csa_sbm_bwd(const csa_sbm_bwd_args* b, void* stream) {
   const Layout L = make_layout(a->B, a->H, a->N, a->M, a->d, a->k, dense);
   hipStream_t st = (hipStream_t)stream;
   if (a->d == 64) {
-    if (dense) return launch_bwd<64, 0>(b, L, st);
-    return L.KT == 1 ? launch_bwd<64, 1>(b, L, st) : L.KT == 2 ? launch_bwd<64, 2>(b, L, st) : launch_bwd<64, 4>(b, L, st);
+    if (dense) return launch_bwd<64, 0, 0>(b, L, st);
+    switch (L.kp) {
+      case 16: return launch_bwd<64, 8, 1>(b, L, st);
+      case 32: return launch_bwd<64, 16, 1>(b, L, st);
+      case 64: return launch_bwd<64, 32, 2>(b, L, st);
+      default: return launch_bwd<64, 64, 4>(b, L, st);
+    }
   }
-  return dense ? launch_bwd<96, 0>(b, L, st) : launch_bwd<96, 1>(b, L, st);
+  if (dense) return launch_bwd<96, 0, 0>(b, L, st);
+  return L.kp <= 16 ? launch_bwd<96, 8, 1>(b, L, st) : launch_bwd<96, 16, 1>(b, L, st);
 }
 
 csa_status csa_ste_sample(const float* pr, const float* u, float* A, int64_t n, float lo, float hi, void* stream) {
