@@ -166,6 +166,18 @@ __device__ __forceinline__ void dma_tile_contig(uint32_t img, __amdgpu_buffer_rs
     __builtin_amdgcn_raw_ptr_buffer_load_lds(src, lds_at(img + 256 * i), 4, voff + 256 * i, 0, 0, 0);
 }
 
+// Contiguous NBYTES (multiple of 1 KiB) from src at src_byte_off into LDS at lds_off: one 16-B-per-lane
+// DMA instruction per KiB (buffer_load_dwordx4 ... lds). lds_off and src must be wave-uniform.
+template <int NBYTES>
+__device__ __forceinline__ void dma_block16(uint32_t lds_off, __amdgpu_buffer_rsrc_t src, int src_byte_off) {
+  static_assert(NBYTES % 1024 == 0, "whole 1 KiB pieces");
+  asm volatile("" : "+s"(lds_off));
+  const int voff = lane_id() * 16;
+#pragma unroll
+  for (int i = 0; i < NBYTES / 1024; ++i)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(src, lds_at(lds_off + 1024 * i), 16, voff, src_byte_off + 1024 * i, 0, 0);
+}
+
 // Zero an LDS image of NF floats before its first DMA, so rows a DMA leaves
 // untouched (out-of-range rows of dma_tile_contig) hold zeros or earlier finite data, never garbage.
 template <int NF>

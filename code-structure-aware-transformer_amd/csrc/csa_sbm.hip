@@ -47,7 +47,7 @@ constexpr float NORM_EPS = 1e-12f;  // F.normalize default eps (sbm_attn.py:62)
 // ------------------------------------------------------------------------------------
 struct Layout {
   int64_t B, H, N, M, D, k, kp, KT, NQB, NKB, Mpad;
-  size_t S, Qh, Kh, T, stats, Abits, Rbits, cnt, Wf[3], WfT[3], Cf, CfT, Sf, SfT, total;
+  size_t S, Qh, Kh, T, stats, Abits, Rbits, cnt, Wf[3], WfT[3], Cf, CfT, Sf, SfT, Act, total;
   // bwd workspace
   size_t w_dQh, w_dT, w_slab, w_dS, w_dC, w_total;
   int64_t G, slab_floats;
@@ -79,6 +79,8 @@ Layout make_layout(int64_t B, int64_t H, int64_t N, int64_t M, int64_t D, int64_
   L.CfT = take(sizeof(float) * H * KP32 * D);
   L.Sf = take(sizeof(float) * H * KP32 * KP32);
   L.SfT = take(sizeof(float) * H * KP32 * KP32);
+  // MLP activations of every 32-row item (h1 | h2 | po | hat), saved by k_proj_fwd for k_proj_bwd
+  L.Act = take(sizeof(float) * (dense ? 0 : B * H * (L.NQB + L.NKB) * (3 * D + KP32) * 32));
   L.total = o;
   // backward workspace
   L.G = dense ? 0 : (B < 64 ? B : 64);
@@ -195,7 +197,7 @@ struct KArgs {
   const float* mask; int64_t mask_sb;
   const float* pb[3];  // proj biases
   const float *Wf[3], *WfT[3], *Cf, *CfT, *Sf, *SfT, *S;
-  float *Qh, *Kh, *T, *stats;
+  float *Qh, *Kh, *T, *stats, *Act;
   uint32_t *Abits, *Rbits;
   unsigned long long* cnt;
   const float* U;
@@ -374,6 +376,25 @@ __device__ __forceinline__ void load_rows(f32x16 (&a)[NT], const float* __restri
 }
 
 // ------------------------------------------------------------------------------------
+// Activation blocks. Per 32-row item, k_proj_fwd saves h1 | h2 | po | hat feature-major:
+// feature f is a 128-B row of the 32 data rows, its 16-B chunks XOR-swizzled by (f>>1)&7.
+// k_proj_bwd DMAs these slices unchanged into its LDS staging regions. There the outer-product
+// reads (ds_read_b128 of 4 rows of feature 32t+c, one 16-lane group = 16 consecutive c) are
+// bank-conflict free: lane c lands in 16-B slot (c&1)*8 + (chunk ^ ((c>>1)&7)) of 256 B.
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ int act_off(int f, int row) { return f * 32 + 4 * ((row >> 2) ^ ((f >> 1) & 7)) + (row & 3); }
+
+// accumulator tiles (feature rows 32t + crow(r,h), data row = lane c) -> block slice (features from 0)
+template <int NT>
+__device__ __forceinline__ void store_act(float* __restrict__ blk, const f32x16 (&a)[NT]) {
+  const int lane = lane_id(), c = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) blk[act_off(32 * t + crow(r, h), c)] = a[t][r];
+}
+
+// ------------------------------------------------------------------------------------
 // F2: per 32-row block of Q or K: Qh = sigmoid(MLP(Q) C^T); Kh likewise and T = Kh S^T.
 // grid (NQB + NKB, B*H), one wave per block.
 // ------------------------------------------------------------------------------------
@@ -394,6 +415,14 @@ __global__ __launch_bounds__(64) void k_proj_fwd(const KArgs p) {
   f32x16 h1[D / 32], h2[D / 32], po[D / 32], hat[KT];
   mlp_fwd<D>(p, x, h1, h2, po, row, bh, isK);
   cluster_hat<D, KT>(p, po, hat, hd);
+  {  // save the activations for k_proj_bwd (item blockIdx.x of this (b,h): Q blocks, then K blocks)
+    constexpr int ABLK = (3 * D + 32 * KT) * 32;
+    float* blk = p.Act + ((int64_t)bh * (p.NQB + p.NKB) + blockIdx.x) * ABLK;
+    store_act<D / 32>(blk, h1);
+    store_act<D / 32>(blk + 32 * D, h2);
+    store_act<D / 32>(blk + 64 * D, po);
+    store_act<KT>(blk + 96 * D, hat);
+  }
   if (!isK) {
     store_rows<KT>(p.Qh + ((int64_t)bh * p.N + row) * p.kp, p.kp, p.kp, hat, rv);
   } else {
@@ -953,83 +982,163 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
 
 // ------------------------------------------------------------------------------------
 // B3: projection backward. Workgroup = 4 waves, grid (G, H): head hd, batch chunk g.
-// Each wave takes one 32-row item (Q or K block) at a time; the per-row weight gradients
-// dW = sum_rows dout (x) in are reduced over the WG's 128 rows through an LDS transpose
-// ([feature][row] staging) and an MFMA whose K dimension is the row index; each wave owns
-// a fixed subset of the output tiles and accumulates them into the WG's private slab
-// (plain read-modify-write, no atomics -> deterministic).
+// Each wave takes one 32-row item (Q or K block) per group of 4. Per item the saved activations
+// (k_proj_fwd) replace any forward recompute. Five weight-gradient products
+//   dS_h += dT^T Kh, dC_h += dZ^T po, dW2 += dp^T h2, dW1 += dh2^T h1, dW0 += dh1^T x
+// reduce over the group's 128 rows. Both operands are staged in LDS in the activation-block
+// layout (one 32-row region per wave): DS from the wave's registers, IN by LDS-DMA of the saved
+// block, issued as soon as the region is free so it lands under the chain MFMAs. The output tiles
+// are dealt round-robin to the waves (tile g -> wave g % 4). When they fit (REGACC: <= 4 tiles per
+// wave) each wave accumulates its tiles in registers over all its items and writes its part of
+// the WG's slab exactly once. Otherwise it read-modify-writes the slab once per group. Neither
+// path uses atomics, so the result is deterministic.
 // ------------------------------------------------------------------------------------
-constexpr int RW = 128 + 4;  // staging row stride (floats)
-
 template <int D, int KT>
 struct ProjBwdShape {
   static constexpr int DT = D / 32, NS = D / 2, KP32 = 32 * KT;
-  static constexpr int ROWS = (D > KP32 ? D : KP32);
-  static constexpr size_t LDS_BYTES = sizeof(float) * 2 * ROWS * RW;
+  static constexpr int F = (D > KP32 ? D : KP32);  // feature rows per staging region
+  static constexpr int REG = F * 32;                // floats per wave region
+  static constexpr size_t LDS_BYTES = sizeof(float) * 8 * REG;  // DS regions, then IN regions
+  static constexpr int ABLK = (3 * D + KP32) * 32;  // activation block floats per item
+  // output tiles in stage order dS | dC | dW2 | dW1 | dW0
+  static constexpr int G_S = 0, G_C = KT * KT, G_W2 = G_C + KT * DT, G_W1 = G_W2 + DT * DT, G_W0 = G_W1 + DT * DT,
+                       NTILE = G_W0 + DT * DT;
+  static constexpr int NACC = (NTILE + 3) / 4;
+  static constexpr bool REGACC = NACC <= 4;
 };
 
-// Stage an accumulator tile set (feature rows, data rows on lanes) into LDS[f][wave*32 + c].
+// act_off(32t + crow(r,h), c) split into a lane base and a compile-time offset: for these features
+// (f>>1)&7 = K(r) ^ (h<<1) with K(r) = ((r>>1)&1) | ((r>>2)&1)<<2, so only 4 lane bases exist
+// (K in {0,1,4,5}); the rest, 32*(32t + (r&3) + 8(r>>2)), folds into the ds instruction offset.
+struct AccLanes { int base[4]; };
+__device__ __forceinline__ AccLanes acc_lanes(int lane) {
+  asm volatile("" : "+v"(lane));  // per call: no address survives across helpers
+  const int c = lane & 31, h = lane >> 5, q = (c >> 2) ^ (h << 1);
+  AccLanes L;
+  const int kv[4] = {0, 1, 4, 5};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) L.base[i] = 128 * h + 4 * (q ^ kv[i]) + (c & 3);
+  return L;
+}
+__device__ __forceinline__ constexpr int acc_kidx(int r) { return ((r >> 1) & 1) | (((r >> 2) & 1) << 1); }
+__device__ __forceinline__ constexpr int acc_coff(int t, int r) { return 32 * (32 * t + (r & 3) + 8 * (r >> 2)); }
+
+// acc tiles (feature rows 32t + crow(r,h), data row c) -> own staging region; features >= nvalid are 0
 template <int NT>
-__device__ __forceinline__ void stage_acc(float* __restrict__ buf, const f32x16 (&a)[NT], int nrows_valid, int tid) {
-  const int lane = tid & 63, c = lane & 31, h = lane >> 5, w = tid >> 6;
+__device__ __forceinline__ void stage_ds(float* __restrict__ reg, const f32x16 (&a)[NT], int nvalid, int lane) {
+  const AccLanes L = acc_lanes(lane);
+  const int h = lane >> 5;
 #pragma unroll
   for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int f = 32 * t + crow(r, h);
-      buf[f * RW + w * 32 + c] = (f < nrows_valid) ? a[t][r] : 0.f;
+      reg[L.base[acc_kidx(r)] + acc_coff(t, r)] = (f < nvalid) ? a[t][r] : 0.f;
     }
 }
 
-// C[32ot.., 32it..] (+)= sum over the 128 staged rows of DS[o][row] * IN[i][row]
-// -> RMW into slab (row-major ldo). Tiles (ot, it) for ot < nto, it < nti assigned round-robin to waves.
-__device__ __forceinline__ void wg_outer(const float* __restrict__ ds, const float* __restrict__ in, int nto, int nti,
-                                         float* __restrict__ slab, int ldo, int orows, int icols, int tid) {
-  const int lane = tid & 63, c = lane & 31, h = lane >> 5, w = tid >> 6;
-  for (int tile = w; tile < nto * nti; tile += 4) {
-    const int ot = tile / nti, it = tile % nti;
-    const int col = 32 * it + c;
-    // issue the slab reads first: their L2 latency hides under the tile's 64 MFMAs
-    f32x16 old = zero16();
-    if (col < icols) {
+// own region -> acc tiles (lane c = data row)
+template <int NT>
+__device__ __forceinline__ void read_act(f32x16 (&a)[NT], const float* __restrict__ reg, int lane) {
+  const AccLanes L = acc_lanes(lane);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = 32 * ot + crow(r, h);
-        if (row < orows) old[r] = slab[row * ldo + col];
-      }
-    }
-    f32x16 acc = zero16();
-    const float* a = ds + (32 * ot + c) * RW + 64 * h;
-    const float* bb = in + (32 * it + c) * RW + 64 * h;
-#pragma unroll 4
-    for (int s4 = 0; s4 < 16; ++s4) {
-      const f32x4 av = *reinterpret_cast<const f32x4*>(a + 4 * s4);
-      const f32x4 bv = *reinterpret_cast<const f32x4*>(bb + 4 * s4);
+  for (int t = 0; t < NT; ++t)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) acc = mfma(av[e], bv[e], acc);
-    }
-    if (col < icols) {
+    for (int r = 0; r < 16; ++r) a[t][r] = reg[L.base[acc_kidx(r)] + acc_coff(t, r)];
+}
+
+// acc += sum over the 128 staged rows of DS[32ot + i][row] * IN[32it + j][row]
+// K-step s of half h takes rows 64h + s: region 2h + s/32, chunk (s%32)/4.
+template <int REG>
+__device__ __forceinline__ f32x16 outer_tile(const float* __restrict__ ds, const float* __restrict__ in, int ot, int it,
+                                             f32x16 acc, int lane) {
+  asm volatile("" : "+v"(lane));
+  const int c = lane & 31, h = lane >> 5, sw = (c >> 1) & 7;
+  const float* a = ds + 2 * h * REG + (32 * ot + c) * 32;
+  const float* b = in + 2 * h * REG + (32 * it + c) * 32;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = 32 * ot + crow(r, h);
-        if (row < orows) slab[row * ldo + col] = old[r] + acc[r];
-      }
+  for (int s4 = 0; s4 < 16; ++s4) {
+    const int off = (s4 >> 3) * REG + 4 * ((s4 & 7) ^ sw);
+    const f32x4 av = *reinterpret_cast<const f32x4*>(a + off);
+    const f32x4 bv = *reinterpret_cast<const f32x4*>(b + off);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc = mfma(av[e], bv[e], acc);
+  }
+  return acc;
+}
+
+// feature f's sum over the 128 staged rows (fixed order)
+template <int REG>
+__device__ __forceinline__ float region_rowsum(const float* __restrict__ ds, int f) {
+  asm volatile("" : "+v"(f));
+  float s = 0.f;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    float sw = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(ds + w * REG + act_off(f, 4 * k));
+      sw += (v[0] + v[1]) + (v[2] + v[3]);
     }
+    s += sw;
+  }
+  return s;
+}
+
+// destination of output tile g inside a WG slab
+template <int D, int KT>
+struct TileDst { float* base; int ldo, orows, icols, ot, it; };
+template <int D, int KT>
+__device__ __forceinline__ TileDst<D, KT> tile_dst(float* slab, int g) {
+  using Sh = ProjBwdShape<D, KT>;
+  constexpr int DT = Sh::DT, KP32 = Sh::KP32;
+  float* sC = slab + 3 * D * D + 3 * D;
+  float* sS = sC + KP32 * D;
+  TileDst<D, KT> t;
+  if (g < Sh::G_C) { t.base = sS; t.ldo = KP32; t.orows = KP32; t.icols = KP32; t.ot = g / KT; t.it = g % KT; }
+  else if (g < Sh::G_W2) { const int q = g - Sh::G_C; t.base = sC; t.ldo = D; t.orows = KP32; t.icols = D; t.ot = q / DT; t.it = q % DT; }
+  else {
+    const int l = g < Sh::G_W1 ? 2 : g < Sh::G_W0 ? 1 : 0;
+    const int q = g - (l == 2 ? Sh::G_W2 : l == 1 ? Sh::G_W1 : Sh::G_W0);
+    t.base = slab + l * D * D; t.ldo = D; t.orows = D; t.icols = D; t.ot = q / DT; t.it = q % DT;
+  }
+  return t;
+}
+
+template <int NTILE>
+__device__ __forceinline__ void tile_store(float* __restrict__ base, int ldo, int orows, int icols, int ot, int it,
+                                           const f32x16& v, bool accumulate, int lane) {
+  const int c = lane & 31, h = lane >> 5;
+  const int col = 32 * it + c;
+  if (col >= icols) return;
+  float old[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = 32 * ot + crow(r, h);
+    old[r] = (accumulate && row < orows) ? base[row * ldo + col] : 0.f;
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = 32 * ot + crow(r, h);
+    if (row < orows) base[row * ldo + col] = old[r] + v[r];
   }
 }
 
-// db[f] += sum over the 128 staged rows of DS[f][row]   (threads f < nf)
-__device__ __forceinline__ void wg_rowsum(const float* __restrict__ ds, int nf, float* __restrict__ slab, int tid) {
-  const int t = tid;
-  if (t < nf) {
-    float s = 0.f;
-    const float* a = ds + t * RW;
-#pragma unroll 8
-    for (int r4 = 0; r4 < 32; ++r4) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(a + 4 * r4);
-      s += (v[0] + v[1]) + (v[2] + v[3]);
+// One product stage: tiles g0 .. g0 + nto*nti - 1 (tile g -> wave g % 4)
+template <int D, int KT, int G0, int NTO, int NTI>
+__device__ __forceinline__ void outer_stage(const float* ds, const float* in, f32x16 (&acc)[ProjBwdShape<D, KT>::NACC],
+                                            float* slab, int w, int lane) {
+  using Sh = ProjBwdShape<D, KT>;
+  if constexpr (Sh::REGACC) {
+#pragma unroll
+    for (int g = G0; g < G0 + NTO * NTI; ++g)
+      if ((g & 3) == w) acc[g >> 2] = outer_tile<Sh::REG>(ds, in, (g - G0) / NTI, (g - G0) % NTI, acc[g >> 2], lane);
+  } else {
+    for (int g = G0 + ((w - G0) & 3); g < G0 + NTO * NTI; g += 4) {
+      const f32x16 v = outer_tile<Sh::REG>(ds, in, (g - G0) / NTI, (g - G0) % NTI, zero16(), lane);
+      const TileDst<D, KT> t = tile_dst<D, KT>(slab, g);
+      tile_store<0>(t.base, t.ldo, t.orows, t.icols, t.ot, t.it, v, true, lane);
     }
-    slab[t] += s;
   }
 }
 
@@ -1057,128 +1166,164 @@ __device__ __forceinline__ void mm_acc(const float* __restrict__ frag, const f32
 template <int D, int KT>
 __global__ __launch_bounds__(256, (D <= 64 && KT <= 1 ? 2 : 1)) void k_proj_bwd(const KArgs p) {
   using Sh = ProjBwdShape<D, KT>;
-  constexpr int DT = Sh::DT, NS = Sh::NS, KP32 = Sh::KP32, ROWS = Sh::ROWS;
+  constexpr int DT = Sh::DT, NS = Sh::NS, KP32 = Sh::KP32, REG = Sh::REG, ABLK = Sh::ABLK, NACC = Sh::NACC;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* DS = lds;
-  float* IN = lds + ROWS * RW;
-  const int lane = lane_id(), c = lane & 31, h = lane >> 5, w = threadIdx.x >> 6;
+  float* IN = lds + 4 * REG;
+  const int lane = lane_id(), c = lane & 31, h = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int hd = blockIdx.y, g = blockIdx.x, G = gridDim.x;
   const int b_lo = (int)((int64_t)g * p.B / G), b_hi = (int)((int64_t)(g + 1) * p.B / G);
   const int per_b = p.NQB + p.NKB;
   const int n_items = (b_hi - b_lo) * per_b;
   float* slab = p.slab + ((int64_t)hd * G + g) * p.slab_floats;
-  float* sW[3] = {slab, slab + D * D, slab + 2 * D * D};
-  float* sb[3] = {slab + 3 * D * D, slab + 3 * D * D + D, slab + 3 * D * D + 2 * D};
-  float* sC = slab + 3 * D * D + 3 * D;
-  float* sS = sC + KP32 * D;
   const float ks = p.proj_p > 0.f ? 1.f / (1.f - p.proj_p) : 1.f;
   const float* CfT = p.CfT + (size_t)hd * KP32 * D;
   const float* SfT = p.SfT + (size_t)hd * KP32 * KP32;
+  float* DSw = DS + w * REG;
+  float* INw = IN + w * REG;
+  const uint32_t INl = lds_offset(IN) + 4 * REG * w;
+  f32x16 acc[NACC];
+#pragma unroll
+  for (int i = 0; i < NACC; ++i) acc[i] = zero16();
+  float dbacc[3] = {0.f, 0.f, 0.f};
+
+  // per-wave item of group grp (wave-uniform scalars)
+  struct Item { int b, r, isK, rb, nrows; bool has; };
+  auto item_of = [&](int grp) {
+    Item it;
+    const int item = grp * 4 + w;
+    it.has = item < n_items;
+    it.b = b_lo + (it.has ? item / per_b : 0);
+    it.r = it.has ? item % per_b : 0;
+    it.isK = it.r >= p.NQB;
+    it.rb = it.isK ? it.r - p.NQB : it.r;
+    it.nrows = it.isK ? p.M : p.N;
+    return it;
+  };
+  auto act_rsrc = [&](const Item& it) {
+    return make_rsrc(p.Act + ((int64_t)(it.b * p.H + hd) * per_b + it.r) * ABLK, ABLK * 4);
+  };
+  // group 0's first operands: hat -> IN, dT / dQh -> registers
+  f32x16 gin[KT];
+  {
+    const Item it = item_of(0);
+    dma_block16<KP32 * 128>(INl, act_rsrc(it), 96 * D * 4);
+    const int row = it.rb * 32 + c, rowc = imin(row, it.nrows - 1), bh = it.b * p.H + hd;
+    load_rows<KT>(gin, (it.isK ? p.dT + ((int64_t)bh * p.M + rowc) * p.kp : p.dQh + ((int64_t)bh * p.N + rowc) * p.kp),
+                  p.kp, it.has && row < it.nrows);
+  }
 
   for (int grp = 0; grp * 4 < n_items; ++grp) {
-    // Opaque copy of the thread id: addresses derived from it are recomputed in the loop instead of
-    // ~100 of them being hoisted to kernel entry and pinned in registers for the whole kernel.
-    int tid = threadIdx.x;
+    int tid = threadIdx.x;  // opaque: per-lane addresses are recomputed in the loop, not hoisted
     asm volatile("" : "+v"(tid));
-    const int item = grp * 4 + w;
-    const bool has = item < n_items;
-    const int b = b_lo + (has ? item / per_b : 0);
-    const int r_ = has ? item % per_b : 0;
-    const int isK = r_ >= p.NQB;
-    const int rb = isK ? r_ - p.NQB : r_;
-    const int nrows = isK ? p.M : p.N;
-    const int row = rb * 32 + c;
-    const bool rv = has && row < nrows;
-    const int rowc = imin(row, nrows - 1);
-    const int bh = b * p.H + hd;
-    const float* X = isK ? p.K + b * p.k_sb + hd * p.k_sh + (int64_t)rowc * p.k_sn
-                         : p.Q + b * p.q_sb + hd * p.q_sh + (int64_t)rowc * p.q_sn;
-    float x[NS];
-    load_run<NS>(x, X + h * NS, rv);
-    f32x16 h2[DT], po[DT], hat[KT];
-    {
-      f32x16 h1[DT];
-      mlp_layer0<D>(p, x, h1, row, bh, isK);
-      mlp_layer<D>(p, h1, h2, 1);
-    }
-    mlp_act<D>(p, h2, 1, row, bh, isK);
-    mlp_layer<D>(p, h2, po, 2);
-    cluster_hat<D, KT>(p, po, hat, hd);
-    // gradient w.r.t. the sigmoid output
-    f32x16 dhat[KT], gin[KT];
-    load_rows<KT>(gin, (isK ? p.dT + ((int64_t)bh * p.M + rowc) * p.kp : p.dQh + ((int64_t)bh * p.N + rowc) * p.kp),
-                  p.kp, rv);
-    // ---- dS_h += sum_rows dT^T Kh^T  (T_j = S Kh_j) ; K items only
-    stage_acc<KT>(DS, gin, isK ? KP32 : 0, tid);
-    stage_acc<KT>(IN, hat, isK ? KP32 : 0, tid);
+    const int ln = tid & 63;
+    const Item it = item_of(grp);
+    const int row = it.rb * 32 + c;
+    const bool rv = it.has && row < it.nrows;
+    const int rowc = imin(row, it.nrows - 1);
+    const int bh = it.b * p.H + hd;
+    const __amdgpu_buffer_rsrc_t ar = act_rsrc(it);
+    // ---- dS_h += sum_rows dT^T Kh^T (K items; Q items stage zeros)
+    wait_vm_all();
+    f32x16 hat[KT];
+    read_act<KT>(hat, INw, ln);
+    stage_ds<KT>(DSw, gin, it.isK ? KP32 : 0, ln);
     __syncthreads();
-    wg_outer(DS, IN, KT, KT, sS, KP32, KP32, KP32, tid);
+    outer_stage<D, KT, Sh::G_S, KT, KT>(DS, IN, acc, slab, w, ln);
     __syncthreads();
-    if (isK) {
-      mm_acc<KT, KT>(SfT, gin, dhat);  // dKh^T = S^T dT^T
+    // ---- dC_h += sum_rows dZ^T p^T
+    dma_block16<D * 128>(INl, ar, 64 * D * 4);  // po
+    f32x16 dz[KT];
+    if (it.isK) {
+      mm_acc<KT, KT>(SfT, gin, dz);  // dKh^T = S^T dT^T
     } else {
 #pragma unroll
-      for (int t = 0; t < KT; ++t) dhat[t] = gin[t];
+      for (int t = 0; t < KT; ++t) dz[t] = gin[t];
     }
-    // dZ = dhat * sigmoid'
 #pragma unroll
     for (int t = 0; t < KT; ++t)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) dhat[t][r] = dhat[t][r] * hat[t][r] * (1.f - hat[t][r]);
-    // ---- dC_h += sum_rows dZ^T p^T
-    stage_acc<KT>(DS, dhat, KP32, tid);
-    stage_acc<DT>(IN, po, D, tid);
+      for (int r = 0; r < 16; ++r) dz[t][r] = dz[t][r] * hat[t][r] * (1.f - hat[t][r]);
+    stage_ds<KT>(DSw, dz, KP32, ln);
+    wait_vm_all();
     __syncthreads();
-    wg_outer(DS, IN, KT, DT, sC, D, KP32, D, tid);
+    outer_stage<D, KT, Sh::G_C, KT, DT>(DS, IN, acc, slab, w, ln);
     __syncthreads();
-    // dp^T = C^T dZ^T
-    f32x16 dcur[DT];
-    mm_acc<DT, KT>(CfT, dhat, dcur);
     // ---- layer 2 (proj.6): dW2 += dp^T h2 ; db2 ; dh2 = W2^T dp
-    stage_acc<DT>(DS, dcur, D, tid);
-    stage_acc<DT>(IN, h2, D, tid);
+    dma_block16<D * 128>(INl, ar, 32 * D * 4);  // h2
+    f32x16 dcur[DT];
+    mm_acc<DT, KT>(CfT, dz, dcur);  // dp^T = C^T dZ^T
+    stage_ds<DT>(DSw, dcur, D, ln);
+    wait_vm_all();
     __syncthreads();
-    wg_outer(DS, IN, DT, DT, sW[2], D, D, D, tid);
-    wg_rowsum(DS, D, sb[2], tid);
+    outer_stage<D, KT, Sh::G_W2, DT, DT>(DS, IN, acc, slab, w, ln);
+    if (tid < D) {
+      const float sred = region_rowsum<REG>(DS, tid);
+      if constexpr (Sh::REGACC) dbacc[2] += sred; else slab[3 * D * D + 2 * D + tid] += sred;
+    }
     __syncthreads();
     {
-      f32x16 dh[DT];
+      f32x16 hv[DT], dh[DT];
+      read_act<DT>(hv, INw, ln);  // own h2 (relu mask)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      dma_block16<D * 128>(INl, ar, 0);  // h1
       mm_acc<DT, DT>(p.WfT[2], dcur, dh);
 #pragma unroll
       for (int t = 0; t < DT; ++t)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) dcur[t][r] = (h2[t][r] > 0.f) ? dh[t][r] * ks : 0.f;
+        for (int r = 0; r < 16; ++r) dcur[t][r] = (hv[t][r] > 0.f) ? dh[t][r] * ks : 0.f;
     }
-    // ---- layer 1 (proj.3): recompute h1 from x (cheaper than keeping it live across the backward)
+    // ---- layer 1 (proj.3): dW1 += dh2^T h1 ; db1 ; dh1 = W1^T dh2
+    stage_ds<DT>(DSw, dcur, D, ln);
+    float x[NS];
     {
-      f32x16 h1[DT];
-      mlp_layer0<D>(p, x, h1, row, bh, isK);
-      stage_acc<DT>(DS, dcur, D, tid);
-      stage_acc<DT>(IN, h1, D, tid);
-      __syncthreads();
-      wg_outer(DS, IN, DT, DT, sW[1], D, D, D, tid);
-      wg_rowsum(DS, D, sb[1], tid);
-      __syncthreads();
-      f32x16 dh[DT];
+      const float* X = it.isK ? p.K + it.b * p.k_sb + hd * p.k_sh + (int64_t)rowc * p.k_sn
+                              : p.Q + it.b * p.q_sb + hd * p.q_sh + (int64_t)rowc * p.q_sn;
+      load_run<NS>(x, X + h * NS, rv);
+    }
+    wait_vm_all();
+    __syncthreads();
+    outer_stage<D, KT, Sh::G_W1, DT, DT>(DS, IN, acc, slab, w, ln);
+    if (tid < D) {
+      const float sred = region_rowsum<REG>(DS, tid);
+      if constexpr (Sh::REGACC) dbacc[1] += sred; else slab[3 * D * D + D + tid] += sred;
+    }
+    __syncthreads();
+    {
+      f32x16 hv[DT], dh[DT];
+      read_act<DT>(hv, INw, ln);  // own h1 (relu mask)
+      // layer 0 input x (lin-perm rows) -> own IN region, feature s + NS*h
+#pragma unroll
+      for (int s = 0; s < NS; ++s) INw[act_off(s + NS * h, c)] = x[s];
       mm_acc<DT, DT>(p.WfT[1], dcur, dh);
 #pragma unroll
       for (int t = 0; t < DT; ++t)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) dcur[t][r] = (h1[t][r] > 0.f) ? dh[t][r] * ks : 0.f;
+        for (int r = 0; r < 16; ++r) dcur[t][r] = (hv[t][r] > 0.f) ? dh[t][r] * ks : 0.f;
     }
-    // ---- layer 0 (proj.0): input x is lin-perm: IN[s + NS*h][row] = x[s]
-    stage_acc<DT>(DS, dcur, D, tid);
-#pragma unroll
-    for (int s = 0; s < NS; ++s) IN[(s + NS * ((tid >> 5) & 1)) * RW + (tid >> 6) * 32 + (tid & 31)] = x[s];
+    // ---- layer 0 (proj.0): dW0 += dh1^T x ; db0
+    stage_ds<DT>(DSw, dcur, D, ln);
     __syncthreads();
-    wg_outer(DS, IN, DT, DT, sW[0], D, D, D, tid);
-    wg_rowsum(DS, D, sb[0], tid);
+    outer_stage<D, KT, Sh::G_W0, DT, DT>(DS, IN, acc, slab, w, ln);
+    if (tid < D) {
+      const float sred = region_rowsum<REG>(DS, tid);
+      if constexpr (Sh::REGACC) dbacc[0] += sred; else slab[3 * D * D + tid] += sred;
+    }
     __syncthreads();
+    // next group's hat / dT operands stream in under the dx chain
+    if ((grp + 1) * 4 < n_items) {
+      const Item nx = item_of(grp + 1);
+      dma_block16<KP32 * 128>(INl, act_rsrc(nx), 96 * D * 4);
+      const int nrow = nx.rb * 32 + c, nrowc = imin(nrow, nx.nrows - 1), nbh = nx.b * p.H + hd;
+      load_rows<KT>(gin, (nx.isK ? p.dT + ((int64_t)nbh * p.M + nrowc) * p.kp : p.dQh + ((int64_t)nbh * p.N + nrowc) * p.kp),
+                    p.kp, nx.has && nrow < nx.nrows);
+    }
     {
       f32x16 dxm[DT];
       mm_acc<DT, DT>(p.WfT[0], dcur, dxm);
       if (rv) {  // second-path gradient: dQ/dK += MLP backward
-        float* dst = isK ? p.dK + ((int64_t)bh * p.M + row) * D : p.dQ + ((int64_t)bh * p.N + row) * D;
+        float* dst = it.isK ? p.dK + ((int64_t)bh * p.M + row) * D : p.dQ + ((int64_t)bh * p.N + row) * D;
 #pragma unroll
         for (int t = 0; t < DT; ++t)
 #pragma unroll
@@ -1192,23 +1337,69 @@ __global__ __launch_bounds__(256, (D <= 64 && KT <= 1 ? 2 : 1)) void k_proj_bwd(
       }
     }
   }
+  if constexpr (Sh::REGACC) {  // this wave's tiles and (wave 0/1) bias sums: written exactly once
+#pragma unroll
+    for (int gt = 0; gt < Sh::NTILE; ++gt)
+      if ((gt & 3) == w) {
+        const TileDst<D, KT> t = tile_dst<D, KT>(slab, gt);
+        tile_store<0>(t.base, t.ldo, t.orows, t.icols, t.ot, t.it, acc[gt >> 2], false, lane);
+      }
+    const int tid = threadIdx.x;
+    if (tid < D) {
+      slab[3 * D * D + tid] = dbacc[0];
+      slab[3 * D * D + D + tid] = dbacc[1];
+      slab[3 * D * D + 2 * D + tid] = dbacc[2];
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------
 // B4: fixed-order reduction of the partial slabs
-//   out dW, db (sum over H x G slabs); dS_h (sum over G) -> workspace
+//   out dW, db (sum over H x G slabs); dC_h, dS_h (sum over the head's G slabs) -> workspace
+// One workgroup per 64 consecutive outputs: lane l owns output e0 + l, wave w sums the slabs
+// w, w+4, w+8, ... with 8 independent accumulators (8 loads in flight per lane, each wave load a
+// coalesced 256 B row of one slab), then the 4 wave partials are combined in a fixed order.
+// The summation order depends only on (H, G), never on timing -> bitwise deterministic.
 // ------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_reduce_slabs(const KArgs p, int D, int KP32, float* __restrict__ dW0,
                                                       float* __restrict__ dW1, float* __restrict__ dW2,
                                                       float* __restrict__ db0, float* __restrict__ db1,
                                                       float* __restrict__ db2, float* __restrict__ dS_ws,
                                                       float* __restrict__ dC_ws) {
-  const int64_t nW = 3LL * D * D + 3LL * D;
-  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  __shared__ float red[4][64];
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t e = (int64_t)blockIdx.x * 64 + l;
   const int G = p.G;
+  const int64_t nW = 3LL * D * D + 3LL * D;
+  const int64_t nC = (int64_t)p.H * KP32 * D, nS = (int64_t)p.H * KP32 * KP32;
+  int64_t off = 0;
+  int s0 = 0, ns = 0;
   if (e < nW) {
-    float s = 0.f;
-    for (int hg = 0; hg < p.H * G; ++hg) s += p.slab[(int64_t)hg * p.slab_floats + e];
+    off = e; s0 = 0; ns = p.H * G;
+  } else if (e < nW + nC) {
+    const int64_t f = e - nW;
+    off = nW + f % (KP32 * D); s0 = (int)(f / (KP32 * D)) * G; ns = G;
+  } else if (e < nW + nC + nS) {
+    const int64_t f = e - nW - nC;
+    off = nW + (int64_t)KP32 * D + f % (KP32 * KP32); s0 = (int)(f / (KP32 * KP32)) * G; ns = G;
+  }
+  const float* src = p.slab + (int64_t)s0 * p.slab_floats + off;
+  float acc[8];
+#pragma unroll
+  for (int a = 0; a < 8; ++a) acc[a] = 0.f;
+  int i = w;
+  for (; i + 28 < ns; i += 32) {
+#pragma unroll
+    for (int a = 0; a < 8; ++a) acc[a] += src[(int64_t)(i + 4 * a) * p.slab_floats];
+  }
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+    if (i + 4 * a < ns) acc[a] += src[(int64_t)(i + 4 * a) * p.slab_floats];
+  red[w][l] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  __syncthreads();
+  if (w != 0 || ns == 0) return;
+  const float s = (red[0][l] + red[1][l]) + (red[2][l] + red[3][l]);
+  if (e < nW) {
     const int64_t DD = (int64_t)D * D;
     if (e < DD) dW0[e] = s;
     else if (e < 2 * DD) dW1[e - DD] = s;
@@ -1216,25 +1407,10 @@ __global__ __launch_bounds__(256) void k_reduce_slabs(const KArgs p, int D, int 
     else if (e < 3 * DD + D) db0[e - 3 * DD] = s;
     else if (e < 3 * DD + 2 * D) db1[e - 3 * DD - D] = s;
     else db2[e - 3 * DD - 2 * D] = s;
-    return;
-  }
-  const int64_t nC = (int64_t)p.H * KP32 * D, nS = (int64_t)p.H * KP32 * KP32;
-  int64_t f = e - nW;
-  if (f < nC) {
-    const int hd = (int)(f / (KP32 * D));
-    const int64_t off = 3LL * D * D + 3LL * D + f % (KP32 * D);
-    float s = 0.f;
-    for (int gg = 0; gg < G; ++gg) s += p.slab[((int64_t)hd * G + gg) * p.slab_floats + off];
-    dC_ws[f] = s;
-    return;
-  }
-  f -= nC;
-  if (f < nS) {
-    const int hd = (int)(f / (KP32 * KP32));
-    const int64_t off = 3LL * D * D + 3LL * D + (int64_t)KP32 * D + f % (KP32 * KP32);
-    float s = 0.f;
-    for (int gg = 0; gg < G; ++gg) s += p.slab[((int64_t)hd * G + gg) * p.slab_floats + off];
-    dS_ws[f] = s;
+  } else if (e < nW + nC) {
+    dC_ws[e - nW] = s;
+  } else {
+    dS_ws[e - nW - nC] = s;
   }
 }
 
@@ -1335,6 +1511,7 @@ KArgs make_kargs(const csa_sbm_fwd_args* a, const Layout& L) {
   p.S = (const float*)((char*)st + L.S);
   p.Qh = (float*)((char*)st + L.Qh); p.Kh = (float*)((char*)st + L.Kh); p.T = (float*)((char*)st + L.T);
   p.stats = (float*)((char*)st + L.stats);
+  p.Act = (float*)((char*)st + L.Act);
   p.Abits = (uint32_t*)((char*)st + L.Abits); p.Rbits = (uint32_t*)((char*)st + L.Rbits);
   p.cnt = (unsigned long long*)((char*)st + L.cnt);
   p.U = a->uniforms;
@@ -1444,9 +1621,9 @@ csa_status launch_bwd(const csa_sbm_bwd_args* b, const Layout& L, hipStream_t st
       constexpr size_t lds_bytes = AttnBwdShape<D, KPH>::KV_BYTES;
       hipLaunchKernelGGL((k_attn_bwd_kv<D, KPH, false>), dim3(xcd_grid((int)L.NKB, BH)), dim3(64), lds_bytes, st, p);
     }
-    if (hipMemsetAsync(p.slab, 0, sizeof(float) * a->H * L.G * L.slab_floats, st) != hipSuccess)
-      return check_launch("memset slabs");
     using Sh = ProjBwdShape<D, KT>;
+    if (!Sh::REGACC && hipMemsetAsync(p.slab, 0, sizeof(float) * a->H * L.G * L.slab_floats, st) != hipSuccess)
+      return check_launch("memset slabs");
     (void)hipFuncSetAttribute((const void*)k_proj_bwd<D, KT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)Sh::LDS_BYTES);
     {
@@ -1458,7 +1635,7 @@ csa_status launch_bwd(const csa_sbm_bwd_args* b, const Layout& L, hipStream_t st
     float* dS_ws = (float*)((char*)b->workspace + L.w_dS);
     float* dC_ws = (float*)((char*)b->workspace + L.w_dC);
     const int64_t total = 3LL * D * D + 3LL * D + (int64_t)a->H * KP32 * D + (int64_t)a->H * KP32 * KP32;
-    hipLaunchKernelGGL(k_reduce_slabs, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, p, D, KP32,
+    hipLaunchKernelGGL(k_reduce_slabs, dim3((unsigned)((total + 63) / 64)), dim3(256), 0, st, p, D, KP32,
                        b->dproj_w[0], b->dproj_w[1], b->dproj_w[2], b->dproj_b[0], b->dproj_b[1], b->dproj_b[2],
                        dS_ws, dC_ws);
     hipLaunchKernelGGL(k_cluster_grad, dim3(a->H), dim3(256), 0, st, p.S, (const float*)dS_ws,
