@@ -22,13 +22,15 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <utility>
+
 namespace csa {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
-__device__ __forceinline__ int crow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+__host__ __device__ __forceinline__ constexpr int crow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
 __device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 acc) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
@@ -140,9 +142,12 @@ __device__ __forceinline__ void dma_rows(uint32_t img, __amdgpu_buffer_rsrc_t sr
   // loop and spills them to VGPR lanes
   asm volatile("" : "+s"(img));
   const int voff = lane_id() * 4;
+  const int smax = (M - 1) * ld_bytes;
+  int soff = imin(r0, M - 1) * ld_bytes;
 #pragma unroll
   for (int r = 0; r < 32; ++r) {
-    const int soff = imin(r0 + r, M - 1) * ld_bytes;
+    // running row offset, opaque per row: computed right before its DMA instead of all 32 up front
+    asm volatile("" : "+s"(soff));
 #pragma unroll
     for (int piece = 0; piece < (D + 63) / 64; ++piece) {
       const uint32_t dst = img + 4 * (r * (D + 4) + 64 * piece);
@@ -152,6 +157,7 @@ __device__ __forceinline__ void dma_rows(uint32_t img, __amdgpu_buffer_rsrc_t sr
         __builtin_amdgcn_raw_ptr_buffer_load_lds(src, lds_at(dst), 4, voff + 256 * piece, soff, 0, 0);
       }
     }
+    soff = imin(soff + ld_bytes, smax);
   }
 }
 
@@ -192,6 +198,16 @@ __device__ __forceinline__ void lds_zero(float* img) {
 
 // Wait for every outstanding vector-memory op of this wave (incl. LDS-DMA) before reading LDS.
 __device__ __forceinline__ void wait_vm_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// v_writelane_b32: dst[LANE] = val (val wave-uniform), other lanes unchanged. The lane is an
+// immediate: an SGPR lane index plus an SGPR value would read the constant bus twice. The s_nop
+// covers the VALU-writes-SGPR -> VALU-reads-SGPR hazard (val is typically a v_cmp ballot issued
+// right before): the hazard recognizer does not look inside inline asm.
+template <int LANE>
+__device__ __forceinline__ uint32_t writelane(uint32_t dst, uint32_t val) {
+  asm("s_nop 4\n\tv_writelane_b32 %0, %1, %2" : "+v"(dst) : "s"(val), "n"(LANE));
+  return dst;
+}
 
 // XCD-aware block mapping. MI355X dispatches consecutive workgroups round-robin over its 8 XCDs,
 // each with a private L2; the NB blocks of one (b,h) re-read the same K/V (or Q/dX) tiles, so they

@@ -211,6 +211,12 @@ struct KArgs {
   int G; int64_t slab_floats;
 };
 
+__device__ __forceinline__ f32x4 philox_u4k(uint32_t a, uint32_t b, uint32_t c, uint32_t stream, uint32_t off,
+                                           uint32_t k0, uint32_t k1) {
+  u32x4 r = philox4x32(u32x4{a, b, c, (stream << 28) ^ off}, k0, k1);
+  f32x4 o; o[0] = u01(r.x); o[1] = u01(r.y); o[2] = u01(r.z); o[3] = u01(r.w);
+  return o;
+}
 __device__ __forceinline__ f32x4 philox_u4(uint32_t a, uint32_t b, uint32_t c, uint32_t stream, const KArgs& p) {
   u32x4 r = philox4x32(u32x4{a, b, c, (stream << 28) ^ p.off}, p.seed_lo, p.seed_hi);
   f32x4 o; o[0] = u01(r.x); o[1] = u01(r.y); o[2] = u01(r.z); o[3] = u01(r.w);
@@ -439,6 +445,31 @@ __global__ __launch_bounds__(64) void k_proj_fwd(const KArgs p) {
 //   Z = sum e, Zg = sum e*A; X = (sum e*A*r V) / (Z * max(Zg/Z, 1e-12))
 // which equals F.normalize(softmax(s) * graph, p=1) @ dropout (sbm_attn.py:59-63).
 // ------------------------------------------------------------------------------------
+// Bit-pack one tile's sampled graph / keep mask: ballot r holds key crow(r,0)'s 32 query bits in its
+// low word and key crow(r,1)'s in its high word; v_writelane drops each word into its key's lane
+// (no per-lane masks or selects).
+template <int R>
+__device__ __forceinline__ void pack_ballot(const bool (&av)[16], const bool (&keep)[16], bool doA, bool doR,
+                                            uint32_t& myA, uint32_t& myR, unsigned long long& cnt) {
+  if (doA) {
+    const unsigned long long bal = __ballot(av[R]);
+    cnt += __popcll(bal);
+    myA = writelane<crow(R, 0)>(myA, (uint32_t)bal);
+    myA = writelane<crow(R, 1)>(myA, (uint32_t)(bal >> 32));
+  }
+  if (doR) {
+    const unsigned long long bal = __ballot(keep[R]);
+    myR = writelane<crow(R, 0)>(myR, (uint32_t)bal);
+    myR = writelane<crow(R, 1)>(myR, (uint32_t)(bal >> 32));
+  }
+}
+template <bool DOA, int... Rs>
+__device__ __forceinline__ void pack_ballots(std::integer_sequence<int, Rs...>, const bool (&av)[16],
+                                             const bool (&keep)[16], bool doR, uint32_t& myA, uint32_t& myR,
+                                             unsigned long long& cnt) {
+  (pack_ballot<Rs>(av, keep, DOA, doR, myA, myR, cnt), ...);
+}
+
 template <int D, int KPH, bool DENSE>
 struct AttnFwdLds {
   static constexpr int DP = D + 4, KP = 2 * KPH;                  // padded K/V row, T row
@@ -523,6 +554,8 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd
     }
     const bool kval = jv && mval == 0.f;
     const uint32_t vw = (uint32_t)__ballot(kval);
+    uint32_t sk0 = p.seed_lo, sk1 = p.seed_hi;  // opaque per tile: round keys are not held across the loop
+    asm volatile("" : "+s"(sk0), "+s"(sk1));
     float sv[16], w[16];
     bool av[16], keep[16];
     float tmax = NEG_INF;
@@ -544,7 +577,7 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd
             uu[e] = (iv && jg + e < p.M) ? v : 2.f;
           }
         } else {
-          uu = philox_u4((uint32_t)i, (uint32_t)(jg >> 2), (uint32_t)bh, RNG_STE, p);
+          uu = philox_u4k((uint32_t)i, (uint32_t)(jg >> 2), (uint32_t)bh, RNG_STE, p.off, sk0, sk1);
         }
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -556,7 +589,7 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd
         for (int e = 0; e < 4; ++e) av[4 * g + e] = iv && (jg + e < p.M);
       }
       if (drop) {
-        const f32x4 ud = philox_u4((uint32_t)i, (uint32_t)(jg >> 2), (uint32_t)bh, RNG_ATTN_DROP, p);
+        const f32x4 ud = philox_u4k((uint32_t)i, (uint32_t)(jg >> 2), (uint32_t)bh, RNG_ATTN_DROP, p.off, sk0, sk1);
 #pragma unroll
         for (int e = 0; e < 4; ++e) keep[4 * g + e] = ud[e] >= p.attn_p;
       } else {
@@ -567,23 +600,10 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd
     // bit-pack the sampled graph / dropout keep mask: word [qb][key] holds 32 query bits
     if (!DENSE || drop) {
       uint32_t myA = 0, myR = 0;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        if (!DENSE) {
-          const unsigned long long bal = __ballot(av[r]);
-          cnt += __popcll(bal);
-          myA |= (c == crow(r, 0)) ? (uint32_t)bal : 0u;
-          myA |= (c == crow(r, 1)) ? (uint32_t)(bal >> 32) : 0u;
-        }
-        if (drop) {
-          const unsigned long long bal = __ballot(keep[r]);
-          myR |= (c == crow(r, 0)) ? (uint32_t)bal : 0u;
-          myR |= (c == crow(r, 1)) ? (uint32_t)(bal >> 32) : 0u;
-        }
-      }
+      pack_ballots<!DENSE>(std::make_integer_sequence<int, 16>{}, av, keep, drop, myA, myR, cnt);
       const int64_t widx = ((int64_t)bh * p.NQB + qb) * p.Mpad + j0 + c;
-      if (!DENSE && h == 0) p.Abits[widx] = myA;
-      if (drop && h == 1) p.Rbits[widx] = myR;
+      if (!DENSE && h == 0) p.Abits[widx] = myA;  // the packed words live in lanes 0..31
+      if (drop && h == 0) p.Rbits[widx] = myR;
     }
     // online softmax update
     tmax = xhalf_max(tmax);
