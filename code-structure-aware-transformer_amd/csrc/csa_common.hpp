@@ -184,6 +184,78 @@ __device__ __forceinline__ void dma_block16(uint32_t lds_off, __amdgpu_buffer_rs
     __builtin_amdgcn_raw_ptr_buffer_load_lds(src, lds_at(lds_off + 1024 * i), 16, voff, src_byte_off + 1024 * i, 0, 0);
 }
 
+// ---------------------------------------------------------------------------------------
+// Unpadded 32 x 64 fp32 tile images (8 KiB) filled by 8 x buffer_load_dwordx4 ... lds (1 KiB each).
+// An x4 DMA writes 1 KiB contiguously, so bank conflicts are avoided by a per-row XOR swizzle of the
+// 16-B chunks instead of row padding: LDS chunk p of row r holds logical chunk p ^ swz(r).
+//   SW_ROW: swz = r & 15         row-segment reads (16 lanes = 16 rows, same logical chunk) are
+//                                conflict-free; a lane's 8 chunks of one half sit at base ^ (16 j).
+//   SW_COL: swz = 8 * bit2(r)    column reads (lanes = 32 consecutive columns of rows R and R + 4)
+//                                are conflict-free and reduce to two lane bases + immediate offsets.
+// Instruction q covers rows 4q..4q+3: lane i -> row 4q + i/16, LDS chunk i%16. The source offset
+// carries the whole row offset in voffset, so rows >= M fall outside the buffer range given by the
+// descriptor (never outside the allocation) and do not load real data; callers zero the image once.
+// ---------------------------------------------------------------------------------------
+enum { SW_ROW = 1, SW_COL = 2 };
+__host__ __device__ constexpr int swz(int sw, int row) { return sw == SW_ROW ? (row & 15) : 8 * ((row >> 2) & 1); }
+
+// Per-lane DMA source patterns (q mod 4 for SW_ROW, q mod 2 for SW_COL). The swizzle kind is a plain
+// argument (callers pass a constant and the helpers are inlined): templated versions of these
+// helpers lost their host-side kernel stubs under hipcc 7.2.
+struct DmaPat { int v[4]; };
+__device__ __forceinline__ DmaPat dma_pat(const int sw, int ld_bytes) {
+  DmaPat P;
+  const int i = lane_id(), s = i >> 4;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) P.v[q] = s * ld_bytes + 16 * ((i & 15) ^ swz(sw, 4 * q + s));
+  return P;
+}
+// Rows row0..row0+31 of a row-major (ld_bytes) fp32 matrix with 64 columns -> swizzled image at img.
+__device__ __forceinline__ void dma64(uint32_t img, __amdgpu_buffer_rsrc_t src, const DmaPat& P, int ld_bytes, int row0) {
+  asm volatile("" : "+s"(img));
+  int rowoff = row0 * ld_bytes;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    asm volatile("" : "+s"(rowoff));
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(src, lds_at(img + 1024 * q), 16, P.v[q & 3] + rowoff, 0, 0, 0);
+    rowoff += 4 * ld_bytes;
+  }
+}
+// SW_ROW image: byte address of logical chunk (8h + j) of row c is row_base ^ (16 j), j < 8.
+__device__ __forceinline__ int row_base64(int c, int h) { return 256 * c + 16 * ((8 * h) ^ (c & 15)); }
+// SW_COL image: element (crow(r,h), 32t + c) is at col_base64(t) + 256 * crow(r, 0).
+__device__ __forceinline__ int col_base64(int t, int c, int h) { return 1024 * h + 128 * (t ^ h) + 4 * c; }
+
+// Narrow row images (32 rows x KP floats, KP in {16,32,64,128}) of a contiguous (rows, KP) matrix:
+// chunk p of row r holds logical chunk p ^ nsw(r), which makes 16-lane row reads conflict-free.
+template <int KP>
+__device__ __forceinline__ int nsw(int row) {
+  return KP == 16 ? ((row >> 2) & 3) : KP == 32 ? ((row >> 1) & 7) : (row & 15);
+}
+// (KP is a plain argument: every caller passes a compile-time constant and the call is inlined.)
+__device__ __forceinline__ void dma_narrow(uint32_t img, __amdgpu_buffer_rsrc_t src, int row0, const int KP) {
+  const int CPR = KP / 4, RB = KP * 4;
+  asm volatile("" : "+s"(img));
+  const int i = lane_id();
+#pragma unroll
+  for (int q = 0; q < KP / 8; ++q) {
+    const int byte = 1024 * q + 16 * i, row = byte / RB, p = (byte / 16) % CPR;
+    const int sw = KP == 16 ? ((row >> 2) & 3) : KP == 32 ? ((row >> 1) & 7) : (row & 15);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(src, lds_at(img + 1024 * q), 16, (row0 + row) * RB + 16 * (p ^ sw), 0, 0,
+                                             0);
+  }
+}
+// byte address of logical chunk (L0 + j) of row c is narrow_base ^ (16 j) (L0 a multiple of the j range)
+template <int KP>
+__device__ __forceinline__ int narrow_base(int c, int L0) { return c * KP * 4 + 16 * (L0 ^ nsw<KP>(c)); }
+
+__device__ __forceinline__ f32x4 lds_f4(const float* lds, int byte) {
+  return *reinterpret_cast<const f32x4*>(reinterpret_cast<const char*>(lds) + byte);
+}
+__device__ __forceinline__ float lds_f1(const float* lds, int byte) {
+  return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(lds) + byte);
+}
+
 // Zero an LDS image of NF floats before its first DMA, so rows a DMA leaves
 // untouched (out-of-range rows of dma_tile_contig) hold zeros or earlier finite data, never garbage.
 template <int NF>
@@ -199,13 +271,14 @@ __device__ __forceinline__ void lds_zero(float* img) {
 // Wait for every outstanding vector-memory op of this wave (incl. LDS-DMA) before reading LDS.
 __device__ __forceinline__ void wait_vm_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// v_writelane_b32: dst[LANE] = val (val wave-uniform), other lanes unchanged. The lane is an
-// immediate: an SGPR lane index plus an SGPR value would read the constant bus twice. The s_nop
-// covers the VALU-writes-SGPR -> VALU-reads-SGPR hazard (val is typically a v_cmp ballot issued
-// right before): the hazard recognizer does not look inside inline asm.
-template <int LANE>
-__device__ __forceinline__ uint32_t writelane(uint32_t dst, uint32_t val) {
-  asm("s_nop 4\n\tv_writelane_b32 %0, %1, %2" : "+v"(dst) : "s"(val), "n"(LANE));
+// v_writelane_b32 x2: dst[LANE0] = lo, dst[LANE1] = hi (wave-uniform halves of one ballot), other
+// lanes unchanged. Measured on gfx950: a v_writelane that reads an SGPR written by the v_cmp right
+// before it gets stale data, and the hazard recognizer does not look inside inline asm, so one
+// s_nop 4 leads each pair (both halves come from the same v_cmp).
+template <int LANE0, int LANE1>
+__device__ __forceinline__ uint32_t writelane2(uint32_t dst, uint32_t lo, uint32_t hi) {
+  asm("s_nop 4\n\tv_writelane_b32 %0, %1, %3\n\tv_writelane_b32 %0, %2, %4"
+      : "+v"(dst) : "s"(lo), "s"(hi), "n"(LANE0), "n"(LANE1));
   return dst;
 }
 

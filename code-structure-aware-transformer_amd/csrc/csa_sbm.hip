@@ -203,6 +203,7 @@ struct KArgs {
   const float* U;
   uint32_t seed_lo, seed_hi, off;
   float attn_p, proj_p, scale;
+  uint32_t drop_thr, pdrop_thr;  // 16-bit keep thresholds: keep <=> u16 >= thr (thr = ceil(p * 65536))
   // outputs
   float* X;
   // backward
@@ -211,16 +212,10 @@ struct KArgs {
   int G; int64_t slab_floats;
 };
 
-__device__ __forceinline__ f32x4 philox_u4k(uint32_t a, uint32_t b, uint32_t c, uint32_t stream, uint32_t off,
-                                           uint32_t k0, uint32_t k1) {
-  u32x4 r = philox4x32(u32x4{a, b, c, (stream << 28) ^ off}, k0, k1);
-  f32x4 o; o[0] = u01(r.x); o[1] = u01(r.y); o[2] = u01(r.z); o[3] = u01(r.w);
-  return o;
-}
-__device__ __forceinline__ f32x4 philox_u4(uint32_t a, uint32_t b, uint32_t c, uint32_t stream, const KArgs& p) {
-  u32x4 r = philox4x32(u32x4{a, b, c, (stream << 28) ^ p.off}, p.seed_lo, p.seed_hi);
-  f32x4 o; o[0] = u01(r.x); o[1] = u01(r.y); o[2] = u01(r.z); o[3] = u01(r.w);
-  return o;
+// One 16-bit uniform per element: Philox word e/2, low half for even e.
+__device__ __forceinline__ uint32_t u16_of(const u32x4& r, int e) {
+  const uint32_t w = (e >> 1) == 0 ? r.x : (e >> 1) == 1 ? r.y : (e >> 1) == 2 ? r.z : r.w;
+  return (e & 1) ? (w >> 16) : (w & 0xffffu);
 }
 
 // MLP forward pieces for one 32-row block held as lin-perm rows x[D/2] (see csa_common.hpp).
@@ -236,15 +231,17 @@ __device__ __forceinline__ void mlp_act(const KArgs& p, f32x16 (&a)[D / 32], int
 #pragma unroll
   for (int ot = 0; ot < DT; ++ot)
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      f32x4 u = {1.f, 1.f, 1.f, 1.f};
-      if (drop) u = philox_u4((uint32_t)row, (uint32_t)(8 * ot + 2 * g + h) | (layer << 16) | (isK << 20),
-                              (uint32_t)bh, RNG_PROJ_DROP, p);
+    for (int gp = 0; gp < 2; ++gp) {
+      // one Philox call -> 8 x 16-bit uniforms for registers 8gp..8gp+7 (keep <=> u16 >= pdrop_thr)
+      u32x4 u = {0u, 0u, 0u, 0u};
+      if (drop)
+        u = philox4x32(u32x4{(uint32_t)row, (uint32_t)(4 * ot + 2 * gp + h) | (layer << 16) | (isK << 20),
+                             (uint32_t)bh, (RNG_PROJ_DROP << 28) ^ p.off}, p.seed_lo, p.seed_hi);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float v = a[ot][4 * g + e];
-        if (drop) v = (u[e] >= p.proj_p) ? v * ks : 0.f;
-        a[ot][4 * g + e] = fmaxf(v, 0.f);
+      for (int e = 0; e < 8; ++e) {
+        float v = a[ot][8 * gp + e];
+        if (drop) v = (u16_of(u, e) >= p.pdrop_thr) ? v * ks : 0.f;
+        a[ot][8 * gp + e] = fmaxf(v, 0.f);
       }
     }
 }
@@ -450,42 +447,44 @@ __global__ __launch_bounds__(64) void k_proj_fwd(const KArgs p) {
 // (no per-lane masks or selects).
 template <int R>
 __device__ __forceinline__ void pack_ballot(const bool (&av)[16], const bool (&keep)[16], bool doA, bool doR,
-                                            uint32_t& myA, uint32_t& myR, unsigned long long& cnt) {
+                                            uint32_t& myA, uint32_t& myR) {
   if (doA) {
     const unsigned long long bal = __ballot(av[R]);
-    cnt += __popcll(bal);
-    myA = writelane<crow(R, 0)>(myA, (uint32_t)bal);
-    myA = writelane<crow(R, 1)>(myA, (uint32_t)(bal >> 32));
+    myA = writelane2<crow(R, 0), crow(R, 1)>(myA, (uint32_t)bal, (uint32_t)(bal >> 32));
   }
   if (doR) {
     const unsigned long long bal = __ballot(keep[R]);
-    myR = writelane<crow(R, 0)>(myR, (uint32_t)bal);
-    myR = writelane<crow(R, 1)>(myR, (uint32_t)(bal >> 32));
+    myR = writelane2<crow(R, 0), crow(R, 1)>(myR, (uint32_t)bal, (uint32_t)(bal >> 32));
   }
 }
 template <bool DOA, int... Rs>
 __device__ __forceinline__ void pack_ballots(std::integer_sequence<int, Rs...>, const bool (&av)[16],
-                                             const bool (&keep)[16], bool doR, uint32_t& myA, uint32_t& myR,
-                                             unsigned long long& cnt) {
-  (pack_ballot<Rs>(av, keep, DOA, doR, myA, myR, cnt), ...);
+                                             const bool (&keep)[16], bool doR, uint32_t& myA, uint32_t& myR) {
+  (pack_ballot<Rs>(av, keep, DOA, doR, myA, myR), ...);
 }
 
-template <int D, int KPH, bool DENSE>
+template <int D, int KPH>
 struct AttnFwdLds {
-  static constexpr int DP = D + 4, KP = 2 * KPH;                  // padded K/V row, T row
-  static constexpr int FLOATS = 2 * 32 * DP + 32 * KP;            // K image, V image, T image
-  static constexpr size_t BYTES = sizeof(float) * FLOATS;
+  static constexpr bool SWZ = (D == 64);                        // x4 DMA into swizzled unpadded tiles
+  static constexpr int DP = D + 4, KP = 2 * KPH;
+  static constexpr int KV_BYTES = SWZ ? 32 * 64 * 4 : 32 * DP * 4;  // one K or V image
+  static constexpr int T_BYTES = 32 * KP * 4;
+  static constexpr int KOFF = 0, VOFF = KV_BYTES, TOFF = 2 * KV_BYTES, BOFF = TOFF + T_BYTES;
+  // K image | V image | T image | key bias row (Mpad floats: 0 = valid key, -inf = padded / beyond M)
+  static size_t bytes(int Mpad) { return (size_t)BOFF + 4 * (size_t)Mpad; }
 };
 
-template <int D, int KPH, bool DENSE>
+// DROP: attention dropout on (keep <=> 16-bit uniform >= drop_thr). HAS_U: STE uniforms supplied by
+// the caller (bit-exact parity path, fp32 compare as torch.bernoulli); otherwise 16-bit Philox
+// uniforms u16 / 65536 (STE.py:13 draws u < p with p = clamp(expA, .01, .99)).
+template <int D, int KPH, bool DENSE, bool HAS_U, bool DROP>
 __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd(const KArgs p) {
-  using LY = AttnFwdLds<D, KPH, DENSE>;
+  using LY = AttnFwdLds<D, KPH>;
   constexpr int DT = D / 32, NS = D / 2, DP = LY::DP, KP = LY::KP;
+  constexpr bool SWZ = LY::SWZ;
+  constexpr int KPN = KP > 0 ? KP : 16;  // T image width (unused when DENSE)
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  const float* Kimg = lds;
-  const float* Vimg = lds + 32 * DP;
-  const float* Timg = lds + 64 * DP;
-  const uint32_t Kl = lds_offset(Kimg), Vl = Kl + 4 * 32 * DP, Tl = Kl + 8 * 32 * DP;
+  const uint32_t Kl = lds_offset(lds), Vl = Kl + LY::VOFF, Tl = Kl + LY::TOFF;
   const int lane = lane_id(), c = lane & 31, h = lane >> 5;
   const BhBlock xb = xcd_block(p.NQB, p.B * p.H);
   if (!xb.valid) return;
@@ -493,47 +492,67 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd
   const int i = qb * 32 + c;
   const bool iv = i < p.N;
   const int ic = imin(i, p.N - 1);
-  const __amdgpu_buffer_rsrc_t kr = make_rsrc(p.K + b * p.k_sb + hd * p.k_sh, 0x7fffffff);
-  const __amdgpu_buffer_rsrc_t vr = make_rsrc(p.V + b * p.v_sb + hd * p.v_sh, 0x7fffffff);
-  const __amdgpu_buffer_rsrc_t tr = make_rsrc(p.T + (int64_t)bh * p.M * p.kp, p.M * p.kp * 4);
   const int kld = (int)p.k_sn * 4, vld = (int)p.v_sn * 4;
-  const float* mk = p.mask ? p.mask + b * p.mask_sb : nullptr;
-  // tile 0 in flight while the query-side operands load
-  dma_rows<D>(Kl, kr, kld, 0, p.M);
-  dma_rows<D>(Vl, vr, vld, 0, p.M);
-  if constexpr (!DENSE) dma_tile_contig<KP>(Tl, tr, 0);
-  float mnext = mk ? mk[imin(c, p.M - 1)] : 0.f;
+  // SWZ descriptors span exactly the M valid rows (rows >= M are out of range, never fetched)
+  const __amdgpu_buffer_rsrc_t kr = make_rsrc(p.K + b * p.k_sb + hd * p.k_sh, SWZ ? (p.M - 1) * kld + D * 4 : 0x7fffffff);
+  const __amdgpu_buffer_rsrc_t vr = make_rsrc(p.V + b * p.v_sb + hd * p.v_sh, SWZ ? (p.M - 1) * vld + D * 4 : 0x7fffffff);
+  const __amdgpu_buffer_rsrc_t tr = make_rsrc(DENSE ? p.K : p.T + (int64_t)bh * p.M * p.kp, p.M * p.kp * 4);
+  if constexpr (SWZ) lds_zero<(2 * LY::KV_BYTES + LY::T_BYTES) / 4>(lds);
+  else if constexpr (!DENSE) lds_zero<LY::T_BYTES / 4>(lds + LY::TOFF / 4);
+  const DmaPat kpat = dma_pat(SW_ROW, kld), vpat = dma_pat(SW_COL, vld);
+#define CSA_ISSUE_FWD(row0)                                   \
+  do {                                                        \
+    if constexpr (SWZ) {                                      \
+      dma64(Kl, kr, kpat, kld, (row0));               \
+      dma64(Vl, vr, vpat, vld, (row0));               \
+    } else {                                                  \
+      dma_rows<D>(Kl, kr, kld, (row0), p.M);                  \
+      dma_rows<D>(Vl, vr, vld, (row0), p.M);                  \
+    }                                                         \
+    if constexpr (!DENSE) dma_narrow(Tl, tr, (row0), KPN); \
+  } while (0)
+  CSA_ISSUE_FWD(0);  // tile 0 in flight while the bias row and the query-side operands load
+  {
+    const float* mk = p.mask ? p.mask + b * p.mask_sb : nullptr;
+    float* bias = lds + LY::BOFF / 4;
+    for (int j = lane; j < p.NKB * 32; j += 64) {
+      const float mv = mk ? mk[imin(j, p.M - 1)] : 0.f;
+      bias[j] = (j < p.M && mv == 0.f) ? 0.f : NEG_INF;  // sbm_attn.py:61 masked_fill(-inf)
+    }
+  }
   float q[NS];
   load_run<NS>(q, p.Q + b * p.q_sb + hd * p.q_sh + (int64_t)ic * p.q_sn + h * NS, iv);
   float qh[KPH > 0 ? KPH : 1];
-  if (!DENSE) load_run<KPH>(qh, p.Qh + ((int64_t)bh * p.N + ic) * p.kp + h * KPH, iv);
-  const bool drop = p.attn_p > 0.f;
-  const float dscale = drop ? 1.f / (1.f - p.attn_p) : 1.f;
+  if constexpr (!DENSE) load_run<KPH>(qh, p.Qh + ((int64_t)bh * p.N + ic) * p.kp + h * KPH, iv);
+  const int kbase = SWZ ? row_base64(c, h) : 4 * (c * DP + NS * h);
+  const int tbase = DENSE ? 0 : LY::TOFF + narrow_base<KPN>(c, (KPH / 4) * h);
+  int vb[DT];
+#pragma unroll
+  for (int t = 0; t < DT; ++t) vb[t] = LY::VOFF + (SWZ ? col_base64(t, c, h) : 4 * (32 * t + c) + 16 * DP * h);
+  const uint32_t qmask = (uint32_t)__ballot(iv);  // valid query bits of a packed word
   float m_run = NEG_INF, zp = 0.f, zgp = 0.f;
   f32x16 o[DT];
 #pragma unroll
   for (int t = 0; t < DT; ++t) o[t] = zero16();
-  unsigned long long cnt = 0;
+  uint32_t cntl = 0;
 
   for (int kt = 0; kt < p.NKB; ++kt) {
-    const int j0 = kt * 32, jl = j0 + c;
-    const bool jv = jl < p.M;
-    wait_vm_all();  // tile kt's K/V/T images and mask value have landed
-    const float mval = mnext;
+    const int j0 = kt * 32;
+    wait_vm_all();  // tile kt's K/V/T images have landed
     // S^T = K Q^T : A operand = K rows from the image (row c, lin-perm chunks of half h)
     f32x16 sacc = zero16();
 #pragma unroll
     for (int j = 0; j < NS / 4; ++j) {
-      const f32x4 kv = *reinterpret_cast<const f32x4*>(Kimg + c * DP + NS * h + 4 * j);
+      const f32x4 kv = lds_f4(lds, SWZ ? (kbase ^ (16 * j)) : kbase + 16 * j);
 #pragma unroll
       for (int e = 0; e < 4; ++e) sacc = mfma(kv[e], q[4 * j + e], sacc);
     }
     f32x16 eacc;
-    if constexpr (!DENSE) {
+    if constexpr (!DENSE) {  // expA^T = T Qh^T (sbm_attn.py:55)
       eacc = zero16();
 #pragma unroll
       for (int j = 0; j < KPH / 4; ++j) {
-        const f32x4 tv = *reinterpret_cast<const f32x4*>(Timg + c * KP + KPH * h + 4 * j);
+        const f32x4 tv = lds_f4(lds, tbase ^ (16 * j));
 #pragma unroll
         for (int e = 0; e < 4; ++e) eacc = mfma(tv[e], qh[4 * j + e], eacc);
       }
@@ -543,85 +562,87 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd
 #pragma unroll
     for (int t = 0; t < DT; ++t)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) vt[t][r] = Vimg[crow(r, h) * DP + 32 * t + c];
+      for (int r = 0; r < 16; ++r) vt[t][r] = lds_f1(lds, vb[t] + (SWZ ? 256 * crow(r, 0) : 4 * DP * crow(r, 0)));
+    f32x4 bz[4];  // key bias of registers 4g..4g+3 (keys j0 + 8g + 4h + e)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) bz[g] = lds_f4(lds, LY::BOFF + 4 * (j0 + 8 * g + 4 * h));
     // all of tile kt is in registers: start tile kt+1's DMA (overlaps the softmax and PV below)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (kt + 1 < p.NKB) {
-      dma_rows<D>(Kl, kr, kld, j0 + 32, p.M);
-      dma_rows<D>(Vl, vr, vld, j0 + 32, p.M);
-      if constexpr (!DENSE) dma_tile_contig<KP>(Tl, tr, j0 + 32);
-      mnext = mk ? mk[imin(jl + 32, p.M - 1)] : 0.f;
-    }
-    const bool kval = jv && mval == 0.f;
-    const uint32_t vw = (uint32_t)__ballot(kval);
-    uint32_t sk0 = p.seed_lo, sk1 = p.seed_hi;  // opaque per tile: round keys are not held across the loop
-    asm volatile("" : "+s"(sk0), "+s"(sk1));
-    float sv[16], w[16];
-    bool av[16], keep[16];
+    if (kt + 1 < p.NKB) CSA_ISSUE_FWD(j0 + 32);
+    float s[16];
     float tmax = NEG_INF;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const bool valid = (vw >> crow(r, h)) & 1u;
-      sv[r] = valid ? sacc[r] * p.scale : NEG_INF;
-      tmax = fmaxf(tmax, sv[r]);
+      s[r] = fmaf(sacc[r], p.scale, bz[r >> 2][r & 3]);
+      tmax = fmaxf(tmax, s[r]);
     }
+    uint32_t sk0 = p.seed_lo, sk1 = p.seed_hi;  // opaque per tile: round keys are not held across the loop
+    asm volatile("" : "+s"(sk0), "+s"(sk1));
+    bool av[16], keep[16];
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int jg = j0 + 8 * g + 4 * h;  // keys jg..jg+3 held in registers 4g..4g+3
-      if (!DENSE) {
-        f32x4 uu;
-        if (p.U) {
+    for (int r = 0; r < 16; ++r) { av[r] = true; keep[r] = true; }
+    if constexpr (!DENSE) {
+      if constexpr (HAS_U) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float v = p.U[((int64_t)bh * p.N + ic) * p.M + imin(jg + e, p.M - 1)];
-            uu[e] = (iv && jg + e < p.M) ? v : 2.f;
+        for (int r = 0; r < 16; ++r) {
+          const int j = j0 + crow(r, h);
+          const float v = p.U[((int64_t)bh * p.N + ic) * p.M + imin(j, p.M - 1)];
+          const float uu = (iv && j < p.M) ? v : 2.f;
+          av[r] = uu < fminf(fmaxf(eacc[r], 0.01f), 0.99f);  // STE.py:11-13
+        }
+      } else {
+#pragma unroll
+        for (int gp = 0; gp < 2; ++gp) {
+          const u32x4 rr = philox4x32(u32x4{(uint32_t)i, (uint32_t)(8 * kt + 4 * gp + h), (uint32_t)bh,
+                                            (RNG_STE << 28) ^ p.off}, sk0, sk1);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const int r = 8 * gp + e;
+            const float pr = fminf(fmaxf(eacc[r], 0.01f), 0.99f);
+            av[r] = (float)u16_of(rr, e) < pr * 65536.f;
           }
-        } else {
-          uu = philox_u4k((uint32_t)i, (uint32_t)(jg >> 2), (uint32_t)bh, RNG_STE, p.off, sk0, sk1);
         }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float pr = fminf(fmaxf(eacc[4 * g + e], 0.01f), 0.99f);  // STE.py:11
-          av[4 * g + e] = iv && (jg + e < p.M) && (uu[e] < pr);          // STE.py:13
-        }
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) av[4 * g + e] = iv && (jg + e < p.M);
-      }
-      if (drop) {
-        const f32x4 ud = philox_u4k((uint32_t)i, (uint32_t)(jg >> 2), (uint32_t)bh, RNG_ATTN_DROP, p.off, sk0, sk1);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) keep[4 * g + e] = ud[e] >= p.attn_p;
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) keep[4 * g + e] = true;
       }
     }
-    // bit-pack the sampled graph / dropout keep mask: word [qb][key] holds 32 query bits
-    if (!DENSE || drop) {
+    if constexpr (DROP) {
+#pragma unroll
+      for (int gp = 0; gp < 2; ++gp) {
+        const u32x4 rr = philox4x32(u32x4{(uint32_t)i, (uint32_t)(8 * kt + 4 * gp + h), (uint32_t)bh,
+                                          (RNG_ATTN_DROP << 28) ^ p.off}, sk0, sk1);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) keep[8 * gp + e] = u16_of(rr, e) >= p.drop_thr;
+      }
+    }
+    // bit-pack the sampled graph / dropout keep mask: word [qb][key] holds 32 query bits (lanes 0..31)
+    if constexpr (!DENSE || DROP) {
       uint32_t myA = 0, myR = 0;
-      pack_ballots<!DENSE>(std::make_integer_sequence<int, 16>{}, av, keep, drop, myA, myR, cnt);
+      pack_ballots<!DENSE>(std::make_integer_sequence<int, 16>{}, av, keep, DROP, myA, myR);
       const int64_t widx = ((int64_t)bh * p.NQB + qb) * p.Mpad + j0 + c;
-      if (!DENSE && h == 0) p.Abits[widx] = myA;  // the packed words live in lanes 0..31
-      if (drop && h == 0) p.Rbits[widx] = myR;
+      if constexpr (!DENSE) {
+        if (h == 0) p.Abits[widx] = myA;
+        if (j0 + c < p.M) cntl += __popc(myA & qmask);  // sampled edges inside [0,N) x [0,M)
+      }
+      if constexpr (DROP) if (h == 0) p.Rbits[widx] = myR;
     }
-    // online softmax update
+    // online softmax update (exp(-inf - m) = 0 covers masked keys; m_use keeps an all-masked prefix finite)
     tmax = xhalf_max(tmax);
     const float m_new = fmaxf(m_run, tmax);
-    const float alpha = (m_new == NEG_INF) ? 1.f : __expf(m_run - m_new);
+    const float m_use = (m_new == NEG_INF) ? 0.f : m_new;
+    const float alpha = __expf(m_run - m_use);
     zp *= alpha;
     zgp *= alpha;
 #pragma unroll
     for (int t = 0; t < DT; ++t)
 #pragma unroll
       for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
+    float w[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const float e = (sv[r] == NEG_INF) ? 0.f : __expf(sv[r] - m_new);
+      const float e = __expf(s[r] - m_use);
       zp += e;
       const float wa = av[r] ? e : 0.f;
       zgp += wa;
-      w[r] = keep[r] ? wa * dscale : 0.f;
+      w[r] = keep[r] ? wa : 0.f;
     }
     m_run = m_new;
     // O^T += V^T W^T (keys beyond M carry w = 0)
@@ -633,7 +654,8 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd
   const float Z = xhalf_sum(zp), Zg = xhalf_sum(zgp);
   const float n = Zg / Z;
   const float Dn = fmaxf(n, NORM_EPS);
-  const float inv = 1.f / (Z * Dn);
+  const float dscale = DROP ? 1.f / (1.f - p.attn_p) : 1.f;  // dropout's 1/(1-p), applied once per row
+  const float inv = dscale / (Z * Dn);
   if (iv) {
     float* xo = p.X + ((int64_t)bh * p.N + i) * D;
 #pragma unroll
@@ -653,7 +675,13 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd
       *reinterpret_cast<f32x4*>(p.stats + ((int64_t)bh * p.N + i) * 4) = st;
     }
   }
-  if (!DENSE && lane == 0 && cnt) atomicAdd(p.cnt + hd, cnt);
+#undef CSA_ISSUE_FWD
+  if constexpr (!DENSE) {
+    cntl = (h == 0) ? cntl : 0u;
+#pragma unroll
+    for (int o2 = 32; o2 >= 1; o2 >>= 1) cntl += __shfl_xor(cntl, o2, 64);
+    if (lane == 0 && cntl) atomicAdd(p.cnt + hd, (unsigned long long)cntl);
+  }
 }
 
 __global__ void k_sparsity_finish(const unsigned long long* __restrict__ cnt, float* __restrict__ sp, int H, float bnm) {
@@ -1537,6 +1565,8 @@ KArgs make_kargs(const csa_sbm_fwd_args* a, const Layout& L) {
   p.U = a->uniforms;
   p.seed_lo = (uint32_t)a->seed; p.seed_hi = (uint32_t)(a->seed >> 32); p.off = (uint32_t)a->offset;
   p.attn_p = a->attn_dropout; p.proj_p = a->proj_dropout;
+  p.drop_thr = (uint32_t)ceil((double)a->attn_dropout * 65536.0);
+  p.pdrop_thr = (uint32_t)ceil((double)a->proj_dropout * 65536.0);
   p.scale = 1.f / sqrtf((float)a->d);
   p.X = a->X;
   return p;
@@ -1563,6 +1593,29 @@ csa_status validate_fwd(const csa_sbm_fwd_args* a) {
     return fail(CSA_INVALID_ARG, "Q/K/V must be 16-byte aligned with strides multiple of 4 elements");
   if (((uintptr_t)a->X) % 16) return fail(CSA_INVALID_ARG, "X must be 16-byte aligned");
   return CSA_OK;
+}
+
+template <int D, int KPH, bool DENSE>
+void launch_attn_fwd(const KArgs& p, int BH, const Layout& L, bool has_u, bool drop, hipStream_t st) {
+  const size_t lds_bytes = AttnFwdLds<D, KPH>::bytes((int)L.Mpad);
+  const dim3 grid(xcd_grid((int)L.NQB, BH));
+  if (lds_bytes > 64 * 1024) {
+    (void)hipFuncSetAttribute((const void*)k_attn_fwd<D, KPH, DENSE, false, false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+    (void)hipFuncSetAttribute((const void*)k_attn_fwd<D, KPH, DENSE, false, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+    (void)hipFuncSetAttribute((const void*)k_attn_fwd<D, KPH, DENSE, !DENSE, false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+    (void)hipFuncSetAttribute((const void*)k_attn_fwd<D, KPH, DENSE, !DENSE, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+  }
+  if (!DENSE && has_u) {
+    if (drop) hipLaunchKernelGGL((k_attn_fwd<D, KPH, DENSE, !DENSE, true>), grid, dim3(64), lds_bytes, st, p);
+    else hipLaunchKernelGGL((k_attn_fwd<D, KPH, DENSE, !DENSE, false>), grid, dim3(64), lds_bytes, st, p);
+  } else {
+    if (drop) hipLaunchKernelGGL((k_attn_fwd<D, KPH, DENSE, false, true>), grid, dim3(64), lds_bytes, st, p);
+    else hipLaunchKernelGGL((k_attn_fwd<D, KPH, DENSE, false, false>), grid, dim3(64), lds_bytes, st, p);
+  }
 }
 
 template <int D, int KPH, int KT>
@@ -1603,15 +1656,13 @@ csa_status launch_fwd(const csa_sbm_fwd_args* a, const Layout& L, hipStream_t st
     }
     {
       Stage sg(a->prof, CSA_STAGE_ATTN_FWD, st);
-      constexpr size_t lds_bytes = AttnFwdLds<D, KPH, false>::BYTES;
-      hipLaunchKernelGGL((k_attn_fwd<D, KPH, false>), dim3(xcd_grid((int)L.NQB, BH)), dim3(64), lds_bytes, st, p);
+      launch_attn_fwd<D, KPH, false>(p, BH, L, a->uniforms != nullptr, a->attn_dropout > 0.f, st);
     }
     hipLaunchKernelGGL(k_sparsity_finish, dim3(1), dim3(64), 0, st, (const unsigned long long*)p.cnt, a->sparsity,
                        (int)a->H, (float)a->B * (float)a->N * (float)a->M);
   } else {
     Stage sg(a->prof, CSA_STAGE_ATTN_FWD, st);
-    constexpr size_t lds_bytes = AttnFwdLds<D, 0, true>::BYTES;
-    hipLaunchKernelGGL((k_attn_fwd<D, 0, true>), dim3(xcd_grid((int)L.NQB, BH)), dim3(64), lds_bytes, st, p);
+    launch_attn_fwd<D, 0, true>(p, BH, L, false, a->attn_dropout > 0.f, st);
   }
   return check_launch("csa_sbm_fwd");
 }
