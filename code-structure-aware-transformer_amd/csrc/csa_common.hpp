@@ -164,11 +164,12 @@ __device__ __forceinline__ void dma_rows(uint32_t img, __amdgpu_buffer_rsrc_t sr
 // Rows r0..r0+31 of a contiguous (M, W) row-major matrix into an unpadded image (32*W floats).
 // src must span exactly M rows: rows >= M fall outside the buffer and are not real data.
 template <int W>
-__device__ __forceinline__ void dma_tile_contig(uint32_t img, __amdgpu_buffer_rsrc_t src, int r0) {
+__device__ __forceinline__ void dma_tile_contig(uint32_t img, __amdgpu_buffer_rsrc_t src, int r0, const int f0 = 0,
+                                                const int f1 = 2) {
   asm volatile("" : "+s"(img));
   const int voff = lane_id() * 4 + r0 * W * 4;
 #pragma unroll
-  for (int i = 0; i < W / 2; ++i)
+  for (int i = f0 * W / 4; i < f1 * W / 4; ++i)
     __builtin_amdgcn_raw_ptr_buffer_load_lds(src, lds_at(img + 256 * i), 4, voff + 256 * i, 0, 0, 0);
 }
 
@@ -192,12 +193,16 @@ __device__ __forceinline__ void dma_block16(uint32_t lds_off, __amdgpu_buffer_rs
 //                                conflict-free; a lane's 8 chunks of one half sit at base ^ (16 j).
 //   SW_COL: swz = 8 * bit2(r)    column reads (lanes = 32 consecutive columns of rows R and R + 4)
 //                                are conflict-free and reduce to two lane bases + immediate offsets.
+//   SW_BOTH: swz = (r & 7) | 8 * (bit2(r) ^ bit3(r))   both patterns conflict-free; a row read sits at
+//                                row_base ^ (16 j), a column read at (col_base_t ^ K_r) + 256 crow(r, 0).
 // Instruction q covers rows 4q..4q+3: lane i -> row 4q + i/16, LDS chunk i%16. The source offset
 // carries the whole row offset in voffset, so rows >= M fall outside the buffer range given by the
 // descriptor (never outside the allocation) and do not load real data; callers zero the image once.
 // ---------------------------------------------------------------------------------------
-enum { SW_ROW = 1, SW_COL = 2 };
-__host__ __device__ constexpr int swz(int sw, int row) { return sw == SW_ROW ? (row & 15) : 8 * ((row >> 2) & 1); }
+enum { SW_ROW = 1, SW_COL = 2, SW_BOTH = 3 };
+__host__ __device__ constexpr int swz(int sw, int row) {
+  return sw == SW_ROW ? (row & 15) : sw == SW_COL ? 8 * ((row >> 2) & 1) : (row & 7) | ((((row >> 2) ^ (row >> 3)) & 1) << 3);
+}
 
 // Per-lane DMA source patterns (q mod 4 for SW_ROW, q mod 2 for SW_COL). The swizzle kind is a plain
 // argument (callers pass a constant and the helpers are inlined): templated versions of these
@@ -211,18 +216,30 @@ __device__ __forceinline__ DmaPat dma_pat(const int sw, int ld_bytes) {
   return P;
 }
 // Rows row0..row0+31 of a row-major (ld_bytes) fp32 matrix with 64 columns -> swizzled image at img.
-__device__ __forceinline__ void dma64(uint32_t img, __amdgpu_buffer_rsrc_t src, const DmaPat& P, int ld_bytes, int row0) {
+// (Instructions q0 <= q < q1 only: rows 4 q0 .. 4 q1 - 1.)
+__device__ __forceinline__ void dma64(uint32_t img, __amdgpu_buffer_rsrc_t src, const DmaPat& P, int ld_bytes, int row0,
+                                      const int q0 = 0, const int q1 = 8) {
   asm volatile("" : "+s"(img));
-  int rowoff = row0 * ld_bytes;
+  int rowoff = (row0 + 4 * q0) * ld_bytes;
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
+  for (int q = q0; q < q1; ++q) {
     asm volatile("" : "+s"(rowoff));
     __builtin_amdgcn_raw_ptr_buffer_load_lds(src, lds_at(img + 1024 * q), 16, P.v[q & 3] + rowoff, 0, 0, 0);
     rowoff += 4 * ld_bytes;
   }
 }
-// SW_ROW image: byte address of logical chunk (8h + j) of row c is row_base ^ (16 j), j < 8.
-__device__ __forceinline__ int row_base64(int c, int h) { return 256 * c + 16 * ((8 * h) ^ (c & 15)); }
+// SW_ROW / SW_BOTH image: byte address of logical chunk (8h + j) of row c is row_base ^ (16 j), j < 8.
+__device__ __forceinline__ int row_base64(int c, int h, const int sw = SW_ROW) { return 256 * c + 16 * ((8 * h) ^ swz(sw, c)); }
+// SW_BOTH image: element (crow(r,h), 32t + c) is at (both_base64(t) ^ both_k(r)) + 256 * crow(r, 0).
+__device__ __forceinline__ int both_base64(int t, int c, int h) {
+  return 1024 * h + 128 * (t ^ h) + 16 * ((c >> 2) ^ (4 * h)) + 4 * (c & 3);
+}
+__host__ __device__ constexpr int both_k(int r) { return 128 * ((r >> 2) & 1) + 16 * (r & 3); }
+// SW_BOTH column read (rows crow(r,h) and crow(r+8,h) share the XOR term; the rest is the offset field)
+__device__ __forceinline__ float both_read(const float* lds, int base_t, int r, int off) {
+  return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(lds) + off + 256 * crow(r, 0) + (base_t ^ both_k(r)));
+}
+
 // SW_COL image: element (crow(r,h), 32t + c) is at col_base64(t) + 256 * crow(r, 0).
 __device__ __forceinline__ int col_base64(int t, int c, int h) { return 1024 * h + 128 * (t ^ h) + 4 * c; }
 
@@ -233,17 +250,24 @@ __device__ __forceinline__ int nsw(int row) {
   return KP == 16 ? ((row >> 2) & 3) : KP == 32 ? ((row >> 1) & 7) : (row & 15);
 }
 // (KP is a plain argument: every caller passes a compile-time constant and the call is inlined.)
-__device__ __forceinline__ void dma_narrow(uint32_t img, __amdgpu_buffer_rsrc_t src, int row0, const int KP) {
+// (Rows [32 f0, 32 f1) / 2 of the tile only when a half range (f0, f1) in {0, 1, 2} is given.)
+__device__ __forceinline__ void dma_narrow(uint32_t img, __amdgpu_buffer_rsrc_t src, int row0, const int KP,
+                                          const int f0 = 0, const int f1 = 2) {
   const int CPR = KP / 4, RB = KP * 4;
   asm volatile("" : "+s"(img));
   const int i = lane_id();
 #pragma unroll
-  for (int q = 0; q < KP / 8; ++q) {
+  for (int q = f0 * KP / 16; q < f1 * KP / 16; ++q) {
     const int byte = 1024 * q + 16 * i, row = byte / RB, p = (byte / 16) % CPR;
     const int sw = KP == 16 ? ((row >> 2) & 3) : KP == 32 ? ((row >> 1) & 7) : (row & 15);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(src, lds_at(img + 1024 * q), 16, (row0 + row) * RB + 16 * (p ^ sw), 0, 0,
                                              0);
   }
+}
+// element (row, col) of a narrow image with KP floats per row
+__device__ __forceinline__ int narrow_elem(int row, int col, const int KP) {
+  const int sw = KP == 16 ? ((row >> 2) & 3) : KP == 32 ? ((row >> 1) & 7) : (row & 15);
+  return row * KP * 4 + 16 * ((col >> 2) ^ sw) + 4 * (col & 3);
 }
 // byte address of logical chunk (L0 + j) of row c is narrow_base ^ (16 j) (L0 a multiple of the j range)
 template <int KP>

@@ -742,46 +742,65 @@ __global__ __launch_bounds__(64) void k_maps(const KArgs p, float* __restrict__ 
 // ------------------------------------------------------------------------------------
 struct Elem { float ds, g, attw; };
 
-__device__ __forceinline__ Elem bwd_elem(float s_raw, float dpp, bool kval, bool a, bool keep, bool inside,
+// kbias: 0 for a valid key, -inf for a padded one (P = exp(s * scale + kbias - lse) = 0). Branch-free:
+// elements outside [0,N) x [0,M) are computed from finite stand-in operands and selected to zero.
+__device__ __forceinline__ Elem bwd_elem(float s_raw, float kbias, float dpp, bool a, bool keep, bool inside,
                                          float lse, float invD, float big, float gamma, float scale, float dscale,
                                          float csp, float dgr) {
   Elem r;
-  if (!inside) { r.ds = 0.f; r.g = 0.f; r.attw = 0.f; return r; }
-  const float P = kval ? __expf(s_raw * scale - lse) : 0.f;
+  const float P = __expf(fmaf(s_raw, scale, kbias) - lse);
   const float rm = keep ? dscale : 0.f;
   const float dattn = dpp * rm;
   const bool mpos = a && (P > 0.f);
   const float dM = (dattn - ((big != 0.f && mpos) ? gamma : 0.f)) * invD;
   const float dPm = a ? dM : 0.f;
   const float rho = (big != 0.f) ? 0.f : gamma;
-  r.ds = P * (dPm - rho) * scale;
+  const bool ain = a && inside;
+  r.ds = inside ? P * (dPm - rho) * scale : 0.f;
   const float dA = dM * P + csp + dgr;
-  r.g = a ? fminf(fmaxf(dA, -1.f), 1.f) : 0.f;  // STE.py:19 hardtanh(A * grad)
-  r.attw = a ? P * invD * rm : 0.f;              // dropout(attn) weight for dV
+  r.g = ain ? fminf(fmaxf(dA, -1.f), 1.f) : 0.f;  // STE.py:19 hardtanh(A * grad)
+  r.attw = ain ? P * invD * rm : 0.f;              // dropout(attn) weight for dV
   return r;
+}
+
+// ------------------------------------------------------------------------------------
+// B2/B1 shared LDS layout
+// ------------------------------------------------------------------------------------
+template <int D, int KPH>
+struct AttnBwdShape {
+  static constexpr bool SWZ = (D == 64);  // x4 DMA into SW_BOTH / SW_ROW swizzled tiles (else padded rows)
+  static constexpr int DP = D + 4, KP = 2 * KPH, KPN = KP > 0 ? KP : 16;
+  static constexpr int KT = KPH == 0 ? 0 : (KP <= 32 ? 1 : KP / 32), KTA = KT > 0 ? KT : 1;
+  static constexpr int IMG = SWZ ? 32 * 64 * 4 : 32 * DP * 4;  // one 32 x D image
+  static constexpr int NIMG = 32 * KPN * 4;                    // one 32 x KP narrow image
+  // bwd_q: K | V | T | key bias row (Mpad floats)
+  static constexpr int QK = 0, QV = IMG, QT = 2 * IMG, QB = 2 * IMG + NIMG;
+  static size_t q_bytes(int Mpad) { return (size_t)QB + 4 * (size_t)Mpad; }
+  // bwd_kv: Q | dX | Qh | stats (32 rows x 4)
+  static constexpr int KQ = 0, KX = IMG, KH = 2 * IMG, KS = 2 * IMG + NIMG;
+  static constexpr size_t KV_BYTES = (size_t)KS + 32 * 16;
+};
+
+// key bias row in LDS: 0 for a valid key, -inf for a padded one or one beyond M (sbm_attn.py:61)
+__device__ __forceinline__ void fill_key_bias(float* bias, const KArgs& p, int b) {
+  const float* mk = p.mask ? p.mask + b * p.mask_sb : nullptr;
+  for (int j = lane_id(); j < p.NKB * 32; j += 64) {
+    const float mv = mk ? mk[imin(j, p.M - 1)] : 0.f;
+    bias[j] = (j < p.M && mv == 0.f) ? 0.f : NEG_INF;
+  }
 }
 
 // ------------------------------------------------------------------------------------
 // B2: per (b,h, query block), S^T orientation: dQ (attention path), dQh, gamma
 // ------------------------------------------------------------------------------------
-template <int D, int KPH>
-struct AttnBwdShape {
-  static constexpr int DP = D + 4, KP = 2 * KPH;
-  static constexpr int KT = KPH == 0 ? 0 : (KP <= 32 ? 1 : KP / 32), KTA = KT > 0 ? KT : 1;
-  // bwd_q images: K, V (padded rows), T; bwd_kv images: Q, dX (padded rows), Qh, stats
-  static constexpr size_t Q_BYTES = sizeof(float) * (2 * 32 * DP + 32 * KP);
-  static constexpr size_t KV_BYTES = sizeof(float) * (2 * 32 * DP + 32 * KP + 32 * 4);
-};
-
-template <int D, int KPH, bool DENSE>
+// DG: an upstream gradient of the graph output is present (p.dgraph)
+template <int D, int KPH, bool DENSE, bool DROP, bool DG>
 __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd_q(const KArgs p) {
   using SH = AttnBwdShape<D, KPH>;
-  constexpr int DT = D / 32, NS = D / 2, DP = SH::DP, KP = SH::KP, KTA = SH::KTA;
+  constexpr int DT = D / 32, NS = D / 2, DP = SH::DP, KP = SH::KP, KPN = SH::KPN, KTA = SH::KTA;
+  constexpr bool SWZ = SH::SWZ;
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  const float* Kimg = lds;
-  const float* Vimg = lds + 32 * DP;
-  const float* Timg = lds + 64 * DP;
-  const uint32_t Kl = lds_offset(Kimg), Vl = Kl + 4 * 32 * DP, Tl = Kl + 8 * 32 * DP;
+  const uint32_t L0 = lds_offset(lds), Kl = L0 + SH::QK, Vl = L0 + SH::QV, Tl = L0 + SH::QT;
   const int lane = lane_id(), c = lane & 31, h = lane >> 5;
   const BhBlock xb = xcd_block(p.NQB, p.B * p.H);
   if (!xb.valid) return;
@@ -789,21 +808,30 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
   const int i = qb * 32 + c;
   const bool iv = i < p.N;
   const int ic = imin(i, p.N - 1);
-  const __amdgpu_buffer_rsrc_t kr = make_rsrc(p.K + b * p.k_sb + hd * p.k_sh, 0x7fffffff);
-  const __amdgpu_buffer_rsrc_t vr = make_rsrc(p.V + b * p.v_sb + hd * p.v_sh, 0x7fffffff);
-  const __amdgpu_buffer_rsrc_t tr = make_rsrc(DENSE ? p.K : p.T + (int64_t)bh * p.M * p.kp, p.M * p.kp * 4);
   const int kld = (int)p.k_sn * 4, vld = (int)p.v_sn * 4;
-  // rows past M lie outside tr: zero the T image once so they never hold garbage (NaN * 0)
-  if constexpr (!DENSE) lds_zero<32 * KP>(const_cast<float*>(Timg));
-  dma_rows<D>(Kl, kr, kld, 0, p.M);
-  dma_rows<D>(Vl, vr, vld, 0, p.M);
-  if constexpr (!DENSE) dma_tile_contig<KP>(Tl, tr, 0);
-  const float* mk = p.mask ? p.mask + b * p.mask_sb : nullptr;
-  const bool drop = p.attn_p > 0.f;
+  const __amdgpu_buffer_rsrc_t kr = make_rsrc(p.K + b * p.k_sb + hd * p.k_sh, SWZ ? (p.M - 1) * kld + D * 4 : 0x7fffffff);
+  const __amdgpu_buffer_rsrc_t vr = make_rsrc(p.V + b * p.v_sb + hd * p.v_sh, SWZ ? (p.M - 1) * vld + D * 4 : 0x7fffffff);
+  const __amdgpu_buffer_rsrc_t tr = make_rsrc(DENSE ? p.K : p.T + (int64_t)bh * p.M * p.kp, p.M * p.kp * 4);
+  // rows past M are never fetched: zero the images once so they only ever hold finite data
+  if constexpr (SWZ) lds_zero<(2 * SH::IMG + SH::NIMG) / 4>(lds);
+  else if constexpr (!DENSE) lds_zero<SH::NIMG / 4>(lds + SH::QT / 4);
+  const DmaPat kpat = dma_pat(SW_BOTH, kld), vpat = dma_pat(SW_ROW, vld);
+#define CSA_ISSUE_BQ(row0)                          \
+  do {                                              \
+    if constexpr (SWZ) {                            \
+      dma64(Kl, kr, kpat, kld, (row0));             \
+      dma64(Vl, vr, vpat, vld, (row0));             \
+    } else {                                        \
+      dma_rows<D>(Kl, kr, kld, (row0), p.M);        \
+      dma_rows<D>(Vl, vr, vld, (row0), p.M);        \
+    }                                               \
+    if constexpr (!DENSE) dma_narrow(Tl, tr, (row0), KPN); \
+  } while (0)
+  CSA_ISSUE_BQ(0);
+  fill_key_bias(lds + SH::QB / 4, p, b);
   const int64_t wrow = ((int64_t)bh * p.NQB + qb) * p.Mpad + c;
-  float mnext = mk ? mk[imin(c, p.M - 1)] : 0.f;
   uint32_t wAn = DENSE ? 0xffffffffu : p.Abits[wrow];
-  uint32_t wRn = drop ? p.Rbits[wrow] : 0xffffffffu;
+  uint32_t wRn = DROP ? p.Rbits[wrow] : 0xffffffffu;
   float q[NS], dx[NS];
   load_run<NS>(q, p.Q + b * p.q_sb + hd * p.q_sh + (int64_t)ic * p.q_sn + h * NS, iv);
   load_run<NS>(dx, p.dX + ((int64_t)bh * p.N + ic) * D + h * NS, iv);
@@ -818,9 +846,8 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
   f32x4 st = *reinterpret_cast<const f32x4*>(p.stats + ((int64_t)bh * p.N + ic) * 4);
   if (iv && h == 0) p.stats[((int64_t)bh * p.N + i) * 4 + 3] = gamma;
   const float lse = st[0], invD = st[1], big = st[2];
-  const float dscale = drop ? 1.f / (1.f - p.attn_p) : 1.f;
+  const float dscale = DROP ? 1.f / (1.f - p.attn_p) : 1.f;
   const float csp = (!DENSE && p.dsp) ? p.dsp[hd] / ((float)p.B * (float)p.N * (float)p.M) : 0.f;
-  const int tcol = imin(c, KP - 1);
   f32x16 dq[DT], dqh[KTA];
 #pragma unroll
   for (int t = 0; t < DT; ++t) dq[t] = zero16();
@@ -830,60 +857,62 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
     int ln = threadIdx.x;  // opaque per iteration: keeps the per-row LDS addresses out of the prologue
     asm volatile("" : "+v"(ln));
     const int c = ln & 31, h = (ln >> 5) & 1;
-    const int j0 = kt * 32, jl = j0 + c;
-    wait_vm_all();  // tile kt's K/V/T images and its mask / bit words have landed
-    const float mval = mnext;
+    const int j0 = kt * 32;
+    wait_vm_all();  // tile kt's K/V/T images and its bit words have landed
     const uint32_t wA = wAn, wR = wRn;
     f32x16 sacc = zero16(), dpacc = zero16();
+    const int kb = SWZ ? row_base64(c, h, SW_BOTH) : 4 * (c * DP + NS * h);
+    const int vb = SH::QV + (SWZ ? row_base64(c, h, SW_ROW) : 4 * (c * DP + NS * h));
 #pragma unroll
     for (int j = 0; j < NS / 4; ++j) {
-      const f32x4 kv = *reinterpret_cast<const f32x4*>(Kimg + c * DP + NS * h + 4 * j);
+      const f32x4 kv = lds_f4(lds, SWZ ? (kb ^ (16 * j)) : kb + 16 * j);
 #pragma unroll
       for (int e = 0; e < 4; ++e) sacc = mfma(kv[e], q[4 * j + e], sacc);
     }
 #pragma unroll
     for (int j = 0; j < NS / 4; ++j) {
-      const f32x4 vv = *reinterpret_cast<const f32x4*>(Vimg + c * DP + NS * h + 4 * j);
+      const f32x4 vv = lds_f4(lds, SWZ ? (vb ^ (16 * j)) : vb + 16 * j);
 #pragma unroll
       for (int e = 0; e < 4; ++e) dpacc = mfma(vv[e], dx[4 * j + e], dpacc);
     }
     // transposed operands of this tile's dQ / dQh products (lane d holds K[key crow(r,h)][d])
     float kT[DT][16], tT[KTA][16];
 #pragma unroll
-    for (int t = 0; t < DT; ++t)
+    for (int t = 0; t < DT; ++t) {
+      const int tb = SWZ ? both_base64(t, c, h) : 4 * (32 * t + c) + 16 * DP * h;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) kT[t][r] = Kimg[crow(r, h) * DP + 32 * t + c];
+      for (int r = 0; r < 16; ++r)
+        kT[t][r] = SWZ ? both_read(lds, tb, r, SH::QK) : lds_f1(lds, tb + 4 * DP * crow(r, 0));
+    }
     if constexpr (!DENSE) {
 #pragma unroll
       for (int at = 0; at < KTA; ++at)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float v = Timg[crow(r, h) * KP + (KP >= 32 ? 32 * at + c : tcol)];
+          const float v = lds_f1(lds, SH::QT + narrow_elem(crow(r, h), imin(32 * at + c, KP - 1), KPN));
           tT[at][r] = (KP >= 32 || c < KP) ? v : 0.f;
         }
     }
+    f32x4 bz[4];  // key bias of registers 4g..4g+3
+#pragma unroll
+    for (int g = 0; g < 4; ++g) bz[g] = lds_f4(lds, SH::QB + 4 * (j0 + 8 * g + 4 * h));
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (kt + 1 < p.NKB) {  // tile kt+1 streams in under the elementwise work and the products below
-      dma_rows<D>(Kl, kr, kld, j0 + 32, p.M);
-      dma_rows<D>(Vl, vr, vld, j0 + 32, p.M);
-      if constexpr (!DENSE) dma_tile_contig<KP>(Tl, tr, j0 + 32);
-      mnext = mk ? mk[imin(jl + 32, p.M - 1)] : 0.f;
+      CSA_ISSUE_BQ(j0 + 32);
       if constexpr (!DENSE) wAn = p.Abits[wrow + j0 + 32];
-      if (drop) wRn = p.Rbits[wrow + j0 + 32];
+      if constexpr (DROP) wRn = p.Rbits[wrow + j0 + 32];
     }
-    const bool kval = jl < p.M && mval == 0.f;
-    const uint32_t vw = (uint32_t)__ballot(kval);
     float dsv[16], gv[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int jj = crow(r, h), j = j0 + jj;
       const uint32_t a_w = DENSE ? 0xffffffffu : (uint32_t)__shfl((int)wA, jj, 64);
-      const uint32_t r_w = drop ? (uint32_t)__shfl((int)wR, jj, 64) : 0xffffffffu;
+      const uint32_t r_w = DROP ? (uint32_t)__shfl((int)wR, jj, 64) : 0xffffffffu;
       const bool a = (a_w >> c) & 1u;
       const bool keep = (r_w >> c) & 1u;
       const bool inside = iv && (j < p.M);
-      const float dgr = p.dgraph ? ldz(p.dgraph, ((int64_t)bh * p.N + ic) * p.M + imin(j, p.M - 1), INT64_MAX, inside) : 0.f;
-      const Elem e = bwd_elem(sacc[r], dpacc[r], (vw >> jj) & 1u, DENSE ? inside : a, keep, inside, lse, invD, big,
+      const float dgr = DG ? ldz(p.dgraph, ((int64_t)bh * p.N + ic) * p.M + imin(j, p.M - 1), INT64_MAX, inside) : 0.f;
+      const Elem e = bwd_elem(sacc[r], bz[r >> 2][r & 3], dpacc[r], DENSE ? inside : a, keep, inside, lse, invD, big,
                               gamma, p.scale, dscale, csp, dgr);
       dsv[r] = e.ds;
       gv[r] = e.g;
@@ -900,6 +929,7 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
         for (int r = 0; r < 16; ++r) dqh[at] = mfma(tT[at][r], gv[r], dqh[at]);
     }
   }
+#undef CSA_ISSUE_BQ
   store_rows<DT>(p.dQ + ((int64_t)bh * p.N + i) * D, D, D, dq, iv);
   if constexpr (!DENSE) store_rows<KTA>(p.dQh + ((int64_t)bh * p.N + i) * p.kp, p.kp, p.kp, dqh, iv);
 }
@@ -907,16 +937,13 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
 // ------------------------------------------------------------------------------------
 // B1: per (b,h, key block), S orientation (queries = acc rows, keys = lanes): dK, dV, dT
 // ------------------------------------------------------------------------------------
-template <int D, int KPH, bool DENSE>
+template <int D, int KPH, bool DENSE, bool DROP, bool DG>
 __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd_kv(const KArgs p) {
   using SH = AttnBwdShape<D, KPH>;
-  constexpr int DT = D / 32, NS = D / 2, DP = SH::DP, KP = SH::KP, KTA = SH::KTA;
+  constexpr int DT = D / 32, NS = D / 2, DP = SH::DP, KP = SH::KP, KPN = SH::KPN, KTA = SH::KTA;
+  constexpr bool SWZ = SH::SWZ;
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  const float* Qimg = lds;
-  const float* Ximg = lds + 32 * DP;   // dX rows
-  const float* Himg = lds + 64 * DP;   // Qh rows
-  const float* Simg = lds + 64 * DP + 32 * KP;  // stats rows (lse, 1/D, big, gamma)
-  const uint32_t Ql = lds_offset(Qimg), Xl = Ql + 4 * 32 * DP, Hl = Ql + 8 * 32 * DP, Sl = Hl + 4 * 32 * KP;
+  const uint32_t L0 = lds_offset(lds), Ql = L0 + SH::KQ, Xl = L0 + SH::KX, Hl = L0 + SH::KH, Sl = L0 + SH::KS;
   const int lane = lane_id(), c = lane & 31, h = lane >> 5;
   const BhBlock xb = xcd_block(p.NKB, p.B * p.H);
   if (!xb.valid) return;
@@ -924,30 +951,35 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
   const int j = kbi * 32 + c;
   const bool jv = j < p.M;
   const int jc = imin(j, p.M - 1);
-  const __amdgpu_buffer_rsrc_t qr_ = make_rsrc(p.Q + b * p.q_sb + hd * p.q_sh, 0x7fffffff);
-  const __amdgpu_buffer_rsrc_t xr_ = make_rsrc(p.dX + (int64_t)bh * p.N * D, 0x7fffffff);
+  const int qld = (int)p.q_sn * 4;
+  const __amdgpu_buffer_rsrc_t qr_ = make_rsrc(p.Q + b * p.q_sb + hd * p.q_sh, SWZ ? (p.N - 1) * qld + D * 4 : 0x7fffffff);
+  const __amdgpu_buffer_rsrc_t xr_ = make_rsrc(p.dX + (int64_t)bh * p.N * D, SWZ ? p.N * D * 4 : 0x7fffffff);
   const __amdgpu_buffer_rsrc_t hr_ = make_rsrc(DENSE ? p.dX : p.Qh + (int64_t)bh * p.N * p.kp, p.N * p.kp * 4);
   const __amdgpu_buffer_rsrc_t sr_ = make_rsrc(p.stats + (int64_t)bh * p.N * 4, p.N * 16);
-  const int qld = (int)p.q_sn * 4;
-  // rows past N lie outside hr_/sr_: zero those images once so they never hold garbage
-  lds_zero<32 * KP + 128>(const_cast<float*>(Himg));
-  dma_rows<D>(Ql, qr_, qld, 0, p.N);
-  dma_rows<D>(Xl, xr_, 4 * D, 0, p.N);
-  if constexpr (!DENSE) dma_tile_contig<KP>(Hl, hr_, 0);
+  // rows past N are never fetched: zero the images once so they only ever hold finite data
+  if constexpr (SWZ) lds_zero<(int)(SH::KV_BYTES / 4)>(lds);
+  else lds_zero<(SH::NIMG + 512) / 4>(lds + SH::KH / 4);
+  const DmaPat qpat = dma_pat(SW_BOTH, qld), xpat = dma_pat(SW_BOTH, 4 * D);
+  if constexpr (SWZ) {
+    dma64(Ql, qr_, qpat, qld, 0);
+    dma64(Xl, xr_, xpat, 4 * D, 0);
+  } else {
+    dma_rows<D>(Ql, qr_, qld, 0, p.N);
+    dma_rows<D>(Xl, xr_, 4 * D, 0, p.N);
+  }
+  if constexpr (!DENSE) dma_narrow(Hl, hr_, 0, KPN);
   dma_tile_contig<4>(Sl, sr_, 0);
-  const bool drop = p.attn_p > 0.f;
   const int64_t wcol = (int64_t)bh * p.NQB * p.Mpad + j;
   uint32_t wAn = DENSE ? 0xffffffffu : p.Abits[wcol];
-  uint32_t wRn = drop ? p.Rbits[wcol] : 0xffffffffu;
+  uint32_t wRn = DROP ? p.Rbits[wcol] : 0xffffffffu;
   const float* mk = p.mask ? p.mask + b * p.mask_sb : nullptr;
   const float mval = mk ? mk[jc] : 0.f;
-  const bool kval = jv && mval == 0.f;
+  const float kbias = (jv && mval == 0.f) ? 0.f : NEG_INF;  // this lane's key (sbm_attn.py:61)
   float kr[NS], vr[NS];
   load_run<NS>(kr, p.K + b * p.k_sb + hd * p.k_sh + (int64_t)jc * p.k_sn + h * NS, jv);
   load_run<NS>(vr, p.V + b * p.v_sb + hd * p.v_sh + (int64_t)jc * p.v_sn + h * NS, jv);
-  const float dscale = drop ? 1.f / (1.f - p.attn_p) : 1.f;
+  const float dscale = DROP ? 1.f / (1.f - p.attn_p) : 1.f;
   const float csp = (!DENSE && p.dsp) ? p.dsp[hd] / ((float)p.B * (float)p.N * (float)p.M) : 0.f;
-  const int hcol = imin(c, KP - 1);
   f32x16 dv[DT], dk[DT], dtt[KTA];
 #pragma unroll
   for (int t = 0; t < DT; ++t) { dv[t] = zero16(); dk[t] = zero16(); }
@@ -963,64 +995,84 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
     const uint32_t wA = wAn, wR = wRn;
     if (more) {
       if constexpr (!DENSE) wAn = p.Abits[wcol + (int64_t)(qb + 1) * p.Mpad];
-      if (drop) wRn = p.Rbits[wcol + (int64_t)(qb + 1) * p.Mpad];
+      if constexpr (DROP) wRn = p.Rbits[wcol + (int64_t)(qb + 1) * p.Mpad];
     }
     f32x16 sacc = zero16(), dpacc = zero16();
+    const int qrb = SWZ ? row_base64(c, h, SW_BOTH) : 4 * (c * DP + NS * h);
 #pragma unroll
     for (int s4 = 0; s4 < NS / 4; ++s4) {
-      const f32x4 qv = *reinterpret_cast<const f32x4*>(Qimg + c * DP + NS * h + 4 * s4);
+      const f32x4 qv = lds_f4(lds, SH::KQ + (SWZ ? (qrb ^ (16 * s4)) : qrb + 16 * s4));
 #pragma unroll
       for (int e = 0; e < 4; ++e) sacc = mfma(qv[e], kr[4 * s4 + e], sacc);
     }
 #pragma unroll
     for (int s4 = 0; s4 < NS / 4; ++s4) {
-      const f32x4 xv = *reinterpret_cast<const f32x4*>(Ximg + c * DP + NS * h + 4 * s4);
+      const f32x4 xv = lds_f4(lds, SH::KX + (SWZ ? (qrb ^ (16 * s4)) : qrb + 16 * s4));
 #pragma unroll
       for (int e = 0; e < 4; ++e) dpacc = mfma(xv[e], vr[4 * s4 + e], dpacc);
     }
-    float dsv[16], gv[16], awv[16];
+    // column read of element (query crow(r,h), d = 32t + c) of the Q / dX image at byte offset off
+    int cb[DT];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int ii = i0 + crow(r, h);
-      const bool inside = (ii < p.N) && jv;
-      const f32x4 st = *reinterpret_cast<const f32x4*>(Simg + 4 * crow(r, h));
-      const bool a = DENSE ? inside : ((wA >> crow(r, h)) & 1u);
-      const bool keep = (wR >> crow(r, h)) & 1u;
-      const float dgr = p.dgraph ? ldz(p.dgraph, ((int64_t)bh * p.N + imin(ii, p.N - 1)) * p.M + jc, INT64_MAX, inside) : 0.f;
-      const Elem e = bwd_elem(sacc[r], dpacc[r], kval, a, keep, inside, st[0], st[1], st[2], st[3], p.scale, dscale,
-                              csp, dgr);
-      dsv[r] = e.ds;
-      gv[r] = e.g;
-      awv[r] = e.attw;
-    }
-    // dV^T += dX^T attw  (A: lane d holds dX[query crow(r,h)][d]; queries beyond N carry attw = 0)
+    for (int t = 0; t < DT; ++t) cb[t] = SWZ ? both_base64(t, c, h) : 4 * (32 * t + c) + 16 * DP * h;
+    auto colv = [&](int off, int t, int r) {
+      return SWZ ? both_read(lds, cb[t], r, off) : lds_f1(lds, off + cb[t] + 4 * DP * crow(r, 0));
+    };
+    // Two halves of the query block (registers r = 8 half .. 8 half + 7 = rows 16 half .. 16 half + 15):
+    // elementwise, then the dV / dK / dT K-steps of those rows, then (SWZ) those rows of query block
+    // qb+1 are DMA'd in while the second half runs.
 #pragma unroll
-    for (int t = 0; t < DT; ++t)
+    for (int half = 0; half < 2; ++half) {
+      float dsv[8], gv[8], awv[8];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) dv[t] = mfma(Ximg[crow(r, h) * DP + 32 * t + c], awv[r], dv[t]);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (more) dma_rows<D>(Xl, xr_, 4 * D, i0 + 32, p.N);
-    // dK^T += Q^T ds
+      for (int rr = 0; rr < 8; ++rr) {
+        const int r = 8 * half + rr;
+        const int ii = i0 + crow(r, h);
+        const bool inside = (ii < p.N) && jv;
+        const f32x4 st = lds_f4(lds, SH::KS + 16 * crow(r, h));
+        const bool a = DENSE ? inside : ((wA >> crow(r, h)) & 1u);
+        const bool keep = (wR >> crow(r, h)) & 1u;
+        const float dgr = DG ? ldz(p.dgraph, ((int64_t)bh * p.N + imin(ii, p.N - 1)) * p.M + jc, INT64_MAX, inside) : 0.f;
+        const Elem e = bwd_elem(sacc[r], kbias, dpacc[r], a, keep, inside, st[0], st[1], st[2], st[3], p.scale, dscale,
+                                csp, dgr);
+        dsv[rr] = e.ds;
+        gv[rr] = e.g;
+        awv[rr] = e.attw;
+      }
+      // dV^T += dX^T attw ; dK^T += Q^T ds ; dT^T += Qh^T G  (queries beyond N carry zeros)
 #pragma unroll
-    for (int t = 0; t < DT; ++t)
+      for (int t = 0; t < DT; ++t)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) dk[t] = mfma(Qimg[crow(r, h) * DP + 32 * t + c], dsv[r], dk[t]);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (more) dma_rows<D>(Ql, qr_, qld, i0 + 32, p.N);
-    // dT^T += Qh^T G
-    if constexpr (!DENSE) {
+        for (int rr = 0; rr < 8; ++rr) dv[t] = mfma(colv(SH::KX, t, 8 * half + rr), awv[rr], dv[t]);
 #pragma unroll
-      for (int at = 0; at < KTA; ++at)
+      for (int t = 0; t < DT; ++t)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float v = Himg[crow(r, h) * KP + (KP >= 32 ? 32 * at + c : hcol)];
-          dtt[at] = mfma((KP >= 32 || c < KP) ? v : 0.f, gv[r], dtt[at]);
+        for (int rr = 0; rr < 8; ++rr) dk[t] = mfma(colv(SH::KQ, t, 8 * half + rr), dsv[rr], dk[t]);
+      if constexpr (!DENSE) {
+#pragma unroll
+        for (int at = 0; at < KTA; ++at)
+#pragma unroll
+          for (int rr = 0; rr < 8; ++rr) {
+            const int r = 8 * half + rr;
+            const float v = lds_f1(lds, SH::KH + narrow_elem(crow(r, h), imin(32 * at + c, KP - 1), KPN));
+            dtt[at] = mfma((KP >= 32 || c < KP) ? v : 0.f, gv[rr], dtt[at]);
+          }
+      }
+      if (more) {
+        if constexpr (SWZ) {  // rows 16 half .. 16 half + 15 of every image are free again
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          dma64(Xl, xr_, xpat, 4 * D, i0 + 32, 4 * half, 4 * half + 4);
+          dma64(Ql, qr_, qpat, qld, i0 + 32, 4 * half, 4 * half + 4);
+          if constexpr (!DENSE) dma_narrow(Hl, hr_, i0 + 32, KPN, half, half + 1);
+          dma_tile_contig<4>(Sl, sr_, i0 + 32, half, half + 1);
+        } else if (half == 1) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          dma_rows<D>(Xl, xr_, 4 * D, i0 + 32, p.N);
+          dma_rows<D>(Ql, qr_, qld, i0 + 32, p.N);
+          if constexpr (!DENSE) dma_narrow(Hl, hr_, i0 + 32, KPN);
+          dma_tile_contig<4>(Sl, sr_, i0 + 32);
         }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (more) {
-      if constexpr (!DENSE) dma_tile_contig<KP>(Hl, hr_, i0 + 32);
-      dma_tile_contig<4>(Sl, sr_, i0 + 32);
+      }
     }
   }
   store_rows<DT>(p.dK + ((int64_t)bh * p.M + j) * D, D, D, dk, jv);
@@ -1667,6 +1719,35 @@ csa_status launch_fwd(const csa_sbm_fwd_args* a, const Layout& L, hipStream_t st
   return check_launch("csa_sbm_fwd");
 }
 
+template <int D, int KPH, bool DENSE, bool DROP, bool DG>
+void launch_attn_bwd_v(const KArgs& p, int BH, const Layout& L, const csa_prof* pf, hipStream_t st) {
+  using SH = AttnBwdShape<D, KPH>;
+  {
+    Stage sg(pf, CSA_STAGE_ATTN_BWD_Q, st);
+    const size_t lds_bytes = SH::q_bytes((int)L.Mpad);
+    if (lds_bytes > 64 * 1024)
+      (void)hipFuncSetAttribute((const void*)k_attn_bwd_q<D, KPH, DENSE, DROP, DG>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+    hipLaunchKernelGGL((k_attn_bwd_q<D, KPH, DENSE, DROP, DG>), dim3(xcd_grid((int)L.NQB, BH)), dim3(64), lds_bytes,
+                       st, p);
+  }
+  Stage sg(pf, CSA_STAGE_ATTN_BWD_KV, st);
+  hipLaunchKernelGGL((k_attn_bwd_kv<D, KPH, DENSE, DROP, DG>), dim3(xcd_grid((int)L.NKB, BH)), dim3(64), SH::KV_BYTES,
+                     st, p);
+}
+
+template <int D, int KPH, bool DENSE>
+void launch_attn_bwd(const KArgs& p, int BH, const Layout& L, bool drop, const csa_prof* pf, hipStream_t st) {
+  const bool dg = p.dgraph != nullptr;
+  if (drop) {
+    if (dg) launch_attn_bwd_v<D, KPH, DENSE, true, true>(p, BH, L, pf, st);
+    else launch_attn_bwd_v<D, KPH, DENSE, true, false>(p, BH, L, pf, st);
+  } else {
+    if (dg) launch_attn_bwd_v<D, KPH, DENSE, false, true>(p, BH, L, pf, st);
+    else launch_attn_bwd_v<D, KPH, DENSE, false, false>(p, BH, L, pf, st);
+  }
+}
+
 template <int D, int KPH, int KT>
 csa_status launch_bwd(const csa_sbm_bwd_args* b, const Layout& L, hipStream_t st) {
   const csa_sbm_fwd_args* a = b->fwd;
@@ -1682,16 +1763,7 @@ csa_status launch_bwd(const csa_sbm_bwd_args* b, const Layout& L, hipStream_t st
   (void)dense;
   const csa_prof* pf = b->prof;
   if constexpr (KT > 0) {
-    {
-      Stage sg(pf, CSA_STAGE_ATTN_BWD_Q, st);
-      constexpr size_t lds_bytes = AttnBwdShape<D, KPH>::Q_BYTES;
-      hipLaunchKernelGGL((k_attn_bwd_q<D, KPH, false>), dim3(xcd_grid((int)L.NQB, BH)), dim3(64), lds_bytes, st, p);
-    }
-    {
-      Stage sg(pf, CSA_STAGE_ATTN_BWD_KV, st);
-      constexpr size_t lds_bytes = AttnBwdShape<D, KPH>::KV_BYTES;
-      hipLaunchKernelGGL((k_attn_bwd_kv<D, KPH, false>), dim3(xcd_grid((int)L.NKB, BH)), dim3(64), lds_bytes, st, p);
-    }
+    launch_attn_bwd<D, KPH, false>(p, BH, L, a->attn_dropout > 0.f, pf, st);
     using Sh = ProjBwdShape<D, KT>;
     if (!Sh::REGACC && hipMemsetAsync(p.slab, 0, sizeof(float) * a->H * L.G * L.slab_floats, st) != hipSuccess)
       return check_launch("memset slabs");
@@ -1712,14 +1784,7 @@ csa_status launch_bwd(const csa_sbm_bwd_args* b, const Layout& L, hipStream_t st
     hipLaunchKernelGGL(k_cluster_grad, dim3(a->H), dim3(256), 0, st, p.S, (const float*)dS_ws,
                        (const float*)dC_ws, a->cluster_w, b->dcluster_w, (int)a->k, D, KP32);
   } else {
-    {
-      Stage sg(pf, CSA_STAGE_ATTN_BWD_Q, st);
-      constexpr size_t lds_bytes = AttnBwdShape<D, 0>::Q_BYTES;
-      hipLaunchKernelGGL((k_attn_bwd_q<D, 0, true>), dim3(xcd_grid((int)L.NQB, BH)), dim3(64), lds_bytes, st, p);
-    }
-    Stage sg(pf, CSA_STAGE_ATTN_BWD_KV, st);
-    constexpr size_t lds_bytes = AttnBwdShape<D, 0>::KV_BYTES;
-    hipLaunchKernelGGL((k_attn_bwd_kv<D, 0, true>), dim3(xcd_grid((int)L.NKB, BH)), dim3(64), lds_bytes, st, p);
+    launch_attn_bwd<D, 0, true>(p, BH, L, a->attn_dropout > 0.f, pf, st);
   }
   return check_launch("csa_sbm_bwd");
 }
