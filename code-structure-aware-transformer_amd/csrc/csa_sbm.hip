@@ -115,6 +115,33 @@ __device__ __forceinline__ f32x4 frag4(const float* __restrict__ f, int it, int 
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, lane_id() * 16, soff, 0));
 }
 
+// out[t] += sum_{s < 4 S4N} frag(t)[s] * bval(s) for t < NTO, fragments fetched exactly one K-group
+// (4 steps) ahead: the 4 NTO MFMAs of a group (>= 256 cycles) cover the L2 latency of the next
+// group's fragment loads, and the sched fence keeps the lookahead (and its registers) at one group.
+template <int NTO, int S4N, typename BF>
+__device__ __forceinline__ void frag_chain(const float* __restrict__ frag, int nsteps, f32x16 (&out)[NTO], BF bval) {
+  f32x4 wc[NTO];
+#pragma unroll
+  for (int t = 0; t < NTO; ++t) wc[t] = frag4(frag, t, nsteps, 0);
+#pragma unroll
+  for (int s4 = 0; s4 < S4N; ++s4) {
+    f32x4 wn[NTO];
+    if (s4 + 1 < S4N) {
+#pragma unroll
+      for (int t = 0; t < NTO; ++t) wn[t] = frag4(frag, t, nsteps, s4 + 1);
+    }
+#pragma unroll
+    for (int t = 0; t < NTO; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) out[t] = mfma(wc[t][e], bval(4 * s4 + e), out[t]);
+    fence_sched();
+    if (s4 + 1 < S4N) {
+#pragma unroll
+      for (int t = 0; t < NTO; ++t) wc[t] = wn[t];
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------
 // F1: S_h = softmax over all k^2 entries of C_h C_h^T, zero-padded to (32KT x 32KT)
 // ------------------------------------------------------------------------------------
@@ -256,16 +283,7 @@ __device__ __forceinline__ void mlp_layer0(const KArgs& p, const float (&x)[D / 
   for (int ot = 0; ot < DT; ++ot)
 #pragma unroll
     for (int r = 0; r < 16; ++r) h1[ot][r] = p.pb[0][32 * ot + crow(r, h)];
-#pragma unroll
-  for (int s4 = 0; s4 < NS / 4; ++s4) {
-#pragma unroll
-    for (int ot = 0; ot < DT; ++ot) {
-      const f32x4 w = frag4(p.Wf[0], ot, NS, s4);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) h1[ot] = mfma(w[j], x[4 * s4 + j], h1[ot]);
-    }
-    if ((s4 & 1) == 1) fence_sched();
-  }
+  frag_chain<DT, NS / 4>(p.Wf[0], NS, h1, [&](int s) { return x[s]; });
   mlp_act<D>(p, h1, 0, row, bh, isK);
 }
 
@@ -278,18 +296,7 @@ __device__ __forceinline__ void mlp_layer(const KArgs& p, const f32x16 (&in)[D /
   for (int ot = 0; ot < DT; ++ot)
 #pragma unroll
     for (int r = 0; r < 16; ++r) out[ot][r] = p.pb[l][32 * ot + crow(r, h)];
-#pragma unroll
-  for (int t = 0; t < DT; ++t)
-#pragma unroll
-    for (int r4 = 0; r4 < 4; ++r4) {
-#pragma unroll
-      for (int ot = 0; ot < DT; ++ot) {
-        const f32x4 w = frag4(p.Wf[l], ot, NS, 4 * t + r4);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) out[ot] = mfma(w[j], in[t][4 * r4 + j], out[ot]);
-      }
-      if ((r4 & 1) == 1) fence_sched();
-    }
+  frag_chain<DT, NS / 4>(p.Wf[l], NS, out, [&](int s) { return in[s / 16][s % 16]; });
 }
 
 template <int D>
@@ -308,17 +315,10 @@ __device__ __forceinline__ void cluster_hat(const KArgs& p, const f32x16 (&po)[D
   const int h = lane_id() >> 5;
   const float* Cf = p.Cf + (size_t)hd * 32 * KT * D;
 #pragma unroll
+  for (int kt = 0; kt < KT; ++kt) hat[kt] = zero16();
+  frag_chain<KT, NS / 4>(Cf, NS, hat, [&](int s) { return po[s / 16][s % 16]; });
+#pragma unroll
   for (int kt = 0; kt < KT; ++kt) {
-    hat[kt] = zero16();
-#pragma unroll
-    for (int s4 = 0; s4 < NS / 4; ++s4) {
-      const f32x4 w = frag4(Cf, kt, NS, s4);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int s = 4 * s4 + j;
-        hat[kt] = mfma(w[j], po[s / 16][s % 16], hat[kt]);
-      }
-    }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int a = 32 * kt + crow(r, h);
@@ -331,18 +331,8 @@ __device__ __forceinline__ void cluster_hat(const KArgs& p, const f32x16 (&po)[D
 template <int KT>
 __device__ __forceinline__ void small_mm(const float* __restrict__ frag, const f32x16 (&in)[KT], f32x16 (&out)[KT]) {
 #pragma unroll
-  for (int at = 0; at < KT; ++at) {
-    out[at] = zero16();
-#pragma unroll
-    for (int s4 = 0; s4 < 4 * KT; ++s4) {
-      const f32x4 w = frag4(frag, at, 16 * KT, s4);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int s = 4 * s4 + j;
-        out[at] = mfma(w[j], in[s / 16][s % 16], out[at]);
-      }
-    }
-  }
+  for (int at = 0; at < KT; ++at) out[at] = zero16();
+  frag_chain<KT, 4 * KT>(frag, 16 * KT, out, [&](int s) { return in[s / 16][s % 16]; });
 }
 
 // Store an accumulator tile set (feature rows, data row = lane) to out[row][0..ncols) (row-major, ld)
@@ -1243,24 +1233,12 @@ __device__ __forceinline__ void outer_stage(const float* ds, const float* in, f3
 }
 
 // out^T = Wfrag^T-style product: out[it] = sum_s frag[it][s] * in[s/16][s%16] (acc-perm input)
-template <int NTO, int NTI>
+// (S4MAX < NSTEP/4: only the first 4 S4MAX K-steps, for inputs known to be zero beyond them.)
+template <int NTO, int NTI, int S4MAX = 4 * NTI>
 __device__ __forceinline__ void mm_acc(const float* __restrict__ frag, const f32x16 (&in)[NTI], f32x16 (&out)[NTO]) {
-  constexpr int NSTEP = 16 * NTI;
 #pragma unroll
   for (int t = 0; t < NTO; ++t) out[t] = zero16();
-#pragma unroll
-  for (int s4 = 0; s4 < NSTEP / 4; ++s4) {
-#pragma unroll
-    for (int t = 0; t < NTO; ++t) {
-      const f32x4 w = frag4(frag, t, NSTEP, s4);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int s = 4 * s4 + e;
-        out[t] = mfma(w[e], in[s / 16][s % 16], out[t]);
-      }
-    }
-    if ((s4 & 1) == 1) fence_sched();
-  }
+  frag_chain<NTO, S4MAX>(frag, 16 * NTI, out, [&](int s) { return in[s / 16][s % 16]; });
 }
 
 template <int D, int KT>
@@ -1449,6 +1427,262 @@ __global__ __launch_bounds__(256, (D <= 64 && KT <= 1 ? 2 : 1)) void k_proj_bwd(
       slab[3 * D * D + tid] = dbacc[0];
       slab[3 * D * D + D + tid] = dbacc[1];
       slab[3 * D * D + 2 * D + tid] = dbacc[2];
+    }
+  }
+}
+
+__device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 acc) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+}
+
+// ------------------------------------------------------------------------------------
+// B3s: projection backward for k <= 16 clusters and d = 64 (config/python.py and java sizes of k).
+// Same math and slab layout as k_proj_bwd. Differences:
+//  * dS_h and dC_h are k x k and k x d: each wave accumulates them over its OWN items with 16x16x4
+//    MFMAs (dT^T Kh from a global-load operand and the hat block; dZ^T po through a wave-private
+//    transpose), so these two small products need no barriers; the 4 wave partials are summed in a
+//    fixed order once per workgroup.
+//  * only the three d x d products dW2, dW1, dW0 go through the shared staging (one 32x32 tile per
+//    wave per stage), and each wave's next chain product runs between the two barriers of a stage:
+//    6 barriers per group of 4 items instead of 10, no idle waves.
+//  * chain products over the cluster index stop at K = 16.
+// ------------------------------------------------------------------------------------
+template <int D>
+struct ProjBwdSmallShape {
+  static constexpr int DT = D / 32, NS = D / 2, REG = D * 32;
+  static constexpr int HATF = 16 * 32;                       // hat block: 16 features x 32 rows
+  static constexpr size_t LDS_BYTES = sizeof(float) * (8 * REG + 4 * HATF);
+};
+
+template <int D>
+__global__ __launch_bounds__(256, 2) void k_proj_bwd_s(const KArgs p) {
+  static_assert(D == 64, "4 d x d tiles per stage = one per wave");
+  using Sh = ProjBwdSmallShape<D>;
+  using Sf = ProjBwdShape<D, 1>;  // slab layout
+  constexpr int DT = Sh::DT, NS = Sh::NS, REG = Sh::REG, ABLK = Sf::ABLK;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* DS = lds;
+  float* IN = lds + 4 * REG;
+  const int lane = lane_id(), c = lane & 31, h = lane >> 5, c16 = lane & 15, g4 = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int hd = blockIdx.y, g = blockIdx.x, G = gridDim.x;
+  const int b_lo = (int)((int64_t)g * p.B / G), b_hi = (int)((int64_t)(g + 1) * p.B / G);
+  const int per_b = p.NQB + p.NKB;
+  const int n_items = (b_hi - b_lo) * per_b;
+  float* slab = p.slab + ((int64_t)hd * G + g) * p.slab_floats;
+  const float ks = p.proj_p > 0.f ? 1.f / (1.f - p.proj_p) : 1.f;
+  const float* CfT = p.CfT + (size_t)hd * 32 * D;
+  const float* SfT = p.SfT + (size_t)hd * 32 * 32;
+  float* DSw = DS + w * REG;
+  float* INw = IN + w * REG;
+  float* HATw = lds + 8 * REG + w * Sh::HATF;
+  const uint32_t INl = lds_offset(IN) + 4 * REG * w, HATl = lds_offset(lds) + 4 * (8 * REG + w * Sh::HATF);
+  f32x16 acc[3];  // this wave's tile (ot = w >> 1, it = w & 1) of dW2, dW1, dW0
+#pragma unroll
+  for (int i = 0; i < 3; ++i) acc[i] = zero16();
+  f32x4 accS = {0.f, 0.f, 0.f, 0.f}, accC[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) accC[t] = accS;
+  float dbacc[3] = {0.f, 0.f, 0.f};
+
+  struct Item { int b, r, isK, rb, nrows; bool has; };
+  auto item_of = [&](int grp) {
+    Item it;
+    const int item = grp * 4 + w;
+    it.has = item < n_items;
+    it.b = b_lo + (it.has ? item / per_b : 0);
+    it.r = it.has ? item % per_b : 0;
+    it.isK = it.r >= p.NQB;
+    it.rb = it.isK ? it.r - p.NQB : it.r;
+    it.nrows = it.isK ? p.M : p.N;
+    return it;
+  };
+  auto act_rsrc = [&](const Item& it) {
+    return make_rsrc(p.Act + ((int64_t)(it.b * p.H + hd) * per_b + it.r) * ABLK, ABLK * 4);
+  };
+  // per-item operands issued one group ahead: hat block (DMA), dT / dQh rows (acc orientation) and,
+  // for K items, dT as the 16x16x4 A operand (lane (c16, g4), step s: dT[row 4s + g4][cluster c16])
+  f32x16 gin[1];
+  float dTt[8];
+  auto prefetch_hat = [&](const Item& it) { dma_block16<2048>(HATl, act_rsrc(it), 96 * D * 4); };
+  auto prefetch = [&](const Item& it) {
+    const int row = it.rb * 32 + c, rowc = imin(row, it.nrows - 1), bh = it.b * p.H + hd;
+    load_rows<1>(gin, (it.isK ? p.dT + ((int64_t)bh * p.M + rowc) * p.kp : p.dQh + ((int64_t)bh * p.N + rowc) * p.kp),
+                 p.kp, it.has && row < it.nrows);
+    const float* dTb = p.dT + (int64_t)bh * p.M * p.kp;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int rr = it.rb * 32 + 4 * s + g4;
+      dTt[s] = ldz(dTb, (int64_t)imin(rr, p.M - 1) * p.kp + c16, INT64_MAX, it.has && it.isK && rr < p.M);
+    }
+  };
+  prefetch_hat(item_of(0));
+  prefetch(item_of(0));
+
+  for (int grp = 0; grp * 4 < n_items; ++grp) {
+    int tid = threadIdx.x;  // opaque: per-lane addresses are recomputed in the loop, not hoisted
+    asm volatile("" : "+v"(tid));
+    const int ln = tid & 63;
+    const Item it = item_of(grp);
+    const int row = it.rb * 32 + c;
+    const bool rv = it.has && row < it.nrows;
+    const int rowc = imin(row, it.nrows - 1);
+    const int bh = it.b * p.H + hd;
+    const __amdgpu_buffer_rsrc_t ar = act_rsrc(it);
+    wait_vm_all();  // hat block, gin, dTt
+    // ---- dS_h += dT^T Kh (K items), private 16x16x4: B = Kh[row 4s + g4][cluster c16] from the hat block
+    if (it.isK) {
+#pragma unroll
+      for (int s = 0; s < 8; ++s) accS = mfma16(dTt[s], HATw[act_off(c16, 4 * s + g4)], accS);
+    }
+    // ---- hat (acc orientation, clusters >= 16 are zero) and dZ = (S^T dT | dQh) * hat (1 - hat)
+    f32x16 hat;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) hat[r] = r < 8 ? HATw[act_off(crow(r, h), c)] : 0.f;
+    f32x16 dz[1];
+    if (it.isK) {
+      mm_acc<1, 1, 2>(SfT, gin, dz);  // dKh^T = S^T dT^T (clusters < 16)
+    } else {
+      dz[0] = gin[0];
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dz[0][r] = r < 8 ? dz[0][r] * hat[r] * (1.f - hat[r]) : 0.f;
+    // dZ -> wave-private transpose scratch in the (free) DS region: [row][cluster], 16 clusters per row
+#pragma unroll
+    for (int g2 = 0; g2 < 2; ++g2) {
+      f32x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = dz[0][4 * g2 + e];
+      *reinterpret_cast<f32x4*>(DSw + c * 16 + 8 * g2 + 4 * h) = v;
+    }
+    dma_block16<D * 128>(INl, ar, 64 * D * 4);  // po -> own IN region
+    // ---- dp^T = C^T dZ^T (clusters < 16)
+    f32x16 dcur[DT];
+    mm_acc<DT, 1, 2>(CfT, dz, dcur);
+    wait_vm_all();  // po
+    // ---- dC_h += dZ^T po, private 16x16x4: A = dZ[row 4s + g4][cluster c16], B = po[row 4s + g4][16t + c16]
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const float a = DSw[(4 * s + g4) * 16 + c16];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) accC[t] = mfma16(a, INw[act_off(16 * t + c16, 4 * s + g4)], accC[t]);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // ---- layer 2 (proj.6): stage dp, h2 -> IN; dh2_pre = W2^T dp under the DMA
+    stage_ds<DT>(DSw, dcur, D, ln);
+    dma_block16<D * 128>(INl, ar, 32 * D * 4);  // h2
+    f32x16 dh[DT];
+    mm_acc<DT, DT>(p.WfT[2], dcur, dh);
+    wait_vm_all();
+    __syncthreads();  // B1: dp, h2 of every wave staged
+    acc[0] = outer_tile<REG>(DS, IN, w >> 1, w & 1, acc[0], ln);
+    if (tid < D) dbacc[2] += region_rowsum<REG>(DS, tid);
+    {
+      f32x16 hv[DT];
+      read_act<DT>(hv, INw, ln);  // own h2 (relu mask)
+#pragma unroll
+      for (int t = 0; t < DT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dcur[t][r] = (hv[t][r] > 0.f) ? dh[t][r] * ks : 0.f;
+    }
+    __syncthreads();  // B2: stage dW2 read out
+    // ---- layer 1 (proj.3): stage dh2, h1 -> IN and x rows under dh1_pre = W1^T dh2
+    stage_ds<DT>(DSw, dcur, D, ln);
+    dma_block16<D * 128>(INl, ar, 0);  // h1
+    float x[NS];
+    {
+      const float* X = it.isK ? p.K + it.b * p.k_sb + hd * p.k_sh + (int64_t)rowc * p.k_sn
+                              : p.Q + it.b * p.q_sb + hd * p.q_sh + (int64_t)rowc * p.q_sn;
+      load_run<NS>(x, X + h * NS, rv);
+    }
+    mm_acc<DT, DT>(p.WfT[1], dcur, dh);
+    wait_vm_all();
+    __syncthreads();  // B3
+    acc[1] = outer_tile<REG>(DS, IN, w >> 1, w & 1, acc[1], ln);
+    if (tid < D) dbacc[1] += region_rowsum<REG>(DS, tid);
+    {
+      f32x16 hv[DT];
+      read_act<DT>(hv, INw, ln);  // own h1 (relu mask)
+#pragma unroll
+      for (int t = 0; t < DT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dcur[t][r] = (hv[t][r] > 0.f) ? dh[t][r] * ks : 0.f;
+    }
+    __syncthreads();  // B4
+    // ---- layer 0 (proj.0): stage dh1, x -> IN; this item's dQ / dK rows load under the last stage
+    stage_ds<DT>(DSw, dcur, D, ln);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) INw[act_off(s + NS * h, c)] = x[s];
+    float* dst = it.isK ? p.dK + ((int64_t)bh * p.M + rowc) * D : p.dQ + ((int64_t)bh * p.N + rowc) * D;
+    f32x4 old[2 * DT];
+#pragma unroll
+    for (int t = 0; t < DT; ++t)
+#pragma unroll
+      for (int g2 = 0; g2 < 4; g2 += 2) old[2 * t + g2 / 2] = *reinterpret_cast<const f32x4*>(dst + 32 * t + 8 * g2 + 4 * h);
+    f32x4 old2[2 * DT];
+#pragma unroll
+    for (int t = 0; t < DT; ++t)
+#pragma unroll
+      for (int g2 = 1; g2 < 4; g2 += 2) old2[2 * t + g2 / 2] = *reinterpret_cast<const f32x4*>(dst + 32 * t + 8 * g2 + 4 * h);
+    const bool more = (grp + 1) * 4 < n_items;
+    if (more) prefetch_hat(item_of(grp + 1));  // hat block is private: free again
+    __syncthreads();  // B5
+    acc[2] = outer_tile<REG>(DS, IN, w >> 1, w & 1, acc[2], ln);
+    if (tid < D) dbacc[0] += region_rowsum<REG>(DS, tid);
+    f32x16 dxm[DT];
+    mm_acc<DT, DT>(p.WfT[0], dcur, dxm);  // second-path dx = W0^T dh1
+    if (rv) {  // dQ / dK += MLP backward
+#pragma unroll
+      for (int t = 0; t < DT; ++t)
+#pragma unroll
+        for (int g2 = 0; g2 < 4; ++g2) {
+          f32x4 v = (g2 & 1) ? old2[2 * t + g2 / 2] : old[2 * t + g2 / 2];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += dxm[t][4 * g2 + e];
+          *reinterpret_cast<f32x4*>(dst + 32 * t + 8 * g2 + 4 * h) = v;
+        }
+    }
+    if (more) prefetch(item_of(grp + 1));  // next group's dT / dQh rows (registers: issued after dx is out)
+    __syncthreads();  // B6: DS / IN free for the next group
+  }
+  // ---- slab: dW tiles and bias sums (written once), dS / dC summed over the 4 waves in a fixed order
+#pragma unroll
+  for (int l = 0; l < 3; ++l) {
+    const TileDst<D, 1> t = tile_dst<D, 1>(slab, (l == 0 ? Sf::G_W2 : l == 1 ? Sf::G_W1 : Sf::G_W0) + w);
+    tile_store<0>(t.base, t.ldo, t.orows, t.icols, t.ot, t.it, acc[l], false, lane);
+  }
+  const int tid = threadIdx.x;
+  if (tid < D) {
+    slab[3 * D * D + tid] = dbacc[0];
+    slab[3 * D * D + D + tid] = dbacc[1];
+    slab[3 * D * D + 2 * D + tid] = dbacc[2];
+  }
+  float* part = lds + w * (16 * 16 + 16 * D);  // [dS 16 x 16 | dC 16 x D] of this wave
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    part[(4 * g4 + e) * 16 + c16] = accS[e];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) part[256 + (4 * g4 + e) * D + 16 * t + c16] = accC[t][e];
+  }
+  __syncthreads();
+  float* sC = slab + 3 * D * D + 3 * D;  // (32 x D), rows >= 16 zero
+  float* sS = sC + 32 * D;               // (32 x 32), rows / cols >= 16 zero
+  for (int e = tid; e < 32 * D + 32 * 32; e += 256) {
+    float v = 0.f;
+    if (e < 32 * D) {
+      const int a = e / D, f = e % D;
+      if (a < 16) {
+#pragma unroll
+        for (int ww = 0; ww < 4; ++ww) v += lds[ww * (256 + 16 * D) + 256 + a * D + f];
+      }
+      sC[e] = v;
+    } else {
+      const int q = e - 32 * D, a = q / 32, bb = q % 32;
+      if (a < 16 && bb < 16) {
+#pragma unroll
+        for (int ww = 0; ww < 4; ++ww) v += lds[ww * (256 + 16 * D) + a * 16 + bb];
+      }
+      sS[q] = v;
     }
   }
 }
@@ -1767,11 +2001,18 @@ csa_status launch_bwd(const csa_sbm_bwd_args* b, const Layout& L, hipStream_t st
     using Sh = ProjBwdShape<D, KT>;
     if (!Sh::REGACC && hipMemsetAsync(p.slab, 0, sizeof(float) * a->H * L.G * L.slab_floats, st) != hipSuccess)
       return check_launch("memset slabs");
-    (void)hipFuncSetAttribute((const void*)k_proj_bwd<D, KT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)Sh::LDS_BYTES);
     {
       Stage sg(pf, CSA_STAGE_PROJ_BWD, st);
-      hipLaunchKernelGGL((k_proj_bwd<D, KT>), dim3(L.G, a->H), dim3(256), Sh::LDS_BYTES, st, p);
+      if constexpr (D == 64 && KPH == 8) {  // k <= 16
+        using Ss = ProjBwdSmallShape<D>;
+        (void)hipFuncSetAttribute((const void*)k_proj_bwd_s<D>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)Ss::LDS_BYTES);
+        hipLaunchKernelGGL((k_proj_bwd_s<D>), dim3(L.G, a->H), dim3(256), Ss::LDS_BYTES, st, p);
+      } else {
+        (void)hipFuncSetAttribute((const void*)k_proj_bwd<D, KT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)Sh::LDS_BYTES);
+        hipLaunchKernelGGL((k_proj_bwd<D, KT>), dim3(L.G, a->H), dim3(256), Sh::LDS_BYTES, st, p);
+      }
     }
     Stage sr(pf, CSA_STAGE_REDUCE, st);
     const int KP32 = 32 * KT;
