@@ -146,19 +146,33 @@ __device__ __forceinline__ void frag_chain(const float* __restrict__ frag, int n
 // F1: S_h = softmax over all k^2 entries of C_h C_h^T, zero-padded to (32KT x 32KT)
 // ------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_cluster_softmax(const float* __restrict__ C, float* __restrict__ S,
-                                                         int k, int D, int KP32) {
+                                                         int k, int D, int KP32, unsigned long long* __restrict__ cnt,
+                                                         int H) {
+  // C_h (k x D <= 128 x 96) staged in LDS; each thread keeps its (up to 64) logits in registers
+  // across the max / sum / normalise passes (one dot product per entry instead of three).
+  constexpr int MAXE = 64;  // k^2 <= 128^2 = 256 threads x 64
   const int hd = blockIdx.x, tid = threadIdx.x;
+  if (hd == 0 && tid < H) cnt[tid] = 0ull;  // this call's edge counters (k_attn_fwd) start at zero
+  __shared__ float Cs[128 * 96];
   __shared__ float red[256];
   const float* Ch = C + (size_t)hd * k * D;
+  for (int e = tid; e < k * D; e += 256) Cs[e] = Ch[e];
+  __syncthreads();
   const int kk = k * k;
-  auto dist = [&](int e) {
-    const int a = e / k, b = e % k;
-    float acc = 0.f;
-    for (int t = 0; t < D; ++t) acc = fmaf(Ch[a * D + t], Ch[b * D + t], acc);
-    return acc;
-  };
+  float v[MAXE];
   float mx = NEG_INF;
-  for (int e = tid; e < kk; e += 256) mx = fmaxf(mx, dist(e));
+#pragma unroll
+  for (int q = 0; q < MAXE; ++q) {
+    const int e = tid + 256 * q;
+    v[q] = NEG_INF;
+    if (e < kk) {
+      const int a = e / k, b = e % k;
+      float acc = 0.f;
+      for (int t = 0; t < D; ++t) acc = fmaf(Cs[a * D + t], Cs[b * D + t], acc);
+      v[q] = acc;
+      mx = fmaxf(mx, acc);
+    }
+  }
   red[tid] = mx;
   __syncthreads();
   for (int s = 128; s > 0; s >>= 1) {
@@ -168,7 +182,12 @@ __global__ __launch_bounds__(256) void k_cluster_softmax(const float* __restrict
   mx = red[0];
   __syncthreads();
   float sm = 0.f;
-  for (int e = tid; e < kk; e += 256) sm += expf(dist(e) - mx);
+#pragma unroll
+  for (int q = 0; q < MAXE; ++q) {
+    const int e = tid + 256 * q;
+    v[q] = e < kk ? expf(v[q] - mx) : 0.f;
+    sm += v[q];
+  }
   red[tid] = sm;
   __syncthreads();
   for (int s = 128; s > 0; s >>= 1) {
@@ -177,9 +196,12 @@ __global__ __launch_bounds__(256) void k_cluster_softmax(const float* __restrict
   }
   sm = red[0];
   float* Sh = S + (size_t)hd * KP32 * KP32;
-  for (int e = tid; e < KP32 * KP32; e += 256) {
-    const int a = e / KP32, b = e % KP32;
-    Sh[e] = (a < k && b < k) ? expf(dist(a * k + b) - mx) / sm : 0.f;
+  for (int e = tid; e < KP32 * KP32; e += 256) Sh[e] = 0.f;
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < MAXE; ++q) {
+    const int e = tid + 256 * q;
+    if (e < kk) Sh[(e / k) * KP32 + e % k] = v[q] / sm;
   }
 }
 
@@ -1913,7 +1935,8 @@ csa_status launch_fwd(const csa_sbm_fwd_args* a, const Layout& L, hipStream_t st
     float* S = (float*)((char*)a->state + L.S);
     {
     Stage sg(a->prof, CSA_STAGE_PREP, st);
-    hipLaunchKernelGGL(k_cluster_softmax, dim3(a->H), dim3(256), 0, st, a->cluster_w, S, (int)a->k, D, KP32);
+    hipLaunchKernelGGL(k_cluster_softmax, dim3(a->H), dim3(256), 0, st, a->cluster_w, S, (int)a->k, D, KP32, p.cnt,
+                       (int)a->H);
     FragJobs J;
     memset(&J, 0, sizeof(J));
     int n = 0;
@@ -1933,8 +1956,6 @@ csa_status launch_fwd(const csa_sbm_fwd_args* a, const Layout& L, hipStream_t st
                        (int64_t)KP32 * KP32};
     J.n = n;
     hipLaunchKernelGGL(k_frag_prep, dim3(16, n), dim3(256), 0, st, J);
-    if (hipMemsetAsync(p.cnt, 0, sizeof(unsigned long long) * a->H, st) != hipSuccess)
-      return check_launch("memset counters");
     }
     {
       Stage sg(a->prof, CSA_STAGE_PROJ_FWD, st);
