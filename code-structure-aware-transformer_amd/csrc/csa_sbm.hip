@@ -145,12 +145,13 @@ __device__ __forceinline__ void frag_chain(const float* __restrict__ frag, int n
 // ------------------------------------------------------------------------------------
 // F1: S_h = softmax over all k^2 entries of C_h C_h^T, zero-padded to (32KT x 32KT)
 // ------------------------------------------------------------------------------------
+// MAXE = ceil(k^2 / 256) rounded up to 1, 4, 16 or 64 (host-selected instantiation)
+template <int MAXE>
 __global__ __launch_bounds__(256) void k_cluster_softmax(const float* __restrict__ C, float* __restrict__ S,
                                                          int k, int D, int KP32, unsigned long long* __restrict__ cnt,
                                                          int H) {
-  // C_h (k x D <= 128 x 96) staged in LDS; each thread keeps its (up to 64) logits in registers
+  // C_h (k x D <= 128 x 96) staged in LDS; each thread keeps its (up to MAXE) logits in registers
   // across the max / sum / normalise passes (one dot product per entry instead of three).
-  constexpr int MAXE = 64;  // k^2 <= 128^2 = 256 threads x 64
   const int hd = blockIdx.x, tid = threadIdx.x;
   if (hd == 0 && tid < H) cnt[tid] = 0ull;  // this call's edge counters (k_attn_fwd) start at zero
   __shared__ float Cs[128 * 96];
@@ -344,7 +345,8 @@ __device__ __forceinline__ void cluster_hat(const KArgs& p, const f32x16 (&po)[D
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int a = 32 * kt + crow(r, h);
-      hat[kt][r] = (a < p.k) ? 1.f / (1.f + expf(-hat[kt][r])) : 0.f;
+      // sigmoid via hardware exp / divide (a few ulp; branch-free): sbm_attn.py:47,53
+      hat[kt][r] = (a < p.k) ? __fdividef(1.f, 1.f + __expf(-hat[kt][r])) : 0.f;
     }
   }
 }
@@ -436,7 +438,13 @@ __global__ __launch_bounds__(64) void k_proj_fwd(const KArgs p) {
     store_act<D / 32>(blk, h1);
     store_act<D / 32>(blk + 32 * D, h2);
     store_act<D / 32>(blk + 64 * D, po);
-    store_act<KT>(blk + 96 * D, hat);
+    if (D == 64 && p.kp <= 16) {  // clusters >= 16 are zero and never read back (k_proj_bwd_s: features 0..15)
+      const int cl = lane_id() & 31, hl = lane_id() >> 5;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) blk[96 * D + act_off(crow(r, hl), cl)] = hat[0][r];
+    } else {
+      store_act<KT>(blk + 96 * D, hat);
+    }
   }
   if (!isK) {
     store_rows<KT>(p.Qh + ((int64_t)bh * p.N + row) * p.kp, p.kp, p.kp, hat, rv);
@@ -1552,6 +1560,7 @@ __global__ __launch_bounds__(256, 2) void k_proj_bwd_s(const KArgs p) {
     const int bh = it.b * p.H + hd;
     const __amdgpu_buffer_rsrc_t ar = act_rsrc(it);
     wait_vm_all();  // hat block, gin, dTt
+    dma_block16<D * 128>(INl, ar, 64 * D * 4);  // po -> own IN region (free since B6), lands under dS / dZ / dp
     // ---- dS_h += dT^T Kh (K items), private 16x16x4: B = Kh[row 4s + g4][cluster c16] from the hat block
     if (it.isK) {
 #pragma unroll
@@ -1577,7 +1586,6 @@ __global__ __launch_bounds__(256, 2) void k_proj_bwd_s(const KArgs p) {
       for (int e = 0; e < 4; ++e) v[e] = dz[0][4 * g2 + e];
       *reinterpret_cast<f32x4*>(DSw + c * 16 + 8 * g2 + 4 * h) = v;
     }
-    dma_block16<D * 128>(INl, ar, 64 * D * 4);  // po -> own IN region
     // ---- dp^T = C^T dZ^T (clusters < 16)
     f32x16 dcur[DT];
     mm_acc<DT, 1, 2>(CfT, dz, dcur);
@@ -1935,8 +1943,12 @@ csa_status launch_fwd(const csa_sbm_fwd_args* a, const Layout& L, hipStream_t st
     float* S = (float*)((char*)a->state + L.S);
     {
     Stage sg(a->prof, CSA_STAGE_PREP, st);
-    hipLaunchKernelGGL(k_cluster_softmax, dim3(a->H), dim3(256), 0, st, a->cluster_w, S, (int)a->k, D, KP32, p.cnt,
-                       (int)a->H);
+    {
+      const int kk = (int)(a->k * a->k);
+      auto csm = kk <= 256 ? k_cluster_softmax<1> : kk <= 1024 ? k_cluster_softmax<4>
+               : kk <= 4096 ? k_cluster_softmax<16> : k_cluster_softmax<64>;
+      hipLaunchKernelGGL(csm, dim3(a->H), dim3(256), 0, st, a->cluster_w, S, (int)a->k, D, KP32, p.cnt, (int)a->H);
+    }
     FragJobs J;
     memset(&J, 0, sizeof(J));
     int n = 0;
