@@ -408,7 +408,7 @@ __device__ __forceinline__ void store_act(float* __restrict__ blk, const f32x16 
 #pragma unroll
   for (int t = 0; t < NT; ++t)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) blk[act_off(32 * t + crow(r, h), c)] = a[t][r];
+    for (int r = 0; r < 16; ++r) __builtin_nontemporal_store(a[t][r], blk + act_off(32 * t + crow(r, h), c));
 }
 
 // ------------------------------------------------------------------------------------
@@ -441,7 +441,7 @@ __global__ __launch_bounds__(64) void k_proj_fwd(const KArgs p) {
     if (D == 64 && p.kp <= 16) {  // clusters >= 16 are zero and never read back (k_proj_bwd_s: features 0..15)
       const int cl = lane_id() & 31, hl = lane_id() >> 5;
 #pragma unroll
-      for (int r = 0; r < 8; ++r) blk[96 * D + act_off(crow(r, hl), cl)] = hat[0][r];
+      for (int r = 0; r < 8; ++r) __builtin_nontemporal_store(hat[0][r], blk + 96 * D + act_off(crow(r, hl), cl));
     } else {
       store_act<KT>(blk + 96 * D, hat);
     }
