@@ -1481,7 +1481,8 @@ template <int D>
 struct ProjBwdSmallShape {
   static constexpr int DT = D / 32, NS = D / 2, REG = D * 32;
   static constexpr int HATF = 16 * 32;                       // hat block: 16 features x 32 rows
-  static constexpr size_t LDS_BYTES = sizeof(float) * (8 * REG + 4 * HATF);
+  static constexpr int GINF = 32 * 16;                       // dT / dQh rows of the item: 32 rows x 16
+  static constexpr size_t LDS_BYTES = sizeof(float) * (8 * REG + 4 * HATF + 4 * GINF);  // 80 KiB: 2 per CU
 };
 
 template <int D>
@@ -1507,6 +1508,8 @@ __global__ __launch_bounds__(256, 2) void k_proj_bwd_s(const KArgs p) {
   float* INw = IN + w * REG;
   float* HATw = lds + 8 * REG + w * Sh::HATF;
   const uint32_t INl = lds_offset(IN) + 4 * REG * w, HATl = lds_offset(lds) + 4 * (8 * REG + w * Sh::HATF);
+  const float* GINw = lds + 8 * REG + 4 * Sh::HATF + w * Sh::GINF;
+  const uint32_t GINl = lds_offset(lds) + 4 * (8 * REG + 4 * Sh::HATF + w * Sh::GINF);
   f32x16 acc[3];  // this wave's tile (ot = w >> 1, it = w & 1) of dW2, dW1, dW0
 #pragma unroll
   for (int i = 0; i < 3; ++i) acc[i] = zero16();
@@ -1530,21 +1533,15 @@ __global__ __launch_bounds__(256, 2) void k_proj_bwd_s(const KArgs p) {
   auto act_rsrc = [&](const Item& it) {
     return make_rsrc(p.Act + ((int64_t)(it.b * p.H + hd) * per_b + it.r) * ABLK, ABLK * 4);
   };
-  // per-item operands issued one group ahead: hat block (DMA), dT / dQh rows (acc orientation) and,
-  // for K items, dT as the 16x16x4 A operand (lane (c16, g4), step s: dT[row 4s + g4][cluster c16])
-  f32x16 gin[1];
-  float dTt[8];
+  // per-item operands DMA'd into LDS one group ahead (register-free, so they are issued early):
+  // the hat block and the item's 32 dT / dQh rows, read at the top of the group both in the acc
+  // orientation (lane = row) and as the 16x16x4 A operand (lane (c16, g4), step s: dT[row 4s + g4][c16]).
   auto prefetch_hat = [&](const Item& it) { dma_block16<2048>(HATl, act_rsrc(it), 96 * D * 4); };
   auto prefetch = [&](const Item& it) {
-    const int row = it.rb * 32 + c, rowc = imin(row, it.nrows - 1), bh = it.b * p.H + hd;
-    load_rows<1>(gin, (it.isK ? p.dT + ((int64_t)bh * p.M + rowc) * p.kp : p.dQh + ((int64_t)bh * p.N + rowc) * p.kp),
-                 p.kp, it.has && row < it.nrows);
-    const float* dTb = p.dT + (int64_t)bh * p.M * p.kp;
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      const int rr = it.rb * 32 + 4 * s + g4;
-      dTt[s] = ldz(dTb, (int64_t)imin(rr, p.M - 1) * p.kp + c16, INT64_MAX, it.has && it.isK && rr < p.M);
-    }
+    const int bh = it.b * p.H + hd, row0 = it.rb * 32;
+    const float* src = it.isK ? p.dT + ((int64_t)bh * p.M + row0) * p.kp : p.dQh + ((int64_t)bh * p.N + row0) * p.kp;
+    // rows past the item's last row are outside the descriptor: not fetched (values masked below)
+    dma_block16<2048>(GINl, make_rsrc(src, imin(32, it.nrows - row0) * p.kp * 4), 0);
   };
   prefetch_hat(item_of(0));
   prefetch(item_of(0));
@@ -1561,6 +1558,21 @@ __global__ __launch_bounds__(256, 2) void k_proj_bwd_s(const KArgs p) {
     const __amdgpu_buffer_rsrc_t ar = act_rsrc(it);
     wait_vm_all();  // hat block, gin, dTt
     dma_block16<D * 128>(INl, ar, 64 * D * 4);  // po -> own IN region (free since B6), lands under dS / dZ / dp
+    f32x16 gin[1];
+    float dTt[8];
+#pragma unroll
+    for (int g2 = 0; g2 < 2; ++g2) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(GINw + c * 16 + 8 * g2 + 4 * h);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) gin[0][4 * g2 + e] = rv ? v[e] : 0.f;
+    }
+#pragma unroll
+    for (int r = 8; r < 16; ++r) gin[0][r] = 0.f;  // clusters >= 16
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const float v = GINw[(4 * s + g4) * 16 + c16];
+      dTt[s] = (it.has && it.isK && it.rb * 32 + 4 * s + g4 < p.M) ? v : 0.f;
+    }
     // ---- dS_h += dT^T Kh (K items), private 16x16x4: B = Kh[row 4s + g4][cluster c16] from the hat block
     if (it.isK) {
 #pragma unroll
@@ -1655,7 +1667,10 @@ __global__ __launch_bounds__(256, 2) void k_proj_bwd_s(const KArgs p) {
 #pragma unroll
       for (int g2 = 1; g2 < 4; g2 += 2) old2[2 * t + g2 / 2] = *reinterpret_cast<const f32x4*>(dst + 32 * t + 8 * g2 + 4 * h);
     const bool more = (grp + 1) * 4 < n_items;
-    if (more) prefetch_hat(item_of(grp + 1));  // hat block is private: free again
+    if (more) {  // private hat / gin regions are free again: next group's operands stream in now
+      prefetch_hat(item_of(grp + 1));
+      prefetch(item_of(grp + 1));
+    }
     __syncthreads();  // B5
     acc[2] = outer_tile<REG>(DS, IN, w >> 1, w & 1, acc[2], ln);
     if (tid < D) dbacc[0] += region_rowsum<REG>(DS, tid);
@@ -1672,7 +1687,6 @@ __global__ __launch_bounds__(256, 2) void k_proj_bwd_s(const KArgs p) {
           *reinterpret_cast<f32x4*>(dst + 32 * t + 8 * g2 + 4 * h) = v;
         }
     }
-    if (more) prefetch(item_of(grp + 1));  // next group's dT / dQh rows (registers: issued after dx is out)
     __syncthreads();  // B6: DS / IN free for the next group
   }
   // ---- slab: dW tiles and bias sums (written once), dS / dC summed over the 4 waves in a fixed order
