@@ -1631,11 +1631,12 @@ __global__ __launch_bounds__(256, 2) void k_proj_bwd_s(const KArgs p) {
     // ---- layer 1 (proj.3): stage dh2, h1 -> IN and x rows under dh1_pre = W1^T dh2
     stage_ds<DT>(DSw, dcur, D, ln);
     dma_block16<D * 128>(INl, ar, 0);  // h1
-    float x[NS];
-    {
+    f32x4 x4[NS / 4];  // raw (clamped-row) loads: the row mask is applied when x is staged, so the
+    {                  // loads do not wait here
       const float* X = it.isK ? p.K + it.b * p.k_sb + hd * p.k_sh + (int64_t)rowc * p.k_sn
                               : p.Q + it.b * p.q_sb + hd * p.q_sh + (int64_t)rowc * p.q_sn;
-      load_run<NS>(x, X + h * NS, rv);
+#pragma unroll
+      for (int j = 0; j < NS / 4; ++j) x4[j] = *reinterpret_cast<const f32x4*>(X + h * NS + 4 * j);
     }
     mm_acc<DT, DT>(p.WfT[1], dcur, dh);
     wait_vm_all();
@@ -1654,7 +1655,7 @@ __global__ __launch_bounds__(256, 2) void k_proj_bwd_s(const KArgs p) {
     // ---- layer 0 (proj.0): stage dh1, x -> IN; this item's dQ / dK rows load under the last stage
     stage_ds<DT>(DSw, dcur, D, ln);
 #pragma unroll
-    for (int s = 0; s < NS; ++s) INw[act_off(s + NS * h, c)] = x[s];
+    for (int s = 0; s < NS; ++s) INw[act_off(s + NS * h, c)] = rv ? x4[s >> 2][s & 3] : 0.f;
     float* dst = it.isK ? p.dK + ((int64_t)bh * p.M + rowc) * D : p.dQ + ((int64_t)bh * p.N + rowc) * D;
     f32x4 old[2 * DT];
 #pragma unroll
