@@ -95,9 +95,9 @@ __device__ __forceinline__ u32x4 philox4x32(u32x4 ctr, uint32_t k0, uint32_t k1)
   const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
 #pragma unroll
   for (int i = 0; i < PHILOX_ROUNDS; ++i) {
-    uint32_t hi0 = __umulhi(M0, ctr.x), lo0 = M0 * ctr.x;
-    uint32_t hi1 = __umulhi(M1, ctr.z), lo1 = M1 * ctr.z;
-    ctr = u32x4{hi1 ^ ctr.y ^ k0, lo1, hi0 ^ ctr.w ^ k1, lo0};
+    // one v_mad_u64_u32 per 32x32->64 product (measured 20% cheaper than mul_hi + mul_lo)
+    const uint64_t p0 = (uint64_t)M0 * ctr.x, p1 = (uint64_t)M1 * ctr.z;
+    ctr = u32x4{(uint32_t)(p1 >> 32) ^ ctr.y ^ k0, (uint32_t)p1, (uint32_t)(p0 >> 32) ^ ctr.w ^ k1, (uint32_t)p0};
     k0 += W0; k1 += W1;
   }
   return ctr;
@@ -294,17 +294,6 @@ __device__ __forceinline__ void lds_zero(float* img) {
 
 // Wait for every outstanding vector-memory op of this wave (incl. LDS-DMA) before reading LDS.
 __device__ __forceinline__ void wait_vm_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
-// v_writelane_b32 x2: dst[LANE0] = lo, dst[LANE1] = hi (wave-uniform halves of one ballot), other
-// lanes unchanged. Measured on gfx950: a v_writelane that reads an SGPR written by the v_cmp right
-// before it gets stale data, and the hazard recognizer does not look inside inline asm, so one
-// s_nop 4 leads each pair (both halves come from the same v_cmp).
-template <int LANE0, int LANE1>
-__device__ __forceinline__ uint32_t writelane2(uint32_t dst, uint32_t lo, uint32_t hi) {
-  asm("s_nop 4\n\tv_writelane_b32 %0, %1, %3\n\tv_writelane_b32 %0, %2, %4"
-      : "+v"(dst) : "s"(lo), "s"(hi), "n"(LANE0), "n"(LANE1));
-  return dst;
-}
 
 // XCD-aware block mapping. MI355X dispatches consecutive workgroups round-robin over its 8 XCDs,
 // each with a private L2; the NB blocks of one (b,h) re-read the same K/V (or Q/dX) tiles, so they

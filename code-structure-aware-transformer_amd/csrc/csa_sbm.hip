@@ -464,23 +464,68 @@ __global__ __launch_bounds__(64) void k_proj_fwd(const KArgs p) {
 // ------------------------------------------------------------------------------------
 // Bit-pack one tile's sampled graph / keep mask: ballot r holds key crow(r,0)'s 32 query bits in its
 // low word and key crow(r,1)'s in its high word; v_writelane drops each word into its key's lane
-// (no per-lane masks or selects).
-template <int R>
-__device__ __forceinline__ void pack_ballot(const bool (&av)[16], const bool (&keep)[16], bool doA, bool doR,
-                                            uint32_t& myA, uint32_t& myR) {
-  if (doA) {
-    const unsigned long long bal = __ballot(av[R]);
-    myA = writelane2<crow(R, 0), crow(R, 1)>(myA, (uint32_t)bal, (uint32_t)(bal >> 32));
-  }
-  if (doR) {
-    const unsigned long long bal = __ballot(keep[R]);
-    myR = writelane2<crow(R, 0), crow(R, 1)>(myR, (uint32_t)bal, (uint32_t)(bal >> 32));
-  }
+// (no per-lane masks or selects). Measured on gfx950: a v_writelane reading an SGPR that a v_cmp wrote
+// just before gets stale data, and the hazard recognizer does not look inside inline asm; the 16
+// ballots are taken first and written in two batches of 8, each led by one s_nop 4.
+template <int R0>
+__device__ __forceinline__ uint32_t writelane_batch(uint32_t dst, const unsigned long long (&b)[16]) {
+  static_assert(R0 == 0 || R0 == 8, "two batches of 8 ballots");
+#define CSA_WL_OPS                                                                                        \
+  : "+v"(dst)                                                                                            \
+  : "s"((uint32_t)b[R0]), "s"((uint32_t)(b[R0] >> 32)), "s"((uint32_t)b[R0 + 1]),                        \
+    "s"((uint32_t)(b[R0 + 1] >> 32)), "s"((uint32_t)b[R0 + 2]), "s"((uint32_t)(b[R0 + 2] >> 32)),        \
+    "s"((uint32_t)b[R0 + 3]), "s"((uint32_t)(b[R0 + 3] >> 32)), "s"((uint32_t)b[R0 + 4]),                \
+    "s"((uint32_t)(b[R0 + 4] >> 32)), "s"((uint32_t)b[R0 + 5]), "s"((uint32_t)(b[R0 + 5] >> 32)),        \
+    "s"((uint32_t)b[R0 + 6]), "s"((uint32_t)(b[R0 + 6] >> 32)), "s"((uint32_t)b[R0 + 7]),                \
+    "s"((uint32_t)(b[R0 + 7] >> 32))
+  if constexpr (R0 == 0)
+    asm("s_nop 4\n\t"
+      "v_writelane_b32 %0, %1, 0\n\t"
+      "v_writelane_b32 %0, %2, 4\n\t"
+      "v_writelane_b32 %0, %3, 1\n\t"
+      "v_writelane_b32 %0, %4, 5\n\t"
+      "v_writelane_b32 %0, %5, 2\n\t"
+      "v_writelane_b32 %0, %6, 6\n\t"
+      "v_writelane_b32 %0, %7, 3\n\t"
+      "v_writelane_b32 %0, %8, 7\n\t"
+      "v_writelane_b32 %0, %9, 8\n\t"
+      "v_writelane_b32 %0, %10, 12\n\t"
+      "v_writelane_b32 %0, %11, 9\n\t"
+      "v_writelane_b32 %0, %12, 13\n\t"
+      "v_writelane_b32 %0, %13, 10\n\t"
+      "v_writelane_b32 %0, %14, 14\n\t"
+      "v_writelane_b32 %0, %15, 11\n\t"
+      "v_writelane_b32 %0, %16, 15"
+        CSA_WL_OPS);
+  else
+    asm("s_nop 4\n\t"
+      "v_writelane_b32 %0, %1, 16\n\t"
+      "v_writelane_b32 %0, %2, 20\n\t"
+      "v_writelane_b32 %0, %3, 17\n\t"
+      "v_writelane_b32 %0, %4, 21\n\t"
+      "v_writelane_b32 %0, %5, 18\n\t"
+      "v_writelane_b32 %0, %6, 22\n\t"
+      "v_writelane_b32 %0, %7, 19\n\t"
+      "v_writelane_b32 %0, %8, 23\n\t"
+      "v_writelane_b32 %0, %9, 24\n\t"
+      "v_writelane_b32 %0, %10, 28\n\t"
+      "v_writelane_b32 %0, %11, 25\n\t"
+      "v_writelane_b32 %0, %12, 29\n\t"
+      "v_writelane_b32 %0, %13, 26\n\t"
+      "v_writelane_b32 %0, %14, 30\n\t"
+      "v_writelane_b32 %0, %15, 27\n\t"
+      "v_writelane_b32 %0, %16, 31"
+        CSA_WL_OPS);
+#undef CSA_WL_OPS
+  return dst;
 }
-template <bool DOA, int... Rs>
-__device__ __forceinline__ void pack_ballots(std::integer_sequence<int, Rs...>, const bool (&av)[16],
-                                             const bool (&keep)[16], bool doR, uint32_t& myA, uint32_t& myR) {
-  (pack_ballot<Rs>(av, keep, DOA, doR, myA, myR), ...);
+__device__ __forceinline__ uint32_t pack_bits(const bool (&v)[16]) {
+  unsigned long long b[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) b[r] = __ballot(v[r]);
+  uint32_t w = 0;
+  w = writelane_batch<0>(w, b);
+  return writelane_batch<8>(w, b);
 }
 
 template <int D, int KPH>
@@ -493,6 +538,34 @@ struct AttnFwdLds {
   // K image | V image | T image | key bias row (Mpad floats: 0 = valid key, -inf = padded / beyond M)
   static size_t bytes(int Mpad) { return (size_t)BOFF + 4 * (size_t)Mpad; }
 };
+
+// Key bias row (0 for a valid unmasked key, -inf otherwise: sbm_attn.py:61 masked_fill) in two halves so the
+// mask loads of the first KB_UNROLL x 64 keys are in flight together with the prologue's other loads and DMAs
+// (a runtime-trip-count loop of load -> store would serialize one memory latency per 64 keys).
+constexpr int KB_UNROLL = 4;
+struct KeyMask { float v[KB_UNROLL]; };
+__device__ __forceinline__ KeyMask key_mask_load(const KArgs& p, int b) {
+  const float* mk = p.mask ? p.mask + b * p.mask_sb : nullptr;
+  KeyMask km;
+#pragma unroll
+  for (int u = 0; u < KB_UNROLL; ++u) {
+    const int j = lane_id() + 64 * u;
+    km.v[u] = (mk && j < p.NKB * 32) ? mk[imin(j, p.M - 1)] : 0.f;
+  }
+  return km;
+}
+__device__ __forceinline__ void key_bias_store(float* bias, const KArgs& p, int b, const KeyMask& km) {
+#pragma unroll
+  for (int u = 0; u < KB_UNROLL; ++u) {
+    const int j = lane_id() + 64 * u;
+    if (j < p.NKB * 32) bias[j] = (j < p.M && km.v[u] == 0.f) ? 0.f : NEG_INF;
+  }
+  const float* mk = p.mask ? p.mask + b * p.mask_sb : nullptr;
+  for (int j = lane_id() + 64 * KB_UNROLL; j < p.NKB * 32; j += 64) {  // M > 256 only
+    const float mv = mk ? mk[imin(j, p.M - 1)] : 0.f;
+    bias[j] = (j < p.M && mv == 0.f) ? 0.f : NEG_INF;
+  }
+}
 
 // DROP: attention dropout on (keep <=> 16-bit uniform >= drop_thr). HAS_U: STE uniforms supplied by
 // the caller (bit-exact parity path, fp32 compare as torch.bernoulli); otherwise 16-bit Philox
@@ -531,19 +604,19 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd
     }                                                         \
     if constexpr (!DENSE) dma_narrow(Tl, tr, (row0), KPN); \
   } while (0)
-  CSA_ISSUE_FWD(0);  // tile 0 in flight while the bias row and the query-side operands load
-  {
-    const float* mk = p.mask ? p.mask + b * p.mask_sb : nullptr;
-    float* bias = lds + LY::BOFF / 4;
-    for (int j = lane; j < p.NKB * 32; j += 64) {
-      const float mv = mk ? mk[imin(j, p.M - 1)] : 0.f;
-      bias[j] = (j < p.M && mv == 0.f) ? 0.f : NEG_INF;  // sbm_attn.py:61 masked_fill(-inf)
-    }
-  }
+  // prologue loads in need order (vmcnt retires in issue order): key mask, query operands, tile 0
+  const KeyMask km = key_mask_load(p, b);
   float q[NS];
   load_run<NS>(q, p.Q + b * p.q_sb + hd * p.q_sh + (int64_t)ic * p.q_sn + h * NS, iv);
   float qh[KPH > 0 ? KPH : 1];
   if constexpr (!DENSE) load_run<KPH>(qh, p.Qh + ((int64_t)bh * p.N + ic) * p.kp + h * KPH, iv);
+  // Philox STE compares u16 < 65536 p: E is computed 65536x scaled (qh scaled by a power of two, exact)
+  constexpr float ESC = HAS_U ? 1.f : 65536.f;
+  if constexpr (!DENSE && !HAS_U)
+#pragma unroll
+    for (int e = 0; e < KPH; ++e) qh[e] *= ESC;
+  CSA_ISSUE_FWD(0);
+  key_bias_store(lds + LY::BOFF / 4, p, b, km);
   const int kbase = SWZ ? row_base64(c, h) : 4 * (c * DP + NS * h);
   const int tbase = DENSE ? 0 : LY::TOFF + narrow_base<KPN>(c, (KPH / 4) * h);
   int vb[DT];
@@ -618,8 +691,7 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             const int r = 8 * gp + e;
-            const float pr = fminf(fmaxf(eacc[r], 0.01f), 0.99f);
-            av[r] = (float)u16_of(rr, e) < pr * 65536.f;
+            av[r] = (float)u16_of(rr, e) < __builtin_amdgcn_fmed3f(eacc[r], 0.01f * ESC, 0.99f * ESC);
           }
         }
       }
@@ -635,8 +707,8 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd
     }
     // bit-pack the sampled graph / dropout keep mask: word [qb][key] holds 32 query bits (lanes 0..31)
     if constexpr (!DENSE || DROP) {
-      uint32_t myA = 0, myR = 0;
-      pack_ballots<!DENSE>(std::make_integer_sequence<int, 16>{}, av, keep, DROP, myA, myR);
+      const uint32_t myA = DENSE ? 0u : pack_bits(av);
+      const uint32_t myR = DROP ? pack_bits(keep) : 0u;
       const int64_t widx = ((int64_t)bh * p.NQB + qb) * p.Mpad + j0 + c;
       if constexpr (!DENSE) {
         if (h == 0) p.Abits[widx] = myA;
@@ -802,13 +874,6 @@ struct AttnBwdShape {
 };
 
 // key bias row in LDS: 0 for a valid key, -inf for a padded one or one beyond M (sbm_attn.py:61)
-__device__ __forceinline__ void fill_key_bias(float* bias, const KArgs& p, int b) {
-  const float* mk = p.mask ? p.mask + b * p.mask_sb : nullptr;
-  for (int j = lane_id(); j < p.NKB * 32; j += 64) {
-    const float mv = mk ? mk[imin(j, p.M - 1)] : 0.f;
-    bias[j] = (j < p.M && mv == 0.f) ? 0.f : NEG_INF;
-  }
-}
 
 // ------------------------------------------------------------------------------------
 // B2: per (b,h, query block), S^T orientation: dQ (attention path), dQh, gamma
@@ -847,8 +912,9 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
     }                                               \
     if constexpr (!DENSE) dma_narrow(Tl, tr, (row0), KPN); \
   } while (0)
+  const KeyMask km = key_mask_load(p, b);
   CSA_ISSUE_BQ(0);
-  fill_key_bias(lds + SH::QB / 4, p, b);
+  key_bias_store(lds + SH::QB / 4, p, b, km);
   const int64_t wrow = ((int64_t)bh * p.NQB + qb) * p.Mpad + c;
   uint32_t wAn = DENSE ? 0xffffffffu : p.Abits[wrow];
   uint32_t wRn = DROP ? p.Rbits[wrow] : 0xffffffffu;
