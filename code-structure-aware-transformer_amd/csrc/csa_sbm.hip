@@ -115,30 +115,29 @@ __device__ __forceinline__ f32x4 frag4(const float* __restrict__ f, int it, int 
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, lane_id() * 16, soff, 0));
 }
 
-// out[t] += sum_{s < 4 S4N} frag(t)[s] * bval(s) for t < NTO, fragments fetched exactly one K-group
-// (4 steps) ahead: the 4 NTO MFMAs of a group (>= 256 cycles) cover the L2 latency of the next
-// group's fragment loads, and the sched fence keeps the lookahead (and its registers) at one group.
-template <int NTO, int S4N, typename BF>
+// out[t] += sum_{s < 4 S4N} frag(t)[s] * bval(s) for t < NTO, fragments fetched LA K-groups (4 steps
+// each) ahead: LA = 1 covers the L2 latency when the 4 NTO MFMAs of a group (>= 256 cycles) and other
+// waves fill the gap; the sched fence keeps the lookahead (and its registers) at LA groups.
+template <int NTO, int S4N, int LA = 1, typename BF>
 __device__ __forceinline__ void frag_chain(const float* __restrict__ frag, int nsteps, f32x16 (&out)[NTO], BF bval) {
-  f32x4 wc[NTO];
+  static_assert(LA == 1 || LA == 2, "lookahead of one or two K-groups");
+  f32x4 wq[LA + 1][NTO];
 #pragma unroll
-  for (int t = 0; t < NTO; ++t) wc[t] = frag4(frag, t, nsteps, 0);
+  for (int a = 0; a < LA; ++a)
+    if (a < S4N)
+#pragma unroll
+      for (int t = 0; t < NTO; ++t) wq[a][t] = frag4(frag, t, nsteps, a);
 #pragma unroll
   for (int s4 = 0; s4 < S4N; ++s4) {
-    f32x4 wn[NTO];
-    if (s4 + 1 < S4N) {
+    if (s4 + LA < S4N) {
 #pragma unroll
-      for (int t = 0; t < NTO; ++t) wn[t] = frag4(frag, t, nsteps, s4 + 1);
+      for (int t = 0; t < NTO; ++t) wq[(s4 + LA) % (LA + 1)][t] = frag4(frag, t, nsteps, s4 + LA);
     }
 #pragma unroll
     for (int t = 0; t < NTO; ++t)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) out[t] = mfma(wc[t][e], bval(4 * s4 + e), out[t]);
+      for (int e = 0; e < 4; ++e) out[t] = mfma(wq[s4 % (LA + 1)][t][e], bval(4 * s4 + e), out[t]);
     fence_sched();
-    if (s4 + 1 < S4N) {
-#pragma unroll
-      for (int t = 0; t < NTO; ++t) wc[t] = wn[t];
-    }
   }
 }
 
@@ -296,6 +295,8 @@ __device__ __forceinline__ void mlp_act(const KArgs& p, f32x16 (&a)[D / 32], int
     }
 }
 
+constexpr int MLP_LA = 2;  // forward MLP chains: fragments two K-groups ahead
+
 // h1 = relu(drop(W0 x + b0)) from lin-perm input rows
 template <int D>
 __device__ __forceinline__ void mlp_layer0(const KArgs& p, const float (&x)[D / 2], f32x16 (&h1)[D / 32], int row,
@@ -306,7 +307,7 @@ __device__ __forceinline__ void mlp_layer0(const KArgs& p, const float (&x)[D / 
   for (int ot = 0; ot < DT; ++ot)
 #pragma unroll
     for (int r = 0; r < 16; ++r) h1[ot][r] = p.pb[0][32 * ot + crow(r, h)];
-  frag_chain<DT, NS / 4>(p.Wf[0], NS, h1, [&](int s) { return x[s]; });
+  frag_chain<DT, NS / 4, MLP_LA>(p.Wf[0], NS, h1, [&](int s) { return x[s]; });
   mlp_act<D>(p, h1, 0, row, bh, isK);
 }
 
@@ -319,7 +320,7 @@ __device__ __forceinline__ void mlp_layer(const KArgs& p, const f32x16 (&in)[D /
   for (int ot = 0; ot < DT; ++ot)
 #pragma unroll
     for (int r = 0; r < 16; ++r) out[ot][r] = p.pb[l][32 * ot + crow(r, h)];
-  frag_chain<DT, NS / 4>(p.Wf[l], NS, out, [&](int s) { return in[s / 16][s % 16]; });
+  frag_chain<DT, NS / 4, MLP_LA>(p.Wf[l], NS, out, [&](int s) { return in[s / 16][s % 16]; });
 }
 
 template <int D>
