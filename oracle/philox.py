@@ -1,0 +1,103 @@
+"""ORACLE (test infrastructure only): numpy restatement of the in-kernel random streams.
+
+The reference draws its STE uniforms (module/STE.py:13, torch.rand_like) and its dropout masks
+(module/sbm_attn.py:14,24,27, nn.Dropout) from torch's stateful generator, which no other
+implementation can reproduce. The HIP path instead draws them from a stateless Philox4x32-7
+(Salmon et al., SC'11) keyed by (seed, offset, element coordinates), so a train-mode forward is
+reproducible on any launch geometry. This module regenerates exactly those draws on the CPU so the
+train-mode kernels can be checked element by element against oracle/closed_form.py:
+
+  * STE sampling      A_ij  = u16 < clamp(expA_ij, .01, .99) * 65536      (k_attn_fwd, RNG_STE)
+  * attention dropout r_ij  = u16 >= ceil(p_attn * 65536)                  (k_attn_fwd, RNG_ATTN_DROP)
+  * proj dropout      keep  = u16 >= ceil(p_proj * 65536), layers 0 and 1  (mlp_act, RNG_PROJ_DROP)
+
+Counter layouts follow code-structure-aware-transformer_amd/csrc/csa_sbm.hip (k_attn_fwd, mlp_act);
+the round function and key schedule are Random123's philox4x32 (checked against its published
+known-answer vectors for 10 rounds in tests/test_oracle_golden.py).
+"""
+import numpy as np
+
+M0, M1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57)
+W0, W1 = 0x9E3779B9, 0xBB67AE85
+RNG_STE, RNG_ATTN_DROP, RNG_PROJ_DROP = 1, 2, 3
+MASK32 = np.uint64(0xFFFFFFFF)
+
+
+def philox4x32(c0, c1, c2, c3, k0, k1, rounds=7):
+    """Vectorised Philox4x32-R over broadcastable uint32 counter words; keys are Python ints."""
+    x, y, z, w = (np.asarray(v, dtype=np.uint64) & MASK32 for v in (c0, c1, c2, c3))
+    x, y, z, w = np.broadcast_arrays(x, y, z, w)
+    k0, k1 = int(k0) & 0xFFFFFFFF, int(k1) & 0xFFFFFFFF
+    for _ in range(rounds):
+        p0 = M0 * x
+        p1 = M1 * z
+        x, y, z, w = ((p1 >> np.uint64(32)) ^ y ^ np.uint64(k0), p1 & MASK32,
+                      (p0 >> np.uint64(32)) ^ w ^ np.uint64(k1), p0 & MASK32)
+        k0 = (k0 + W0) & 0xFFFFFFFF
+        k1 = (k1 + W1) & 0xFFFFFFFF
+    return x, y, z, w
+
+
+def u16_of(words, e):
+    """16-bit uniform e (0..7) of one Philox output: word e // 2, low half for even e (u16_of)."""
+    e = np.asarray(e)
+    sel = np.choose(e >> 1, words)
+    return np.where(e & 1, sel >> np.uint64(16), sel & np.uint64(0xFFFF)).astype(np.uint32)
+
+
+def _reg_of(jj):
+    """Accumulator register r and half h holding tile row jj: crow(r, h) = (r&3) + 8(r>>2) + 4h."""
+    jj = np.asarray(jj)
+    h = (jj >> 2) & 1
+    r = (jj & 3) + 4 * (jj >> 3)
+    return r, h
+
+
+def keep_threshold(p):
+    """ceil(p * 65536) of the fp32 probability (make_kargs): keep <=> u16 >= threshold."""
+    return int(np.ceil(np.float64(np.float32(p)) * 65536.0))
+
+
+def attn_uniforms(B, H, N, M, seed, offset, stream):
+    """(B, H, N, M) uint32 16-bit draws of the attention-tile streams (RNG_STE / RNG_ATTN_DROP).
+
+    k_attn_fwd: lane (query i, half h) of key tile kt makes Philox calls gp = 0, 1 with counter
+    (i, 8 kt + 4 gp + h, b*H + head, (stream << 28) ^ offset); register r = 8 gp + e holds key
+    32 kt + crow(r, h)."""
+    i = np.arange(N).reshape(1, 1, N, 1)
+    j = np.arange(M).reshape(1, 1, 1, M)
+    bh = np.arange(B * H).reshape(B, H, 1, 1)
+    kt, jj = j // 32, j % 32
+    r, h = _reg_of(jj)
+    gp, e = r // 8, r % 8
+    words = philox4x32(i, 8 * kt + 4 * gp + h, bh, ((stream << 28) ^ (int(offset) & 0xFFFFFFFF)) & 0xFFFFFFFF,
+                       int(seed) & 0xFFFFFFFF, int(seed) >> 32)
+    return u16_of(words, np.broadcast_to(e, words[0].shape))
+
+
+def ste_graph(expA, u16):
+    """A = u16 < clamp(expA, .01, .99) * 65536 in fp32 (the kernel's comparison)."""
+    p = np.clip(np.asarray(expA, dtype=np.float32), np.float32(0.01), np.float32(0.99))
+    return u16.astype(np.float32) < p * np.float32(65536.0)
+
+
+def attn_keep(B, H, N, M, seed, offset, p):
+    """(B, H, N, M) bool attention-dropout keep mask (sbm_attn.py:63 drop_attn)."""
+    return attn_uniforms(B, H, N, M, seed, offset, RNG_ATTN_DROP) >= keep_threshold(p)
+
+
+def proj_keep(B, H, rows, d, seed, offset, p, layer, is_k):
+    """(B, H, rows, d) bool keep mask of proj dropout `layer` (0: proj.1, 1: proj.4) for the Q (is_k=0)
+    or K (is_k=1) MLP (sbm_attn.py:22-30). mlp_act: data row `row`, feature f = 32 ot + crow(r, h),
+    Philox counter (row, (4 ot + 2 gp + h) | layer << 16 | is_k << 20, b*H + head,
+    (RNG_PROJ_DROP << 28) ^ offset), register r = 8 gp + e."""
+    row = np.arange(rows).reshape(1, 1, rows, 1)
+    f = np.arange(d).reshape(1, 1, 1, d)
+    bh = np.arange(B * H).reshape(B, H, 1, 1)
+    ot, ff = f // 32, f % 32
+    r, h = _reg_of(ff)
+    gp, e = r // 8, r % 8
+    words = philox4x32(row, (4 * ot + 2 * gp + h) | (layer << 16) | (is_k << 20), bh,
+                       ((RNG_PROJ_DROP << 28) ^ (int(offset) & 0xFFFFFFFF)) & 0xFFFFFFFF,
+                       int(seed) & 0xFFFFFFFF, int(seed) >> 32)
+    return u16_of(words, np.broadcast_to(e, words[0].shape)) >= keep_threshold(p)

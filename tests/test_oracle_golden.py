@@ -3,7 +3,7 @@ import numpy as np
 import pytest
 import torch
 
-from oracle import closed_form, cse_ref, sbm_ref
+from oracle import closed_form, cse_ref, philox, sbm_ref
 
 SBM_CASES = ["sbm_n37", "sbm_n1", "sbm_n7_d96_k16", "sbm_n64_noncontig", "sbm_n150", "sbm_n33_d96"]
 
@@ -119,3 +119,38 @@ def test_disentangled_oracle(golden):
     np.testing.assert_allclose(rq.grad.numpy(), z["drel_q"], rtol=1e-4, atol=1e-5)
     for pk, p in params.items():
         np.testing.assert_allclose(p.grad.numpy(), z["g:" + pk], rtol=1e-4, atol=1e-5, err_msg=pk)
+
+
+# Random123 kat_vectors, philox4x32 with 10 rounds: (counter, key) -> output
+PHILOX_KAT = [
+    ((0x00000000, 0x00000000, 0x00000000, 0x00000000), (0x00000000, 0x00000000),
+     (0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8)),
+    ((0xFFFFFFFF, 0xFFFFFFFF, 0xFFFFFFFF, 0xFFFFFFFF), (0xFFFFFFFF, 0xFFFFFFFF),
+     (0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD)),
+    ((0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344), (0xA4093822, 0x299F31D0),
+     (0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1)),
+]
+
+
+@pytest.mark.parametrize("ctr,key,out", PHILOX_KAT)
+def test_philox_round_function_known_answers(ctr, key, out):
+    """The oracle's Philox (the kernels' train-mode random streams run 7 rounds of it) against the
+    published 10-round known-answer vectors."""
+    got = philox.philox4x32(*ctr, *key, rounds=10)
+    assert tuple(int(v) for v in got) == out
+
+
+def test_philox_stream_layout():
+    """Draw layouts: 16-bit halves in word order, distinct streams, keep thresholds of fp32 p."""
+    u = philox.attn_uniforms(1, 2, 5, 40, seed=(7 << 32) | 3, offset=9, stream=philox.RNG_STE)
+    assert u.shape == (1, 2, 5, 40) and u.max() < 65536
+    w = philox.philox4x32(0, 0, 0, (philox.RNG_STE << 28) ^ 9, 3, 7)
+    assert int(u[0, 0, 0, 0]) == int(w[0]) & 0xFFFF        # key 0 = register 0, half 0: word x low
+    assert int(u[0, 0, 0, 1]) == int(w[0]) >> 16            # key 1 = register 1: word x high
+    assert int(u[0, 0, 0, 8]) == int(w[2]) & 0xFFFF        # key 8 = register 4: word z low
+    assert int(u[0, 0, 0, 4]) != int(u[0, 0, 0, 0])         # key 4 = half 1: its own counter
+    d = philox.attn_uniforms(1, 2, 5, 40, seed=(7 << 32) | 3, offset=9, stream=philox.RNG_ATTN_DROP)
+    assert not np.array_equal(u, d)
+    assert philox.keep_threshold(0.2) == 13108 and philox.keep_threshold(0.0) == 0
+    k = philox.proj_keep(2, 2, 64, 64, seed=123, offset=0, p=0.25, layer=0, is_k=0)
+    assert abs(k.mean() - 0.75) < 0.02

@@ -224,3 +224,47 @@ def test_train_mode_dropout_statistics_and_determinism():
     ref, _ = closed_form.sbm_fwd_bwd(Q, K, V, mask, params, u, k, dX, dsp)
     # E[sparsity_h] = mean clamp(expA) (proj dropout perturbs expA slightly in train mode)
     np.testing.assert_allclose(r1[1].numpy(), ref["expA"].clamp(0.01, 0.99).mean((0, 2, 3)).numpy(), rtol=0.05)
+
+
+@pytest.mark.skipif(not has_gpu(), reason="needs GPU")
+@pytest.mark.parametrize("shape", [(2, 2, 150, 64, 10), (1, 2, 45, 96, 5)])
+def test_train_mode_matches_oracle_with_regenerated_masks(shape):
+    """Train mode end to end: the oracle regenerates the kernels' Philox streams (oracle/philox.py) --
+    attention dropout, both proj-dropout layers of the Q and K MLPs -- and the STE draws; the sampled
+    graph must equal u16 < clamp(expA) * 65536 away from fp32 ties, and X / sparsity / every gradient
+    must match the fp64 closed form run with those masks."""
+    from oracle import philox
+    B, H, N, d, k = shape
+    Q, K, V, mask, _, dX, dsp, params = _rand_case(B, H, N, d, k, seed=3 * sum(shape))
+    seed, offset, attn_p, proj_p = (0x1234567 << 32) | 0x89ABCDE, 77, 0.2, 0.1
+    cw = params["layer.weight"].cuda()
+    pw = [params[f"proj.{i}.weight"].cuda() for i in (0, 3, 6)]
+    pb = [params[f"proj.{i}.bias"].cuda() for i in (0, 3, 6)]
+    q, kk, v, mk = Q.cuda(), K.cuda(), V.cuda(), mask.cuda()
+    X, sp, state = torch.ops.csa.sbm_fwd(q, kk, v, mk, cw, pw, pb, None, k, seed, offset, attn_p, proj_p, False)
+    graph, _ = torch.ops.csa.sbm_maps(q, kk, v, mk, state, k, False)
+    g = torch.ops.csa.sbm_bwd(q, kk, v, mk, cw, pw, pb, k, attn_p, proj_p, seed, offset, False, state, X,
+                              dX.cuda(), dsp.cuda(), None)
+    torch.cuda.synchronize()
+    graph = graph.cpu()
+    keep = philox.attn_keep(B, H, N, N, seed, offset, attn_p)
+    ks = 1.0 / (1.0 - np.float32(proj_p))
+    pk = {f"{s}{l}": torch.from_numpy(philox.proj_keep(B, H, N, d, seed, offset, proj_p, l, int(s == "k")) * ks)
+          for s in "qk" for l in (0, 1)}
+    assert 0.75 < keep.mean() < 0.85 and all(0.85 < float((t > 0).double().mean()) < 0.95 for t in pk.values())
+    ref, rg = closed_form.sbm_fwd_bwd(Q, K, V, mask, params, None, k, dX, dsp,
+                                     attn_keep=torch.from_numpy(keep / (1.0 - np.float32(attn_p))), proj_keep=pk,
+                                     graph_override=graph)
+    # STE draws: the GPU graph is the regenerated u16 draws against the oracle's expA (fp32 ties aside)
+    u16 = philox.attn_uniforms(B, H, N, N, seed, offset, philox.RNG_STE)
+    want = philox.ste_graph(ref["expA"].numpy(), u16)
+    thr = np.clip(ref["expA"].numpy(), 0.01, 0.99) * 65536.0
+    diff = want != graph.numpy().astype(bool)
+    assert np.all(np.abs(u16[diff] - thr[diff]) < 0.5), f"{int(diff.sum())} graph flips away from ties"
+    assert diff.mean() < 1e-4
+    np.testing.assert_allclose(X.cpu().numpy(), ref["X"].numpy(), rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(sp.cpu().numpy(), ref["sparsity"].numpy(), rtol=1e-6)
+    names = ["Q", "K", "V", "layer.weight", "proj.0.weight", "proj.0.bias", "proj.3.weight", "proj.3.bias",
+             "proj.6.weight", "proj.6.bias"]
+    for name, t in zip(names, g):
+        np.testing.assert_allclose(t.cpu().numpy(), rg[name].numpy(), rtol=RTOL, atol=ATOL, err_msg=name)
