@@ -284,8 +284,9 @@ def main():
         if os.path.exists(pmc):
             with open(pmc) as f:
                 tr = json.load(f).get(kernel_of[dom])
-            if tr:
-                roofline["traffic"] = tr
+            if tr:  # HBM bytes per launch from the committed PMC passes (tools/pmc_traffic.py)
+                roofline["traffic"] = tr["bytes"]
+                roofline["traffic_unit"] = "bytes/launch (rocprofv3 2xFETCH_SIZE+WRITE_SIZE, profiles/pmc_traffic.json)"
     total_flops = sum(flops.values()) * B
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "ASTs/s", "n_gpus": world, "steps": args.steps,

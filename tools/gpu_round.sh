@@ -12,4 +12,6 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY --output-format csv -d "$OUT/pmc1" -o run -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-train > "$OUT/pmc1.log" 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc2" -o run -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-train > "$OUT/pmc2.log" 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc3" -o run -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-train > "$OUT/pmc3.log" 2>&1 || exit $?
+python tools/pmc_traffic.py "$OUT/pmc2/run_counter_collection.csv" "$OUT/pmc3/run_counter_collection.csv" > "$OUT/pmc_traffic.json" || exit $?
+python tools/pmc_summary.py "$OUT"/pmc*/run_counter_collection.csv > "$OUT/pmc_summary.txt"
 echo done
