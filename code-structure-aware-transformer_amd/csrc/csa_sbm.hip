@@ -297,17 +297,33 @@ __device__ __forceinline__ void mlp_act(const KArgs& p, f32x16 (&a)[D / 32], int
 
 constexpr int MLP_LA = 2;  // forward MLP chains: fragments two K-groups ahead
 
+// Linear bias as one more MFMA K-step after the weight chain (x W^T + b, summed last like addmm):
+// A = b[32 ot + c] on every lane (raw load issued before the chain, no select on it), B = 1 on the
+// h = 0 lanes and 0 on the h = 1 lanes, so D[f][row] += b[f].
+template <int D>
+__device__ __forceinline__ void bias_operand(const float* __restrict__ b, float (&ba)[D / 32]) {
+  const int c = lane_id() & 31;
+#pragma unroll
+  for (int ot = 0; ot < D / 32; ++ot) ba[ot] = b[32 * ot + c];
+}
+template <int D>
+__device__ __forceinline__ void add_bias(const float (&ba)[D / 32], f32x16 (&a)[D / 32]) {
+  const float one = (lane_id() >> 5) == 0 ? 1.f : 0.f;
+#pragma unroll
+  for (int ot = 0; ot < D / 32; ++ot) a[ot] = mfma(ba[ot], one, a[ot]);
+}
+
 // h1 = relu(drop(W0 x + b0)) from lin-perm input rows
 template <int D>
 __device__ __forceinline__ void mlp_layer0(const KArgs& p, const float (&x)[D / 2], f32x16 (&h1)[D / 32], int row,
                                            int bh, int isK) {
   constexpr int DT = D / 32, NS = D / 2;
-  const int h = lane_id() >> 5;
+  float ba[DT];
+  bias_operand<D>(p.pb[0], ba);
 #pragma unroll
-  for (int ot = 0; ot < DT; ++ot)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) h1[ot][r] = p.pb[0][32 * ot + crow(r, h)];
+  for (int ot = 0; ot < DT; ++ot) h1[ot] = zero16();
   frag_chain<DT, NS / 4, MLP_LA>(p.Wf[0], NS, h1, [&](int s) { return x[s]; });
+  add_bias<D>(ba, h1);
   mlp_act<D>(p, h1, 0, row, bh, isK);
 }
 
@@ -315,12 +331,12 @@ __device__ __forceinline__ void mlp_layer0(const KArgs& p, const float (&x)[D / 
 template <int D>
 __device__ __forceinline__ void mlp_layer(const KArgs& p, const f32x16 (&in)[D / 32], f32x16 (&out)[D / 32], int l) {
   constexpr int DT = D / 32, NS = D / 2;
-  const int h = lane_id() >> 5;
+  float ba[DT];
+  bias_operand<D>(p.pb[l], ba);
 #pragma unroll
-  for (int ot = 0; ot < DT; ++ot)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) out[ot][r] = p.pb[l][32 * ot + crow(r, h)];
+  for (int ot = 0; ot < DT; ++ot) out[ot] = zero16();
   frag_chain<DT, NS / 4, MLP_LA>(p.Wf[l], NS, out, [&](int s) { return in[s / 16][s % 16]; });
+  add_bias<D>(ba, out);
 }
 
 template <int D>
@@ -1331,11 +1347,11 @@ __device__ __forceinline__ void outer_stage(const float* ds, const float* in, f3
 
 // out^T = Wfrag^T-style product: out[it] = sum_s frag[it][s] * in[s/16][s%16] (acc-perm input)
 // (S4MAX < NSTEP/4: only the first 4 S4MAX K-steps, for inputs known to be zero beyond them.)
-template <int NTO, int NTI, int S4MAX = 4 * NTI>
+template <int NTO, int NTI, int S4MAX = 4 * NTI, int LA = 1>
 __device__ __forceinline__ void mm_acc(const float* __restrict__ frag, const f32x16 (&in)[NTI], f32x16 (&out)[NTO]) {
 #pragma unroll
   for (int t = 0; t < NTO; ++t) out[t] = zero16();
-  frag_chain<NTO, S4MAX>(frag, 16 * NTI, out, [&](int s) { return in[s / 16][s % 16]; });
+  frag_chain<NTO, S4MAX, LA>(frag, 16 * NTI, out, [&](int s) { return in[s / 16][s % 16]; });
 }
 
 template <int D, int KT>
