@@ -33,24 +33,31 @@ constexpr float NEG_INF = -__builtin_inff();
 // element addresses: X[(bat / H2) * x_b1 + (bat % H2) * x_b2 + r * x_r + m * x_m + k * x_k]
 // One wave per 32x32 C tile; K consumed in chunks of 32 (16 MFMA K-steps, lin perm).
 // ------------------------------------------------------------------------------------
+// R-split (rsplit > 1): blockIdx.z = split * nbat + bat; split s sums r in [s R / rsplit, (s+1) R / rsplit)
+// into its own partial C at C + s * c_split (summed in split order by k_sum_splits: deterministic).
 struct GemmArgs {
   const float* A; int64_t a_m, a_k, a_b1, a_b2, a_r;
   const float* B; int64_t b_n, b_k, b_b1, b_b2, b_r;
   float* C; int64_t c_m, c_n, c_b1, c_b2;
   int M, N, K, H2, R;
   float alpha; int accumulate;
+  int rsplit, nbat; int64_t c_split;
 };
 
 __global__ __launch_bounds__(64) void k_bgemm(const GemmArgs g) {
   const int lane = lane_id(), c = lane & 31, h = lane >> 5;
-  const int n0 = blockIdx.x * 32, m0 = blockIdx.y * 32, bat = blockIdx.z;
+  const int n0 = blockIdx.x * 32, m0 = blockIdx.y * 32;
+  const int bat = g.rsplit > 1 ? (int)blockIdx.z % g.nbat : (int)blockIdx.z;
+  const int split = g.rsplit > 1 ? (int)blockIdx.z / g.nbat : 0;
+  const int r_lo = (int)((int64_t)split * g.R / (g.rsplit > 1 ? g.rsplit : 1));
+  const int r_hi = (int)((int64_t)(split + 1) * g.R / (g.rsplit > 1 ? g.rsplit : 1));
   const int b1 = bat / g.H2, b2 = bat % g.H2;
   const float* A = g.A + b1 * g.a_b1 + b2 * g.a_b2;
   const float* Bp = g.B + b1 * g.b_b1 + b2 * g.b_b2;
   const int m = m0 + c, n = n0 + c;
   const bool mv = m < g.M, nv = n < g.N;
   f32x16 acc = zero16();
-  for (int r = 0; r < g.R; ++r) {
+  for (int r = r_lo; r < r_hi; ++r) {
     const float* Ar = A + r * g.a_r + (int64_t)m * g.a_m;
     const float* Br = Bp + r * g.b_r + (int64_t)n * g.b_n;
     for (int k0 = 0; k0 < g.K; k0 += 32) {
@@ -65,7 +72,7 @@ __global__ __launch_bounds__(64) void k_bgemm(const GemmArgs g) {
       for (int s = 0; s < 16; ++s) acc = mfma(av[s], bv[s], acc);
     }
   }
-  float* C = g.C + b1 * g.c_b1 + b2 * g.c_b2;
+  float* C = g.C + b1 * g.c_b1 + b2 * g.c_b2 + split * g.c_split;
   if (nv) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -75,6 +82,16 @@ __global__ __launch_bounds__(64) void k_bgemm(const GemmArgs g) {
         *p = g.accumulate ? *p + g.alpha * acc[r] : g.alpha * acc[r];
       }
     }
+  }
+}
+
+// out[e] = sum_{s < RS} part[s * stride + e], in split order
+__global__ __launch_bounds__(256) void k_sum_splits(const float* __restrict__ part, float* __restrict__ out, int64_t n,
+                                                    int RS, int64_t stride) {
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
+    float v = 0.f;
+    for (int s = 0; s < RS; ++s) v += part[s * stride + e];
+    out[e] = v;
   }
 }
 
@@ -333,21 +350,25 @@ csa_status rcheck(const char* what) {
 }
 
 void gemm(hipStream_t st, const GemmArgs& g, int nbat) {
-  dim3 grid((unsigned)((g.N + 31) / 32), (unsigned)((g.M + 31) / 32), (unsigned)nbat);
+  dim3 grid((unsigned)((g.N + 31) / 32), (unsigned)((g.M + 31) / 32), (unsigned)(nbat * (g.rsplit > 1 ? g.rsplit : 1)));
   hipLaunchKernelGGL(k_bgemm, grid, dim3(64), 0, st, g);
 }
 
 struct RelLayout {
   int64_t Lp;
-  size_t c2p, p2ct, state_total;       // forward state
-  size_t G, P, gc2p, gp2ct, ws_total;  // backward workspace
+  int RS;                                    // batch splits of the dlq / dlk reductions
+  size_t c2p, p2ct, state_total;             // forward state
+  size_t G, P, gc2p, gp2ct, part, ws_total;  // backward workspace
 };
 
 inline size_t ral(size_t x) { return (x + 255) & ~size_t(255); }
 
-RelLayout rel_layout(int64_t B, int64_t H, int64_t N, int64_t L) {
+RelLayout rel_layout(int64_t B, int64_t H, int64_t N, int64_t L, int64_t d) {
   RelLayout R;
   R.Lp = ((L + 3) / 4) * 4;
+  // dlq / dlk sum over the whole batch: RS partial sums of B / RS elements each fill the GPU
+  // (a single reduction chain per output tile left only H * 10 waves)
+  R.RS = (int)(B < 16 ? B : 16);
   size_t o = 0;
   auto take = [&](size_t bytes) { size_t r = o; o += ral(bytes); return r; };
   R.c2p = take(sizeof(float) * B * H * N * R.Lp);
@@ -358,6 +379,7 @@ RelLayout rel_layout(int64_t B, int64_t H, int64_t N, int64_t L) {
   R.P = take(sizeof(float) * B * H * N * N);
   R.gc2p = take(sizeof(float) * B * H * N * R.Lp);
   R.gp2ct = take(sizeof(float) * B * H * N * R.Lp);
+  R.part = take(sizeof(float) * R.RS * H * L * d);
   R.ws_total = o;
   return R;
 }
@@ -421,19 +443,17 @@ void rel_logits(const csa_rel_attn_args* a, const RelLayout& R, hipStream_t st) 
 extern "C" {
 
 size_t csa_rel_attn_state_bytes(int64_t B, int64_t H, int64_t N, int64_t L, int64_t d) {
-  (void)d;
-  return rel_layout(B, H, N, L).state_total;
+  return rel_layout(B, H, N, L, d).state_total;
 }
 
 size_t csa_rel_attn_bwd_workspace_bytes(int64_t B, int64_t H, int64_t N, int64_t L, int64_t d) {
-  (void)d;
-  return rel_layout(B, H, N, L).ws_total;
+  return rel_layout(B, H, N, L, d).ws_total;
 }
 
 csa_status csa_rel_attn_fwd(const csa_rel_attn_args* a, void* stream) {
   csa_status s = validate_rel(a);
   if (s != CSA_OK) return s;
-  const RelLayout R = rel_layout(a->B, a->H, a->N, a->L);
+  const RelLayout R = rel_layout(a->B, a->H, a->N, a->L, a->d);
   hipStream_t st = (hipStream_t)stream;
   rel_logits(a, R, st);
   RelArgs p = make_rel(a, R);
@@ -452,7 +472,7 @@ csa_status csa_rel_attn_bwd(const csa_rel_attn_bwd_args* b, void* stream) {
   if (s != CSA_OK) return s;
   if (!b->dout || !b->dq || !b->dk || !b->dv || !b->dlq || !b->dlk || !b->workspace)
     return rfail(CSA_INVALID_ARG, "null gradient pointer / workspace");
-  const RelLayout R = rel_layout(a->B, a->H, a->N, a->L);
+  const RelLayout R = rel_layout(a->B, a->H, a->N, a->L, a->d);
   hipStream_t st = (hipStream_t)stream;
   void* ws = b->workspace;
   RelArgs p = make_rel(a, R);
@@ -505,9 +525,17 @@ csa_status csa_rel_attn_bwd(const csa_rel_attn_bwd_args* b, void* stream) {
     const float* X = which == 0 ? a->q : a->k;
     g.B = X; g.b_n = 1; g.b_k = which == 0 ? a->q_sn : a->k_sn; g.b_b1 = 0;
     g.b_b2 = which == 0 ? a->q_sh : a->k_sh; g.b_r = which == 0 ? a->q_sb : a->k_sb;
-    g.C = which == 0 ? b->dlk : b->dlq; g.c_m = D; g.c_n = 1; g.c_b1 = 0; g.c_b2 = (int64_t)L * D;
+    float* part = (float*)((char*)ws + R.part);
+    g.C = R.RS > 1 ? part : (which == 0 ? b->dlk : b->dlq);
+    g.c_m = D; g.c_n = 1; g.c_b1 = 0; g.c_b2 = (int64_t)L * D;
     g.M = L; g.N = D; g.K = N; g.H2 = H; g.R = B; g.alpha = 1.f; g.accumulate = 0;
+    g.rsplit = R.RS; g.nbat = H; g.c_split = (int64_t)H * L * D;
     gemm(st, g, H);
+    if (R.RS > 1) {
+      const int64_t n = (int64_t)H * L * D;
+      hipLaunchKernelGGL(k_sum_splits, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part,
+                         which == 0 ? b->dlk : b->dlq, n, R.RS, g.c_split);
+    }
   }
   return rcheck("csa_rel_attn_bwd");
 }
