@@ -44,6 +44,36 @@ struct GemmArgs {
   int rsplit, nbat; int64_t c_split;
 };
 
+// One 32-wide K chunk of lane operands: 16 consecutive k (lin permutation: half h takes
+// [16h, 16h+16)). VEC: k is the contiguous dimension (x_k == 1, 16-B aligned rows whose
+// allocation covers K rounded up to 4), loaded as dwordx4; otherwise strided scalar loads (the
+// 32 lanes of a half are then the contiguous dimension). Addresses are always in bounds
+// (clamped); validity only selects the value, so no branch surrounds a load.
+template <bool VEC>
+__device__ __forceinline__ void chunk_load(float* v, const float* __restrict__ row, int64_t xk, int kb, int K,
+                                           bool rv) {
+  if constexpr (VEC) {
+#pragma unroll
+    for (int s = 0; s < 16; s += 4) {
+      const int kk = kb + s;
+      const f32x4 x = *reinterpret_cast<const f32x4*>(row + (kk < K ? kk : 0));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[s + e] = (rv && kk + e < K) ? x[e] : 0.f;
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int kk = kb + s;
+      const float x = row[(int64_t)(kk < K ? kk : 0) * xk];
+      v[s] = (rv && kk < K) ? x : 0.f;
+    }
+  }
+}
+
+// AV && BV: register double buffering, chunk k0 + 32 in flight while chunk k0's 16 MFMAs run.
+// Otherwise single-buffered (the strided scalar operand's address math already holds ~100 VGPRs;
+// double buffering it halved occupancy and ran slower).
+template <bool AV, bool BV>
 __global__ __launch_bounds__(64) void k_bgemm(const GemmArgs g) {
   const int lane = lane_id(), c = lane & 31, h = lane >> 5;
   const int n0 = blockIdx.x * 32, m0 = blockIdx.y * 32;
@@ -57,19 +87,51 @@ __global__ __launch_bounds__(64) void k_bgemm(const GemmArgs g) {
   const int m = m0 + c, n = n0 + c;
   const bool mv = m < g.M, nv = n < g.N;
   f32x16 acc = zero16();
-  for (int r = r_lo; r < r_hi; ++r) {
-    const float* Ar = A + r * g.a_r + (int64_t)m * g.a_m;
-    const float* Br = Bp + r * g.b_r + (int64_t)n * g.b_n;
-    for (int k0 = 0; k0 < g.K; k0 += 32) {
+  if constexpr (AV && BV) {
+    const int mc = imin(m, g.M - 1), nc = imin(n, g.N - 1);
+    for (int r = r_lo; r < r_hi; ++r) {
+      const float* Ar = A + r * g.a_r + (int64_t)mc * g.a_m;
+      const float* Br = Bp + r * g.b_r + (int64_t)nc * g.b_n;
       float av[16], bv[16];
+      chunk_load<true>(av, Ar, 1, 16 * h, g.K, mv);
+      chunk_load<true>(bv, Br, 1, 16 * h, g.K, nv);
+      for (int k0 = 0; k0 < g.K; k0 += 32) {
+        float an[16], bn[16];
+        chunk_load<true>(an, Ar, 1, k0 + 32 + 16 * h, g.K, mv);
+        chunk_load<true>(bn, Br, 1, k0 + 32 + 16 * h, g.K, nv);
 #pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        const int kk = k0 + 16 * h + s;
-        av[s] = (mv && kk < g.K) ? Ar[(int64_t)kk * g.a_k] : 0.f;
-        bv[s] = (nv && kk < g.K) ? Br[(int64_t)kk * g.b_k] : 0.f;
+        for (int s = 0; s < 16; ++s) acc = mfma(av[s], bv[s], acc);
+#pragma unroll
+        for (int s = 0; s < 16; ++s) { av[s] = an[s]; bv[s] = bn[s]; }
       }
+    }
+  } else {
+    for (int r = r_lo; r < r_hi; ++r) {
+      const float* Ar = A + r * g.a_r + (int64_t)(AV ? imin(m, g.M - 1) : m) * g.a_m;
+      const float* Br = Bp + r * g.b_r + (int64_t)(BV ? imin(n, g.N - 1) : n) * g.b_n;
+      for (int k0 = 0; k0 < g.K; k0 += 32) {
+        float av[16], bv[16];
+        if constexpr (AV) {
+          chunk_load<true>(av, Ar, 1, k0 + 16 * h, g.K, mv);
+        } else {
 #pragma unroll
-      for (int s = 0; s < 16; ++s) acc = mfma(av[s], bv[s], acc);
+          for (int s = 0; s < 16; ++s) {
+            const int kk = k0 + 16 * h + s;
+            av[s] = (mv && kk < g.K) ? Ar[(int64_t)kk * g.a_k] : 0.f;
+          }
+        }
+        if constexpr (BV) {
+          chunk_load<true>(bv, Br, 1, k0 + 16 * h, g.K, nv);
+        } else {
+#pragma unroll
+          for (int s = 0; s < 16; ++s) {
+            const int kk = k0 + 16 * h + s;
+            bv[s] = (nv && kk < g.K) ? Br[(int64_t)kk * g.b_k] : 0.f;
+          }
+        }
+#pragma unroll
+        for (int s = 0; s < 16; ++s) acc = mfma(av[s], bv[s], acc);
+      }
     }
   }
   float* C = g.C + b1 * g.c_b1 + b2 * g.c_b2 + split * g.c_split;
@@ -97,6 +159,7 @@ __global__ __launch_bounds__(256) void k_sum_splits(const float* __restrict__ pa
 
 struct RelArgs {
   int B, H, N, L, Lp, NQB, NKB, group;
+  int ldg;  // row stride of the G^T / P^T images (N rounded up to 4: 16-B aligned rows)
   const float *q, *k, *v; int64_t q_sb, q_sh, q_sn, k_sb, k_sh, k_sn, v_sb, v_sh, v_sn;
   const uint8_t *rel, *mask; int64_t rel_sb, rel_sh, mask_sb, mask_sh;
   const float *c2p, *p2ct;  // (B,H,N,Lp), (B,H,N,Lp)
@@ -243,8 +306,8 @@ __global__ __launch_bounds__(64) void k_rel_bwd_q(const RelArgs p) {
   const uint8_t* mp = p.mask + plane_off(p, b, hd, p.mask_sb, p.mask_sh);
   const float* c2p = p.c2p + (int64_t)bh * p.N * p.Lp;
   const float* p2ct = p.p2ct + (int64_t)bh * p.N * p.Lp;
-  float* Gb = p.G + (int64_t)bh * p.N * p.N;
-  float* Pb = p.P + (int64_t)bh * p.N * p.N;
+  float* __restrict__ Gb = p.G + (int64_t)bh * p.N * p.ldg;
+  float* __restrict__ Pb = p.P + (int64_t)bh * p.N * p.ldg;
   f32x16 dq[DT];
 #pragma unroll
   for (int t = 0; t < DT; ++t) dq[t] = zero16();
@@ -265,18 +328,28 @@ __global__ __launch_bounds__(64) void k_rel_bwd_q(const RelArgs p) {
 #pragma unroll
       for (int s = 0; s < NS; ++s) dpacc = mfma(vr[s], dO[s], dpacc);
     }
+    // all of the tile's score gathers first, so they are issued back to back instead of each
+    // waiting behind the previous element's G/P stores (G/P are __restrict__)
+    float sc[16];
+    bool msk[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int y = j0 + crow(r, h);
+      sc[r] = rel_score(p, sacc[r], i, y, rp, mp, c2p, p2ct);
+      msk[r] = mp[(int64_t)ic * p.N + imin(y, p.N - 1)] != 0;
+    }
     float gv[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int y = j0 + crow(r, h);
-      const float sc = rel_score(p, sacc[r], i, y, rp, mp, c2p, p2ct);
-      const bool inside = sc != NEG_INF;
-      const bool masked = mp[(int64_t)ic * p.N + imin(y, p.N - 1)] != 0;
-      const float P = inside ? __expf(sc - rmax) * rinv : 0.f;
-      const float g = (inside && !masked) ? P * (dpacc[r] - delta) * p.inv_scale : 0.f;
+      const bool inside = sc[r] != NEG_INF;
+      const float P = inside ? __expf(sc[r] - rmax) * rinv : 0.f;
+      const float g = (inside && !msk[r]) ? P * (dpacc[r] - delta) * p.inv_scale : 0.f;
+      // transposed images G^T / P^T [y][x] (row stride ldg): the 32 query lanes store one
+      // contiguous 128-B run per key
       if (inside) {
-        Gb[(int64_t)i * p.N + y] = g;
-        Pb[(int64_t)i * p.N + y] = P;
+        Gb[(int64_t)y * p.ldg + i] = g;
+        Pb[(int64_t)y * p.ldg + i] = P;
       }
       gv[r] = g;
     }
@@ -316,18 +389,18 @@ __global__ __launch_bounds__(64) void k_rel_scatter(const RelArgs p, float* __re
     const int bh = (int)(rowid / p.N), x = (int)(rowid % p.N);
     const int b = bh / p.H, hd = bh % p.H;
     const uint8_t* rp = p.rel + plane_off(p, b, hd, p.rel_sb, p.rel_sh);
-    const float* Gb = p.G + (int64_t)bh * p.N * p.N;
+    const float* Gb = p.G + (int64_t)bh * p.N * p.ldg;  // G^T [y][x]
     if (mode == 0) {
       for (int y = 0; y < p.N; ++y) {
         int r = rp[(int64_t)x * p.N + y];
         r = r < p.L ? r : p.L - 1;
-        my[r] += Gb[(int64_t)x * p.N + y];
+        my[r] += Gb[(int64_t)y * p.ldg + x];
       }
     } else {
       for (int xx = 0; xx < p.N; ++xx) {
         int r = rp[(int64_t)x * p.N + xx];  // rel[y = x][xx]
         r = r < p.L ? r : p.L - 1;
-        my[r] += Gb[(int64_t)xx * p.N + x];
+        my[r] += Gb[(int64_t)x * p.ldg + xx];
       }
     }
     float* o = out + rowid * p.Lp;
@@ -351,11 +424,19 @@ csa_status rcheck(const char* what) {
 
 void gemm(hipStream_t st, const GemmArgs& g, int nbat) {
   dim3 grid((unsigned)((g.N + 31) / 32), (unsigned)((g.M + 31) / 32), (unsigned)(nbat * (g.rsplit > 1 ? g.rsplit : 1)));
-  hipLaunchKernelGGL(k_bgemm, grid, dim3(64), 0, st, g);
+  // dwordx4 operand loads where k is contiguous and every row start is 16-B aligned
+  auto vec = [](const float* base, int64_t xk, int64_t xm, int64_t xb1, int64_t xb2, int64_t xr) {
+    return xk == 1 && ((uintptr_t)base) % 16 == 0 && xm % 4 == 0 && xb1 % 4 == 0 && xb2 % 4 == 0 && xr % 4 == 0;
+  };
+  const bool av = vec(g.A, g.a_k, g.a_m, g.a_b1, g.a_b2, g.a_r), bv = vec(g.B, g.b_k, g.b_n, g.b_b1, g.b_b2, g.b_r);
+  if (av && bv) hipLaunchKernelGGL((k_bgemm<true, true>), grid, dim3(64), 0, st, g);
+  else if (av) hipLaunchKernelGGL((k_bgemm<true, false>), grid, dim3(64), 0, st, g);
+  else if (bv) hipLaunchKernelGGL((k_bgemm<false, true>), grid, dim3(64), 0, st, g);
+  else hipLaunchKernelGGL((k_bgemm<false, false>), grid, dim3(64), 0, st, g);
 }
 
 struct RelLayout {
-  int64_t Lp;
+  int64_t Lp, ldg;
   int RS;                                    // batch splits of the dlq / dlk reductions
   size_t c2p, p2ct, state_total;             // forward state
   size_t G, P, gc2p, gp2ct, part, ws_total;  // backward workspace
@@ -375,8 +456,9 @@ RelLayout rel_layout(int64_t B, int64_t H, int64_t N, int64_t L, int64_t d) {
   R.p2ct = take(sizeof(float) * B * H * N * R.Lp);
   R.state_total = o;
   o = 0;
-  R.G = take(sizeof(float) * B * H * N * N);
-  R.P = take(sizeof(float) * B * H * N * N);
+  R.ldg = ((N + 3) / 4) * 4;
+  R.G = take(sizeof(float) * B * H * N * R.ldg);
+  R.P = take(sizeof(float) * B * H * N * R.ldg);
   R.gc2p = take(sizeof(float) * B * H * N * R.Lp);
   R.gp2ct = take(sizeof(float) * B * H * N * R.Lp);
   R.part = take(sizeof(float) * R.RS * H * L * d);
@@ -407,7 +489,7 @@ RelArgs make_rel(const csa_rel_attn_args* a, const RelLayout& R) {
   RelArgs p;
   memset(&p, 0, sizeof(p));
   p.B = (int)a->B; p.H = (int)a->H; p.N = (int)a->N; p.L = (int)a->L; p.Lp = (int)R.Lp;
-  p.NQB = (int)((a->N + 31) / 32); p.NKB = p.NQB; p.group = (int)a->rel_head_group;
+  p.NQB = (int)((a->N + 31) / 32); p.NKB = p.NQB; p.group = (int)a->rel_head_group; p.ldg = (int)R.ldg;
   p.q = a->q; p.k = a->k; p.v = a->v;
   p.q_sb = a->q_sb; p.q_sh = a->q_sh; p.q_sn = a->q_sn;
   p.k_sb = a->k_sb; p.k_sh = a->k_sh; p.k_sn = a->k_sn;
@@ -481,7 +563,7 @@ csa_status csa_rel_attn_bwd(const csa_rel_attn_bwd_args* b, void* stream) {
   p.P = (float*)((char*)ws + R.P);
   const int B = (int)a->B, H = (int)a->H, N = (int)a->N, L = (int)a->L, D = (int)a->d;
   const int64_t Lp = R.Lp;
-  // zero G/P (entries beyond N are never written; the GEMMs read only [0,N))
+  // G^T / P^T: columns x >= N of each row are never written; the GEMMs select zeros there
   const dim3 grid(xcd_grid(p.NQB, B * H));
   if (D == 64) hipLaunchKernelGGL(k_rel_bwd_q<64>, grid, dim3(64), 0, st, p);
   else if (D == 32) hipLaunchKernelGGL(k_rel_bwd_q<32>, grid, dim3(64), 0, st, p);
@@ -491,7 +573,8 @@ csa_status csa_rel_attn_bwd(const csa_rel_attn_bwd_args* b, void* stream) {
   for (int which = 0; which < 2; ++which) {
     GemmArgs g;
     memset(&g, 0, sizeof(g));
-    g.A = which == 0 ? p.P : p.G; g.a_m = 1; g.a_k = N; g.a_b1 = (int64_t)H * N * N; g.a_b2 = (int64_t)N * N;
+    g.A = which == 0 ? p.P : p.G; g.a_m = R.ldg; g.a_k = 1; g.a_b1 = (int64_t)H * N * R.ldg;
+    g.a_b2 = (int64_t)N * R.ldg;
     if (which == 0) { g.B = b->dout; g.b_n = 1; g.b_k = D; g.b_b1 = (int64_t)H * N * D; g.b_b2 = (int64_t)N * D; }
     else { g.B = a->q; g.b_n = 1; g.b_k = a->q_sn; g.b_b1 = a->q_sb; g.b_b2 = a->q_sh; }
     g.C = which == 0 ? b->dv : b->dk; g.c_m = D; g.c_n = 1; g.c_b1 = (int64_t)H * N * D; g.c_b2 = (int64_t)N * D;
