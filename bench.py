@@ -68,6 +68,10 @@ class HipEvents:
     def elapsed_ms(self, a, b):
         ms = ctypes.c_float()
         if self.hip.hipEventElapsedTime(ctypes.byref(ms), a, b) != 0:
+            # a stage that did not run (e.g. the projection stages of the dense ablation) left its
+            # events unrecorded: clear the thread's HIP error so the next library call does not
+            # report it as its own launch failure
+            self.hip.hipGetLastError()
             return float("nan")
         return ms.value
 
@@ -107,7 +111,7 @@ def cpu_baseline(seconds, B=16, H=8, N=150, d=64, k=10):
         if el >= seconds and n >= 2:
             break
     return {"value": round(n * B / el, 2), "unit": "ASTs/s", "cores": threads, "kind": "port",
-            "sample": f"{n} oracle fwd+bwd steps of B={B} (H=8,N=150,d=64,k=10, train mode) in {el:.1f}s"}
+            "sample": f"{n} oracle fwd+bwd steps of B={B} (H={H},N={N},d={d},k={k}, train mode) in {el:.1f}s"}
 
 
 def train_step_bench(world, rank, dev, steps, warmup, config="java", per_gpu_batch=64, nbatches=3):
@@ -152,6 +156,8 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--seq-len", type=int, default=150, help="AST nodes N (config 5 long-AST stress: 1024)")
+    ap.add_argument("--clusters", type=int, default=10, help="SBM clusters k (config 5 sweep: 16..128)")
     ap.add_argument("--dense", action="store_true", help="FullAttention ablation (config/python_full_att.py)")
     ap.add_argument("--eval", action="store_true", help="eval mode (no dropout)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -172,7 +178,7 @@ def main():
     from csa_amd._lib import STAGES, CsaProf, KERNEL_OF_STAGE
     from csa_amd.module.sbm_attn import FullAttention, SBMAttention
 
-    B, H, N, d, k = args.batch, 8, 150, 64, 10
+    B, H, N, d, k = args.batch, 8, args.seq_len, 64, args.clusters
     torch.manual_seed(1234 + rank)
     cfg = {"attention_dropout": 0.2, "head_dim": d, "num_head": H, "num_clusters": [k], "return_maps": False}
     mod = (FullAttention(cfg, 0) if args.dense else SBMAttention(cfg, 0)).to(dev)
@@ -291,9 +297,9 @@ def main():
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "ASTs/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "f32", "data": "synthetic (N(0,1) Q/K/V, 150-node ASTs, no padding)",
+        "vs_baseline": None, "dtype": "f32", "data": f"synthetic (N(0,1) Q/K/V, {N}-node ASTs, no padding)",
         "config": {"workload": "SBMAttention fwd+bwd (config/python.py dims) " + ("dense FullAttention" if args.dense
-                   else "SBM"), "global_batch": B * world, "per_gpu_batch": B, "seq_len": N, "heads": H,
+                   else "SBM") + ("" if N == 150 else f", long-AST stress N={N} k={k}"), "global_batch": B * world, "per_gpu_batch": B, "seq_len": N, "heads": H,
                    "head_dim": d, "clusters": 0 if args.dense else k, "mode": "eval" if args.eval else "train",
                    "parallelism": f"dp{world}"},
         "roofline": roofline,
@@ -305,7 +311,7 @@ def main():
     if not args.no_train:
         out["train"] = train_step_bench(world, rank, dev, args.train_steps, max(2, args.warmup))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, B=16 if N <= 150 else 1, N=N, k=k)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -161,9 +161,10 @@ def _run_module(Q, K, V, mask, u, dX, dsp, params, k, training=False):
 
 @pytest.mark.skipif(not has_gpu(), reason="needs GPU")
 @pytest.mark.parametrize("shape", [(2, 2, 45, 64, 5), (2, 2, 200, 64, 64), (1, 2, 70, 64, 128), (1, 3, 150, 96, 20),
-                                   (1, 2, 33, 64, 32)])
+                                   (1, 2, 33, 64, 32), (1, 1, 1024, 64, 16), (1, 1, 1024, 64, 128)])
 def test_sbm_shapes_vs_oracle(shape):
-    """Shapes beyond the golden set (small k, k up to 128 = config-5 sweep, N > 150) vs the pinned oracle."""
+    """Shapes beyond the golden set (small k, k up to 128 = config-5 sweep, N > 150 up to the
+    config-5 long-AST N = 1024) vs the pinned oracle."""
     B, H, N, d, k = shape
     Q, K, V, mask, u, dX, dsp, params = _rand_case(B, H, N, d, k, seed=sum(shape))
     X, sp, graph, dQ, dK, dV, grads = _run_module(Q, K, V, mask, u, dX, dsp, params, k)
