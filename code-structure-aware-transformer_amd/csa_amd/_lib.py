@@ -82,6 +82,18 @@ class RelAttnBwdArgs(ctypes.Structure):
     ]
 
 
+class AdamwArgs(ctypes.Structure):
+    _fields_ = [
+        ("tensors", vp), ("chunk_tensor", vp), ("chunk_start", vp),
+        ("ntensors", i64), ("nchunks", i64),
+        ("beta1", f32), ("beta2", f32), ("one_minus_beta1", f32), ("one_minus_beta2", f32),
+        ("eps", f32), ("step_size", f32), ("decay", f32),
+    ]
+
+
+ADAMW_CHUNK = 4096  # CSA_ADAMW_CHUNK
+
+
 class CsaError(RuntimeError):
     pass
 
@@ -124,6 +136,8 @@ def lib():
     L.csa_rel_attn_fwd.argtypes = [ctypes.POINTER(RelAttnArgs), vp]
     L.csa_rel_attn_bwd.restype = ctypes.c_int
     L.csa_rel_attn_bwd.argtypes = [ctypes.POINTER(RelAttnBwdArgs), vp]
+    L.csa_adamw_step.restype = ctypes.c_int
+    L.csa_adamw_step.argtypes = [ctypes.POINTER(AdamwArgs), vp]
     if L.csa_abi_version() != CSA_ABI_VERSION:
         raise CsaError(f"ABI mismatch: library {L.csa_abi_version()} != binding {CSA_ABI_VERSION}")
     _lib = L
@@ -140,4 +154,5 @@ EXPORTED_SYMBOLS = (
     "csa_abi_version", "csa_status_str", "csa_last_error_str", "csa_sbm_supported", "csa_sbm_state_bytes",
     "csa_sbm_bwd_workspace_bytes", "csa_sbm_fwd", "csa_sbm_maps", "csa_sbm_bwd", "csa_ste_sample",
     "csa_ste_backward", "csa_rel_attn_state_bytes", "csa_rel_attn_bwd_workspace_bytes", "csa_rel_attn_fwd", "csa_rel_attn_bwd",
+    "csa_adamw_step",
 )

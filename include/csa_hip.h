@@ -10,6 +10,7 @@
  *   csa_ste_sample     module/STE.py:10-15        standalone sampler (bit-exact test surface)
  *   csa_rel_attn_fwd   module/disentangled_attn.py:44-65 DisentangledAttn.rel_attn
  *   csa_rel_attn_bwd   autograd of rel_attn (gather backward = deterministic scatter-add)
+ *   csa_adamw_step     script/optimizer.py:49-106 AdamW.step (all parameters in one launch)
  *
  * Conventions (all entry points):
  *   - fp32 data; device pointers; sizes and strides are int64 ELEMENT counts; the last
@@ -139,6 +140,28 @@ size_t csa_rel_attn_state_bytes(int64_t B, int64_t H, int64_t N, int64_t L, int6
 size_t csa_rel_attn_bwd_workspace_bytes(int64_t B, int64_t H, int64_t N, int64_t L, int64_t d);
 csa_status csa_rel_attn_fwd(const csa_rel_attn_args* a, void* stream);
 csa_status csa_rel_attn_bwd(const csa_rel_attn_bwd_args* a, void* stream);
+
+/* ---- AdamW step (script/optimizer.py:49-106; script/train.py:80 uses correct_bias=False) ----
+ * Per element, in the reference's op order:
+ *   m = b1 m + (1-b1) g;  v = b2 v + (1-b2) g^2;  p += -step_size * m / (sqrt(v) + eps);
+ *   p += -decay * p  (decay = lr * weight_decay, applied after the Adam update as in the reference)
+ * step_size = lr, or lr * sqrt(1 - b2^t) / (1 - b1^t) with correct_bias (computed by the caller).
+ * Gradients are read as given: GradScaler's unscale_ / inf check run before (torch.amp semantics). */
+#define CSA_ADAMW_CHUNK 4096
+typedef struct csa_adamw_tensor { /* one parameter tensor, contiguous fp32 (device pointers) */
+  float* param; const float* grad; float* exp_avg; float* exp_avg_sq; int64_t numel;
+} csa_adamw_tensor;
+
+typedef struct csa_adamw_args {
+  const csa_adamw_tensor* tensors; /* device array, ntensors entries */
+  const int32_t* chunk_tensor;     /* device (nchunks): tensor of each CSA_ADAMW_CHUNK-element chunk */
+  const int64_t* chunk_start;      /* device (ntensors): first chunk of each tensor */
+  int64_t ntensors, nchunks;
+  float beta1, beta2, one_minus_beta1, one_minus_beta2; /* 1-b as the reference's fp32 alpha/value */
+  float eps, step_size, decay;
+} csa_adamw_args;
+
+csa_status csa_adamw_step(const csa_adamw_args* a, void* stream);
 
 #ifdef __cplusplus
 }

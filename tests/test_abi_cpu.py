@@ -67,3 +67,14 @@ def test_ops_refuse_cpu_tensors():
     x = torch.zeros(4)
     with pytest.raises(RuntimeError):
         torch.ops.csa.ste_sample(x, x, 0.01, 0.99)
+
+
+def test_adamw_step_validates_without_gpu():
+    from csa_amd import _lib
+    L = _lib.lib()
+    assert L.csa_adamw_step(None, None) == 1
+    a = _lib.AdamwArgs(nchunks=0, beta1=0.9, beta2=0.999)  # nothing to update: OK, no launch
+    assert L.csa_adamw_step(ctypes.byref(a), None) == 0
+    a = _lib.AdamwArgs(nchunks=3, ntensors=1, beta1=0.9, beta2=0.999)  # null tables
+    assert L.csa_adamw_step(ctypes.byref(a), None) == 1
+    assert b"null tensor table" in L.csa_last_error_str()
