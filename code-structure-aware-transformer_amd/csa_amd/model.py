@@ -221,7 +221,9 @@ class BaseDecoder(nn.Module):
 
 
 class Generator(nn.Module):
-    """components.py:Generator: log(softmax(dropout(linear)))  (log of softmax, not log_softmax)."""
+    """components.py:95-102 Generator: log(softmax(dropout(linear(x))))  (log of softmax, not
+    log_softmax). The linear stays on hipBLASLt; dropout + softmax + log is one HIP kernel per
+    direction (csa_amd/gen_ops.py, csrc/csa_gen.hip). Module/param names as the reference."""
 
     def __init__(self, tgt_vocab_size, hidden_size, dropout):
         super().__init__()
@@ -230,7 +232,8 @@ class Generator(nn.Module):
         self.linear = nn.Linear(hidden_size, tgt_vocab_size)
 
     def forward(self, x):
-        return torch.log(self.soft_max(self.dropout(self.linear(x))))
+        from .gen_ops import gen_log_softmax
+        return gen_log_softmax(self.linear(x), self.dropout.p if self.training else 0.0)
 
 
 def make_std_mask(tgt, pad=PAD):
@@ -292,15 +295,52 @@ class CSATrans(nn.Module):
         return out, sparsity, pe, graphs, attns
 
 
+class LabelSmoothing(nn.Module):
+    """utils/label_smooth.py:15-40 without materialising true_dist (B*T x V: 251 MB per step at the java
+    config). true_dist is `confidence` at the target, 0 in the padding column and in padded rows, and
+    eps = smoothing / (V - 2) elsewhere, so the KLDiv(sum) / ntokens closes to, per non-pad row,
+        conf (log conf - x_t) + eps ((V-2) log eps - sum_{j != t, pad} x_j)
+    (the row sum is read only when smoothing > 0). torch's kl_div gives 0 * (-inf) = NaN wherever
+    true_dist is 0 and x is -inf (an underflowed log-probability); that NaN is reproduced with one
+    detached compare over x. ntokens = (target != 0).sum() literally, as the reference."""
+
+    def __init__(self, padding_idx, smoothing=0.0):
+        super().__init__()
+        self.padding_idx = padding_idx
+        self.confidence = 1.0 - smoothing
+        self.smoothing = smoothing
+        self.true_dist = None  # never materialised
+
+    def forward(self, x, target):
+        V = x.size(-1)
+        x = x.reshape(-1, V)
+        t = target.reshape(-1)
+        ntokens = (target != 0).sum()
+        valid = t != self.padding_idx
+        xt = x.gather(1, t.unsqueeze(1)).squeeze(1)
+        conf, sm = self.confidence, self.smoothing
+        row = -conf * xt + (conf * math.log(conf) if conf > 0.0 else 0.0)
+        with torch.no_grad():
+            bad = ~(x > float("-inf"))  # -inf or NaN
+            n_bad = bad.sum()
+            if sm > 0.0:
+                n_at_td = (bad[valid].sum() - bad[valid, self.padding_idx].sum()) if V > 2 else 0
+            else:
+                n_at_td = (bad.gather(1, t.unsqueeze(1)).squeeze(1) & valid).sum()
+            poison = torch.where(n_bad > n_at_td, float("nan"), 0.0).to(x.dtype)
+        if sm > 0.0:
+            eps = sm / (V - 2)
+            col = torch.arange(V, device=x.device).unsqueeze(0)
+            off = (col == t.unsqueeze(1)) | (col == self.padding_idx)  # true_dist != eps there
+            rest = torch.where(off, torch.zeros_like(x), x).sum(1)
+            row = row + eps * ((V - 2) * math.log(eps) - rest)
+        loss = torch.where(valid, row, torch.zeros_like(row)).sum() + poison
+        return loss / ntokens
+
+
 def label_smoothing_loss(logp, target, padding_idx=PAD):
-    """utils/label_smooth.py:15-40 at smoothing=0 (all configs): KLDiv(sum) against the one-hot
-    true_dist with padded rows zeroed, divided by the non-pad token count — computed without
-    materialising the (B*T, V) true_dist: sum over non-pad rows of -logp[target]."""
-    x = logp.reshape(-1, logp.size(-1))
-    t = target.reshape(-1)
-    ntokens = (t != padding_idx).sum()
-    picked = x.gather(1, t.unsqueeze(1)).squeeze(1)
-    return -(picked * (t != padding_idx)).sum() / ntokens
+    """LabelSmoothing(padding_idx, smoothing=0) as a function (all configs use smoothing 0)."""
+    return LabelSmoothing(padding_idx, 0.0)(logp, target)
 
 
 def batch_to_device(sb, device):

@@ -11,6 +11,7 @@
  *   csa_rel_attn_fwd   module/disentangled_attn.py:44-65 DisentangledAttn.rel_attn
  *   csa_rel_attn_bwd   autograd of rel_attn (gather backward = deterministic scatter-add)
  *   csa_adamw_step     script/optimizer.py:49-106 AdamW.step (all parameters in one launch)
+ *   csa_gen_logsoftmax_fwd/_bwd  module/components.py:95-102 Generator: log(softmax(dropout(logits)))
  *
  * Conventions (all entry points):
  *   - fp32 data; device pointers; sizes and strides are int64 ELEMENT counts; the last
@@ -162,6 +163,16 @@ typedef struct csa_adamw_args {
 } csa_adamw_args;
 
 csa_status csa_adamw_step(const csa_adamw_args* a, void* stream);
+
+/* ---- Generator head (module/components.py:95-102): logp = log(softmax(dropout(logits), -1)) ----
+ * logits/logp/dlogp/dlogits: (rows, V) contiguous fp32. dropout p in [0,1) (0 = eval); the keep mask
+ * is regenerated in the backward from (seed, offset): Philox stream 4, element (row, col) ->
+ * u16 (col & 7) of philox({col >> 3, row, 0, (4 << 28) ^ offset}), keep <=> u16 >= ceil(p * 65536).
+ * Backward is the reference autograd chain: t = dlogp / s, dz = keep / (1-p) * s * (t - sum(t * s)). */
+csa_status csa_gen_logsoftmax_fwd(const float* logits, float* logp, int64_t rows, int64_t V, float dropout,
+                                  uint64_t seed, uint64_t offset, void* stream);
+csa_status csa_gen_logsoftmax_bwd(const float* dlogp, const float* logp, float* dlogits, int64_t rows, int64_t V,
+                                  float dropout, uint64_t seed, uint64_t offset, void* stream);
 
 #ifdef __cplusplus
 }

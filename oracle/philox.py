@@ -101,3 +101,17 @@ def proj_keep(B, H, rows, d, seed, offset, p, layer, is_k):
                        ((RNG_PROJ_DROP << 28) ^ (int(offset) & 0xFFFFFFFF)) & 0xFFFFFFFF,
                        int(seed) & 0xFFFFFFFF, int(seed) >> 32)
     return u16_of(words, np.broadcast_to(e, words[0].shape)) >= keep_threshold(p)
+
+
+RNG_GEN_DROP = 4
+
+
+def gen_keep(rows, V, seed, offset, p):
+    """(rows, V) bool keep mask of the Generator's dropout (module/components.py:100, nn.Dropout on the
+    logits) as csrc/csa_gen.hip draws it: element (row, col) -> 16-bit uniform (col & 7) of
+    philox({col >> 3, row, 0, (RNG_GEN_DROP << 28) ^ offset}, seed)."""
+    row = np.arange(rows).reshape(rows, 1)
+    col = np.arange(V).reshape(1, V)
+    words = philox4x32(col >> 3, row, 0, ((RNG_GEN_DROP << 28) ^ (int(offset) & 0xFFFFFFFF)) & 0xFFFFFFFF,
+                       int(seed) & 0xFFFFFFFF, int(seed) >> 32)
+    return u16_of(words, np.broadcast_to(col & 7, words[0].shape)) >= keep_threshold(p)

@@ -119,3 +119,45 @@ def test_ddp_two_ranks_average_gradients():
             np.testing.assert_allclose(gd, gm.numpy(), rtol=1e-5, atol=1e-6)
     for wa, wb in zip(res[0][1], res[1][1]):  # replicas stay identical after the step
         np.testing.assert_array_equal(wa, wb)
+
+
+def _reference_label_smoothing(x, target, padding_idx, smoothing):
+    """utils/label_smooth.py:24-40 restated (materialised true_dist + KLDiv(sum) / ntokens)."""
+    x = x.contiguous().view(-1, x.size(-1))
+    ntokens = (target != 0).sum()
+    t = target.contiguous().view(-1)
+    td = torch.full_like(x, smoothing / (x.size(1) - 2))
+    td.scatter_(1, t.unsqueeze(1), 1.0 - smoothing)
+    td[:, padding_idx] = 0
+    td[t == padding_idx] = 0
+    return torch.nn.functional.kl_div(x, td, reduction="sum") / ntokens
+
+
+@pytest.mark.parametrize("case,smoothing", [("label_smoothing", 0.0), ("label_smoothing_s01", 0.1)])
+def test_label_smoothing_module_matches_reference_golden(golden, case, smoothing):
+    from csa_amd.model import LabelSmoothing
+    z = golden(case)
+    logits = torch.from_numpy(z["logits"]).requires_grad_(True)
+    x = torch.log(torch.softmax(logits, -1))
+    loss = LabelSmoothing(0, smoothing)(x, torch.from_numpy(z["target"]))
+    np.testing.assert_allclose(loss.item(), z["loss"][0], rtol=1e-6)
+    loss.backward()
+    np.testing.assert_allclose(logits.grad.numpy(), z["dlogits"], rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize("smoothing", [0.0, 0.1])
+def test_label_smoothing_nan_semantics_of_underflowed_logprobs(smoothing):
+    """kl_div's 0 * (-inf) = NaN where true_dist is 0, +inf where it is > 0 (reference behaviour)."""
+    from csa_amd.model import LabelSmoothing
+    g = torch.Generator().manual_seed(9)
+    x = torch.log_softmax(torch.randn(2, 4, 11, generator=g), -1)
+    target = torch.randint(2, 11, (2, 4), generator=g)
+    target[1, 3] = 0
+    cases = []
+    a = x.clone(); a[0, 1, 0] = float("-inf"); cases.append(a)  # padding column (td = 0)
+    b = x.clone(); b[1, 3, 5] = float("-inf"); cases.append(b)  # padded row
+    c = x.clone(); c[0, 0, target[0, 0]] = float("-inf"); cases.append(c)  # at the target: +inf
+    for xx in cases:
+        mine = LabelSmoothing(0, smoothing)(xx, target).item()
+        ref = _reference_label_smoothing(xx, target, 0, smoothing).item()
+        assert (np.isnan(mine) and np.isnan(ref)) or mine == pytest.approx(ref, rel=1e-6), (mine, ref)

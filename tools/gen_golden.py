@@ -225,8 +225,9 @@ def disentangled_case(name, B, N, d_model, L, seed):
     print(f"{name}: ok")
 
 
-def label_smoothing_case(name, seed):
-    """utils/label_smooth.py:15-40 (smoothing=0 as in every config) on log(softmax) outputs with padding."""
+def label_smoothing_case(name, seed, smoothing=0.0):
+    """utils/label_smooth.py:15-40 (smoothing=0 as in every config; 0.1 for the general closed form) on
+    log(softmax) outputs with padding."""
     s = importlib.util.spec_from_file_location("ref_label_smooth", f"{REF}/utils/label_smooth.py")
     m = importlib.util.module_from_spec(s)
     s.loader.exec_module(m)
@@ -237,12 +238,36 @@ def label_smoothing_case(name, seed):
     target = torch.randint(4, V, (B, T), generator=g)
     target[0, 5:] = 0
     target[2, 3:] = 0
-    crit = m.LabelSmoothing(padding_idx=0, smoothing=0.0)
+    crit = m.LabelSmoothing(padding_idx=0, smoothing=smoothing)
     loss = crit(x, target)
     loss.backward()
     np.savez_compressed(os.path.join(OUT, f"{name}.npz"), logits=np32(logits), target=target.numpy(),
                         loss=np.array([loss.item()], np.float32), dlogits=np32(logits.grad))
     print(f"{name}: loss={loss.item():.5f}")
+
+
+def generator_case(name, seed):
+    """module/components.py:95-102 Generator in eval mode (dropout off): log(softmax(linear(x))), with
+    one row whose softmax underflows (log -> -inf, NaN gradient row, as the reference computes it)."""
+    comp = sys.modules["module.components"]
+    g = torch.Generator().manual_seed(seed)
+    B, T, D, V = 2, 5, 16, 1003
+    gen = comp.Generator(V, D, 0.2).eval()
+    with torch.no_grad():
+        gen.linear.weight.copy_(torch.randn(V, D, generator=g) * 0.3)
+        gen.linear.bias.copy_(torch.randn(V, generator=g) * 0.1)
+    x = torch.randn(B, T, D, generator=g)
+    x[1, 4] *= 400.0  # extreme logits: most probabilities underflow to 0 in fp32
+    x.requires_grad_(True)
+    out = gen(x)
+    dout = torch.randn(B, T, V, generator=g)
+    dout[0, :, :] = 0.0
+    dout[0, torch.arange(T), torch.randint(0, V, (T,), generator=g)] = -0.25  # label-smoothing-like one-hot rows
+    out.backward(dout)
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), x=np32(x), weight=np32(gen.linear.weight),
+                        bias=np32(gen.linear.bias), out=np32(out), dout=np32(dout), dx=np32(x.grad),
+                        dweight=np32(gen.linear.weight.grad), dbias=np32(gen.linear.bias.grad))
+    print(f"{name}: -inf entries {int(torch.isinf(out).sum())}, nan grads {int(torch.isnan(x.grad).sum())}")
 
 
 def adamw_case(name, seed):
@@ -374,6 +399,8 @@ def main():
     rel_attn_case("rel_attn_n20_dk64", B=1, N=20, dk=64, L=150, seed=43)
     disentangled_case("disentangled_n23", B=2, N=23, d_model=128, L=150, seed=51)
     label_smoothing_case("label_smoothing", seed=61)
+    label_smoothing_case("label_smoothing_s01", seed=63, smoothing=0.1)
+    generator_case("generator_v1003", seed=64)
     adamw_case("adamw_nobias", seed=62)
     csatrans_case("csatrans_tiny", seed=71)
 
