@@ -153,10 +153,13 @@ __global__ __launch_bounds__(256) void k_cluster_softmax(const float* __restrict
   // across the max / sum / normalise passes (one dot product per entry instead of three).
   const int hd = blockIdx.x, tid = threadIdx.x;
   if (hd == 0 && tid < H) cnt[tid] = 0ull;  // this call's edge counters (k_attn_fwd) start at zero
-  __shared__ float Cs[128 * 96];
+  // rows padded to D + 1 floats: consecutive threads read consecutive rows b, which then sit in
+  // different banks (an unpadded stride of D = 64 put every thread of a wave on one bank)
+  __shared__ float Cs[128 * 97];
   __shared__ float red[256];
   const float* Ch = C + (size_t)hd * k * D;
-  for (int e = tid; e < k * D; e += 256) Cs[e] = Ch[e];
+  const int LD = D + 1;
+  for (int e = tid; e < k * D; e += 256) Cs[(e / D) * LD + e % D] = Ch[e];
   __syncthreads();
   const int kk = k * k;
   float v[MAXE];
@@ -168,7 +171,7 @@ __global__ __launch_bounds__(256) void k_cluster_softmax(const float* __restrict
     if (e < kk) {
       const int a = e / k, b = e % k;
       float acc = 0.f;
-      for (int t = 0; t < D; ++t) acc = fmaf(Cs[a * D + t], Cs[b * D + t], acc);
+      for (int t = 0; t < D; ++t) acc = fmaf(Cs[a * LD + t], Cs[b * LD + t], acc);
       v[q] = acc;
       mx = fmaxf(mx, acc);
     }
@@ -1877,32 +1880,37 @@ __global__ __launch_bounds__(256) void k_reduce_slabs(const KArgs p, int D, int 
 }
 
 // dC_h = dC_ws[h] + (dD + dD^T) C_h, dD = S o (dS - <S, dS>)   (softmax over k^2, sbm_attn.py:39)
-__global__ __launch_bounds__(256) void k_cluster_grad(const float* __restrict__ S, const float* __restrict__ dS_ws,
+// One workgroup per (cluster row a, head): the k coefficients dD(a,b) + dD(b,a) go to LDS once and
+// the D outputs of row a are k-term fmaf chains over coalesced rows of C (b ascending; the <S, dS>
+// reduction is a fixed-order tree), so the result is deterministic.
+__global__ __launch_bounds__(128) void k_cluster_grad(const float* __restrict__ S, const float* __restrict__ dS_ws,
                                                       const float* __restrict__ dC_ws, const float* __restrict__ C,
                                                       float* __restrict__ dC, int k, int D, int KP32) {
-  const int hd = blockIdx.x, tid = threadIdx.x;
-  __shared__ float red[256];
+  const int a = blockIdx.x, hd = blockIdx.y, tid = threadIdx.x;
+  __shared__ float red[128];
+  __shared__ float coef[128];
   const float* Sh = S + (size_t)hd * KP32 * KP32;
   const float* dSh = dS_ws + (size_t)hd * KP32 * KP32;
   float acc = 0.f;
-  for (int e = tid; e < k * k; e += 256) {
-    const int a = e / k, b = e % k;
-    acc += Sh[a * KP32 + b] * dSh[a * KP32 + b];
+  for (int e = tid; e < k * k; e += 128) {
+    const int r = e / k, c = e % k;
+    acc += Sh[r * KP32 + c] * dSh[r * KP32 + c];
   }
   red[tid] = acc;
   __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
+  for (int s = 64; s > 0; s >>= 1) {
     if (tid < s) red[tid] += red[tid + s];
     __syncthreads();
   }
   const float dot = red[0];
-  auto dD = [&](int a, int b) { return Sh[a * KP32 + b] * (dSh[a * KP32 + b] - dot); };
+  if (tid < k)
+    coef[tid] = Sh[a * KP32 + tid] * (dSh[a * KP32 + tid] - dot) + Sh[tid * KP32 + a] * (dSh[tid * KP32 + a] - dot);
+  __syncthreads();
   const float* Ch = C + (size_t)hd * k * D;
-  for (int e = tid; e < k * D; e += 256) {
-    const int a = e / D, t = e % D;
+  for (int t = tid; t < D; t += 128) {
     float s = dC_ws[((size_t)hd * KP32 + a) * D + t];
-    for (int b = 0; b < k; ++b) s = fmaf(dD(a, b) + dD(b, a), Ch[b * D + t], s);
-    dC[(size_t)hd * k * D + e] = s;
+    for (int b = 0; b < k; ++b) s = fmaf(coef[b], Ch[b * D + t], s);
+    dC[((size_t)hd * k + a) * D + t] = s;
   }
 }
 
@@ -2153,7 +2161,7 @@ csa_status launch_bwd(const csa_sbm_bwd_args* b, const Layout& L, hipStream_t st
     hipLaunchKernelGGL(k_reduce_slabs, dim3((unsigned)((total + 63) / 64)), dim3(256), 0, st, p, D, KP32,
                        b->dproj_w[0], b->dproj_w[1], b->dproj_w[2], b->dproj_b[0], b->dproj_b[1], b->dproj_b[2],
                        dS_ws, dC_ws);
-    hipLaunchKernelGGL(k_cluster_grad, dim3(a->H), dim3(256), 0, st, p.S, (const float*)dS_ws,
+    hipLaunchKernelGGL(k_cluster_grad, dim3((unsigned)a->k, (unsigned)a->H), dim3(128), 0, st, p.S, (const float*)dS_ws,
                        (const float*)dC_ws, a->cluster_w, b->dcluster_w, (int)a->k, D, KP32);
   } else {
     launch_attn_bwd<D, 0, true>(p, BH, L, a->attn_dropout > 0.f, pf, st);
