@@ -88,6 +88,7 @@ class AdamwArgs(ctypes.Structure):
         ("ntensors", i64), ("nchunks", i64),
         ("beta1", f32), ("beta2", f32), ("one_minus_beta1", f32), ("one_minus_beta2", f32),
         ("eps", f32), ("step_size", f32), ("decay", f32),
+        ("grad_scale", vp), ("found_inf", vp),
     ]
 
 

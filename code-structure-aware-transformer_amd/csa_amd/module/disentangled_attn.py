@@ -2,7 +2,9 @@
 return tuple and state_dict keys; the relation attention runs in torch.ops.csa.rel_attn_*."""
 import copy
 
+import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 from .. import rel_ops
 
@@ -33,13 +35,20 @@ class DisentangledAttn(nn.Module):
         self.t_linear = _get_clones(nn.Linear(d_model, self.d_k * 4), 2)
 
     def forward(self, query, key, value, rel_emb, rel, mask):
-        query, key, value = [transpose_for_scores(l(x), self.h) for l, x in zip(self.linear_layers, (query, key, value))]
+        if query is key and key is value:  # self-attention (CSE_layer, csa_trans.py:231-233): one QKV GEMM
+            qkv = self.linear_layers[:3]
+            w = torch.cat([l.weight for l in qkv], 0)
+            b = torch.cat([l.bias for l in qkv], 0)
+            query, key, value = (transpose_for_scores(t, self.h)
+                                 for t in F.linear(query, w, b).split(w.size(0) // 3, dim=-1))
+        else:
+            query, key, value = [transpose_for_scores(l(x), self.h)
+                                 for l, x in zip(self.linear_layers, (query, key, value))]
         lq = rel_emb[0]
         l = lq[0].unsqueeze(0)  # 1, L, d
         t = lq[1].unsqueeze(0)
         lq, lk = [transpose_for_scores(lin(x), 4) for lin, x in zip(self.l_linear, (l, l))]
         tq, tk = [transpose_for_scores(lin(x), 4) for lin, x in zip(self.t_linear, (t, t))]
-        import torch
         lq = torch.cat([lq, tq], dim=1)  # 1, 8, L, d
         lk = torch.cat([lk, tk], dim=1)
         output = self.rel_attn(query, key, value, lq, lk, rel, mask)

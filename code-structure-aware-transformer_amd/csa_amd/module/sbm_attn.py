@@ -13,6 +13,7 @@ Extensions (all default to the reference behaviour):
 """
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 from .. import ops
 
@@ -90,9 +91,12 @@ class Attention(nn.Module):
 
     def forward(self, inputs):
         X, mask, deliver = inputs
-        Q = self.split_heads(self.W_q(X))  # B, H, N, d (strided view, consumed in place by the kernel)
-        K = self.split_heads(self.W_k(X))
-        V = self.split_heads(self.W_v(X))
+        # W_q / W_k / W_v as ONE (3 H d x dim) GEMM (parameters and state_dict keys unchanged); Q, K, V
+        # are strided (B, H, N, d) views of its output, consumed in place by the kernels
+        hd = self.num_head * self.head_dim
+        w = torch.cat([self.W_q.weight, self.W_k.weight, self.W_v.weight], 0)
+        b = torch.cat([self.W_q.bias, self.W_k.bias, self.W_v.bias], 0)
+        Q, K, V = (self.split_heads(t) for t in F.linear(X, w, b).split(hd, dim=-1))
         with torch.autocast(device_type="cuda", enabled=False):  # sbm_attn.py:120
             attn_out, sparsity, graph, attn = self.attn(Q.float(), K.float(), V.float(), mask.float())
         attn_out = self.combine_heads(attn_out)

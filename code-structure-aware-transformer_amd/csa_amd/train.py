@@ -25,7 +25,16 @@ import torch.distributed as dist
 
 class AdamW(torch.optim.Optimizer):
     """script/optimizer.py:10-106 (decoupled weight decay, optional bias correction): one csa_adamw_step
-    launch for all CUDA parameters, foreach ops on CPU."""
+    launch for all CUDA parameters, foreach ops on CPU.
+
+    Under torch.amp.GradScaler the optimizer takes the scaler's device-side `grad_scale` and
+    `found_inf` (_step_supports_amp_scaling): the kernel unscales the gradients and skips the update
+    on inf/NaN itself, so `scaler.step()` needs no host sync. The skip then happens on the device
+    while the host-side step counter still advances; bias correction depends on that counter, so
+    groups with correct_bias=True (not the reference's configuration, script/train.py:80) take the
+    host-synchronised skip instead."""
+
+    _step_supports_amp_scaling = True
 
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-6, weight_decay=0.0, correct_bias=True):
         if lr < 0.0 or not 0.0 <= betas[0] < 1.0 or not 0.0 <= betas[1] < 1.0 or eps < 0.0:
@@ -62,7 +71,7 @@ class AdamW(torch.optim.Optimizer):
             self._tables = {sizes: lay, desc_key: desc}
         return desc, lay[0], lay[1], len(ps), lay[2]
 
-    def _fused_step(self, group, ps, grads, m, v, step_size):
+    def _fused_step(self, group, ps, grads, m, v, step_size, grad_scale=None, found_inf=None):
         from ._lib import AdamwArgs, check, lib
         for t in ps + grads + m + v:
             if t.dtype != torch.float32 or not t.is_contiguous():
@@ -72,13 +81,24 @@ class AdamW(torch.optim.Optimizer):
         a = AdamwArgs(tensors=desc.data_ptr(), chunk_tensor=owner.data_ptr(), chunk_start=start.data_ptr(),
                       ntensors=nt, nchunks=nc, beta1=b1, beta2=b2, one_minus_beta1=1.0 - b1,
                       one_minus_beta2=1.0 - b2, eps=group["eps"], step_size=step_size,
-                      decay=group["lr"] * group["weight_decay"] if group["weight_decay"] > 0.0 else 0.0)
+                      decay=group["lr"] * group["weight_decay"] if group["weight_decay"] > 0.0 else 0.0,
+                      grad_scale=None if grad_scale is None else grad_scale.data_ptr(),
+                      found_inf=None if found_inf is None else found_inf.data_ptr())
         stream = ctypes.c_void_p(torch.cuda.current_stream(ps[0].device).cuda_stream)
         check(lib().csa_adamw_step(ctypes.byref(a), stream), "csa_adamw_step")
 
     @torch.no_grad()
     def step(self, closure=None):
         loss = closure() if closure is not None else None
+        grad_scale = getattr(self, "grad_scale", None)  # set by GradScaler.step (device tensors)
+        found_inf = getattr(self, "found_inf", None)
+        if grad_scale is not None:
+            grad_scale = grad_scale.to(torch.float32).contiguous()
+        if found_inf is not None:
+            found_inf = found_inf.to(torch.float32).contiguous()
+            on_host = any(p.grad is not None and not p.is_cuda for g in self.param_groups for p in g["params"])
+            if (on_host or any(g["correct_bias"] for g in self.param_groups)) and found_inf.item() != 0.0:
+                return loss  # GradScaler skip, decided on the host (no state change)
         for group in self.param_groups:
             ps = [p for p in group["params"] if p.grad is not None]
             if not ps:
@@ -100,8 +120,10 @@ class AdamW(torch.optim.Optimizer):
                 t = self.state[ps[0]]["step"]
                 step_size = step_size * (1.0 - b2 ** t) ** 0.5 / (1.0 - b1 ** t)
             if ps[0].is_cuda:
-                self._fused_step(group, ps, grads, m, v, step_size)
+                self._fused_step(group, ps, grads, m, v, step_size, grad_scale, found_inf)
                 continue
+            if grad_scale is not None:
+                grads = torch._foreach_mul(grads, (1.0 / grad_scale.double()).float().item())
             torch._foreach_mul_(m, b1)
             torch._foreach_add_(m, grads, alpha=1.0 - b1)
             torch._foreach_mul_(v, b2)

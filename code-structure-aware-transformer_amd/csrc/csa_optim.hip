@@ -7,6 +7,9 @@
 // once (param, grad, exp_avg, exp_avg_sq) and written once (param, exp_avg, exp_avg_sq): 28 B per
 // parameter, HBM-bound.
 //
+// Mixed precision: GradScaler hands the optimizer its scale and found_inf as device tensors
+// (_step_supports_amp_scaling), so unscaling and the skip-on-inf happen here, with no host sync.
+//
 // Work decomposition: each tensor is cut into CSA_ADAMW_CHUNK-element chunks; one 256-thread
 // workgroup per chunk; chunk_tensor[] / chunk_start[] (built once per parameter layout by the
 // caller) map a chunk to its tensor and offset without a search.
@@ -31,7 +34,11 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
 
 __global__ __launch_bounds__(256) void k_adamw(const csa_adamw_tensor* __restrict__ tensors,
                                                const int32_t* __restrict__ chunk_tensor,
-                                               const int64_t* __restrict__ chunk_start, const AdamElem c) {
+                                               const int64_t* __restrict__ chunk_start, AdamElem c,
+                                               const float* __restrict__ grad_scale,
+                                               const float* __restrict__ found_inf) {
+  if (found_inf != nullptr && *found_inf != 0.f) return;  // GradScaler: skip the step on inf/NaN grads
+  const float inv = grad_scale != nullptr ? (float)(1.0 / (double)*grad_scale) : 1.f;
   const int64_t chunk = blockIdx.x;
   const int t = chunk_tensor[chunk];
   const csa_adamw_tensor T = tensors[t];
@@ -53,18 +60,18 @@ __global__ __launch_bounds__(256) void k_adamw(const csa_adamw_tensor* __restric
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           float pe = pv[e], me = mv[e], ve = vv[e];
-          adam_elem(pe, gv[e], me, ve, c);
+          adam_elem(pe, gv[e] * inv, me, ve, c);
           pv[e] = pe; mv[e] = me; vv[e] = ve;
         }
         *reinterpret_cast<f32x4*>(p + i) = pv;
         *reinterpret_cast<f32x4*>(m + i) = mv;
         *reinterpret_cast<f32x4*>(v + i) = vv;
       } else {
-        for (int e = i; e < n; ++e) adam_elem(p[e], g[e], m[e], v[e], c);
+        for (int e = i; e < n; ++e) adam_elem(p[e], g[e] * inv, m[e], v[e], c);
       }
     }
   } else {
-    for (int i = threadIdx.x; i < n; i += 256) adam_elem(p[i], g[i], m[i], v[i], c);
+    for (int i = threadIdx.x; i < n; i += 256) adam_elem(p[i], g[i] * inv, m[i], v[i], c);
   }
 }
 
@@ -92,7 +99,7 @@ extern "C" csa_status csa_adamw_step(const csa_adamw_args* a, void* stream) {
   c.b1 = a->beta1; c.b2 = a->beta2; c.om_b1 = a->one_minus_beta1; c.om_b2 = a->one_minus_beta2;
   c.eps = a->eps; c.neg_step = -a->step_size; c.neg_decay = -a->decay;
   hipLaunchKernelGGL(k_adamw, dim3((unsigned)a->nchunks), dim3(256), 0, (hipStream_t)stream, a->tensors,
-                     a->chunk_tensor, a->chunk_start, c);
+                     a->chunk_tensor, a->chunk_start, c, a->grad_scale, a->found_inf);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     csa::set_error("csa_adamw_step: %s", hipGetErrorString(e));

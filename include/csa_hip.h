@@ -147,7 +147,9 @@ csa_status csa_rel_attn_bwd(const csa_rel_attn_bwd_args* a, void* stream);
  *   m = b1 m + (1-b1) g;  v = b2 v + (1-b2) g^2;  p += -step_size * m / (sqrt(v) + eps);
  *   p += -decay * p  (decay = lr * weight_decay, applied after the Adam update as in the reference)
  * step_size = lr, or lr * sqrt(1 - b2^t) / (1 - b1^t) with correct_bias (computed by the caller).
- * Gradients are read as given: GradScaler's unscale_ / inf check run before (torch.amp semantics). */
+ * torch.amp GradScaler semantics without a host sync: when found_inf is non-NULL and *found_inf != 0
+ * the whole step is skipped (nothing written); when grad_scale is non-NULL each gradient is used as
+ * g * (float)(1.0 / (double)*grad_scale), GradScaler.unscale_'s inv_scale (grads are not written back). */
 #define CSA_ADAMW_CHUNK 4096
 typedef struct csa_adamw_tensor { /* one parameter tensor, contiguous fp32 (device pointers) */
   float* param; const float* grad; float* exp_avg; float* exp_avg_sq; int64_t numel;
@@ -160,6 +162,8 @@ typedef struct csa_adamw_args {
   int64_t ntensors, nchunks;
   float beta1, beta2, one_minus_beta1, one_minus_beta2; /* 1-b as the reference's fp32 alpha/value */
   float eps, step_size, decay;
+  const float* grad_scale;         /* device scalar or NULL (gradients already unscaled) */
+  const float* found_inf;          /* device scalar or NULL (no inf check) */
 } csa_adamw_args;
 
 csa_status csa_adamw_step(const csa_adamw_args* a, void* stream);

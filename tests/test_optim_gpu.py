@@ -47,3 +47,35 @@ def test_fused_adamw_ragged_unaligned_matches_per_op_path(correct_bias, wd):
         for key in ("exp_avg", "exp_avg_sq"):
             np.testing.assert_allclose(o_gpu.state[pg][key].cpu().numpy(), o_cpu.state[pc][key].numpy(),
                                        rtol=1e-5, atol=1e-12)
+
+
+def test_fused_adamw_under_gradscaler_unscales_and_skips_on_inf():
+    """script/train.py:109-111 (GradScaler.scale(loss).backward(); step; update) with the device-side
+    unscale / skip path: same parameters as unscaled grads through the per-op CPU path; an inf
+    gradient leaves parameters and moments untouched and halves the scale, with no host sync."""
+    from csa_amd.train import AdamW
+    g = torch.Generator().manual_seed(11)
+    w0 = torch.randn(300, 7, generator=g)
+    x = torch.randn(64, 300, generator=g)
+    pg = torch.nn.Parameter(w0.cuda())
+    pc = torch.nn.Parameter(w0.clone())
+    og, oc = AdamW([pg], lr=1e-3, correct_bias=False), AdamW([pc], lr=1e-3, correct_bias=False)
+    scaler = torch.amp.GradScaler("cuda", init_scale=2.0 ** 16)
+    for step in range(3):
+        og.zero_grad(set_to_none=True)
+        oc.zero_grad(set_to_none=True)
+        scaler.scale((x.cuda() @ pg).square().mean()).backward()
+        (x @ pc).square().mean().backward()
+        scaler.step(og)
+        scaler.update()
+        oc.step()
+    np.testing.assert_allclose(pg.detach().cpu().numpy(), pc.detach().numpy(), rtol=1e-5, atol=1e-7)
+    before = pg.detach().clone()
+    m_before = og.state[pg]["exp_avg"].clone()
+    og.zero_grad(set_to_none=True)
+    scale = scaler.get_scale()
+    scaler.scale((x.cuda() @ pg).square().mean() * float("inf")).backward()
+    scaler.step(og)
+    scaler.update()
+    assert torch.equal(pg.detach(), before) and torch.equal(og.state[pg]["exp_avg"], m_before)
+    assert scaler.get_scale() == scale * 0.5
