@@ -21,6 +21,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .glue import Linear
 from .module.disentangled_attn import DisentangledAttn
 from .module.sbm_attn import Attention
 
@@ -67,8 +68,8 @@ class Embeddings(nn.Module):
 class FeedForward(nn.Module):
     def __init__(self, d_model, dim_feed_forward, dropout=0.1):
         super().__init__()
-        self.linear1 = nn.Linear(d_model, dim_feed_forward)
-        self.linear2 = nn.Linear(dim_feed_forward, d_model)
+        self.linear1 = Linear(d_model, dim_feed_forward)
+        self.linear2 = Linear(dim_feed_forward, d_model)
         self.dropout = nn.Dropout(dropout)
 
     def forward(self, x):
@@ -144,9 +145,9 @@ class Transformer(nn.Module):
         self.dropout1 = nn.Dropout(p=config["dropout_prob"])
         self.norm2 = nn.LayerNorm(config["transformer_dim"])
         self.mlpblock = nn.Sequential(
-            nn.Linear(config["transformer_dim"], config["transformer_hidden_dim"]), nn.GELU(),
+            Linear(config["transformer_dim"], config["transformer_hidden_dim"]), nn.GELU(),
             nn.Dropout(p=config["dropout_prob"]),
-            nn.Linear(config["transformer_hidden_dim"], config["transformer_dim"]), nn.Dropout(p=config["dropout_prob"]))
+            Linear(config["transformer_hidden_dim"], config["transformer_dim"]), nn.Dropout(p=config["dropout_prob"]))
 
     def forward(self, X, mask, deliver):
         out, sparsity, graph, attn = self.mha([self.norm1(X), mask, deliver])
@@ -164,11 +165,11 @@ class SBM(nn.Module):
         for idx in range(self.num_layers):
             setattr(self, f"transformer_{idx}", Transformer(config, idx))
         self.norm = nn.LayerNorm(sbm_enc_dim)
-        self.out = nn.Linear(sbm_enc_dim, config["out_dim"])
+        self.out = Linear(sbm_enc_dim, config["out_dim"])
         if use_pegen == "sequential":
             self.pe = PositionalEncoding(sbm_enc_dim, config["max_src_len"])
         else:
-            self.pe_expand = nn.Linear(pegen_dim, pe_dim)
+            self.pe_expand = Linear(pegen_dim, pe_dim)
         self.use_pegen = use_pegen
 
     def forward(self, data, src_pe, use_pe):
@@ -229,7 +230,7 @@ class Generator(nn.Module):
         super().__init__()
         self.soft_max = nn.Softmax(-1)
         self.dropout = nn.Dropout(dropout)
-        self.linear = nn.Linear(hidden_size, tgt_vocab_size)
+        self.linear = Linear(hidden_size, tgt_vocab_size)
 
     def forward(self, x):
         from .gen_ops import gen_log_softmax

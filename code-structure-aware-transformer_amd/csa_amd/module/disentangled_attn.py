@@ -7,6 +7,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import rel_ops
+from ..glue import Linear, linear
 
 __all__ = ["DisentangledAttn", "transpose_for_scores", "_get_clones"]
 
@@ -28,11 +29,11 @@ class DisentangledAttn(nn.Module):
         assert d_model % h == 0
         self.d_k = d_model // h
         self.h = h
-        self.linear_layers = _get_clones(nn.Linear(d_model, d_model), 4)
+        self.linear_layers = _get_clones(Linear(d_model, d_model), 4)
         self.attn = None
         self.dropout = nn.Dropout(p=dropout)  # unused, as in the reference
-        self.l_linear = _get_clones(nn.Linear(d_model, self.d_k * 4), 2)
-        self.t_linear = _get_clones(nn.Linear(d_model, self.d_k * 4), 2)
+        self.l_linear = _get_clones(Linear(d_model, self.d_k * 4), 2)
+        self.t_linear = _get_clones(Linear(d_model, self.d_k * 4), 2)
 
     def forward(self, query, key, value, rel_emb, rel, mask):
         if query is key and key is value:  # self-attention (CSE_layer, csa_trans.py:231-233): one QKV GEMM
@@ -40,7 +41,7 @@ class DisentangledAttn(nn.Module):
             w = torch.cat([l.weight for l in qkv], 0)
             b = torch.cat([l.bias for l in qkv], 0)
             query, key, value = (transpose_for_scores(t, self.h)
-                                 for t in F.linear(query, w, b).split(w.size(0) // 3, dim=-1))
+                                 for t in linear(query, w, b).split(w.size(0) // 3, dim=-1))
         else:
             query, key, value = [transpose_for_scores(l(x), self.h)
                                  for l, x in zip(self.linear_layers, (query, key, value))]

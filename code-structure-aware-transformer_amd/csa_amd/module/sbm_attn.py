@@ -16,6 +16,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
+from ..glue import Linear, linear
 
 __all__ = ["SBMAttention", "FullAttention", "Attention"]
 
@@ -80,14 +81,14 @@ class Attention(nn.Module):
         self.head_dim = config["head_dim"]
         self.num_head = config["num_head"]
         self.attn_type = config["attn_type"]
-        self.W_q = nn.Linear(self.dim, self.num_head * self.head_dim)
-        self.W_k = nn.Linear(self.dim, self.num_head * self.head_dim)
-        self.W_v = nn.Linear(self.dim, self.num_head * self.head_dim)
+        self.W_q = Linear(self.dim, self.num_head * self.head_dim)
+        self.W_k = Linear(self.dim, self.num_head * self.head_dim)
+        self.W_v = Linear(self.dim, self.num_head * self.head_dim)
         if full_att:
             self.attn = FullAttention(config, idx)
         else:
             self.attn = SBMAttention(config, idx)
-        self.ff = nn.Linear(self.num_head * self.head_dim, self.dim)
+        self.ff = Linear(self.num_head * self.head_dim, self.dim)
 
     def forward(self, inputs):
         X, mask, deliver = inputs
@@ -96,7 +97,7 @@ class Attention(nn.Module):
         hd = self.num_head * self.head_dim
         w = torch.cat([self.W_q.weight, self.W_k.weight, self.W_v.weight], 0)
         b = torch.cat([self.W_q.bias, self.W_k.bias, self.W_v.bias], 0)
-        Q, K, V = (self.split_heads(t) for t in F.linear(X, w, b).split(hd, dim=-1))
+        Q, K, V = (self.split_heads(t) for t in linear(X, w, b).split(hd, dim=-1))
         with torch.autocast(device_type="cuda", enabled=False):  # sbm_attn.py:120
             attn_out, sparsity, graph, attn = self.attn(Q.float(), K.float(), V.float(), mask.float())
         attn_out = self.combine_heads(attn_out)

@@ -12,6 +12,7 @@
  *   csa_rel_attn_bwd   autograd of rel_attn (gather backward = deterministic scatter-add)
  *   csa_adamw_step     script/optimizer.py:49-106 AdamW.step (all parameters in one launch)
  *   csa_gen_logsoftmax_fwd/_bwd  module/components.py:95-102 Generator: log(softmax(dropout(logits)))
+ *   csa_bias_grad      Linear bias gradient (column sums of dY) of the encoder/decoder glue
  *
  * Conventions (all entry points):
  *   - fp32 data; device pointers; sizes and strides are int64 ELEMENT counts; the last
@@ -177,6 +178,12 @@ csa_status csa_gen_logsoftmax_fwd(const float* logits, float* logp, int64_t rows
                                   uint64_t seed, uint64_t offset, void* stream);
 csa_status csa_gen_logsoftmax_bwd(const float* dlogp, const float* logp, float* dlogits, int64_t rows, int64_t V,
                                   float dropout, uint64_t seed, uint64_t offset, void* stream);
+
+/* ---- Linear bias gradient: db[c] (+)= sum_r dy[r, c], dy (rows, cols) contiguous fp32 ----
+ * Two passes (row-slice partials into the caller's workspace, then a fixed-order sum): deterministic. */
+size_t csa_bias_grad_workspace_bytes(int64_t rows, int64_t cols);
+csa_status csa_bias_grad(const float* dy, float* db, int64_t rows, int64_t cols, int accumulate, void* workspace,
+                         void* stream);
 
 #ifdef __cplusplus
 }
