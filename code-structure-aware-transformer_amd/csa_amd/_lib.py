@@ -145,6 +145,8 @@ def lib():
     L.csa_bias_grad_workspace_bytes.argtypes = [i64, i64]
     L.csa_bias_grad.restype = ctypes.c_int
     L.csa_bias_grad.argtypes = [vp, vp, i64, i64, ctypes.c_int, vp, vp]
+    L.csa_ast_relations.restype = ctypes.c_int
+    L.csa_ast_relations.argtypes = [vp, vp, i64, i64, vp, vp, vp, vp, ctypes.c_int]
     L.csa_adamw_step.restype = ctypes.c_int
     L.csa_adamw_step.argtypes = [ctypes.POINTER(AdamwArgs), vp]
     if L.csa_abi_version() != CSA_ABI_VERSION:
@@ -164,5 +166,5 @@ EXPORTED_SYMBOLS = (
     "csa_sbm_bwd_workspace_bytes", "csa_sbm_fwd", "csa_sbm_maps", "csa_sbm_bwd", "csa_ste_sample",
     "csa_ste_backward", "csa_rel_attn_state_bytes", "csa_rel_attn_bwd_workspace_bytes", "csa_rel_attn_fwd", "csa_rel_attn_bwd",
     "csa_adamw_step", "csa_gen_logsoftmax_fwd", "csa_gen_logsoftmax_bwd",
-    "csa_bias_grad_workspace_bytes", "csa_bias_grad",
+    "csa_bias_grad_workspace_bytes", "csa_bias_grad", "csa_ast_relations",
 )

@@ -6,7 +6,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(os.path.dirname(HERE), "csrc")
 OUT = os.path.join(HERE, "lib", "libcsa_hip.so")
-SOURCES = ["csa_sbm.hip", "csa_rel.hip", "csa_optim.hip", "csa_gen.hip", "csa_glue.hip"]
+SOURCES = ["csa_sbm.hip", "csa_rel.hip", "csa_optim.hip", "csa_gen.hip", "csa_glue.hip", "csa_host.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-shared", "-fPIC", "-Wall", "-Wno-unused-result",
          "-Wno-unused-function"]

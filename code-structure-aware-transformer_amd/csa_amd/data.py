@@ -84,13 +84,33 @@ def collate_relations(raw):
     return idx, mask
 
 
+def relation_planes(parents, n_nodes, max_size, nthreads=None):
+    """Native (csrc/csa_host.cpp: csa_ast_relations) relation planes of a batch of pre-order trees:
+    parents (B, max_size) int32 (parent[v] < v, root -1), n_nodes (B,) -> L, T (B,N,N) uint8 relation
+    indices and L_mask, T_mask (B,N,N) bool, identical to relation_matrices + collate_relations."""
+    import ctypes
+    import os
+    from ._lib import check, lib
+    parents = np.ascontiguousarray(parents, dtype=np.int32)
+    n_nodes = np.ascontiguousarray(n_nodes, dtype=np.int32)
+    B = parents.shape[0]
+    out = [np.empty((B, max_size, max_size), np.uint8) for _ in range(4)]
+    p = lambda a: ctypes.c_void_p(a.ctypes.data)
+    nt = nthreads or min(16, os.cpu_count() or 1)
+    check(lib().csa_ast_relations(p(parents), p(n_nodes), B, max_size, *(p(o) for o in out), nt),
+          "csa_ast_relations")
+    L, T, Lm, Tm = out
+    return L, T, Lm.view(bool), Tm.view(bool)
+
+
 def synthetic_batch(batch, max_size=150, seed=1, min_nodes=None, max_nodes=None, src_vocab=10000,
-                    tgt_vocab=20000, max_tgt_len=50):
+                    tgt_vocab=20000, max_tgt_len=50, native=True):
     """A batch of synthetic ASTs. Returns a dict of numpy arrays:
 
     L, T (B,N,N) uint8 relation indices; L_mask, T_mask (B,N,N) bool; src_mask (B,N) bool
     (True = padded node); num_node (B,); src_seq (B,N) int64 in [2, src_vocab) with PAD beyond
-    num_node; tgt_seq/target (B, max_tgt_len-1) int64 (BOS ... EOS, PAD)."""
+    num_node; tgt_seq/target (B, max_tgt_len-1) int64 (BOS ... EOS, PAD). Relation planes come from
+    the native builder (relation_planes) unless native=False."""
     rng = np.random.default_rng(seed)
     lo = max_size if min_nodes is None else min_nodes
     hi = max_size if max_nodes is None else max_nodes
@@ -101,18 +121,28 @@ def synthetic_batch(batch, max_size=150, seed=1, min_nodes=None, max_nodes=None,
     nn = np.zeros(batch, np.int64)
     src = np.zeros((batch, max_size), np.int64)
     tgt = np.zeros((batch, max_tgt_len), np.int64)
+    parents = np.full((batch, max_size), -1, np.int32)
     for b in range(batch):
         n = int(rng.integers(lo, hi + 1))
-        par, kids = random_tree(n, rng)
-        rl, rt = relation_matrices(par, kids, max_size)
-        L[b], Lm[b] = collate_relations(rl)
-        T[b], Tm[b] = collate_relations(rt)
+        par, _ = random_tree(n, rng)
+        parents[b, :n] = par
         nn[b] = n
         src[b, :n] = rng.integers(2, src_vocab, n)
         tl = int(rng.integers(5, max_tgt_len - 1))
         tgt[b, 0] = BOS
         tgt[b, 1:tl + 1] = rng.integers(4, tgt_vocab, tl)
         tgt[b, tl + 1] = EOS
+    if native:
+        L, T, Lm, Tm = relation_planes(parents, nn, max_size)
+    else:  # the Python restatement (tests compare the two)
+        for b in range(batch):
+            n = int(nn[b])
+            kids = [[] for _ in range(n)]
+            for v in range(1, n):
+                kids[parents[b, v]].append(v)
+            rl, rt = relation_matrices(parents[b, :n].astype(np.int64), kids, max_size)
+            L[b], Lm[b] = collate_relations(rl)
+            T[b], Tm[b] = collate_relations(rt)
     src_mask = np.arange(max_size)[None, :] >= nn[:, None]
     return dict(L=L, T=T, L_mask=Lm, T_mask=Tm, num_node=nn, src_seq=src, src_mask=src_mask,
                 tgt_seq=tgt[:, :-1], target=tgt[:, 1:])

@@ -13,6 +13,7 @@
  *   csa_adamw_step     script/optimizer.py:49-106 AdamW.step (all parameters in one launch)
  *   csa_gen_logsoftmax_fwd/_bwd  module/components.py:95-102 Generator: log(softmax(dropout(logits)))
  *   csa_bias_grad      Linear bias gradient (column sums of dY) of the encoder/decoder glue
+ *   csa_ast_relations  my_ast.py:198-273 + dataset/base_data_set.py:33-36 (host C++, no GPU)
  *
  * Conventions (all entry points):
  *   - fp32 data; device pointers; sizes and strides are int64 ELEMENT counts; the last
@@ -184,6 +185,14 @@ csa_status csa_gen_logsoftmax_bwd(const float* dlogp, const float* logp, float* 
 size_t csa_bias_grad_workspace_bytes(int64_t rows, int64_t cols);
 csa_status csa_bias_grad(const float* dy, float* db, int64_t rows, int64_t cols, int accumulate, void* workspace,
                          void* stream);
+
+/* ---- Host data path: AST relation planes (my_ast.py:198-273, dataset/base_data_set.py:33-36) ----
+ * parent: (B, max_size) int32, pre-order ids (parent[v] < v, parent[0] = -1); n_nodes: (B,) int32
+ * (trees longer than max_size are truncated to their pre-order prefix). Outputs (B, max_size,
+ * max_size) uint8 host arrays: L / T = clamp(raw + 75, 0, 149), L_mask / T_mask = (raw == 0).
+ * Runs on the host (nthreads std::threads); no HIP call. */
+csa_status csa_ast_relations(const int32_t* parent, const int32_t* n_nodes, int64_t B, int64_t max_size, uint8_t* L,
+                             uint8_t* T, uint8_t* L_mask, uint8_t* T_mask, int nthreads);
 
 #ifdef __cplusplus
 }

@@ -161,3 +161,24 @@ def test_label_smoothing_nan_semantics_of_underflowed_logprobs(smoothing):
         mine = LabelSmoothing(0, smoothing)(xx, target).item()
         ref = _reference_label_smoothing(xx, target, 0, smoothing).item()
         assert (np.isnan(mine) and np.isnan(ref)) or mine == pytest.approx(ref, rel=1e-6), (mine, ref)
+
+
+def test_native_relation_planes_match_python_restatement():
+    """csa_ast_relations (csrc/csa_host.cpp) == relation_matrices + collate_relations
+    (my_ast.py:198-273, dataset/base_data_set.py:33-36), bit-exact, incl. 1-node and deep trees."""
+    from csa_amd.data import synthetic_batch
+    for kw in (dict(batch=6, max_size=150, seed=5, min_nodes=1, max_nodes=150),
+               dict(batch=3, max_size=40, seed=6, min_nodes=40, max_nodes=40)):
+        a = synthetic_batch(**kw)
+        b = synthetic_batch(native=False, **kw)
+        for k in ("L", "T", "L_mask", "T_mask", "src_seq", "tgt_seq"):
+            assert np.array_equal(a[k], b[k]), k
+
+
+def test_native_relation_planes_reject_malformed_tree():
+    from csa_amd._lib import CsaError
+    from csa_amd.data import relation_planes
+    par = np.full((1, 8), -1, np.int32)
+    par[0, 1:4] = [0, 2, 1]  # node 2's parent 2 is not < 2
+    with pytest.raises(CsaError, match="pre-order"):
+        relation_planes(par, np.array([4]), 8)
