@@ -145,6 +145,14 @@ def lib():
     L.csa_bias_grad_workspace_bytes.argtypes = [i64, i64]
     L.csa_bias_grad.restype = ctypes.c_int
     L.csa_bias_grad.argtypes = [vp, vp, i64, i64, ctypes.c_int, vp, vp]
+    L.csa_layernorm_supported.restype = ctypes.c_int
+    L.csa_layernorm_supported.argtypes = [i64]
+    L.csa_layernorm_bwd_workspace_bytes.restype = ctypes.c_size_t
+    L.csa_layernorm_bwd_workspace_bytes.argtypes = [i64, i64]
+    L.csa_layernorm_fwd.restype = ctypes.c_int
+    L.csa_layernorm_fwd.argtypes = [vp, vp, vp, vp, vp, i64, i64, f32, vp]
+    L.csa_layernorm_bwd.restype = ctypes.c_int
+    L.csa_layernorm_bwd.argtypes = [vp, vp, vp, vp, vp, vp, vp, i64, i64, vp, vp]
     L.csa_ast_relations.restype = ctypes.c_int
     L.csa_ast_relations.argtypes = [vp, vp, i64, i64, vp, vp, vp, vp, ctypes.c_int]
     L.csa_adamw_step.restype = ctypes.c_int
@@ -167,4 +175,5 @@ EXPORTED_SYMBOLS = (
     "csa_ste_backward", "csa_rel_attn_state_bytes", "csa_rel_attn_bwd_workspace_bytes", "csa_rel_attn_fwd", "csa_rel_attn_bwd",
     "csa_adamw_step", "csa_gen_logsoftmax_fwd", "csa_gen_logsoftmax_bwd",
     "csa_bias_grad_workspace_bytes", "csa_bias_grad", "csa_ast_relations",
+    "csa_layernorm_supported", "csa_layernorm_bwd_workspace_bytes", "csa_layernorm_fwd", "csa_layernorm_bwd",
 )

@@ -21,7 +21,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .glue import Linear
+from .glue import LayerNorm, Linear
 from .module.disentangled_attn import DisentangledAttn
 from .module.sbm_attn import Attention
 
@@ -55,7 +55,7 @@ class Embeddings(nn.Module):
         super().__init__()
         self.word_embeddings = nn.Embedding(vocab_size, hidden_size, padding_idx=0)
         self.pos_emb = PositionalEncoding(hidden_size) if with_pos else None
-        self.norm = nn.LayerNorm(hidden_size)
+        self.norm = LayerNorm(hidden_size)
         self.dropout = nn.Dropout(dropout)
 
     def forward(self, x):
@@ -81,7 +81,7 @@ class SublayerConnection(nn.Module):
 
     def __init__(self, size, dropout):
         super().__init__()
-        self.norm = nn.LayerNorm(size)
+        self.norm = LayerNorm(size)
         self.dropout = nn.Dropout(dropout)
 
     def forward(self, x, sublayer):
@@ -120,7 +120,7 @@ class CSE(nn.Module):
         self.T_q = nn.Embedding(max_src_len, hidden_size)
         self.f = nn.ReLU()
         self.dropout = nn.Dropout(dropout)
-        self.norm = nn.LayerNorm(hidden_size)
+        self.norm = LayerNorm(hidden_size)
 
     def build_rel_emb(self):
         return [torch.stack([self.L_q.weight, self.T_q.weight])]
@@ -140,10 +140,10 @@ class Transformer(nn.Module):
 
     def __init__(self, config, idx):
         super().__init__()
-        self.norm1 = nn.LayerNorm(config["transformer_dim"])
+        self.norm1 = LayerNorm(config["transformer_dim"])
         self.mha = Attention(config, idx, config["full_att"])
         self.dropout1 = nn.Dropout(p=config["dropout_prob"])
-        self.norm2 = nn.LayerNorm(config["transformer_dim"])
+        self.norm2 = LayerNorm(config["transformer_dim"])
         self.mlpblock = nn.Sequential(
             Linear(config["transformer_dim"], config["transformer_hidden_dim"]), nn.GELU(),
             nn.Dropout(p=config["dropout_prob"]),
@@ -164,7 +164,7 @@ class SBM(nn.Module):
         self.num_layers = config["sbm_layers"]
         for idx in range(self.num_layers):
             setattr(self, f"transformer_{idx}", Transformer(config, idx))
-        self.norm = nn.LayerNorm(sbm_enc_dim)
+        self.norm = LayerNorm(sbm_enc_dim)
         self.out = Linear(sbm_enc_dim, config["out_dim"])
         if use_pegen == "sequential":
             self.pe = PositionalEncoding(sbm_enc_dim, config["max_src_len"])
@@ -268,7 +268,7 @@ class CSATrans(nn.Module):
                   "return_maps": return_maps}
         self.SBM = SBM(config, sbm_enc_dim, pe_dim, pegen_dim, use_pegen)
         self.decoder = BaseDecoder(DecoderLayer(hidden_size, num_heads, dim_feed_forward, dropout, "gelu"), 4,
-                                   norm=nn.LayerNorm(hidden_size))
+                                   norm=LayerNorm(hidden_size))
         self.generator = Generator(tgt_vocab_size, hidden_size, dropout)
         if state_dict is None:
             for p in self.parameters():

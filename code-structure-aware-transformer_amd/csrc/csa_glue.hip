@@ -50,7 +50,7 @@ __global__ __launch_bounds__(256) void k_bias_grad_part(const float* __restrict_
 }
 
 __global__ __launch_bounds__(256) void k_bias_grad_sum(const float* __restrict__ part, float* __restrict__ db,
-                                                       int64_t cols, int rs, int accumulate) {
+                                                       int64_t cols, int rs, int accumulate, int64_t stride) {
   const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (c >= cols) return;
   // loads issued 8 at a time (independent), then added in slice order: the sum is the same fixed
@@ -59,7 +59,7 @@ __global__ __launch_bounds__(256) void k_bias_grad_sum(const float* __restrict__
   for (int i0 = 0; i0 < rs; i0 += 8) {
     float v[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = i0 + u < rs ? part[(int64_t)(i0 + u) * cols + c] : 0.f;
+    for (int u = 0; u < 8; ++u) v[u] = i0 + u < rs ? part[(int64_t)(i0 + u) * stride + c] : 0.f;
 #pragma unroll
     for (int u = 0; u < 8; ++u) s += v[u];
   }
@@ -69,6 +69,138 @@ __global__ __launch_bounds__(256) void k_bias_grad_sum(const float* __restrict__
 inline int bg_slices(int64_t rows) {
   const int64_t rs = (rows + 255) / 256;  // >= 256 rows per slice
   return (int)(rs < 1 ? 1 : rs > 64 ? 64 : rs);
+}
+
+// ------------------------------------------------------------------------------------
+// LayerNorm over the last dim (nn.LayerNorm(size), eps 1e-5, the encoder's pre-norm sublayers):
+// one wave per row, the row in registers (CPL dwordx4 chunks per lane, cols <= 256 CPL), two-pass
+// mean / variance in registers (no E[x^2] - mean^2 cancellation). Backward: dx per row from the
+// saved (mean, rstd); dgamma / dbeta as per-workgroup column partials (fixed order) summed by
+// k_bias_grad_sum, so the whole backward is deterministic.
+// ------------------------------------------------------------------------------------
+constexpr int LN_ROWS_PER_WG = 32;  // 4 waves x 8 rows (300 workgroups at 9600 rows)
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int CPL>
+__global__ __launch_bounds__(256) void k_ln_fwd(const float* __restrict__ x, const float* __restrict__ gamma,
+                                                const float* __restrict__ beta, float* __restrict__ y,
+                                                float* __restrict__ stats, int64_t rows, int cols, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* xr = x + row * cols;
+  f32x4 v[CPL];
+  float s = 0.f;
+#pragma unroll
+  for (int q = 0; q < CPL; ++q) {
+    const int c = 4 * (lane + 64 * q);
+    v[q] = c < cols ? *reinterpret_cast<const f32x4*>(xr + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    s += (v[q][0] + v[q][1]) + (v[q][2] + v[q][3]);
+  }
+  const float mean = wave_sum(s) / (float)cols;
+  float ss = 0.f;
+#pragma unroll
+  for (int q = 0; q < CPL; ++q) {
+    const int c = 4 * (lane + 64 * q);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float d = c < cols ? v[q][e] - mean : 0.f;
+      ss = fmaf(d, d, ss);
+    }
+  }
+  const float rstd = 1.f / sqrtf(wave_sum(ss) / (float)cols + eps);
+  float* yr = y + row * cols;
+#pragma unroll
+  for (int q = 0; q < CPL; ++q) {
+    const int c = 4 * (lane + 64 * q);
+    if (c < cols) {
+      const f32x4 g = *reinterpret_cast<const f32x4*>(gamma + c);
+      const f32x4 b = *reinterpret_cast<const f32x4*>(beta + c);
+      f32x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = fmaf((v[q][e] - mean) * rstd, g[e], b[e]);
+      *reinterpret_cast<f32x4*>(yr + c) = o;
+    }
+  }
+  if (lane == 0) { stats[2 * row] = mean; stats[2 * row + 1] = rstd; }
+}
+
+template <int CPL>
+__global__ __launch_bounds__(256) void k_ln_bwd(const float* __restrict__ dy, const float* __restrict__ x,
+                                                const float* __restrict__ stats, const float* __restrict__ gamma,
+                                                float* __restrict__ dx, float* __restrict__ part, int64_t rows,
+                                                int cols) {
+  __shared__ float red[4][2][256 * CPL > 1024 ? 1024 : 256 * CPL];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  f32x4 g[CPL], pg[CPL], pb[CPL];
+#pragma unroll
+  for (int q = 0; q < CPL; ++q) {
+    const int c = 4 * (lane + 64 * q);
+    g[q] = c < cols ? *reinterpret_cast<const f32x4*>(gamma + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    pg[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    pb[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * LN_ROWS_PER_WG + w;
+  for (int i = 0; i < LN_ROWS_PER_WG / 4; ++i) {
+    const int64_t row = r0 + 4 * i;
+    if (row >= rows) break;
+    const float mean = stats[2 * row], rstd = stats[2 * row + 1];
+    f32x4 xh[CPL], gy[CPL];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < CPL; ++q) {
+      const int c = 4 * (lane + 64 * q);
+      const f32x4 xv = c < cols ? *reinterpret_cast<const f32x4*>(x + row * cols + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+      const f32x4 dv = c < cols ? *reinterpret_cast<const f32x4*>(dy + row * cols + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        xh[q][e] = c < cols ? (xv[e] - mean) * rstd : 0.f;
+        gy[q][e] = dv[e] * g[q][e];
+        s1 += gy[q][e];
+        s2 = fmaf(gy[q][e], xh[q][e], s2);
+        pg[q][e] = fmaf(dv[e], xh[q][e], pg[q][e]);
+        pb[q][e] += dv[e];
+      }
+    }
+    const float m1 = wave_sum(s1) / (float)cols, m2 = wave_sum(s2) / (float)cols;
+#pragma unroll
+    for (int q = 0; q < CPL; ++q) {
+      const int c = 4 * (lane + 64 * q);
+      if (c < cols) {
+        f32x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = rstd * (gy[q][e] - m1 - xh[q][e] * m2);
+        *reinterpret_cast<f32x4*>(dx + row * cols + c) = o;
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < CPL; ++q)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int c = 4 * (lane + 64 * q) + e;
+      red[w][0][c] = pg[q][e];
+      red[w][1][c] = pb[q][e];
+    }
+  __syncthreads();
+  // part layout: [slice][0: dgamma | 1: dbeta][cols]
+  for (int c = threadIdx.x; c < cols; c += 256) {
+    const float a = (red[0][0][c] + red[1][0][c]) + (red[2][0][c] + red[3][0][c]);
+    const float b = (red[0][1][c] + red[1][1][c]) + (red[2][1][c] + red[3][1][c]);
+    part[(int64_t)blockIdx.x * 2 * cols + c] = a;
+    part[(int64_t)blockIdx.x * 2 * cols + cols + c] = b;
+  }
+}
+
+inline int ln_cpl(int64_t cols) {
+  if (cols < 4 || cols % 4) return 0;
+  const int64_t cpl = (cols + 255) / 256;
+  return cpl <= 4 ? (int)cpl : 0;
 }
 
 }  // namespace
@@ -104,10 +236,87 @@ csa_status csa_bias_grad(const float* dy, float* db, int64_t rows, int64_t cols,
   hipLaunchKernelGGL(k_bias_grad_part, dim3((unsigned)((cols + BG_COLS - 1) / BG_COLS), (unsigned)rs), dim3(256), 0,
                      st, dy, part, rows, cols, per);
   hipLaunchKernelGGL(k_bias_grad_sum, dim3((unsigned)((cols + 255) / 256)), dim3(256), 0, st, part, db, cols, rs,
-                     accumulate);
+                     accumulate, cols);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     csa::set_error("csa_bias_grad: %s", hipGetErrorString(e));
+    return CSA_LAUNCH_FAILED;
+  }
+  return CSA_OK;
+}
+
+int csa_layernorm_supported(int64_t cols) { return ln_cpl(cols) > 0 ? 1 : 0; }
+
+size_t csa_layernorm_bwd_workspace_bytes(int64_t rows, int64_t cols) {
+  return sizeof(float) * 2 * (size_t)((rows + LN_ROWS_PER_WG - 1) / LN_ROWS_PER_WG) * (size_t)(cols > 0 ? cols : 0);
+}
+
+csa_status csa_layernorm_fwd(const float* x, const float* gamma, const float* beta, float* y, float* stats,
+                             int64_t rows, int64_t cols, float eps, void* stream) {
+  const int cpl = ln_cpl(cols);
+  if (rows < 0 || cpl == 0) {
+    csa::set_error("csa_layernorm_fwd: cols must be a multiple of 4 in [4, 1024]");
+    return CSA_UNSUPPORTED_SHAPE;
+  }
+  if (rows == 0) return CSA_OK;
+  if (!x || !gamma || !beta || !y || !stats || ((((uintptr_t)x) | ((uintptr_t)y) | ((uintptr_t)gamma) |
+                                                 ((uintptr_t)beta)) & 15)) {
+    csa::set_error("csa_layernorm_fwd: null or misaligned pointer");
+    return CSA_INVALID_ARG;
+  }
+  const hipStream_t st = (hipStream_t)stream;
+  const dim3 grid((unsigned)((rows + 3) / 4));
+  switch (cpl) {
+    case 1: hipLaunchKernelGGL(k_ln_fwd<1>, grid, dim3(256), 0, st, x, gamma, beta, y, stats, rows, (int)cols, eps); break;
+    case 2: hipLaunchKernelGGL(k_ln_fwd<2>, grid, dim3(256), 0, st, x, gamma, beta, y, stats, rows, (int)cols, eps); break;
+    case 3: hipLaunchKernelGGL(k_ln_fwd<3>, grid, dim3(256), 0, st, x, gamma, beta, y, stats, rows, (int)cols, eps); break;
+    default: hipLaunchKernelGGL(k_ln_fwd<4>, grid, dim3(256), 0, st, x, gamma, beta, y, stats, rows, (int)cols, eps);
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    csa::set_error("csa_layernorm_fwd: %s", hipGetErrorString(e));
+    return CSA_LAUNCH_FAILED;
+  }
+  return CSA_OK;
+}
+
+csa_status csa_layernorm_bwd(const float* dy, const float* x, const float* stats, const float* gamma, float* dx,
+                             float* dgamma, float* dbeta, int64_t rows, int64_t cols, void* workspace, void* stream) {
+  const int cpl = ln_cpl(cols);
+  if (rows < 0 || cpl == 0) {
+    csa::set_error("csa_layernorm_bwd: cols must be a multiple of 4 in [4, 1024]");
+    return CSA_UNSUPPORTED_SHAPE;
+  }
+  if (!dgamma || !dbeta || (rows > 0 && (!dy || !x || !stats || !gamma || !dx || !workspace)) ||
+      ((((uintptr_t)dy) | ((uintptr_t)x) | ((uintptr_t)dx) | ((uintptr_t)gamma)) & 15)) {
+    csa::set_error("csa_layernorm_bwd: null or misaligned pointer");
+    return CSA_INVALID_ARG;
+  }
+  const hipStream_t st = (hipStream_t)stream;
+  if (rows == 0) {
+    if (hipMemsetAsync(dgamma, 0, sizeof(float) * cols, st) != hipSuccess ||
+        hipMemsetAsync(dbeta, 0, sizeof(float) * cols, st) != hipSuccess) {
+      csa::set_error("csa_layernorm_bwd: memset failed");
+      return CSA_LAUNCH_FAILED;
+    }
+    return CSA_OK;
+  }
+  const int nwg = (int)((rows + LN_ROWS_PER_WG - 1) / LN_ROWS_PER_WG);
+  float* part = (float*)workspace;
+  const dim3 grid((unsigned)nwg);
+  switch (cpl) {
+    case 1: hipLaunchKernelGGL(k_ln_bwd<1>, grid, dim3(256), 0, st, dy, x, stats, gamma, dx, part, rows, (int)cols); break;
+    case 2: hipLaunchKernelGGL(k_ln_bwd<2>, grid, dim3(256), 0, st, dy, x, stats, gamma, dx, part, rows, (int)cols); break;
+    case 3: hipLaunchKernelGGL(k_ln_bwd<3>, grid, dim3(256), 0, st, dy, x, stats, gamma, dx, part, rows, (int)cols); break;
+    default: hipLaunchKernelGGL(k_ln_bwd<4>, grid, dim3(256), 0, st, dy, x, stats, gamma, dx, part, rows, (int)cols);
+  }
+  // dgamma = rows 0, 2, 4, ... of part; dbeta = rows 1, 3, 5, ... (stride 2 cols between slices)
+  const dim3 g2((unsigned)((cols + 255) / 256));
+  hipLaunchKernelGGL(k_bias_grad_sum, g2, dim3(256), 0, st, part, dgamma, cols, nwg, 0, (int64_t)2 * cols);
+  hipLaunchKernelGGL(k_bias_grad_sum, g2, dim3(256), 0, st, part + cols, dbeta, cols, nwg, 0, (int64_t)2 * cols);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    csa::set_error("csa_layernorm_bwd: %s", hipGetErrorString(e));
     return CSA_LAUNCH_FAILED;
   }
   return CSA_OK;

@@ -13,6 +13,7 @@
  *   csa_adamw_step     script/optimizer.py:49-106 AdamW.step (all parameters in one launch)
  *   csa_gen_logsoftmax_fwd/_bwd  module/components.py:95-102 Generator: log(softmax(dropout(logits)))
  *   csa_bias_grad      Linear bias gradient (column sums of dY) of the encoder/decoder glue
+ *   csa_layernorm_fwd/_bwd  nn.LayerNorm of the encoder glue (module/components.py SublayerConnection)
  *   csa_ast_relations  my_ast.py:198-273 + dataset/base_data_set.py:33-36 (host C++, no GPU)
  *
  * Conventions (all entry points):
@@ -185,6 +186,17 @@ csa_status csa_gen_logsoftmax_bwd(const float* dlogp, const float* logp, float* 
 size_t csa_bias_grad_workspace_bytes(int64_t rows, int64_t cols);
 csa_status csa_bias_grad(const float* dy, float* db, int64_t rows, int64_t cols, int accumulate, void* workspace,
                          void* stream);
+
+/* ---- LayerNorm over the last dim (nn.LayerNorm(cols), affine) of the encoder/decoder glue ----
+ * x, y, dy, dx: (rows, cols) contiguous fp32, cols % 4 == 0 and cols <= 1024 (csa_layernorm_supported);
+ * stats: (rows, 2) saved (mean, rstd). Backward writes dx, dgamma, dbeta (deterministic: fixed-order
+ * column partials in the caller's workspace). */
+int csa_layernorm_supported(int64_t cols);
+size_t csa_layernorm_bwd_workspace_bytes(int64_t rows, int64_t cols);
+csa_status csa_layernorm_fwd(const float* x, const float* gamma, const float* beta, float* y, float* stats,
+                             int64_t rows, int64_t cols, float eps, void* stream);
+csa_status csa_layernorm_bwd(const float* dy, const float* x, const float* stats, const float* gamma, float* dx,
+                             float* dgamma, float* dbeta, int64_t rows, int64_t cols, void* workspace, void* stream);
 
 /* ---- Host data path: AST relation planes (my_ast.py:198-273, dataset/base_data_set.py:33-36) ----
  * parent: (B, max_size) int32, pre-order ids (parent[v] < v, parent[0] = -1); n_nodes: (B,) int32

@@ -32,3 +32,24 @@ def test_glue_linear_matches_nn_linear():
     mine(xb).backward(gy)
     for a, b in ((xa.grad, xb.grad), (ref.weight.grad, mine.weight.grad), (ref.bias.grad, mine.bias.grad)):
         np.testing.assert_allclose(b.cpu().numpy(), a.cpu().numpy(), rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("rows,cols", [(1, 4), (37, 512), (9600, 768), (130, 1024), (65, 100)])
+def test_layernorm_matches_torch(rows, cols):
+    from csa_amd.glue import LayerNorm
+    torch.manual_seed(rows + cols)
+    ref = torch.nn.LayerNorm(cols).cuda()
+    with torch.no_grad():
+        ref.weight.normal_()
+        ref.bias.normal_()
+    mine = LayerNorm(cols).cuda()
+    mine.load_state_dict(ref.state_dict())
+    x = (torch.randn(rows, cols, device="cuda") * 3 + 1)
+    xa, xb = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
+    gy = torch.randn(rows, cols, device="cuda")
+    ya, yb = ref(xa), mine(xb)
+    np.testing.assert_allclose(yb.detach().cpu().numpy(), ya.detach().cpu().numpy(), rtol=1e-4, atol=1e-5)
+    ya.backward(gy)
+    yb.backward(gy)
+    for a, b in ((xa.grad, xb.grad), (ref.weight.grad, mine.weight.grad), (ref.bias.grad, mine.bias.grad)):
+        np.testing.assert_allclose(b.cpu().numpy(), a.cpu().numpy(), rtol=1e-4, atol=1e-4)
