@@ -46,6 +46,8 @@ class _LinearFn(torch.autograd.Function):
 def linear(x, w, b=None):
     if b is None or not x.is_cuda or x.dtype != torch.float32:
         return F.linear(x, w, b)
+    if _batch_major(x):  # rows are independent: run on the batch-first memory, return the same view
+        return _LinearFn.apply(x.transpose(0, 1), w, b).transpose(0, 1)
     return _LinearFn.apply(x, w, b)
 
 
@@ -93,7 +95,72 @@ class LayerNorm(nn.LayerNorm):
 
     def forward(self, x):
         if (x.is_cuda and x.dtype == torch.float32 and len(self.normalized_shape) == 1 and self.weight is not None
-                and self.bias is not None and lib().csa_layernorm_supported(x.shape[-1])
-                and x.is_contiguous()):
-            return _LayerNormFn.apply(x, self.weight, self.bias, float(self.eps))
+                and self.bias is not None and lib().csa_layernorm_supported(x.shape[-1])):
+            if x.is_contiguous():
+                return _LayerNormFn.apply(x, self.weight, self.bias, float(self.eps))
+            if _batch_major(x):  # per-row op: normalise the batch-first memory, return the same view
+                return _LayerNormFn.apply(x.transpose(0, 1), self.weight, self.bias, float(self.eps)).transpose(0, 1)
         return super().forward(x)
+
+
+def _batch_major(x):
+    """A (T, B, E) tensor whose memory is (B, T, E)-contiguous (a permuted batch-first tensor)."""
+    return x.dim() == 3 and not x.is_contiguous() and x.transpose(0, 1).is_contiguous()
+
+
+def _float_mask(m, dtype):
+    """F._canonical_mask for a bool mask: True -> -inf, False -> 0."""
+    if m.dtype == torch.bool:
+        return torch.zeros(m.shape, dtype=dtype, device=m.device).masked_fill_(m, float("-inf"))
+    return m.to(dtype)
+
+
+class MultiheadAttention(nn.MultiheadAttention):
+    """nn.MultiheadAttention (same parameters / state_dict keys; the decoder's self- and
+    cross-attention, reference module/base_seq2seq.py DecoderLayer) without its layout copies.
+
+    The decoder's sequence-first inputs are permuted views of batch-first tensors
+    (csa_trans.py passes `tgt_emb.permute(1, 0, 2)` and `enc.permute(1, 0, 2)`). torch's
+    multi_head_attention_forward makes those contiguous, packs q/k/v as (3, T, B, E) copies and,
+    in the backward, zero-fills and accumulates a full (3, T, B, E) gradient per select. Here the
+    projections run on the batch-first memory, q/k/v are strided (B, H, T, hd) views of the packed
+    projection (their backward is one stack), and the output is returned as a (T, B, E) view of a
+    batch-first tensor. Same math as the need_weights=False path of F.multi_head_attention_forward:
+    bool masks -> -inf additive masks, key padding merged per head, the (B*H, T, S) attn_mask read
+    as view(B, H, T, S), SDPA with dropout_p = dropout when training, out_proj. Any other use
+    (need_weights, bias_k, kdim != embed_dim, batch_first, ...) takes nn.MultiheadAttention's path."""
+
+    def forward(self, query, key, value, key_padding_mask=None, need_weights=True, attn_mask=None,
+                average_attn_weights=True, is_causal=False):
+        if (need_weights or is_causal or self.batch_first or not self._qkv_same_embed_dim or self.bias_k is not None
+                or self.add_zero_attn or self.in_proj_bias is None or query.dim() != 3 or not query.is_cuda
+                or key is not value):
+            return super().forward(query, key, value, key_padding_mask=key_padding_mask, need_weights=need_weights,
+                                   attn_mask=attn_mask, average_attn_weights=average_attn_weights,
+                                   is_causal=is_causal)
+        T, B, E = query.shape
+        S = key.shape[0]
+        H = self.num_heads
+        hd = E // H
+        qb = query.transpose(0, 1)  # (B, T, E), contiguous when query is a permuted batch-first tensor
+        if query is key:
+            qkv = linear(qb, self.in_proj_weight, self.in_proj_bias).view(B, T, 3, H, hd)
+            q, k, v = (t.transpose(1, 2) for t in qkv.unbind(2))
+        else:
+            w_q, w_kv = self.in_proj_weight.split([E, 2 * E])
+            b_q, b_kv = self.in_proj_bias.split([E, 2 * E])
+            q = linear(qb, w_q, b_q).view(B, T, H, hd).transpose(1, 2)
+            kv = linear(key.transpose(0, 1), w_kv, b_kv).view(B, S, 2, H, hd)
+            k, v = (t.transpose(1, 2) for t in kv.unbind(2))
+        m = None
+        if attn_mask is not None:
+            m = _float_mask(attn_mask, q.dtype)
+            m = m.unsqueeze(0) if m.dim() == 2 else m
+        if key_padding_mask is not None:
+            kpm = _float_mask(key_padding_mask, q.dtype).view(B, 1, 1, S).expand(-1, H, -1, -1).reshape(B * H, 1, S)
+            m = kpm if m is None else m + kpm
+        if m is not None:
+            m = m.unsqueeze(0) if m.size(0) == 1 else m.view(B, H, -1, S)
+        o = F.scaled_dot_product_attention(q, k, v, m, self.dropout if self.training else 0.0)
+        o = o.transpose(1, 2).reshape(B, T, E)
+        return linear(o, self.out_proj.weight, self.out_proj.bias).transpose(0, 1), None

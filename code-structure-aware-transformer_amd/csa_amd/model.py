@@ -10,8 +10,10 @@ reference's and reference checkpoints load. What changes:
 * CSE relation attention = csa_amd.module.disentangled_attn.DisentangledAttn fed the compact
   (B,2,N,N) uint8 relation planes (parent L, sibling T) directly, instead of the reference's
   repeat(4)+cat int64 (B,8,N,N) copies (module/csa_trans.py:206-211).
-* Everything else (embeddings, LayerNorm, FFN, nn.MultiheadAttention decoder, generator) is
-  stock PyTorch-ROCm, exactly as in the reference.
+* Glue (csa_amd/glue.py): Linear (bias gradient kernel), LayerNorm kernels and the decoder's
+  MultiheadAttention keep nn's parameters and state_dict keys; they run the decoder's permuted
+  sequence-first views on their batch-first memory instead of copying them. Embeddings, dropout,
+  GELU and SDPA are stock PyTorch-ROCm, as in the reference.
 """
 import copy
 import math
@@ -21,7 +23,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .glue import LayerNorm, Linear
+from .glue import LayerNorm, Linear, MultiheadAttention
 from .module.disentangled_attn import DisentangledAttn
 from .module.sbm_attn import Attention
 
@@ -193,8 +195,8 @@ class SBM(nn.Module):
 class DecoderLayer(nn.Module):
     def __init__(self, d_model, nhead, dim_feedforward=2048, dropout=0.1, activation="gelu"):
         super().__init__()
-        self.self_attn = nn.MultiheadAttention(d_model, nhead, dropout=dropout)
-        self.multihead_attn = nn.MultiheadAttention(d_model, nhead, dropout=dropout)
+        self.self_attn = MultiheadAttention(d_model, nhead, dropout=dropout)
+        self.multihead_attn = MultiheadAttention(d_model, nhead, dropout=dropout)
         self.feed_forward = FeedForward(d_model, dim_feedforward, dropout=dropout)
         self.sublayer = _clones(SublayerConnection(d_model, dropout), 3)
         self.dropout3 = nn.Dropout(dropout)

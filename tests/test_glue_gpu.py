@@ -53,3 +53,92 @@ def test_layernorm_matches_torch(rows, cols):
     yb.backward(gy)
     for a, b in ((xa.grad, xb.grad), (ref.weight.grad, mine.weight.grad), (ref.bias.grad, mine.bias.grad)):
         np.testing.assert_allclose(b.cpu().numpy(), a.cpu().numpy(), rtol=1e-4, atol=1e-4)
+
+
+def _perm_view(x):
+    """(B, T, E) batch-first tensor -> its (T, B, E) permuted view, as csa_trans.py hands the decoder."""
+    return x.permute(1, 0, 2)
+
+
+@pytest.mark.parametrize("train_dropout", [0.0, 0.2])
+def test_glue_mha_matches_nn_mha(train_dropout):
+    """Decoder self-attention (pad|future bool mask repeated per head, read back as view(B, H, T, S)
+    exactly as torch does) and cross-attention (key padding mask) vs nn.MultiheadAttention, outputs and
+    all gradients. With dropout the two draw the same SDPA Philox stream from the same seed."""
+    from csa_amd.glue import MultiheadAttention
+    from csa_amd.model import make_std_mask
+    torch.manual_seed(5)
+    B, T, S, E, H = 6, 11, 17, 64, 8
+    ref_sa = torch.nn.MultiheadAttention(E, H, dropout=train_dropout).cuda()
+    ref_ca = torch.nn.MultiheadAttention(E, H, dropout=train_dropout).cuda()
+    sa = MultiheadAttention(E, H, dropout=train_dropout).cuda()
+    ca = MultiheadAttention(E, H, dropout=train_dropout).cuda()
+    with torch.no_grad():
+        for m in (ref_sa, ref_ca):
+            m.in_proj_bias.normal_()
+            m.out_proj.bias.normal_()
+    sa.load_state_dict(ref_sa.state_dict())
+    ca.load_state_dict(ref_ca.state_dict())
+    for m in (ref_sa, ref_ca, sa, ca):
+        m.train(train_dropout > 0)
+    tgt = torch.randint(1, 50, (B, T), device="cuda")
+    tgt[:, 7:] = 0
+    tgt[2, 4:] = 0
+    tmask = make_std_mask(tgt, 0).repeat(H, 1, 1)
+    src_pad = torch.zeros(B, S, dtype=torch.bool, device="cuda")
+    src_pad[1, 9:] = True
+    src_pad[4, 3:] = True
+    x0 = torch.randn(B, T, E, device="cuda")
+    m0 = torch.randn(B, S, E, device="cuda")
+    gy = torch.randn(T, B, E, device="cuda")
+
+    def run(mods, x, mem, contiguous):
+        xs, ms = _perm_view(x), _perm_view(mem)
+        if contiguous:
+            xs, ms = xs.contiguous(), ms.contiguous()
+        torch.manual_seed(11)
+        h, _ = mods[0](xs, xs, xs, attn_mask=tmask, need_weights=False)
+        y, _ = mods[1](h, ms, ms, key_padding_mask=src_pad, need_weights=False)
+        y.backward(gy)
+        return y
+
+    for contiguous in (False, True):
+        xa, xb = x0.clone().requires_grad_(True), x0.clone().requires_grad_(True)
+        ma, mb = m0.clone().requires_grad_(True), m0.clone().requires_grad_(True)
+        for m in (ref_sa, ref_ca, sa, ca):
+            m.zero_grad(set_to_none=True)
+        ya = run((ref_sa, ref_ca), xa, ma, contiguous)
+        yb = run((sa, ca), xb, mb, contiguous)
+        assert yb.shape == ya.shape == (T, B, E)
+        np.testing.assert_allclose(yb.detach().cpu().numpy(), ya.detach().cpu().numpy(), rtol=1e-4, atol=1e-5)
+        pairs = [(xa.grad, xb.grad), (ma.grad, mb.grad)]
+        pairs += [(p.grad, q.grad) for r, g in ((ref_sa, sa), (ref_ca, ca))
+                  for p, q in zip(r.parameters(), g.parameters())]
+        for a, b in pairs:
+            np.testing.assert_allclose(b.cpu().numpy(), a.cpu().numpy(), rtol=1e-4, atol=1e-4)
+
+
+def test_glue_linear_layernorm_on_permuted_views():
+    """Linear and LayerNorm on a (T, B, E) permuted view of batch-first memory run on that memory and
+    return the same view layout; values and gradients as nn.Linear / nn.LayerNorm."""
+    from csa_amd.glue import LayerNorm, Linear
+    torch.manual_seed(9)
+    ref_ln, ref_lin = torch.nn.LayerNorm(96).cuda(), torch.nn.Linear(96, 40).cuda()
+    with torch.no_grad():
+        ref_ln.weight.normal_()
+        ref_ln.bias.normal_()
+    ln, lin = LayerNorm(96).cuda(), Linear(96, 40).cuda()
+    ln.load_state_dict(ref_ln.state_dict())
+    lin.load_state_dict(ref_lin.state_dict())
+    x = torch.randn(5, 23, 96, device="cuda") * 2 + 0.5
+    xa, xb = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
+    gy = torch.randn(23, 5, 40, device="cuda")
+    ya = ref_lin(ref_ln(_perm_view(xa)))
+    yb = lin(ln(_perm_view(xb)))
+    assert yb.transpose(0, 1).is_contiguous(), "output keeps the batch-first memory"
+    np.testing.assert_allclose(yb.detach().cpu().numpy(), ya.detach().cpu().numpy(), rtol=1e-4, atol=1e-5)
+    ya.backward(gy)
+    yb.backward(gy)
+    for a, b in ((xa.grad, xb.grad), (ref_ln.weight.grad, ln.weight.grad), (ref_ln.bias.grad, ln.bias.grad),
+                 (ref_lin.weight.grad, lin.weight.grad), (ref_lin.bias.grad, lin.bias.grad)):
+        np.testing.assert_allclose(b.cpu().numpy(), a.cpu().numpy(), rtol=1e-4, atol=1e-4)
