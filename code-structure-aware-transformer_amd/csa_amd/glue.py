@@ -164,3 +164,80 @@ class MultiheadAttention(nn.MultiheadAttention):
         o = F.scaled_dot_product_attention(q, k, v, m, self.dropout if self.training else 0.0)
         o = o.transpose(1, 2).reshape(B, T, E)
         return linear(o, self.out_proj.weight, self.out_proj.bias).transpose(0, 1), None
+
+
+class _SplitHeads3(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, y, num_heads):
+        B, N, C = y.shape
+        ctx.shape = (B, N, C)
+        v = y.view(B, N, 3, num_heads, C // (3 * num_heads))
+        return tuple(v[:, :, i].transpose(1, 2) for i in range(3))
+
+    @staticmethod
+    def backward(ctx, dq, dk, dv):
+        B, N, C = ctx.shape
+        ref = next(g for g in (dq, dk, dv) if g is not None)
+        out = torch.empty(B, N, C, device=ref.device, dtype=ref.dtype)
+        ov = out.view(B, N, 3, ref.shape[1], C // (3 * ref.shape[1]))
+        for i, g in enumerate((dq, dk, dv)):  # three strided copies (a strided-input stack is 3x slower)
+            if g is None:
+                ov[:, :, i].zero_()
+            else:
+                ov[:, :, i].transpose(1, 2).copy_(g)
+        return out, None
+
+
+def split_heads3(y, num_heads):
+    """Packed QKV projection (B, N, 3*H*d) -> Q, K, V as strided (B, H, N, d) views, the same values as
+    split(H*d, -1) followed by view(B, N, H, d).transpose(1, 2) (sbm_attn.py:137-140,
+    components.py:transpose_for_scores). The backward copies the three head-major gradients straight
+    into one packed (B, N, 3*H*d) tensor; torch's reshape/view + split backward copies each gradient
+    twice."""
+    if y.dim() != 3 or not y.is_contiguous() or y.shape[-1] % (3 * num_heads):
+        B, N, C = y.shape
+        return tuple(t.reshape(B, N, num_heads, -1).transpose(1, 2) for t in y.split(C // 3, dim=-1))
+    return _SplitHeads3.apply(y, num_heads)
+
+
+class _ResidualDropoutFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, o, p):
+        from .ops import _draw_seed
+        bm = not x.is_contiguous()  # batch-major (T, B, E) view: run on the (B, T, E) memory
+        xm, om = (x.transpose(0, 1), o.transpose(0, 1)) if bm else (x, o)
+        y = torch.empty_like(xm)
+        seed = _draw_seed()
+        p_ = lambda t: ctypes.c_void_p(t.data_ptr())
+        check(lib().csa_residual_dropout_fwd(p_(xm), p_(om), p_(y), y.numel(), p, seed, 0,
+                                             ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)),
+              "csa_residual_dropout_fwd")
+        ctx.cfg = (bm, p, seed)
+        return y.transpose(0, 1) if bm else y
+
+    @staticmethod
+    def backward(ctx, gy):
+        bm, p, seed = ctx.cfg
+        g = (gy.transpose(0, 1) if bm else gy).contiguous()  # same memory order as the forward
+        d_o = torch.empty_like(g)
+        p_ = lambda t: ctypes.c_void_p(t.data_ptr())
+        check(lib().csa_residual_dropout_bwd(p_(g), p_(d_o), g.numel(), p, seed, 0,
+                                             ctypes.c_void_p(torch.cuda.current_stream(g.device).cuda_stream)),
+              "csa_residual_dropout_bwd")
+        return gy, (d_o.transpose(0, 1) if bm else d_o), None
+
+
+def _aligned(t):
+    return t.data_ptr() % 16 == 0
+
+
+def residual_dropout(x, o, dropout: nn.Dropout):
+    """x + dropout(o) (module/components.py SublayerConnection, module/sbm_model.py:29-31) as one
+    csa_residual_dropout kernel per direction in training (Philox stream 5, oracle/philox.py:res_keep;
+    no mask stored). Eval mode, p outside (0, 1), CPU tensors or mismatched layouts take torch's ops."""
+    p = float(dropout.p)
+    if (dropout.training and 0.0 < p < 1.0 and x.is_cuda and x.dtype == torch.float32 and o.dtype == torch.float32
+            and x.shape == o.shape and x.stride() == o.stride() and _aligned(x) and _aligned(o)
+            and (x.is_contiguous() or _batch_major(x))):
+        return _ResidualDropoutFn.apply(x, o, p)
+    return x + dropout(o)

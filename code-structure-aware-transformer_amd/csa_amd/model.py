@@ -23,7 +23,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .glue import LayerNorm, Linear, MultiheadAttention
+from .glue import LayerNorm, Linear, MultiheadAttention, residual_dropout
 from .module.disentangled_attn import DisentangledAttn
 from .module.sbm_attn import Attention
 
@@ -88,7 +88,7 @@ class SublayerConnection(nn.Module):
 
     def forward(self, x, sublayer):
         out, w = sublayer(self.norm(x))
-        return x + self.dropout(out), w
+        return residual_dropout(x, out, self.dropout), w
 
 
 class CSE_layer(nn.Module):  # noqa: N801 (reference name)
@@ -153,8 +153,11 @@ class Transformer(nn.Module):
 
     def forward(self, X, mask, deliver):
         out, sparsity, graph, attn = self.mha([self.norm1(X), mask, deliver])
-        X = self.dropout1(out) + X
-        X = self.mlpblock(self.norm2(X)) + X
+        X = residual_dropout(X, out, self.dropout1)  # dropout1(out) + X
+        h = self.norm2(X)
+        for m in self.mlpblock[:-1]:
+            h = m(h)
+        X = residual_dropout(X, h, self.mlpblock[-1])  # mlpblock(norm2(X)) + X: its last module is the Dropout
         return X, sparsity, graph, attn
 
 
@@ -298,6 +301,28 @@ class CSATrans(nn.Module):
         return out, sparsity, pe, graphs, attns
 
 
+class _GatherTargets(torch.autograd.Function):
+    """x.gather(1, t[:, None])[:, 0] whose backward scatters into a fresh zero tensor in place (torch's
+    gather backward is an out-of-place scatter_add, i.e. zeros + a full clone of the (B*T, V) grad)."""
+
+    @staticmethod
+    def forward(ctx, x, t):
+        ctx.save_for_backward(t)
+        ctx.shape = x.shape
+        return x.gather(1, t.unsqueeze(1)).squeeze(1)
+
+    @staticmethod
+    def backward(ctx, g):
+        (t,) = ctx.saved_tensors
+        gx = torch.zeros(ctx.shape, device=g.device, dtype=g.dtype)
+        gx.scatter_add_(1, t.unsqueeze(1), g.unsqueeze(1))
+        return gx, None
+
+
+def _gather_targets(x, t):
+    return _GatherTargets.apply(x, t)
+
+
 class LabelSmoothing(nn.Module):
     """utils/label_smooth.py:15-40 without materialising true_dist (B*T x V: 251 MB per step at the java
     config). true_dist is `confidence` at the target, 0 in the padding column and in padded rows, and
@@ -320,7 +345,7 @@ class LabelSmoothing(nn.Module):
         t = target.reshape(-1)
         ntokens = (target != 0).sum()
         valid = t != self.padding_idx
-        xt = x.gather(1, t.unsqueeze(1)).squeeze(1)
+        xt = _gather_targets(x, t)
         conf, sm = self.confidence, self.smoothing
         row = -conf * xt + (conf * math.log(conf) if conf > 0.0 else 0.0)
         with torch.no_grad():

@@ -7,7 +7,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import rel_ops
-from ..glue import Linear, linear
+from ..glue import Linear, linear, split_heads3
 
 __all__ = ["DisentangledAttn", "transpose_for_scores", "_get_clones"]
 
@@ -40,8 +40,7 @@ class DisentangledAttn(nn.Module):
             qkv = self.linear_layers[:3]
             w = torch.cat([l.weight for l in qkv], 0)
             b = torch.cat([l.bias for l in qkv], 0)
-            query, key, value = (transpose_for_scores(t, self.h)
-                                 for t in linear(query, w, b).split(w.size(0) // 3, dim=-1))
+            query, key, value = split_heads3(linear(query, w, b), self.h)
         else:
             query, key, value = [transpose_for_scores(l(x), self.h)
                                  for l, x in zip(self.linear_layers, (query, key, value))]

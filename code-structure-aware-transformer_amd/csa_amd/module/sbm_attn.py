@@ -16,7 +16,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
-from ..glue import Linear, linear
+from ..glue import Linear, linear, split_heads3
 
 __all__ = ["SBMAttention", "FullAttention", "Attention"]
 
@@ -94,10 +94,9 @@ class Attention(nn.Module):
         X, mask, deliver = inputs
         # W_q / W_k / W_v as ONE (3 H d x dim) GEMM (parameters and state_dict keys unchanged); Q, K, V
         # are strided (B, H, N, d) views of its output, consumed in place by the kernels
-        hd = self.num_head * self.head_dim
         w = torch.cat([self.W_q.weight, self.W_k.weight, self.W_v.weight], 0)
         b = torch.cat([self.W_q.bias, self.W_k.bias, self.W_v.bias], 0)
-        Q, K, V = (self.split_heads(t) for t in linear(X, w, b).split(hd, dim=-1))
+        Q, K, V = split_heads3(linear(X, w, b), self.num_head)
         with torch.autocast(device_type="cuda", enabled=False):  # sbm_attn.py:120
             attn_out, sparsity, graph, attn = self.attn(Q.float(), K.float(), V.float(), mask.float())
         attn_out = self.combine_heads(attn_out)

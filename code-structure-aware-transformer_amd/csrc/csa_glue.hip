@@ -7,10 +7,15 @@
 // (rows / RS) slab with dwordx4 loads (16 threads per row x 16 rows in flight), reduces its 16 row
 // lanes through LDS in a fixed order and writes one partial row; pass 2 sums the RS partials in
 // slice order. The summation order depends only on (rows, cols): deterministic.
+#include <algorithm>
+#include <cmath>
+
 #include "csa_common.hpp"
 #include "../../include/csa_hip.h"
 
 using csa::f32x4;
+using csa::philox4x32;
+using csa::u32x4;
 
 namespace {
 
@@ -320,6 +325,112 @@ csa_status csa_layernorm_bwd(const float* dy, const float* x, const float* stats
     return CSA_LAUNCH_FAILED;
   }
   return CSA_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------------------
+// Residual + dropout of the pre-LN blocks (module/components.py SublayerConnection
+// `x + dropout(sublayer(norm(x)))`, module/sbm_model.py:29-31 `dropout1(out) + X`):
+//   y = x + keep(i) * o * scale,  do = keep(i) * dy * scale   (dx = dy needs no kernel).
+// keep(i) for memory element i is 16-bit uniform (i & 7) of Philox4x32-7
+// {lo32(i >> 3), hi32(i >> 3), 0, (RNG_RES_DROP << 28) ^ offset} keyed by the 64-bit seed, keep <=>
+// u16 >= ceil(p * 65536) (oracle/philox.py:res_keep). The backward regenerates the bits, so no
+// mask is stored. One thread per 8 consecutive elements (two dwordx4 loads per operand).
+constexpr uint32_t RNG_RES_DROP = 5u;
+
+struct ResArgs {
+  uint32_t seed_lo, seed_hi, off, thr;
+  float scale;
+  int64_t n;
+};
+
+__device__ __forceinline__ uint32_t res_keep8(const ResArgs& a, int64_t g) {
+  const u32x4 r = philox4x32(u32x4{(uint32_t)g, (uint32_t)((uint64_t)g >> 32), 0u, (RNG_RES_DROP << 28) ^ a.off},
+                             a.seed_lo, a.seed_hi);
+  const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+  uint32_t k = 0;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) k |= ((((e & 1) ? (w[e >> 1] >> 16) : (w[e >> 1] & 0xffffu)) >= a.thr) ? 1u : 0u) << e;
+  return k;
+}
+
+// BWD: x == nullptr, o = dy, y = do.
+template <bool BWD>
+__global__ __launch_bounds__(256) void k_res_drop(const float* __restrict__ x, const float* __restrict__ o,
+                                                  float* __restrict__ y, ResArgs a) {
+#pragma clang fp contract(off)  // dropout then add, two roundings as torch (no fma of o * scale + x)
+  const int64_t groups = (a.n + 7) >> 3;
+  for (int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x; g < groups; g += (int64_t)gridDim.x * 256) {
+    const uint32_t keep = res_keep8(a, g);
+    const int64_t i0 = g << 3;
+    if (i0 + 8 <= a.n) {
+      const f32x4 o0 = *reinterpret_cast<const f32x4*>(o + i0), o1 = *reinterpret_cast<const f32x4*>(o + i0 + 4);
+      f32x4 r0, r1;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        r0[e] = ((keep >> e) & 1u) ? o0[e] * a.scale : 0.f * o0[e];
+        r1[e] = ((keep >> (e + 4)) & 1u) ? o1[e] * a.scale : 0.f * o1[e];
+      }
+      if (!BWD) {
+        const f32x4 x0 = *reinterpret_cast<const f32x4*>(x + i0), x1 = *reinterpret_cast<const f32x4*>(x + i0 + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { r0[e] = x0[e] + r0[e]; r1[e] = x1[e] + r1[e]; }
+      }
+      *reinterpret_cast<f32x4*>(y + i0) = r0;
+      *reinterpret_cast<f32x4*>(y + i0 + 4) = r1;
+    } else {
+      for (int e = 0; i0 + e < a.n; ++e) {
+        const float v = ((keep >> e) & 1u) ? o[i0 + e] * a.scale : 0.f * o[i0 + e];
+        y[i0 + e] = BWD ? v : x[i0 + e] + v;
+      }
+    }
+  }
+}
+
+static csa_status res_launch(bool bwd, const float* x, const float* o, float* y, int64_t n, float p, uint64_t seed,
+                             uint64_t offset, void* stream, const char* name) {
+  if (n < 0 || !(p > 0.f && p < 1.f)) {
+    csa::set_error("%s: need n >= 0 and 0 < p < 1", name);
+    return CSA_INVALID_ARG;
+  }
+  if (n == 0) return CSA_OK;
+  if (!o || !y || (!bwd && !x)) {
+    csa::set_error("%s: null pointer", name);
+    return CSA_INVALID_ARG;
+  }
+  if ((((uintptr_t)o | (uintptr_t)y | (uintptr_t)x) & 15u) != 0) {
+    csa::set_error("%s: pointers must be 16-byte aligned", name);
+    return CSA_INVALID_ARG;
+  }
+  ResArgs a;
+  a.seed_lo = (uint32_t)seed; a.seed_hi = (uint32_t)(seed >> 32); a.off = (uint32_t)offset;
+  a.thr = (uint32_t)ceil((double)p * 65536.0);
+  a.scale = 1.f / (1.f - p);
+  a.n = n;
+  const int64_t groups = (n + 7) >> 3;
+  const unsigned blocks = (unsigned)std::min<int64_t>((groups + 255) / 256, 256 * 16);
+  const hipStream_t st = (hipStream_t)stream;
+  if (bwd) hipLaunchKernelGGL(k_res_drop<true>, dim3(blocks), dim3(256), 0, st, nullptr, o, y, a);
+  else hipLaunchKernelGGL(k_res_drop<false>, dim3(blocks), dim3(256), 0, st, x, o, y, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    csa::set_error("%s: %s", name, hipGetErrorString(e));
+    return CSA_LAUNCH_FAILED;
+  }
+  return CSA_OK;
+}
+
+extern "C" {
+
+csa_status csa_residual_dropout_fwd(const float* x, const float* o, float* y, int64_t n, float p, uint64_t seed,
+                                    uint64_t offset, void* stream) {
+  return res_launch(false, x, o, y, n, p, seed, offset, stream, "csa_residual_dropout_fwd");
+}
+
+csa_status csa_residual_dropout_bwd(const float* dy, float* d_o, int64_t n, float p, uint64_t seed, uint64_t offset,
+                                    void* stream) {
+  return res_launch(true, nullptr, dy, d_o, n, p, seed, offset, stream, "csa_residual_dropout_bwd");
 }
 
 }  // extern "C"

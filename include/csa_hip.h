@@ -198,6 +198,17 @@ csa_status csa_layernorm_fwd(const float* x, const float* gamma, const float* be
 csa_status csa_layernorm_bwd(const float* dy, const float* x, const float* stats, const float* gamma, float* dx,
                              float* dgamma, float* dbeta, int64_t rows, int64_t cols, void* workspace, void* stream);
 
+/* ---- Residual + dropout of the pre-LN blocks (module/components.py SublayerConnection
+ * `x + self.dropout(sublayer(self.norm(x)))`; module/sbm_model.py:29-31 `self.dropout1(out) + X` and
+ * `self.mlpblock(self.norm2(X)) + X`, whose last mlpblock module is the Dropout) ----
+ * x, o, y, dy, d_o: n fp32 elements in the same memory order, 16-byte aligned; 0 < p < 1.
+ * y = x + keep * o / (1 - p); d_o = keep * dy / (1 - p) (the residual gradient is dy itself).
+ * keep for element i: Philox4x32-7 stream 5 (oracle/philox.py:res_keep), regenerated by the backward. */
+csa_status csa_residual_dropout_fwd(const float* x, const float* o, float* y, int64_t n, float p, uint64_t seed,
+                                    uint64_t offset, void* stream);
+csa_status csa_residual_dropout_bwd(const float* dy, float* d_o, int64_t n, float p, uint64_t seed, uint64_t offset,
+                                    void* stream);
+
 /* ---- Host data path: AST relation planes (my_ast.py:198-273, dataset/base_data_set.py:33-36) ----
  * parent: (B, max_size) int32, pre-order ids (parent[v] < v, parent[0] = -1); n_nodes: (B,) int32
  * (trees longer than max_size are truncated to their pre-order prefix). Outputs (B, max_size,

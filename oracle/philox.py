@@ -115,3 +115,19 @@ def gen_keep(rows, V, seed, offset, p):
     words = philox4x32(col >> 3, row, 0, ((RNG_GEN_DROP << 28) ^ (int(offset) & 0xFFFFFFFF)) & 0xFFFFFFFF,
                        int(seed) & 0xFFFFFFFF, int(seed) >> 32)
     return u16_of(words, np.broadcast_to(col & 7, words[0].shape)) >= keep_threshold(p)
+
+
+RNG_RES_DROP = 5
+
+
+def res_keep(n, seed, offset, p):
+    """(n,) bool keep mask of the fused residual + dropout (csrc/csa_glue.hip k_res_drop; the
+    nn.Dropout of module/components.py SublayerConnection and module/sbm_model.py:29-31) over memory
+    element i: 16-bit uniform (i & 7) of philox({lo32(i >> 3), hi32(i >> 3), 0, (RNG_RES_DROP << 28) ^
+    offset}, seed)."""
+    i = np.arange(n, dtype=np.int64)
+    g = (i >> 3).astype(np.uint64)
+    words = philox4x32(g & np.uint64(0xFFFFFFFF), g >> np.uint64(32), 0,
+                       ((RNG_RES_DROP << 28) ^ (int(offset) & 0xFFFFFFFF)) & 0xFFFFFFFF,
+                       int(seed) & 0xFFFFFFFF, int(seed) >> 32)
+    return u16_of(words, i & 7) >= keep_threshold(p)

@@ -142,3 +142,47 @@ def test_glue_linear_layernorm_on_permuted_views():
     for a, b in ((xa.grad, xb.grad), (ref_ln.weight.grad, ln.weight.grad), (ref_ln.bias.grad, ln.bias.grad),
                  (ref_lin.weight.grad, lin.weight.grad), (ref_lin.bias.grad, lin.bias.grad)):
         np.testing.assert_allclose(b.cpu().numpy(), a.cpu().numpy(), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("shape,batch_major", [((64, 150, 512), False), ((49, 64, 512), True), ((3, 5, 7), False),
+                                               ((1, 1, 1), False), ((11, 3, 12), True)])
+def test_residual_dropout_matches_oracle(shape, batch_major):
+    """csa_residual_dropout_fwd/_bwd vs the oracle keep mask (oracle/philox.py:res_keep over the memory
+    order): y = x + keep * o / (1 - p) and d_o = keep * dy / (1 - p) bit-exact, dx = dy; eval mode is
+    the identity dropout."""
+    import sys
+    import os
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from oracle.philox import res_keep
+    from csa_amd.glue import residual_dropout
+    from csa_amd.ops import _draw_seed
+    p = 0.2
+    drop = torch.nn.Dropout(p).train()
+    g = torch.Generator().manual_seed(sum(shape))
+    mem = (shape[1], shape[0], shape[2]) if batch_major else shape
+    x0, o0, gy0 = (torch.randn(*mem, generator=g) for _ in range(3))
+    if batch_major:
+        x0, o0, gy0 = (t.transpose(0, 1) for t in (x0, o0, gy0))
+    x = x0.cuda().requires_grad_(True)
+    o = o0.cuda().requires_grad_(True)
+    if batch_major:  # (T, B, E) views of batch-first memory, as the decoder sees them
+        x = x0.transpose(0, 1).contiguous().cuda().transpose(0, 1).detach().requires_grad_(True)
+        o = o0.transpose(0, 1).contiguous().cuda().transpose(0, 1).detach().requires_grad_(True)
+    torch.manual_seed(77)
+    y = residual_dropout(x, o, drop)
+    torch.manual_seed(77)
+    seed = _draw_seed()
+    n = x0.numel()
+    to_mem = (lambda t: t.transpose(0, 1).contiguous()) if batch_major else (lambda t: t.contiguous())
+    keep = torch.from_numpy(res_keep(n, seed, 0, p)).view(to_mem(x0).shape)
+    scale = np.float32(1.0 / (1.0 - np.float32(p)))
+    o_m, x_m = to_mem(o0), to_mem(x0)
+    ref = x_m + torch.where(keep, o_m * float(scale), 0.0 * o_m)
+    assert torch.equal(to_mem(y.detach().cpu()), ref)
+    y.backward(gy0.cuda())
+    gy_m = to_mem(gy0)
+    assert torch.equal(to_mem(o.grad.cpu()), torch.where(keep, gy_m * float(scale), 0.0 * gy_m))
+    assert torch.equal(x.grad.cpu(), gy0)
+    assert 0.7 < keep.float().mean().item() < 0.9 or n < 100
+    drop.eval()
+    assert torch.equal(residual_dropout(x, o, drop).detach(), (x + o).detach())
