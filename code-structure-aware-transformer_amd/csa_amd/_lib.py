@@ -157,6 +157,10 @@ def lib():
     L.csa_residual_dropout_fwd.argtypes = [vp, vp, vp, i64, f32, u64, u64, vp]
     L.csa_residual_dropout_bwd.restype = ctypes.c_int
     L.csa_residual_dropout_bwd.argtypes = [vp, vp, i64, f32, u64, u64, vp]
+    L.csa_gelu_dropout_fwd.restype = ctypes.c_int
+    L.csa_gelu_dropout_fwd.argtypes = [vp, vp, i64, f32, u64, u64, vp]
+    L.csa_gelu_dropout_bwd.restype = ctypes.c_int
+    L.csa_gelu_dropout_bwd.argtypes = [vp, vp, vp, i64, f32, u64, u64, vp]
     L.csa_ast_relations.restype = ctypes.c_int
     L.csa_ast_relations.argtypes = [vp, vp, i64, i64, vp, vp, vp, vp, ctypes.c_int]
     L.csa_adamw_step.restype = ctypes.c_int
@@ -180,5 +184,5 @@ EXPORTED_SYMBOLS = (
     "csa_adamw_step", "csa_gen_logsoftmax_fwd", "csa_gen_logsoftmax_bwd",
     "csa_bias_grad_workspace_bytes", "csa_bias_grad", "csa_ast_relations",
     "csa_layernorm_supported", "csa_layernorm_bwd_workspace_bytes", "csa_layernorm_fwd", "csa_layernorm_bwd",
-    "csa_residual_dropout_fwd", "csa_residual_dropout_bwd",
+    "csa_residual_dropout_fwd", "csa_residual_dropout_bwd", "csa_gelu_dropout_fwd", "csa_gelu_dropout_bwd",
 )

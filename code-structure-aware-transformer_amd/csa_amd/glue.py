@@ -241,3 +241,43 @@ def residual_dropout(x, o, dropout: nn.Dropout):
             and (x.is_contiguous() or _batch_major(x))):
         return _ResidualDropoutFn.apply(x, o, p)
     return x + dropout(o)
+
+
+class _GeluDropoutFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, p):
+        from .ops import _draw_seed
+        bm = not h.is_contiguous()  # batch-major (T, B, F) view: run on the (B, T, F) memory
+        hm = h.transpose(0, 1) if bm else h
+        y = torch.empty_like(hm)
+        seed = _draw_seed() if p > 0.0 else 0
+        p_ = lambda t: ctypes.c_void_p(t.data_ptr())
+        check(lib().csa_gelu_dropout_fwd(p_(hm), p_(y), y.numel(), p, seed, 0,
+                                         ctypes.c_void_p(torch.cuda.current_stream(h.device).cuda_stream)),
+              "csa_gelu_dropout_fwd")
+        ctx.save_for_backward(hm)
+        ctx.cfg = (bm, p, seed)
+        return y.transpose(0, 1) if bm else y
+
+    @staticmethod
+    def backward(ctx, gy):
+        (hm,) = ctx.saved_tensors
+        bm, p, seed = ctx.cfg
+        g = (gy.transpose(0, 1) if bm else gy).contiguous()
+        dh = torch.empty_like(hm)
+        p_ = lambda t: ctypes.c_void_p(t.data_ptr())
+        check(lib().csa_gelu_dropout_bwd(p_(g), p_(hm), p_(dh), g.numel(), p, seed, 0,
+                                         ctypes.c_void_p(torch.cuda.current_stream(g.device).cuda_stream)),
+              "csa_gelu_dropout_bwd")
+        return (dh.transpose(0, 1) if bm else dh), None
+
+
+def gelu_dropout(h, dropout: nn.Dropout):
+    """dropout(gelu(h)) (exact erf GELU; module/components.py FeedForward, module/sbm_model.py:22-26) as
+    one csa_gelu_dropout kernel per direction (Philox stream 6, oracle/philox.py:ffn_keep; only h is
+    saved). CPU tensors, non-fp32 or other layouts take torch's ops."""
+    p = float(dropout.p) if dropout.training else 0.0
+    if (h.is_cuda and h.dtype == torch.float32 and 0.0 <= p < 1.0 and _aligned(h)
+            and (h.is_contiguous() or _batch_major(h))):
+        return _GeluDropoutFn.apply(h, p)
+    return dropout(F.gelu(h))

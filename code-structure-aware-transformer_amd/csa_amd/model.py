@@ -23,7 +23,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .glue import LayerNorm, Linear, MultiheadAttention, residual_dropout
+from .glue import LayerNorm, Linear, MultiheadAttention, gelu_dropout, residual_dropout
 from .module.disentangled_attn import DisentangledAttn
 from .module.sbm_attn import Attention
 
@@ -75,7 +75,7 @@ class FeedForward(nn.Module):
         self.dropout = nn.Dropout(dropout)
 
     def forward(self, x):
-        return self.linear2(self.dropout(F.gelu(self.linear1(x)))), None
+        return self.linear2(gelu_dropout(self.linear1(x), self.dropout)), None
 
 
 class SublayerConnection(nn.Module):
@@ -154,10 +154,12 @@ class Transformer(nn.Module):
     def forward(self, X, mask, deliver):
         out, sparsity, graph, attn = self.mha([self.norm1(X), mask, deliver])
         X = residual_dropout(X, out, self.dropout1)  # dropout1(out) + X
-        h = self.norm2(X)
-        for m in self.mlpblock[:-1]:
-            h = m(h)
-        X = residual_dropout(X, h, self.mlpblock[-1])  # mlpblock(norm2(X)) + X: its last module is the Dropout
+        lin1, gelu, drop, lin2, drop2 = self.mlpblock  # Linear, GELU, Dropout, Linear, Dropout
+        if gelu.approximate == "none":
+            h = lin2(gelu_dropout(lin1(self.norm2(X)), drop))
+        else:
+            h = lin2(drop(gelu(lin1(self.norm2(X)))))
+        X = residual_dropout(X, h, drop2)  # mlpblock(norm2(X)) + X: its last module is the Dropout
         return X, sparsity, graph, attn
 
 

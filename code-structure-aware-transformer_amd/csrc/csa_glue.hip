@@ -365,8 +365,9 @@ struct ResArgs {
   int64_t n;
 };
 
+template <uint32_t STREAM = RNG_RES_DROP>
 __device__ __forceinline__ uint32_t res_keep8(const ResArgs& a, int64_t g) {
-  const u32x4 r = philox4x32(u32x4{(uint32_t)g, (uint32_t)((uint64_t)g >> 32), 0u, (RNG_RES_DROP << 28) ^ a.off},
+  const u32x4 r = philox4x32(u32x4{(uint32_t)g, (uint32_t)((uint64_t)g >> 32), 0u, (STREAM << 28) ^ a.off},
                              a.seed_lo, a.seed_hi);
   const uint32_t w[4] = {r.x, r.y, r.z, r.w};
   uint32_t k = 0;
@@ -451,6 +452,114 @@ csa_status csa_residual_dropout_fwd(const float* x, const float* o, float* y, in
 csa_status csa_residual_dropout_bwd(const float* dy, float* d_o, int64_t n, float p, uint64_t seed, uint64_t offset,
                                     void* stream) {
   return res_launch(true, nullptr, dy, d_o, n, p, seed, offset, stream, "csa_residual_dropout_bwd");
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------------------
+// GELU + dropout of the feed-forward blocks (module/components.py FeedForward
+// `linear2(dropout(gelu(linear1(x))))`, module/sbm_model.py:22-26 mlpblock GELU -> Dropout):
+//   y = keep(i) * gelu(h) * scale,  dh = keep(i) * scale * dy * gelu'(h)   (exact erf GELU, torch's
+// formulas: gelu = h * 0.5 * (1 + erf(h / sqrt 2)), gelu' = cdf + h * exp(-h^2 / 2) / sqrt(2 pi)).
+// keep(i): Philox stream 6 over memory order, same layout as the residual stream
+// (oracle/philox.py:ffn_keep); p = 0 keeps everything (plain GELU).
+constexpr uint32_t RNG_FFN_DROP = 6u;
+
+__device__ __forceinline__ float gelu_f(float h) { return h * 0.5f * (1.f + erff(h * 0.70710678118654752440f)); }
+__device__ __forceinline__ float gelu_d(float h) {
+  const float cdf = 0.5f * (1.f + erff(h * 0.70710678118654752440f));
+  const float pdf = expf(-0.5f * h * h) * 0.39894228040143267794f;
+  return cdf + h * pdf;
+}
+
+template <bool BWD>
+__global__ __launch_bounds__(256) void k_gelu_drop(const float* __restrict__ h, const float* __restrict__ dy,
+                                                   float* __restrict__ out, ResArgs a) {
+#pragma clang fp contract(off)
+  const int64_t groups = (a.n + 7) >> 3;
+  for (int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x; g < groups; g += (int64_t)gridDim.x * 256) {
+    const uint32_t keep = a.thr ? res_keep8<RNG_FFN_DROP>(a, g) : 0xffu;
+    const int64_t i0 = g << 3;
+    float hv[8], gv[8], r[8];
+    const bool full = i0 + 8 <= a.n;
+    if (full) {
+      const f32x4 h0 = *reinterpret_cast<const f32x4*>(h + i0), h1 = *reinterpret_cast<const f32x4*>(h + i0 + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { hv[e] = h0[e]; hv[e + 4] = h1[e]; }
+      if (BWD) {
+        const f32x4 g0 = *reinterpret_cast<const f32x4*>(dy + i0), g1 = *reinterpret_cast<const f32x4*>(dy + i0 + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { gv[e] = g0[e]; gv[e + 4] = g1[e]; }
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        hv[e] = i0 + e < a.n ? h[i0 + e] : 0.f;
+        gv[e] = (BWD && i0 + e < a.n) ? dy[i0 + e] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      if (BWD) {
+        const float gd = a.thr ? (((keep >> e) & 1u) ? gv[e] * a.scale : 0.f * gv[e]) : gv[e];  // dropout bwd
+        r[e] = gd * gelu_d(hv[e]);
+      } else {
+        const float z = gelu_f(hv[e]);
+        r[e] = a.thr ? (((keep >> e) & 1u) ? z * a.scale : 0.f * z) : z;
+      }
+    }
+    if (full) {
+      *reinterpret_cast<f32x4*>(out + i0) = f32x4{r[0], r[1], r[2], r[3]};
+      *reinterpret_cast<f32x4*>(out + i0 + 4) = f32x4{r[4], r[5], r[6], r[7]};
+    } else {
+      for (int e = 0; i0 + e < a.n; ++e) out[i0 + e] = r[e];
+    }
+  }
+}
+
+static csa_status ffn_launch(bool bwd, const float* h, const float* dy, float* out, int64_t n, float p, uint64_t seed,
+                             uint64_t offset, void* stream, const char* name) {
+  if (n < 0 || !(p >= 0.f && p < 1.f)) {
+    csa::set_error("%s: need n >= 0 and 0 <= p < 1", name);
+    return CSA_INVALID_ARG;
+  }
+  if (n == 0) return CSA_OK;
+  if (!h || !out || (bwd && !dy)) {
+    csa::set_error("%s: null pointer", name);
+    return CSA_INVALID_ARG;
+  }
+  if ((((uintptr_t)h | (uintptr_t)out | (uintptr_t)dy) & 15u) != 0) {
+    csa::set_error("%s: pointers must be 16-byte aligned", name);
+    return CSA_INVALID_ARG;
+  }
+  ResArgs a;
+  a.seed_lo = (uint32_t)seed; a.seed_hi = (uint32_t)(seed >> 32); a.off = (uint32_t)offset;
+  a.thr = p > 0.f ? (uint32_t)ceil((double)p * 65536.0) : 0u;
+  a.scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  a.n = n;
+  const int64_t groups = (n + 7) >> 3;
+  const unsigned blocks = (unsigned)std::min<int64_t>((groups + 255) / 256, 256 * 16);
+  const hipStream_t st = (hipStream_t)stream;
+  if (bwd) hipLaunchKernelGGL(k_gelu_drop<true>, dim3(blocks), dim3(256), 0, st, h, dy, out, a);
+  else hipLaunchKernelGGL(k_gelu_drop<false>, dim3(blocks), dim3(256), 0, st, h, nullptr, out, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    csa::set_error("%s: %s", name, hipGetErrorString(e));
+    return CSA_LAUNCH_FAILED;
+  }
+  return CSA_OK;
+}
+
+extern "C" {
+
+csa_status csa_gelu_dropout_fwd(const float* h, float* y, int64_t n, float p, uint64_t seed, uint64_t offset,
+                                void* stream) {
+  return ffn_launch(false, h, nullptr, y, n, p, seed, offset, stream, "csa_gelu_dropout_fwd");
+}
+
+csa_status csa_gelu_dropout_bwd(const float* dy, const float* h, float* dh, int64_t n, float p, uint64_t seed,
+                                uint64_t offset, void* stream) {
+  return ffn_launch(true, h, dy, dh, n, p, seed, offset, stream, "csa_gelu_dropout_bwd");
 }
 
 }  // extern "C"

@@ -209,6 +209,16 @@ csa_status csa_residual_dropout_fwd(const float* x, const float* o, float* y, in
 csa_status csa_residual_dropout_bwd(const float* dy, float* d_o, int64_t n, float p, uint64_t seed, uint64_t offset,
                                     void* stream);
 
+/* ---- GELU + dropout of the feed-forward blocks (module/components.py FeedForward
+ * `linear2(dropout(gelu(linear1(x))))`; module/sbm_model.py:22-26 mlpblock GELU -> Dropout) ----
+ * h, y, dy, dh: n fp32 elements in the same memory order, 16-byte aligned; 0 <= p < 1.
+ * y = keep * gelu(h) / (1 - p) (exact erf GELU); dh = keep * dy / (1 - p) * gelu'(h).
+ * keep for element i: Philox4x32-7 stream 6 (oracle/philox.py:ffn_keep), regenerated by the backward. */
+csa_status csa_gelu_dropout_fwd(const float* h, float* y, int64_t n, float p, uint64_t seed, uint64_t offset,
+                                void* stream);
+csa_status csa_gelu_dropout_bwd(const float* dy, const float* h, float* dh, int64_t n, float p, uint64_t seed,
+                                uint64_t offset, void* stream);
+
 /* ---- Host data path: AST relation planes (my_ast.py:198-273, dataset/base_data_set.py:33-36) ----
  * parent: (B, max_size) int32, pre-order ids (parent[v] < v, parent[0] = -1); n_nodes: (B,) int32
  * (trees longer than max_size are truncated to their pre-order prefix). Outputs (B, max_size,

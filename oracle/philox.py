@@ -120,6 +120,25 @@ def gen_keep(rows, V, seed, offset, p):
 RNG_RES_DROP = 5
 
 
+def _flat_keep(n, seed, offset, p, stream):
+    i = np.arange(n, dtype=np.int64)
+    g = (i >> 3).astype(np.uint64)
+    words = philox4x32(g & np.uint64(0xFFFFFFFF), g >> np.uint64(32), 0,
+                       ((stream << 28) ^ (int(offset) & 0xFFFFFFFF)) & 0xFFFFFFFF,
+                       int(seed) & 0xFFFFFFFF, int(seed) >> 32)
+    return u16_of(words, i & 7) >= keep_threshold(p)
+
+
+RNG_FFN_DROP = 6
+
+
+def ffn_keep(n, seed, offset, p):
+    """(n,) bool keep mask of the fused GELU + dropout (csrc/csa_glue.hip k_gelu_drop; the nn.Dropout
+    after GELU in module/components.py FeedForward and module/sbm_model.py:22-26) over memory order:
+    the res_keep layout on Philox stream RNG_FFN_DROP."""
+    return _flat_keep(n, seed, offset, p, RNG_FFN_DROP)
+
+
 def res_keep(n, seed, offset, p):
     """(n,) bool keep mask of the fused residual + dropout (csrc/csa_glue.hip k_res_drop; the
     nn.Dropout of module/components.py SublayerConnection and module/sbm_model.py:29-31) over memory

@@ -186,3 +186,38 @@ def test_residual_dropout_matches_oracle(shape, batch_major):
     assert 0.7 < keep.float().mean().item() < 0.9 or n < 100
     drop.eval()
     assert torch.equal(residual_dropout(x, o, drop).detach(), (x + o).detach())
+
+
+@pytest.mark.parametrize("shape,batch_major,p", [((64, 150, 768), False, 0.2), ((49, 64, 2048), True, 0.2),
+                                                 ((3, 5, 7), False, 0.2), ((9, 4, 16), True, 0.0)])
+def test_gelu_dropout_matches_oracle(shape, batch_major, p):
+    """csa_gelu_dropout_fwd/_bwd vs torch's exact GELU under the oracle keep mask
+    (oracle/philox.py:ffn_keep over the memory order): y = keep * gelu(h) / (1 - p),
+    dh = keep * dy / (1 - p) * gelu'(h) (torch autograd of gelu); fp32 tolerance 1e-5 (device erff vs the
+    host's differ by an ulp or two)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from oracle.philox import ffn_keep
+    from csa_amd.glue import gelu_dropout
+    from csa_amd.ops import _draw_seed
+    drop = torch.nn.Dropout(p).train()
+    g = torch.Generator().manual_seed(sum(shape))
+    mem = (shape[1], shape[0], shape[2]) if batch_major else shape
+    h_mem, gy_mem = torch.randn(*mem, generator=g) * 3, torch.randn(*mem, generator=g)
+    to_logical = (lambda t: t.transpose(0, 1)) if batch_major else (lambda t: t)
+    to_mem = (lambda t: t.transpose(0, 1).contiguous()) if batch_major else (lambda t: t.contiguous())
+    h = to_logical(h_mem.cuda()).detach().requires_grad_(True)
+    torch.manual_seed(91)
+    y = gelu_dropout(h, drop)
+    torch.manual_seed(91)
+    seed = _draw_seed() if p > 0 else 0
+    keep = (torch.from_numpy(ffn_keep(h_mem.numel(), seed, 0, p)).view(mem) if p > 0
+            else torch.ones(mem, dtype=torch.bool))
+    scale = float(np.float32(1.0 / (1.0 - np.float32(p))))
+    hr = h_mem.clone().requires_grad_(True)
+    yr = torch.where(keep, torch.nn.functional.gelu(hr) * scale, 0.0 * hr)
+    np.testing.assert_allclose(to_mem(y.detach().cpu()).numpy(), yr.detach().numpy(), rtol=1e-5, atol=1e-5)
+    y.backward(to_logical(gy_mem.cuda()))
+    yr.backward(gy_mem)
+    np.testing.assert_allclose(to_mem(h.grad.cpu()).numpy(), hr.grad.numpy(), rtol=1e-5, atol=1e-5)
