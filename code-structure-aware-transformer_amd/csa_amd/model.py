@@ -351,12 +351,15 @@ class LabelSmoothing(nn.Module):
         conf, sm = self.confidence, self.smoothing
         row = -conf * xt + (conf * math.log(conf) if conf > 0.0 else 0.0)
         with torch.no_grad():
-            bad = ~(x > float("-inf"))  # -inf or NaN
-            n_bad = bad.sum()
             if sm > 0.0:
+                bad = ~(x > float("-inf"))  # -inf or NaN
+                n_bad = bad.sum()
                 n_at_td = (bad[valid].sum() - bad[valid, self.padding_idx].sum()) if V > 2 else 0
             else:
-                n_at_td = (bad.gather(1, t.unsqueeze(1)).squeeze(1) & valid).sum()
+                # per-row fp32 counts (exact: V < 2^24) summed in fp64: a bool .sum() would first cast
+                # the whole (B*T, V) mask to int64 (500 MB at the java config)
+                n_bad = torch.where(x > float("-inf"), 0.0, 1.0).sum(1).double().sum()
+                n_at_td = (~(xt.detach() > float("-inf")) & valid).sum()
             poison = torch.where(n_bad > n_at_td, float("nan"), 0.0).to(x.dtype)
         if sm > 0.0:
             eps = sm / (V - 2)
