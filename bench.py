@@ -129,13 +129,65 @@ def train_step_bench(world, rank, dev, steps, warmup, config="java", per_gpu_bat
                for i in range(nbatches)]
     for i in range(warmup):
         step(*batches[i % nbatches])
-    torch.cuda.synchronize()
+    losses = []
+    el = timed_region(world, dev, steps, lambda i: losses.append(step(*batches[i % nbatches])))
+    mean_loss = float(torch.stack(losses).mean())
+    nparam = sum(p.numel() for p in model.parameters())
+    return {"config": f"config/{config}.py CSATrans summary train step (DDP over RCCL)", "per_gpu_batch": per_gpu_batch,
+            "global_batch": per_gpu_batch * world, "steps": steps, "warmup": warmup,
+            "ms_per_step": round(el * 1000 / steps, 3), "samples_per_s": round(world * per_gpu_batch * steps / el, 1),
+            "params": nparam, "mean_loss": round(mean_loss, 4), "n_ranks": world,
+            "exchange": "DDP gradient all-reduce over RCCL (64 MB buckets)" if world > 1 else "none (1 GPU)"}
+
+
+def launch_ranks(nproc):
+    """--gpus N > 1 without a torchrun environment: start N ranks with torch.distributed.run and exit
+    with its status. This parent never touches the GPU (no HIP call happens before the children
+    start), so each rank initialises its own device, as script/train.py's launcher does
+    (torch.distributed.launch --nproc_per_node N, README.md:18)."""
+    import socket
+    import subprocess
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.call(cmd, env=env)
+
+
+def init_ranks(args):
+    """(world, rank, local, device) from the torchrun environment; RCCL ("nccl") on GPUs, gloo for the
+    CPU launcher self-test. The world size is the process group's, and must equal --gpus."""
+    env_world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if env_world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}")
+    if args.device == "cpu":
+        dev = torch.device("cpu")
+        if env_world > 1:
+            dist.init_process_group("gloo")
+    else:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        if env_world > 1:
+            dist.init_process_group("nccl", device_id=dev)
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    return world, rank, local, dev
+
+
+def timed_region(world, dev, steps, step):
+    """The contract's timed region: barrier + device sync on both sides of exactly `steps` steps;
+    returns the max over ranks of the elapsed wall time (s)."""
+    sync = torch.cuda.synchronize if dev.type == "cuda" else (lambda: None)
     if world > 1:
         dist.barrier()
+    sync()
     t0 = time.perf_counter()
     for i in range(steps):
-        loss = step(*batches[i % nbatches])
-    torch.cuda.synchronize()
+        step(i)
+    sync()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
@@ -143,11 +195,29 @@ def train_step_bench(world, rank, dev, steps, warmup, config="java", per_gpu_bat
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    nparam = sum(p.numel() for p in model.parameters())
-    return {"config": f"config/{config}.py CSATrans summary train step (DDP over RCCL)", "per_gpu_batch": per_gpu_batch,
-            "global_batch": per_gpu_batch * world, "steps": steps, "warmup": warmup,
-            "ms_per_step": round(el * 1000 / steps, 3), "samples_per_s": round(world * per_gpu_batch * steps / el, 1),
-            "params": nparam, "last_loss": round(float(loss), 4)}
+    return el
+
+
+def launcher_selftest(args, world, rank, dev):
+    """--device cpu: exercises the launcher, the process group and the max-over-ranks timing on host
+    CPUs (gloo) with a DDP-wrapped Linear; no kernel of this repo runs, so the line says so."""
+    torch.manual_seed(rank)
+    lin = torch.nn.Linear(64, 64)
+    model = torch.nn.parallel.DistributedDataParallel(lin) if world > 1 else lin
+    x = torch.randn(32, 64)
+
+    def step(i):
+        lin.zero_grad(set_to_none=True)
+        model(x).square().mean().backward()
+
+    for i in range(args.warmup):
+        step(i)
+    el = timed_region(world, dev, args.steps, step)
+    return {"metric": "launcher self-test (DDP Linear on CPU/gloo; not the hot path)", "value": round(world * 32 *
+            args.steps / el, 1), "unit": "samples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(el * 1000 / args.steps, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": "launcher self-test", "parallelism": f"dp{world}"}}
 
 
 def main():
@@ -163,16 +233,22 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-train", action="store_true", help="skip the full train-step measurement")
-    ap.add_argument("--train-steps", type=int, default=10)
+    ap.add_argument("--train-steps", type=int, default=50)
+    ap.add_argument("--train-warmup", type=int, default=20)
+    ap.add_argument("--device", choices=("cuda", "cpu"), default="cuda",
+                    help="cpu = launcher self-test over gloo (no HIP kernels)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
+    world, rank, local, dev = init_ranks(args)
+    if args.device == "cpu":
+        out = launcher_selftest(args, world, rank, dev)
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     from csa_amd import ops
     from csa_amd._lib import STAGES, CsaProf, KERNEL_OF_STAGE
@@ -189,14 +265,14 @@ def main():
         torch.nn.init.orthogonal_(mod.layer.weight)
     mod.train(not args.eval)
     model = mod
-    if world > 1 and not args.dense:
+    if world > 1 and not args.dense:  # FullAttention has no parameters: no gradient exchange exists
         model = torch.nn.parallel.DistributedDataParallel(mod, device_ids=[local])
     Q, K, V = (torch.randn(B, H, N, d, device=dev).requires_grad_(True) for _ in range(3))
     mask = torch.zeros(B, N, device=dev)
     dX = torch.randn(B, H, N, d, device=dev)
     dsp = torch.full((H,), 3.125e-4, device=dev)
 
-    def step():
+    def step(i=0):
         for t in (Q, K, V):
             t.grad = None
         for p in mod.parameters():
@@ -259,22 +335,13 @@ def main():
 
     # 2) timed region: events only around the dominant kernel (its live average launch duration)
     profs = make_profs(args.steps, [dom] if dom else [])
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
+
+    def timed_step(i):
         ops.set_stage_profiler(*profs[i])
         step()
+
+    elapsed = timed_region(world, dev, args.steps, timed_step)
     ops.set_stage_profiler(None, None)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
     dom_ms = stage_times(profs, [dom]).get(dom) if dom else None
     ev.destroy()
 
@@ -301,7 +368,9 @@ def main():
         "config": {"workload": "SBMAttention fwd+bwd (config/python.py dims) " + ("dense FullAttention" if args.dense
                    else "SBM") + ("" if N == 150 else f", long-AST stress N={N} k={k}"), "global_batch": B * world, "per_gpu_batch": B, "seq_len": N, "heads": H,
                    "head_dim": d, "clusters": 0 if args.dense else k, "mode": "eval" if args.eval else "train",
-                   "parallelism": f"dp{world}"},
+                   "parallelism": f"dp{world}",
+                   "exchange": "none (FullAttention has no parameters)" if args.dense else
+                   ("DDP gradient all-reduce over RCCL" if world > 1 else "none (1 GPU)")},
         "roofline": roofline,
         "step_tflops": round(total_flops / (ms_per_step * 1e-3) / 1e12, 2),
         "step_frac_of_f32_mfma_peak": round(total_flops / (ms_per_step * 1e-3) / 1e12 / PEAK_F32_MFMA_TFLOPS, 4),
@@ -309,7 +378,7 @@ def main():
 
     }
     if not args.no_train:
-        out["train"] = train_step_bench(world, rank, dev, args.train_steps, max(2, args.warmup))
+        out["train"] = train_step_bench(world, rank, dev, args.train_steps, args.train_warmup)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, B=16 if N <= 150 else 1, N=N, k=k)
     if rank == 0:

@@ -112,6 +112,7 @@ def lib():
                        "(there is no CPU fallback for the hot path)")
     L = ctypes.CDLL(LIB_PATH)
     L.csa_abi_version.restype = ctypes.c_int
+    L.csa_source_hash.restype = ctypes.c_char_p
     L.csa_status_str.restype = ctypes.c_char_p
     L.csa_status_str.argtypes = [ctypes.c_int]
     L.csa_last_error_str.restype = ctypes.c_char_p
@@ -171,6 +172,11 @@ def lib():
     return L
 
 
+def loaded_source_hash():
+    """sha256 of the sources the loaded library was built from (csa_source_hash())."""
+    return lib().csa_source_hash().decode()
+
+
 def check(status, what):
     if status != 0:
         L = lib()
@@ -178,7 +184,7 @@ def check(status, what):
 
 
 EXPORTED_SYMBOLS = (
-    "csa_abi_version", "csa_status_str", "csa_last_error_str", "csa_sbm_supported", "csa_sbm_state_bytes",
+    "csa_abi_version", "csa_source_hash", "csa_status_str", "csa_last_error_str", "csa_sbm_supported", "csa_sbm_state_bytes",
     "csa_sbm_bwd_workspace_bytes", "csa_sbm_fwd", "csa_sbm_maps", "csa_sbm_bwd", "csa_ste_sample",
     "csa_ste_backward", "csa_rel_attn_state_bytes", "csa_rel_attn_bwd_workspace_bytes", "csa_rel_attn_fwd", "csa_rel_attn_bwd",
     "csa_adamw_step", "csa_gen_logsoftmax_fwd", "csa_gen_logsoftmax_bwd",

@@ -1,4 +1,9 @@
-"""Build libcsa_hip.so in-tree with hipcc for gfx950 (no torch extension toolchain involved)."""
+"""Build libcsa_hip.so in-tree with hipcc for gfx950 (no torch extension toolchain involved).
+
+The library carries the sha256 of the sources it was compiled from (csa_source_hash(), also written
+next to it as libcsa_hip.so.sha256); build() recompiles whenever the tree's hash differs, so a
+stale prebuilt binary is never reused, and smoke() asserts the loaded library matches the tree."""
+import hashlib
 import os
 import subprocess
 import sys
@@ -12,18 +17,45 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-shared", "-fPIC", "-Wal
          "-Wno-unused-function"]
 
 
-def build(force=False, verbose=True):
+HEADER = os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "csa_hip.h")
+
+
+def _deps():
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
-    deps = srcs + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hpp", ".h"))]
-    deps.append(os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "csa_hip.h"))
-    if not force and os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps):
+    hdrs = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hpp", ".h")))
+    return srcs, srcs + hdrs + [HEADER]
+
+
+def source_hash():
+    """sha256 over (name, content) of every source and header the library is built from."""
+    h = hashlib.sha256()
+    for p in _deps()[1]:
+        h.update(os.path.basename(p).encode() + b"\0")
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
+def built_hash():
+    try:
+        with open(OUT + ".sha256") as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
+def build(force=False, verbose=True):
+    srcs, deps = _deps()
+    digest = source_hash()
+    if not force and os.path.exists(OUT) and built_hash() == digest:
         return OUT
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
     objs = []
     procs = []
     for s in srcs:
         o = os.path.join(os.path.dirname(OUT), os.path.basename(s) + ".o")
-        cmd = [HIPCC] + FLAGS[:-3] + ["-c", "-fPIC", "-Wall", "-Wno-unused-result", "-o", o, s]
+        cmd = [HIPCC] + FLAGS[:-3] + ["-c", "-fPIC", "-Wall", "-Wno-unused-result", f'-DCSA_SOURCE_HASH="{digest}"',
+                                      "-o", o, s]
         cmd = [c for c in cmd if c != "-shared"]
         procs.append((subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT), cmd))
         objs.append(o)
@@ -35,6 +67,8 @@ def build(force=False, verbose=True):
     cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", OUT + ".tmp"] + objs
     subprocess.check_call(cmd)
     os.replace(OUT + ".tmp", OUT)
+    with open(OUT + ".sha256", "w") as f:
+        f.write(digest + "\n")
     if verbose:
         print("built", OUT)
     return OUT

@@ -23,6 +23,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .data import BOS, UNK
 from .glue import LayerNorm, Linear, MultiheadAttention, gelu_dropout, residual_dropout
 from .module.disentangled_attn import DisentangledAttn
 from .module.sbm_attn import Attention
@@ -287,20 +288,68 @@ class CSATrans(nn.Module):
         else:
             self.load_state_dict(state_dict)
 
-    def forward(self, data):
+    def base_process(self, data):
+        """base_seq2seq.py:43-54: masks and embeddings; the target side only when tgt_seq is given
+        (GreedyGenerator runs with tgt_seq None and fills tgt_mask / tgt_emb per step)."""
         data.src_mask = data.src_seq.eq(PAD)
         data.src_emb = self.src_embedding(data.src_seq)
         data.src_pe_emb = self.src_pe_embedding(data.src_seq)
-        data.tgt_mask = make_std_mask(data.tgt_seq, PAD)
-        data.tgt_emb = self.tgt_embedding(data.tgt_seq)
+        if getattr(data, "tgt_seq", None) is not None:
+            data.tgt_mask = make_std_mask(data.tgt_seq, PAD)
+            data.tgt_emb = self.tgt_embedding(data.tgt_seq)
+
+    def process_data(self, data):
+        """base_seq2seq.py:56-57."""
+        self.base_process(data)
+
+    def encode(self, data):
+        """base_seq2seq.py:67-97 (pegen branch): CSE -> SBM; sparsity = mean over the SBM layers' head
+        sparsities, or 1 for the dense ablation. Returns (enc, sparsity, pe, graphs, attns)."""
         src_pe = self.pegen(data)
         enc, sparsity, graphs, attns, pe = self.SBM(data, src_pe, self.use_pegen)
-        sparsity = 1 if sparsity[0] is None else torch.mean(torch.stack(sparsity))  # base_seq2seq.py:92-95
+        sparsity = 1 if sparsity[0] is None else torch.mean(torch.stack(sparsity))
+        return enc, sparsity, pe, graphs, attns
+
+    def decode(self, data, encoder_outputs):
+        """base_seq2seq.py:99-114: returns (decoder outputs (B,T,E), last cross-attention weights)."""
         tgt_mask = data.tgt_mask.repeat(self.num_heads, 1, 1)
-        dec, _ = self.decoder(data.tgt_emb.permute(1, 0, 2), enc.permute(1, 0, 2), tgt_mask=tgt_mask,
+        dec, w = self.decoder(data.tgt_emb.permute(1, 0, 2), encoder_outputs.permute(1, 0, 2), tgt_mask=tgt_mask,
                               memory_key_padding_mask=data.src_mask)
-        out = self.generator(dec.permute(1, 0, 2))
+        return dec.permute(1, 0, 2), w
+
+    def forward(self, data):
+        """base_seq2seq.py:59-65."""
+        self.process_data(data)
+        enc, sparsity, pe, graphs, attns = self.encode(data)
+        dec, _ = self.decode(data, enc)
+        out = self.generator(dec)
         return out, sparsity, pe, graphs, attns
+
+
+class GreedyGenerator(nn.Module):
+    """module/base_seq2seq.py:117-145: one encode, then max_tgt_len-1 steps of decode + generator +
+    argmax over the last position, starting from BOS; returns the generated ids without BOS."""
+
+    def __init__(self, model, max_tgt_len, multi_gpu=False):
+        super().__init__()
+        self.model = model.module if multi_gpu else model
+        self.max_tgt_len = max_tgt_len
+        self.start_pos = BOS
+        self.unk_pos = UNK
+
+    def forward(self, data):
+        m = self.model
+        m.process_data(data)
+        enc, _, _, _, _ = m.encode(data)
+        ys = torch.full((enc.size(0), 1), self.start_pos, dtype=torch.long, device=enc.device)
+        for _ in range(self.max_tgt_len - 1):
+            data.tgt_mask = make_std_mask(ys, PAD)
+            data.tgt_emb = m.tgt_embedding(ys)
+            dec, _ = m.decode(data, enc)
+            out = m.generator(dec)[:, -1, :]
+            next_word = torch.max(out, dim=1)[1]
+            ys = torch.cat([ys, next_word.unsqueeze(1)], dim=1)
+        return ys[:, 1:]
 
 
 class _GatherTargets(torch.autograd.Function):

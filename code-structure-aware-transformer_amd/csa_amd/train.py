@@ -41,42 +41,42 @@ class AdamW(torch.optim.Optimizer):
             raise ValueError("invalid AdamW hyper-parameters")
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
                                       correct_bias=correct_bias))
-        self._tables = {}  # parameter layout -> device chunk tables for csa_adamw_step
+        self._tables = {}  # param-group index -> device chunk tables + descriptors for csa_adamw_step
 
-    def _chunk_tables(self, ps, grads, m, v):
-        """Device tables for csa_adamw_step: chunk -> tensor and first chunk per tensor (cached per
-        parameter layout), and the (param, grad, exp_avg, exp_avg_sq, numel) descriptors, re-sent
-        only when a pointer changes (set_to_none grads may come back elsewhere) through a pinned
-        non-blocking copy, so the step never waits for the device."""
+    def _chunk_tables(self, key, ps, grads, m, v):
+        """Device tables for csa_adamw_step, cached per parameter group (`key`): chunk -> tensor and
+        first chunk per tensor (rebuilt only when the group's sizes change), and the (param, grad,
+        exp_avg, exp_avg_sq, numel) descriptors, re-sent only when a pointer changes (set_to_none grads
+        may come back elsewhere) through a pinned non-blocking copy, so the step never waits for the
+        device. Each group keeps its own entry, so a decay/no-decay split does not rebuild per step."""
         from ._lib import ADAMW_CHUNK
         dev = ps[0].device
         sizes = tuple(p.numel() for p in ps)
-        lay = self._tables.get(sizes)
-        if lay is None:
+        ent = self._tables.get(key)
+        if ent is None or ent["sizes"] != sizes:
             nchunk = [(n + ADAMW_CHUNK - 1) // ADAMW_CHUNK for n in sizes]
             start = torch.zeros(len(sizes), dtype=torch.int64)
             if len(sizes) > 1:
                 start[1:] = torch.cumsum(torch.tensor(nchunk[:-1], dtype=torch.int64), 0)
             owner = torch.repeat_interleave(torch.arange(len(sizes), dtype=torch.int32),
                                             torch.tensor(nchunk, dtype=torch.int64))
-            lay = (owner.to(dev), start.to(dev), sum(nchunk))
-            self._tables = {sizes: lay}
-        desc_key = tuple(x for q in zip(ps, grads, m, v) for x in (q[0].data_ptr(), q[1].data_ptr(),
-                                                                   q[2].data_ptr(), q[3].data_ptr()))
-        desc = self._tables.get(desc_key)
-        if desc is None:
-            host = torch.tensor([x for i in range(len(ps)) for x in (*desc_key[4 * i:4 * i + 4], sizes[i])],
+            ent = {"sizes": sizes, "owner": owner.to(dev), "start": start.to(dev), "nchunks": sum(nchunk),
+                   "ptrs": None, "desc": None}
+            self._tables[key] = ent
+        ptrs = tuple(x for q in zip(ps, grads, m, v) for x in (q[0].data_ptr(), q[1].data_ptr(),
+                                                               q[2].data_ptr(), q[3].data_ptr()))
+        if ent["ptrs"] != ptrs:
+            host = torch.tensor([x for i in range(len(ps)) for x in (*ptrs[4 * i:4 * i + 4], sizes[i])],
                                 dtype=torch.int64).pin_memory()
-            desc = host.to(dev, non_blocking=True)
-            self._tables = {sizes: lay, desc_key: desc}
-        return desc, lay[0], lay[1], len(ps), lay[2]
+            ent["desc"], ent["ptrs"] = host.to(dev, non_blocking=True), ptrs
+        return ent["desc"], ent["owner"], ent["start"], len(ps), ent["nchunks"]
 
-    def _fused_step(self, group, ps, grads, m, v, step_size, grad_scale=None, found_inf=None):
+    def _fused_step(self, gi, group, ps, grads, m, v, step_size, grad_scale=None, found_inf=None):
         from ._lib import AdamwArgs, check, lib
         for t in ps + grads + m + v:
             if t.dtype != torch.float32 or not t.is_contiguous():
                 raise RuntimeError("csa_adamw_step: parameters, grads and state must be contiguous fp32")
-        desc, owner, start, nt, nc = self._chunk_tables(ps, grads, m, v)
+        desc, owner, start, nt, nc = self._chunk_tables(gi, ps, grads, m, v)
         b1, b2 = group["betas"]
         a = AdamwArgs(tensors=desc.data_ptr(), chunk_tensor=owner.data_ptr(), chunk_start=start.data_ptr(),
                       ntensors=nt, nchunks=nc, beta1=b1, beta2=b2, one_minus_beta1=1.0 - b1,
@@ -99,7 +99,7 @@ class AdamW(torch.optim.Optimizer):
             on_host = any(p.grad is not None and not p.is_cuda for g in self.param_groups for p in g["params"])
             if (on_host or any(g["correct_bias"] for g in self.param_groups)) and found_inf.item() != 0.0:
                 return loss  # GradScaler skip, decided on the host (no state change)
-        for group in self.param_groups:
+        for gi, group in enumerate(self.param_groups):
             ps = [p for p in group["params"] if p.grad is not None]
             if not ps:
                 continue
@@ -120,7 +120,7 @@ class AdamW(torch.optim.Optimizer):
                 t = self.state[ps[0]]["step"]
                 step_size = step_size * (1.0 - b2 ** t) ** 0.5 / (1.0 - b1 ** t)
             if ps[0].is_cuda:
-                self._fused_step(group, ps, grads, m, v, step_size, grad_scale, found_inf)
+                self._fused_step(gi, group, ps, grads, m, v, step_size, grad_scale, found_inf)
                 continue
             if grad_scale is not None:
                 grads = torch._foreach_mul(grads, (1.0 / grad_scale.double()).float().item())

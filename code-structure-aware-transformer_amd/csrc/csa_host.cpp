@@ -118,3 +118,10 @@ extern "C" csa_status csa_ast_relations(const int32_t* parent, const int32_t* n_
     }
   return CSA_OK;
 }
+
+// Build provenance: sha256 of every source and header the library was compiled from, passed in by
+// csa_amd/build.py (-DCSA_SOURCE_HASH). smoke() and the tests compare it with the tree they run in.
+#ifndef CSA_SOURCE_HASH
+#define CSA_SOURCE_HASH "unknown"
+#endif
+extern "C" const char* csa_source_hash(void) { return CSA_SOURCE_HASH; }

@@ -99,6 +99,9 @@ typedef struct csa_sbm_bwd_args {
 } csa_sbm_bwd_args;
 
 int csa_abi_version(void);
+/* sha256 (hex) of the csrc/ sources + headers and this header the library was built from
+ * (csa_amd/build.py:source_hash); lets a caller prove the loaded binary matches its source tree. */
+const char* csa_source_hash(void);
 const char* csa_status_str(csa_status s);
 const char* csa_last_error_str(void);
 /* 1 if (d, k, flags) is a compiled instantiation */

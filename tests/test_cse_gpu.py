@@ -55,3 +55,73 @@ def test_disentangled_attn_module_matches_reference(golden):
     np.testing.assert_allclose(rq.grad.cpu().numpy(), z["drel_q"], rtol=RTOL, atol=ATOL)
     for pn, p in m.named_parameters():
         np.testing.assert_allclose(p.grad.cpu().numpy(), z["g:" + pn], rtol=RTOL, atol=ATOL, err_msg=pn)
+
+
+def _large_case(z):
+    import golden_inputs as gi
+    B, H, N, dk, L, seed = (int(v) for v in z["meta"])
+    return gi.rel_inputs(B, H, N, dk, L, seed)
+
+
+@pytest.mark.skipif(not has_gpu(), reason="needs GPU")
+@pytest.mark.parametrize("layout", ["reference", "compact"])
+def test_rel_attn_production_head_size_matches_reference(golden, layout):
+    """rel_attn at the CSE's production shape (d_k = pegen_dim/8 = 64, N = L = 150) vs the reference
+    (tests/golden/rel_attn_n150_dk64.npz; inputs regenerated from PCG64, tests/golden_inputs.py)."""
+    from csa_amd import rel_ops
+    z = golden("rel_attn_n150_dk64")
+    qn, kn, vn, lqn, lkn, dOn = _large_case(z)
+    if layout == "reference":
+        rel, mask = (t.cuda() for t in ref_rel_mask(z))
+    else:
+        rel = dev(np.stack([z["L"], z["T"]], 1).astype(np.uint8))
+        mask = dev(np.stack([z["L_mask"], z["T_mask"]], 1).astype(np.uint8))
+    q, k, v, lq, lk = (dev(a, True) for a in (qn, kn, vn, lqn, lkn))
+    o = rel_ops.rel_attn(q, k, v, lq, lk, rel, mask)
+    np.testing.assert_allclose(o.detach().cpu().numpy(), z["out"], rtol=RTOL, atol=ATOL)
+    (o * dev(dOn)).sum().backward()
+    for n, x in (("dq", q), ("dk", k), ("dv", v), ("dlq", lq), ("dlk", lk)):
+        np.testing.assert_allclose(x.grad.cpu().numpy(), z[n], rtol=RTOL, atol=ATOL, err_msg=n)
+
+
+def _run_rel(q, k, v, lq, lk, rel, mask, dO):
+    from csa_amd import rel_ops
+    t = [x.cuda().requires_grad_(True) for x in (q, k, v, lq, lk)]
+    o = rel_ops.rel_attn(*t, rel.cuda(), mask.cuda())
+    (o * dO.cuda()).sum().backward()
+    torch.cuda.synchronize()
+    return [o.detach().cpu()] + [x.grad.cpu() for x in t]
+
+
+@pytest.mark.skipif(not has_gpu(), reason="needs GPU")
+def test_rel_attn_full_size_rows_match_oracle_and_deterministic():
+    """The java train step's CSE shape (B=64 per GPU, H=8, N=L=150, d_k=64) in the compact layout:
+    two runs are bitwise identical; out/dq/dk/dv of sampled batch rows match the fp64 oracle run on
+    those rows alone (each row depends only on its AST); dlq/dlk (sums over the whole batch) match
+    the fp64 oracle over all 64 rows."""
+    from csa_amd.data import synthetic_batch
+    from oracle import cse_ref
+    B, H, N, dk, L = 64, 8, 150, 64, 150
+    sb = synthetic_batch(B, max_size=N, seed=5, min_nodes=60, max_nodes=N)
+    g = torch.Generator().manual_seed(9)
+    q, k, v, dO = (torch.randn(B, H, N, dk, generator=g) for _ in range(4))
+    lq, lk = (torch.randn(1, H, L, dk, generator=g) for _ in range(2))
+    rel = torch.from_numpy(np.stack([sb["L"], sb["T"]], 1).astype(np.uint8))
+    mask = torch.from_numpy(np.stack([sb["L_mask"], sb["T_mask"]], 1).astype(np.uint8))
+    r1 = _run_rel(q, k, v, lq, lk, rel, mask, dO)
+    r2 = _run_rel(q, k, v, lq, lk, rel, mask, dO)
+    for a, b in zip(r1, r2):
+        assert torch.equal(a, b)
+    refrel, refmask = cse_ref.build_rel_mask(*(torch.from_numpy(sb[n]) for n in ("L", "T", "L_mask", "T_mask")))
+    t = [x.double().requires_grad_(True) for x in (q, k, v, lq, lk)]
+    o = cse_ref.rel_attn(*t, refrel, refmask)
+    (o * dO.double()).sum().backward()
+    for b in (0, 17, 63):
+        np.testing.assert_allclose(r1[0][b].numpy(), o[b].detach().numpy(), rtol=RTOL, atol=ATOL)
+        for i, n in ((1, "dq"), (2, "dk"), (3, "dv")):
+            np.testing.assert_allclose(r1[i][b].numpy(), t[i - 1].grad[b].numpy(), rtol=RTOL, atol=ATOL, err_msg=n)
+    # dlq / dlk sum B*N terms per bin: fp32 accumulation error grows with the bin's population
+    for i, n in ((4, "dlq"), (5, "dlk")):
+        ref = t[i - 1].grad.numpy()
+        np.testing.assert_allclose(r1[i].numpy(), ref, rtol=RTOL, atol=ATOL * max(1.0, np.abs(ref).max() / 100),
+                                   err_msg=n)

@@ -11,15 +11,7 @@ TINY = dict(src_vocab_size=50, tgt_vocab_size=60, hidden_size=64, num_heads=8, n
             clusters=[10, 12], full_att=False)
 
 
-def fill_params_deterministic(model, seed):
-    """Same fill as tools/gen_golden.py (numpy PCG64, sorted parameter names)."""
-    rng = np.random.default_rng(seed)
-    named = dict(model.named_parameters())
-    with torch.no_grad():
-        for k in sorted(named):
-            p = named[k]
-            fan = p.shape[-1] if p.dim() > 1 else 1
-            p.copy_(torch.from_numpy((rng.standard_normal(p.shape) * (0.5 / np.sqrt(fan))).astype(np.float32)))
+from golden_inputs import fill_params_deterministic  # same fill as tools/gen_golden.py  # noqa: E402
 
 
 def test_state_dict_keys_match_reference(golden):
@@ -56,3 +48,88 @@ def test_csatrans_forward_backward_matches_reference(golden):
             np.testing.assert_allclose(named[k[2:]].grad.cpu().numpy(), z[k], rtol=1e-3, atol=2e-5, err_msg=k)
             checked += 1
     assert checked >= 10
+
+
+def _java_model_and_batch(dev):
+    import golden_inputs as gi
+    from csa_amd.data import synthetic_batch
+    from csa_amd.model import CSATrans, batch_to_device
+    m = CSATrans(**gi.JAVA)
+    gi.fill_params_deterministic(m, gi.JAVA_SEED)
+    sb = synthetic_batch(gi.JAVA_B, max_size=gi.JAVA_N, seed=gi.JAVA_SEED, min_nodes=100, max_nodes=gi.JAVA_N)
+    return m, batch_to_device(sb, dev)
+
+
+def test_java_state_dict_keys_match_reference(golden):
+    """config/java.py CSATrans: reference checkpoints load unchanged (module/csa_trans.py:176-177)."""
+    import golden_inputs as gi
+    from csa_amd.model import CSATrans
+    z = golden("csatrans_java")
+    assert sorted(CSATrans(**gi.JAVA).state_dict().keys()) == list(z["state_keys"])
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not has_gpu(), reason="needs GPU")
+def test_csatrans_java_dims_match_reference(golden):
+    """Production shapes end to end: config/java.py dims (SBM d=96, k=10; CSE d_k=64; N=150; 4+4 layers;
+    20000-word generator) vs the reference CSATrans on identical weights, batch and STE uniforms
+    (tests/golden/csatrans_java.npz, tools/gen_golden.py:csatrans_java_case). The uniforms were moved
+    >= 5e-4 away from the reference's clamp(expA) so no edge sits on an fp32 tie.
+    Tolerances: the logits pass 8 encoder + 4 decoder layers of fp32 sums in a different order than
+    the CPU reference; log-probabilities within 2e-4 absolute, gradients within rtol 2e-3 / atol 1e-5
+    of the largest gradient entry."""
+    import golden_inputs as gi
+    from csa_amd.model import label_smoothing_loss
+    z = golden("csatrans_java")
+    m, (x, y) = _java_model_and_batch(torch.device("cuda"))
+    m = m.cuda().eval()
+    for i in range(4):
+        u = gi.apply_nudges(gi.java_uniforms(i), z[f"nudge_idx{i}"], z[f"nudge_val{i}"])
+        getattr(m.SBM, f"transformer_{i}").mha.attn.uniforms = torch.from_numpy(u).cuda()
+    out, sparsity, pe, graphs, attns = m(x)
+    loss = label_smoothing_loss(out, y)
+    o = out.detach()
+    np.testing.assert_allclose(o[:, :, ::gi.JAVA_OUT_COL_STRIDE].cpu().numpy(), z["out_cols"], rtol=1e-4, atol=2e-4)
+    np.testing.assert_allclose(o.max(-1).values.cpu().numpy(), z["out_rowmax"], rtol=1e-4, atol=2e-4)
+    np.testing.assert_allclose(sparsity.item(), z["sparsity"][0], rtol=1e-6)  # exact edge counts
+    np.testing.assert_allclose(loss.item(), z["loss"][0], rtol=2e-5)
+    (loss + 1e-2 * sparsity).backward()
+    named = dict(m.named_parameters())
+    checked = 0
+    for k in z:
+        if k.startswith("g:"):
+            ref = z[k]
+            np.testing.assert_allclose(named[k[2:]].grad.cpu().numpy(), ref, rtol=2e-3,
+                                       atol=1e-5 * max(float(np.abs(ref).max()), 1e-6), err_msg=k)
+            checked += 1
+    assert checked >= 20
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not has_gpu(), reason="needs GPU")
+def test_greedy_generator_matches_reference(golden):
+    """GreedyGenerator (module/base_seq2seq.py:117-145) through CSATrans.process_data / encode / decode in
+    eval mode: per-step last-position log-probabilities and the generated ids vs the reference
+    (tests/golden/greedy_tiny.npz)."""
+    from types import SimpleNamespace
+
+    from csa_amd.model import CSATrans, GreedyGenerator
+    z = golden("greedy_tiny")
+    seed, max_len = (int(v) for v in z["meta"])
+    m = CSATrans(**TINY)
+    fill_params_deterministic(m, seed)
+    with torch.no_grad():
+        m.generator.linear.weight.mul_(8.0)
+    m = m.cuda().eval()
+    for i in range(2):
+        getattr(m.SBM, f"transformer_{i}").mha.attn.uniforms = torch.from_numpy(z[f"u{i}"]).cuda()
+    c = lambda k, dt: torch.from_numpy(z[k]).to(dt).cuda()
+    data = SimpleNamespace(src_seq=c("src_seq", torch.int64), tgt_seq=None, L=c("L", torch.uint8),
+                           T=c("T", torch.uint8), L_mask=c("L_mask", torch.uint8), T_mask=c("T_mask", torch.uint8))
+    steps = []
+    h = m.generator.register_forward_hook(lambda mod, i, o: steps.append(o[:, -1, :].detach().cpu()))
+    with torch.no_grad():
+        ys = GreedyGenerator(m, max_len)(data)
+    h.remove()
+    np.testing.assert_allclose(torch.stack(steps).numpy(), z["step_logp"], rtol=1e-4, atol=1e-4)
+    np.testing.assert_array_equal(ys.cpu().numpy(), z["ys"])

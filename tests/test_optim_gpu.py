@@ -79,3 +79,36 @@ def test_fused_adamw_under_gradscaler_unscales_and_skips_on_inf():
     scaler.update()
     assert torch.equal(pg.detach(), before) and torch.equal(og.state[pg]["exp_avg"], m_before)
     assert scaler.get_scale() == scale * 0.5
+
+
+def test_fused_adamw_two_param_groups_cache_per_group():
+    """A decay / no-decay split (two param groups): each group keeps its own chunk tables and
+    descriptors, so after the first step no table is rebuilt or re-sent; results match the per-op
+    CPU path."""
+    from csa_amd.train import AdamW
+    g = torch.Generator().manual_seed(8)
+    shapes = [(300, 7), (5000,), (64, 64), (9,)]
+    base = [torch.randn(s, generator=g) for s in shapes]
+    cpu = [torch.nn.Parameter(t.clone()) for t in base]
+    gpu = [torch.nn.Parameter(t.cuda()) for t in base]
+    groups = lambda ps: [{"params": ps[:2], "weight_decay": 0.01}, {"params": ps[2:], "weight_decay": 0.0}]
+    o_cpu = AdamW(groups(cpu), lr=2e-3, correct_bias=False)
+    o_gpu = AdamW(groups(gpu), lr=2e-3, correct_bias=False)
+    seen = None
+    for step in range(3):
+        for pc, pg in zip(cpu, gpu):
+            gr = torch.randn(pc.shape, generator=g)
+            if pg.grad is None:
+                pc.grad, pg.grad = gr.clone(), gr.cuda()
+            else:  # grads stay in place (zero_grad(set_to_none=False) semantics): descriptors reused
+                pc.grad.copy_(gr)
+                pg.grad.copy_(gr.cuda())
+        o_cpu.step()
+        o_gpu.step()
+        now = {k: (id(e["desc"]), id(e["owner"])) for k, e in o_gpu._tables.items()}
+        assert len(now) == 2
+        if seen is not None:
+            assert now == seen
+        seen = now
+    for pc, pg in zip(cpu, gpu):
+        np.testing.assert_allclose(pg.detach().cpu().numpy(), pc.detach().numpy(), rtol=1e-5, atol=1e-7)

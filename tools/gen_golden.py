@@ -7,7 +7,8 @@ re-verifies that this is bit-identical to the real CPU draw), runs forward + bac
 seeded inputs, and writes small ``.npz`` fixtures to tests/golden/. The reference never
 travels to the GPU box; only these fixtures do.
 
-Run:  PYTHONDONTWRITEBYTECODE=1 python tools/gen_golden.py
+Run:  PYTHONDONTWRITEBYTECODE=1 python tools/gen_golden.py [large]
+      (`large` = only the production-shape fixtures: rel_attn_n150_dk64, greedy_tiny, csatrans_java)
 """
 import importlib.util
 import math
@@ -21,7 +22,9 @@ import torch
 REF = "/root/reference"
 OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tests", "golden")
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "code-structure-aware-transformer_amd"))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tests"))
 from csa_amd.data import synthetic_batch  # noqa: E402
+import golden_inputs as gi  # noqa: E402
 
 
 def load_reference():
@@ -376,12 +379,122 @@ def csatrans_case(name, seed):
     print(f"{name}: loss={loss.item():.5f} sparsity={sparsity.item():.5f} keys={len(model.state_dict())}")
 
 
+def rel_attn_large_case(name, B, N, dk, L, seed):
+    """rel_attn at the production head size (d_k = pegen_dim/8 = 64, N = L = 150). Inputs are
+    regenerated from PCG64 (tests/golden_inputs.py:rel_inputs), so only relations and outputs are stored."""
+    H = 8
+    sb, rel, msk = relations(B, N, seed)
+    q, k, v, lq, lk, dO = (torch.from_numpy(a) for a in gi.rel_inputs(B, H, N, dk, L, seed))
+    for t in (q, k, v, lq, lk):
+        t.requires_grad_(True)
+    o = DA.DisentangledAttn.rel_attn(q, k, v, lq, lk, rel, msk)
+    (o * dO).sum().backward()
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), L=sb["L"], T=sb["T"], L_mask=sb["L_mask"],
+                        T_mask=sb["T_mask"], out=np32(o), dq=np32(q.grad), dk=np32(k.grad), dv=np32(v.grad),
+                        dlq=np32(lq.grad), dlk=np32(lk.grad), meta=np.array([B, H, N, dk, L, seed], np.int64))
+    print(f"{name}: ok")
+
+
+def _java_batch(B, N, seed):
+    return synthetic_batch(B, max_size=N, seed=seed, min_nodes=100, max_nodes=N)
+
+
+def csatrans_java_case(name):
+    """CSATrans at config/java.py dims (sbm_enc_dim 768 -> SBM d=96, pe 128, pegen 512 -> CSE d_k=64,
+    N=150, 4 CSE + 4 SBM layers), eval mode, loss + sw*sparsity backward. Weights and STE uniforms are
+    regenerated from PCG64 (tests/golden_inputs.py); the uniforms are moved off fp32 ties with the
+    probability the reference's sampler actually sees, and only those moves are stored."""
+    refmod, Data = load_full_reference_package()
+    s = importlib.util.spec_from_file_location("ref_label_smooth", f"{REF}/utils/label_smooth.py")
+    ls = importlib.util.module_from_spec(s)
+    s.loader.exec_module(ls)
+    torch.manual_seed(gi.JAVA_SEED)
+    model = refmod.CSATrans(**gi.JAVA).eval()
+    gi.fill_params_deterministic(model, gi.JAVA_SEED)
+    B, N = gi.JAVA_B, gi.JAVA_N
+    sb = _java_batch(B, N, gi.JAVA_SEED)
+    f = lambda a: torch.from_numpy(np.asarray(a))
+    data = Data(src_seq=f(sb["src_seq"]), tgt_seq=f(sb["tgt_seq"]), L=f(sb["L"]).float(), T=f(sb["T"]).float(),
+                L_mask=f(sb["L_mask"]), T_mask=f(sb["T_mask"]))
+    nudges = []
+
+    def bern(p):
+        layer = len(nudges)
+        u, idx, val = gi.nudge_uniforms(gi.java_uniforms(layer), p.detach().numpy())
+        nudges.append((idx, val))
+        return (torch.from_numpy(u) < p).to(p.dtype)
+
+    torch.bernoulli = bern
+    try:
+        out, sparsity, src_pe, graphs, attns = model(data)
+    finally:
+        torch.bernoulli = _real_bernoulli
+    assert len(nudges) == 4
+    loss = ls.LabelSmoothing(padding_idx=0, smoothing=0.0)(out, f(sb["target"]))
+    (loss + 1e-2 * sparsity).backward()
+    res = {"out_cols": np32(out[:, :, ::gi.JAVA_OUT_COL_STRIDE]), "sparsity": np.array([sparsity.item()], np.float32),
+           "loss": np.array([loss.item()], np.float32), "out_rowmax": np32(out.max(-1).values),
+           "out_argmax": out.argmax(-1).numpy().astype(np.int32)}
+    for i, (idx, val) in enumerate(nudges):
+        res[f"nudge_idx{i}"], res[f"nudge_val{i}"] = idx, val
+    res["state_keys"] = np.array(sorted(model.state_dict().keys()))
+    for k, p in model.named_parameters():
+        if any(k.startswith(t) for t in gi.JAVA_GRAD_KEYS):
+            res["g:" + k] = np32(p.grad)
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **res)
+    print(f"{name}: loss={loss.item():.5f} sparsity={sparsity.item():.5f} nudged={[len(n[0]) for n in nudges]}"
+          f" grads={sum(k.startswith('g:') for k in res)}")
+
+
+def greedy_tiny_case(name, seed, max_tgt_len=7):
+    """GreedyGenerator (module/base_seq2seq.py:117-145) over the tiny CSATrans in eval mode: process_data,
+    one encode, then max_tgt_len-1 decode + generator + argmax steps (script/train.py:271-282)."""
+    refmod, Data = load_full_reference_package()
+    from module.base_seq2seq import GreedyGenerator
+    kw = dict(src_vocab_size=50, tgt_vocab_size=60, hidden_size=64, num_heads=8, num_layers=1, sbm_layers=2,
+              use_pegen="pegen", dim_feed_forward=128, dropout=0.2, pe_dim=32, pegen_dim=128, sbm_enc_dim=512,
+              clusters=[10, 12], full_att=False)
+    torch.manual_seed(seed)
+    model = refmod.CSATrans(**kw).eval()
+    fill_params_deterministic(model, seed)
+    B, N = 3, 20
+    sb = synthetic_batch(B, max_size=N, seed=seed, min_nodes=12, max_nodes=N, src_vocab=50, tgt_vocab=60,
+                         max_tgt_len=9)
+    f = lambda a: torch.from_numpy(np.asarray(a))
+    data = Data(src_seq=f(sb["src_seq"]), tgt_seq=None, L=f(sb["L"]).float(), T=f(sb["T"]).float(),
+                L_mask=f(sb["L_mask"]), T_mask=f(sb["T_mask"]))
+    g = torch.Generator().manual_seed(seed + 1)
+    us = [torch.rand(B, 8, N, N, generator=g) for _ in range(2)]
+    it = iter(us)
+    with torch.no_grad():  # a spread-out generator so the greedy path is not one repeated token
+        model.generator.linear.weight.mul_(8.0)
+    steps = []
+    hook = model.generator.register_forward_hook(lambda m, i, o: steps.append(o[:, -1, :].clone()))
+    torch.bernoulli = lambda p: (next(it) < p).to(p.dtype)
+    try:
+        with torch.no_grad():
+            ys = GreedyGenerator(model, max_tgt_len)(data)
+    finally:
+        torch.bernoulli = _real_bernoulli
+        hook.remove()
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), src_seq=sb["src_seq"], L=sb["L"], T=sb["T"],
+                        L_mask=sb["L_mask"], T_mask=sb["T_mask"], u0=np32(us[0]), u1=np32(us[1]),
+                        ys=ys.numpy().astype(np.int64), step_logp=np32(torch.stack(steps)),
+                        meta=np.array([seed, max_tgt_len], np.int64))
+    print(f"{name}: ys={ys.tolist()}")
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     torch.set_num_threads(8)
     eq = verify_bernoulli_equivalence()
     print("bernoulli == rand<p (CPU):", eq)
     assert eq, "host-uniform recipe does not reproduce torch.bernoulli"
+    if sys.argv[1:] == ["large"]:  # only the round-2 production-shape fixtures
+        rel_attn_large_case("rel_attn_n150_dk64", B=1, N=150, dk=64, L=150, seed=44)
+        greedy_tiny_case("greedy_tiny", seed=72)
+        csatrans_java_case("csatrans_java")
+        return
     np.savez(os.path.join(OUT, "bernoulli_equivalence.npz"), ok=np.array([eq]))
     sbm_case("sbm_n37", B=2, H=2, N=37, d=64, k=10, pad_counts=[0, 7], seed=11)
     sbm_case("sbm_n1", B=2, H=2, N=1, d=64, k=10, pad_counts=[0, 0], seed=12)
@@ -403,6 +516,10 @@ def main():
     generator_case("generator_v1003", seed=64)
     adamw_case("adamw_nobias", seed=62)
     csatrans_case("csatrans_tiny", seed=71)
+    if True:
+        rel_attn_large_case("rel_attn_n150_dk64", B=1, N=150, dk=64, L=150, seed=44)
+        greedy_tiny_case("greedy_tiny", seed=72)
+        csatrans_java_case("csatrans_java")
 
 
 if __name__ == "__main__":
