@@ -114,6 +114,100 @@ def cpu_baseline(seconds, B=16, H=8, N=150, d=64, k=10):
             "sample": f"{n} oracle fwd+bwd steps of B={B} (H={H},N={N},d={d},k={k}, train mode) in {el:.1f}s"}
 
 
+def cpu_config1(reps=2, B=32, N=150):
+    """BASELINE config 1: the csa_trans_time_memory.py:100-150 protocol on the host cores, restated on
+    the oracle CSATrans (oracle/csatrans_ref.py, pinned to the reference's own CSATrans output):
+    config/python.py dims, B synthetic 150-node ASTs, model.train() (dropouts and STE sampling from
+    torch's CPU generator), three timings -- forward under no_grad; forward + out.mean().backward();
+    LabelSmoothing + sw*sparsity forward + backward (script/train.py:107-109) -- 1 warm-up + `reps`
+    timed passes each (the script runs 20 sweeps of the test loader; bounded here)."""
+    from csa_amd.data import synthetic_batch
+    from csa_amd.model import CONFIGS
+    from oracle import csatrans_ref
+    import platform
+    threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+    torch.set_num_threads(threads)
+    torch.manual_seed(0)
+    cfg = csatrans_ref.config(**CONFIGS["python"])
+    params = {k: v.requires_grad_(True) for k, v in csatrans_ref.init_params(cfg, seed=0).items()}
+    model = csatrans_ref.Model(cfg, params, training=True)
+    sb = synthetic_batch(B, N, seed=1)
+    f = lambda k, dt: torch.as_tensor(sb[k]).to(dt)
+    args = (f("src_seq", torch.int64), f("tgt_seq", torch.int64), f("L", torch.int64), f("T", torch.int64),
+            f("L_mask", torch.bool), f("T_mask", torch.bool))
+    tgt = f("target", torch.int64)
+
+    def zero():
+        for v in params.values():
+            v.grad = None
+
+    def fwd():
+        with torch.no_grad():
+            model.forward(*args)
+
+    def fwd_bwd_mean():
+        zero()
+        out, _ = model.forward(*args)
+        out.mean().backward()
+
+    def train_loss():
+        zero()
+        out, sp = model.forward(*args)
+        (csatrans_ref.label_smoothing(out, tgt) + 1e-2 * sp).backward()
+
+    res = {}
+    for name, fn in (("fwd_no_grad", fwd), ("fwd_bwd_out_mean", fwd_bwd_mean), ("loss_sparsity_fwd_bwd", train_loss)):
+        fn()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        res[name] = round(B * reps / (time.perf_counter() - t0), 2)
+    cpu = platform.processor() or platform.machine()
+    try:
+        with open("/proc/cpuinfo") as fh:
+            cpu = next(ln.split(":", 1)[1].strip() for ln in fh if ln.startswith("model name"))
+    except (OSError, StopIteration):
+        pass
+    return {"unit": "samples/s", "cores": threads, "cpu": cpu, "kind": "port", **res,
+            "sample": f"oracle CSATrans config/python.py, B={B}, N={N}, train mode, 1 warm-up + {reps} timed passes each"}
+
+
+def gpu_config1(dev, reps=10, B=32, N=150):
+    """The same config-1 protocol on the MI355X path (csa_amd.model.CSATrans, config/python.py dims, B=32,
+    train mode), beside cpu_config1: samples/s for fwd (no_grad), fwd + out.mean().backward() and
+    loss + sw*sparsity fwd + bwd."""
+    from csa_amd.data import synthetic_batch
+    from csa_amd.model import CONFIGS, CSATrans, batch_to_device, label_smoothing_loss
+    torch.manual_seed(0)
+    model = CSATrans(**CONFIGS["python"]).to(dev).train()
+    x, y = batch_to_device(synthetic_batch(B, N, seed=1), dev)
+
+    def fwd():
+        with torch.no_grad():
+            model(x)
+
+    def fwd_bwd_mean():
+        model.zero_grad(set_to_none=True)
+        model(x)[0].mean().backward()
+
+    def train_loss():
+        model.zero_grad(set_to_none=True)
+        out, sp = model(x)[:2]
+        (label_smoothing_loss(out, y) + 1e-2 * sp).backward()
+
+    res = {}
+    for name, fn in (("fwd_no_grad", fwd), ("fwd_bwd_out_mean", fwd_bwd_mean), ("loss_sparsity_fwd_bwd", train_loss)):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        res[name] = round(B * reps / (time.perf_counter() - t0), 1)
+    return {"unit": "samples/s", "config": f"config/python.py CSATrans, B={B}, N={N}, train mode", **res}
+
+
 def train_step_bench(world, rank, dev, steps, warmup, config="java", per_gpu_batch=64, nbatches=3):
     """script/train.py:_update (config/java.py dims) under DDP/RCCL; returns samples/s over all ranks."""
     from csa_amd.data import synthetic_batch
@@ -232,6 +326,7 @@ def main():
     ap.add_argument("--eval", action="store_true", help="eval mode (no dropout)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-cpu-config1", action="store_true", help="skip the config-1 CPU CSATrans protocol")
     ap.add_argument("--no-train", action="store_true", help="skip the full train-step measurement")
     ap.add_argument("--train-steps", type=int, default=50)
     ap.add_argument("--train-warmup", type=int, default=20)
@@ -379,8 +474,12 @@ def main():
     }
     if not args.no_train:
         out["train"] = train_step_bench(world, rank, dev, args.train_steps, args.train_warmup)
+        if world == 1:
+            out["config1_gpu"] = gpu_config1(dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, B=16 if N <= 150 else 1, N=N, k=k)
+        if not args.no_cpu_config1:
+            out["cpu_config1"] = cpu_config1()
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

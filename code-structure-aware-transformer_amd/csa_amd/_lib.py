@@ -164,6 +164,8 @@ def lib():
     L.csa_gelu_dropout_bwd.argtypes = [vp, vp, vp, i64, f32, u64, u64, vp]
     L.csa_ast_relations.restype = ctypes.c_int
     L.csa_ast_relations.argtypes = [vp, vp, i64, i64, vp, vp, vp, vp, ctypes.c_int]
+    L.csa_collate_relations.restype = ctypes.c_int
+    L.csa_collate_relations.argtypes = [vp, vp, i64, vp, vp, vp, vp, ctypes.c_int]
     L.csa_adamw_step.restype = ctypes.c_int
     L.csa_adamw_step.argtypes = [ctypes.POINTER(AdamwArgs), vp]
     if L.csa_abi_version() != CSA_ABI_VERSION:
@@ -191,4 +193,5 @@ EXPORTED_SYMBOLS = (
     "csa_bias_grad_workspace_bytes", "csa_bias_grad", "csa_ast_relations",
     "csa_layernorm_supported", "csa_layernorm_bwd_workspace_bytes", "csa_layernorm_fwd", "csa_layernorm_bwd",
     "csa_residual_dropout_fwd", "csa_residual_dropout_bwd", "csa_gelu_dropout_fwd", "csa_gelu_dropout_bwd",
+    "csa_collate_relations",
 )

@@ -103,6 +103,38 @@ def relation_planes(parents, n_nodes, max_size, nthreads=None):
     return L, T, Lm.view(bool), Tm.view(bool)
 
 
+def collect_fn(batch, nthreads=None):
+    """BaseASTDataSet.collect_fn (dataset/base_data_set.py:20-75) for the accelerated path: `batch` is a
+    list of (item, _) with item dicts holding the preprocessed per-AST tensors -- src_seq, tgt_seq,
+    target (equal lengths across the batch), raw fp32 L / T (N, N) from split_matrices.npz, num_node.
+    Returns (namespace, target) like the reference's (Data, target), with the relation planes encoded
+    by the native csa_collate_relations as the uint8 L, T and bool L_mask, T_mask the kernels read
+    (idx = clamp(raw + 75, 0, 149), mask = raw == 0). The ablation-only fields of the reference
+    (adj, tree_pos, triplet) are not on this path and are not collated."""
+    import ctypes
+    import os
+    from types import SimpleNamespace
+
+    import torch
+    from ._lib import check, lib
+    items = [it for it, _ in batch]
+    stack = lambda k: torch.stack([torch.as_tensor(it[k]) for it in items], 0)
+    Lr = stack("L").to(torch.float32).contiguous()
+    Tr = stack("T").to(torch.float32).contiguous()
+    if Lr.shape != Tr.shape:
+        raise ValueError("L and T must have the same shape")
+    outs = [torch.empty(Lr.shape, dtype=torch.uint8) for _ in range(4)]
+    nt = nthreads or min(16, os.cpu_count() or 1)
+    check(lib().csa_collate_relations(ctypes.c_void_p(Lr.data_ptr()), ctypes.c_void_p(Tr.data_ptr()), Lr.numel(),
+                                      *(ctypes.c_void_p(o.data_ptr()) for o in outs), nt), "csa_collate_relations")
+    L, T, Lm, Tm = outs
+    target = stack("target")
+    data = SimpleNamespace(src_seq=stack("src_seq"), tgt_seq=stack("tgt_seq"), target=target, L=L, T=T,
+                           L_mask=Lm.view(torch.bool), T_mask=Tm.view(torch.bool),
+                           num_node=torch.tensor([int(it["num_node"]) for it in items]))
+    return data, target
+
+
 def synthetic_batch(batch, max_size=150, seed=1, min_nodes=None, max_nodes=None, src_vocab=10000,
                     tgt_vocab=20000, max_tgt_len=50, native=True):
     """A batch of synthetic ASTs. Returns a dict of numpy arrays:

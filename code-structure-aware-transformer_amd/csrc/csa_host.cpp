@@ -119,6 +119,41 @@ extern "C" csa_status csa_ast_relations(const int32_t* parent, const int32_t* n_
   return CSA_OK;
 }
 
+// collect_fn's relation encoding (dataset/base_data_set.py:33-36) of already-built raw fp32 L / T
+// matrices (the preprocessed split_matrices.npz format): idx = clamp(raw + 75, 0, 149) as uint8 and
+// mask = (raw == 0), n elements, split over nthreads std::threads. Raw values are integral distances;
+// the float is converted the way torch.clamp(x + 75, 0, 149) then .to(int64) rounds (toward zero).
+extern "C" csa_status csa_collate_relations(const float* L_raw, const float* T_raw, int64_t n, uint8_t* L, uint8_t* T,
+                                            uint8_t* L_mask, uint8_t* T_mask, int nthreads) {
+  if (n < 0 || !L_raw || !T_raw || !L || !T || !L_mask || !T_mask) {
+    csa::set_error("csa_collate_relations: null pointer or negative size");
+    return CSA_INVALID_ARG;
+  }
+  const int nt = nthreads < 1 ? 1 : nthreads;
+  auto enc = [](float raw) -> uint8_t {
+    const float v = raw + (float)REL_OFFSET;
+    const float c = v < 0.f ? 0.f : v > (float)REL_MAX ? (float)REL_MAX : v;
+    return (uint8_t)(int)c;
+  };
+  auto work = [&](int t) {
+    const int64_t lo = n * t / nt, hi = n * (t + 1) / nt;
+    for (int64_t e = lo; e < hi; ++e) {
+      L[e] = enc(L_raw[e]);
+      T[e] = enc(T_raw[e]);
+      L_mask[e] = L_raw[e] == 0.f;
+      T_mask[e] = T_raw[e] == 0.f;
+    }
+  };
+  if (nt == 1 || n < (1 << 16)) {
+    for (int t = 0; t < nt; ++t) work(t);
+  } else {
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t) th.emplace_back(work, t);
+    for (auto& x : th) x.join();
+  }
+  return CSA_OK;
+}
+
 // Build provenance: sha256 of every source and header the library was compiled from, passed in by
 // csa_amd/build.py (-DCSA_SOURCE_HASH). smoke() and the tests compare it with the tree they run in.
 #ifndef CSA_SOURCE_HASH

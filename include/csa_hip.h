@@ -230,6 +230,12 @@ csa_status csa_gelu_dropout_bwd(const float* dy, const float* h, float* dh, int6
 csa_status csa_ast_relations(const int32_t* parent, const int32_t* n_nodes, int64_t B, int64_t max_size, uint8_t* L,
                              uint8_t* T, uint8_t* L_mask, uint8_t* T_mask, int nthreads);
 
+/* collect_fn's encoding (dataset/base_data_set.py:33-36) of raw fp32 relation matrices (any shape, n
+ * elements, e.g. a stacked (B, N, N) batch of split_matrices.npz L / T): idx = clamp(raw + 75, 0, 149),
+ * mask = (raw == 0). Host only; replaces the per-item torch.clamp / eq / stack of the reference. */
+csa_status csa_collate_relations(const float* L_raw, const float* T_raw, int64_t n, uint8_t* L, uint8_t* T,
+                                 uint8_t* L_mask, uint8_t* T_mask, int nthreads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -48,54 +48,66 @@ def cluster_matrix(cluster_weight, num_head, num_clusters):
     return clusters, S
 
 
-def proj_mlp(x, params, keep0=None, keep1=None):
+def proj_mlp(x, params, keep0=None, keep1=None, p=0.0):
     """module/sbm_attn.py:22-30: Linear -> Dropout -> ReLU -> Linear -> Dropout -> ReLU -> Linear.
 
     ``keep0``/``keep1`` are optional pre-scaled dropout multipliers (0 or 1/(1-p)) applied
-    after the first/second Linear (eval mode when None)."""
+    after the first/second Linear (eval mode when None); p > 0 instead draws torch's own dropout
+    (train mode, the reference's RNG use)."""
     h = F.linear(x, params["proj.0.weight"], params["proj.0.bias"])
     if keep0 is not None:
         h = h * keep0
+    elif p > 0.0:
+        h = F.dropout(h, p, True)
     h = F.relu(h)
     h = F.linear(h, params["proj.3.weight"], params["proj.3.bias"])
     if keep1 is not None:
         h = h * keep1
+    elif p > 0.0:
+        h = F.dropout(h, p, True)
     h = F.relu(h)
     return F.linear(h, params["proj.6.weight"], params["proj.6.bias"])
 
 
-def sbm_attention(Q, K, V, mask, params, u, num_clusters, attn_keep=None, proj_keep=None):
+def sbm_attention(Q, K, V, mask, params, u, num_clusters, attn_keep=None, proj_keep=None, attn_p=0.0, proj_p=0.0):
     """module/sbm_attn.py:32-66. Returns (X, sparsity, graph, attn).
 
     Q,K,V: (B,H,N,d) fp32; mask: (B,M) float, 1.0 = padded key; params: dict with the
     reference state_dict keys ('layer.weight', 'proj.*'); u: (B,H,N,M) uniforms.
     attn_keep: optional (B,H,N,M) pre-scaled attention-dropout multiplier (sbm_attn.py:63);
-    proj_keep: optional dict {q0,q1,k0,k1} of pre-scaled proj-dropout multipliers."""
+    proj_keep: optional dict {q0,q1,k0,k1} of pre-scaled proj-dropout multipliers.
+    attn_p / proj_p > 0 (without keep tensors): torch's own dropout draws (train mode)."""
     b, h, n, d = Q.shape
     m = V.shape[2]
     clusters, S = cluster_matrix(params["layer.weight"], h, num_clusters)
     S = S.unsqueeze(0).repeat((b, 1, 1, 1))  # sbm_attn.py:39
     pk = proj_keep or {}
-    Qhat = torch.sigmoid(torch.matmul(proj_mlp(Q, params, pk.get("q0"), pk.get("q1")), clusters.transpose(-1, -2)))
-    Khat = torch.sigmoid(torch.matmul(proj_mlp(K, params, pk.get("k0"), pk.get("k1")), clusters.transpose(-1, -2)))
+    Qhat = torch.sigmoid(torch.matmul(proj_mlp(Q, params, pk.get("q0"), pk.get("q1"), proj_p),
+                                      clusters.transpose(-1, -2)))
+    Khat = torch.sigmoid(torch.matmul(proj_mlp(K, params, pk.get("k0"), pk.get("k1"), proj_p),
+                                      clusters.transpose(-1, -2)))
     expA = torch.matmul(Qhat, torch.matmul(S, Khat.transpose(-1, -2)))  # sbm_attn.py:55
     graph = STESample.apply(expA, u)  # sbm_attn.py:57
     dot = torch.matmul(Q, K.transpose(-2, -1)) / math.sqrt(d)  # sbm_attn.py:59-60
     dot = dot.masked_fill(mask[:, None, None, :] == 1, float("-inf"))  # sbm_attn.py:61
     attn = F.normalize(torch.softmax(dot, dim=-1) * graph, p=1, dim=-1)  # sbm_attn.py:62
     a = attn if attn_keep is None else attn * attn_keep
+    if attn_keep is None and attn_p > 0.0:
+        a = F.dropout(attn, attn_p, True)
     X = torch.matmul(a, V)  # sbm_attn.py:63
     sparsity = torch.sum(graph, dim=(0, -1, -2)) / (b * n * m)  # sbm_attn.py:64
     return X, sparsity, graph, attn
 
 
-def full_attention(Q, K, V, mask, attn_keep=None):
+def full_attention(Q, K, V, mask, attn_keep=None, attn_p=0.0):
     """module/sbm_attn.py:77-87 (dense ablation). Returns (X, None, mask, attn)."""
     d = Q.shape[-1]
     dot = torch.matmul(Q, K.transpose(-2, -1)) / math.sqrt(d)
     dot = dot.masked_fill(mask[:, None, None, :] == 1, float("-inf"))
     attn = F.normalize(torch.softmax(dot, dim=-1), p=1, dim=-1)
     a = attn if attn_keep is None else attn * attn_keep
+    if attn_keep is None and attn_p > 0.0:
+        a = F.dropout(attn, attn_p, True)
     X = torch.matmul(a, V)
     return X, None, mask, attn
 
@@ -111,7 +123,7 @@ def combine_heads(X, num_head, head_dim):
     return X.reshape(X.size(0), X.size(1), num_head * head_dim)
 
 
-def attention_layer(X, mask, params, u, num_head, head_dim, num_clusters, full_att=False):
+def attention_layer(X, mask, params, u, num_head, head_dim, num_clusters, full_att=False, attn_p=0.0, proj_p=0.0):
     """module/sbm_attn.py:113-130 (Attention.forward with attn = SBM or Full).
 
     params holds the Attention state_dict keys: W_q/W_k/W_v/ff .weight/.bias and
@@ -120,9 +132,10 @@ def attention_layer(X, mask, params, u, num_head, head_dim, num_clusters, full_a
     K = split_heads(F.linear(X, params["W_k.weight"], params["W_k.bias"]), num_head, head_dim)
     V = split_heads(F.linear(X, params["W_v.weight"], params["W_v.bias"]), num_head, head_dim)
     if full_att:
-        out, sparsity, graph, attn = full_attention(Q.float(), K.float(), V.float(), mask.float())
+        out, sparsity, graph, attn = full_attention(Q.float(), K.float(), V.float(), mask.float(), attn_p=attn_p)
     else:
         sp = {k[len("attn."):]: v for k, v in params.items() if k.startswith("attn.")}
-        out, sparsity, graph, attn = sbm_attention(Q.float(), K.float(), V.float(), mask.float(), sp, u, num_clusters)
+        out, sparsity, graph, attn = sbm_attention(Q.float(), K.float(), V.float(), mask.float(), sp, u, num_clusters,
+                                                   attn_p=attn_p, proj_p=proj_p)
     out = combine_heads(out, num_head, head_dim)
     return F.linear(out, params["ff.weight"], params["ff.bias"]), sparsity, graph, attn

@@ -60,3 +60,16 @@ def rel_inputs(B, H, N, dk, L, seed):
     rng = np.random.default_rng(seed)
     f = lambda *s: rng.standard_normal(s, dtype=np.float32)
     return f(B, H, N, dk), f(B, H, N, dk), f(B, H, N, dk), f(1, H, L, dk), f(1, H, L, dk), f(B, H, N, dk)
+
+
+def fill_dict_deterministic(shapes, seed):
+    """fill_params_deterministic over a {name: shape} dict (the oracle's parameter dict): same draws in the
+    same sorted-name order as over a model's named_parameters()."""
+    import torch
+    rng = np.random.default_rng(seed)
+    out = {}
+    for k in sorted(shapes):
+        s = tuple(shapes[k])
+        fan = s[-1] if len(s) > 1 else 1
+        out[k] = torch.from_numpy((rng.standard_normal(s) * (0.5 / np.sqrt(fan))).astype(np.float32))
+    return out

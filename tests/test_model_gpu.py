@@ -93,16 +93,32 @@ def test_csatrans_java_dims_match_reference(golden):
     np.testing.assert_allclose(o.max(-1).values.cpu().numpy(), z["out_rowmax"], rtol=1e-4, atol=2e-4)
     np.testing.assert_allclose(sparsity.item(), z["sparsity"][0], rtol=1e-6)  # exact edge counts
     np.testing.assert_allclose(loss.item(), z["loss"][0], rtol=2e-5)
-    (loss + 1e-2 * sparsity).backward()
+    # the train step's backward + optimizer step (script/train.py:109-111): GradScaler (dynamic scale
+    # 2^16, a power of two, so scaled gradients are exact multiples) + the fused AdamW (lr 1e-4,
+    # config/java.py:49, correct_bias=False, script/train.py:80) vs the reference AdamW step
+    from csa_amd.train import AdamW
+    opt = AdamW(m.parameters(), lr=1e-4, correct_bias=False)
+    scaler = torch.amp.GradScaler("cuda")
+    scaler.scale(loss + 1e-2 * sparsity).backward()
+    scale = float(scaler.get_scale())
     named = dict(m.named_parameters())
     checked = 0
     for k in z:
         if k.startswith("g:"):
             ref = z[k]
-            np.testing.assert_allclose(named[k[2:]].grad.cpu().numpy(), ref, rtol=2e-3,
+            np.testing.assert_allclose(named[k[2:]].grad.cpu().numpy() / scale, ref, rtol=2e-3,
                                        atol=1e-5 * max(float(np.abs(ref).max()), 1e-6), err_msg=k)
             checked += 1
     assert checked >= 20
+    scaler.step(opt)
+    scaler.update()
+    stepped = 0
+    for k in z:
+        if k.startswith("p1:"):
+            # first Adam step: p - lr * g / (|g| + eps); gradient errors enter only through |g| ~ eps
+            np.testing.assert_allclose(named[k[3:]].detach().cpu().numpy(), z[k], rtol=1e-6, atol=2e-7, err_msg=k)
+            stepped += 1
+    assert stepped == checked
 
 
 @pytest.mark.gpu

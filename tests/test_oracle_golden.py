@@ -154,3 +154,38 @@ def test_philox_stream_layout():
     assert philox.keep_threshold(0.2) == 13108 and philox.keep_threshold(0.0) == 0
     k = philox.proj_keep(2, 2, 64, 64, seed=123, offset=0, p=0.25, layer=0, is_k=0)
     assert abs(k.mean() - 0.75) < 0.02
+
+
+def test_csatrans_oracle_matches_reference_tiny(golden):
+    """oracle/csatrans_ref.py (the whole model restated over a parameter dict; bench.py's config-1 CPU
+    baseline) vs the reference CSATrans: same state_dict keys, forward log-probabilities, sparsity,
+    loss and parameter gradients (tests/golden/csatrans_tiny.npz)."""
+    import golden_inputs as gi
+    from oracle import csatrans_ref
+    z = golden("csatrans_tiny")
+    cfg = csatrans_ref.config(**TINY_CFG)
+    shapes = csatrans_ref.param_shapes(cfg)
+    ref_keys = [k for k in z["state_keys"] if "orth_clusters" not in k and not k.endswith("pos_emb.pe")]
+    assert sorted(shapes) == sorted(ref_keys)
+    params = {k: v.requires_grad_(True) for k, v in gi.fill_dict_deterministic(shapes, 71).items()}
+    f = lambda k, dt: torch.from_numpy(z[k]).to(dt)
+    model = csatrans_ref.Model(cfg, params, training=False)
+    out, sp = model.forward(f("src_seq", torch.int64), f("tgt_seq", torch.int64), f("L", torch.int64),
+                            f("T", torch.int64), f("L_mask", torch.bool), f("T_mask", torch.bool),
+                            u_list=[f("u0", torch.float32), f("u1", torch.float32)])
+    loss = csatrans_ref.label_smoothing(out, f("target", torch.int64))
+    np.testing.assert_allclose(out.detach().numpy(), z["out"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(sp.item(), z["sparsity"][0], rtol=1e-6)
+    np.testing.assert_allclose(loss.item(), z["loss"][0], rtol=1e-6)
+    (loss + 1e-2 * sp).backward()
+    n = 0
+    for k in z:
+        if k.startswith("g:"):
+            np.testing.assert_allclose(params[k[2:]].grad.numpy(), z[k], rtol=1e-4, atol=1e-6, err_msg=k)
+            n += 1
+    assert n >= 10
+
+
+TINY_CFG = dict(src_vocab_size=50, tgt_vocab_size=60, hidden_size=64, num_heads=8, num_layers=1, sbm_layers=2,
+                use_pegen="pegen", dim_feed_forward=128, dropout=0.2, pe_dim=32, pegen_dim=128, sbm_enc_dim=512,
+                clusters=[10, 12], full_att=False)

@@ -182,3 +182,80 @@ def test_native_relation_planes_reject_malformed_tree():
     par[0, 1:4] = [0, 2, 1]  # node 2's parent 2 is not < 2
     with pytest.raises(CsaError, match="pre-order"):
         relation_planes(par, np.array([4]), 8)
+
+
+def test_native_relation_planes_match_reference_my_ast(golden):
+    """F2 pinned to the reference: csa_ast_relations (native) and the Python restatement vs
+    MyAst.__get_matrices + BaseASTDataSet.collect_fn run on the same trees, including trees longer
+    than max_size (MyAst.__sub_tree truncation) and 1-node trees (tests/golden/ast_relations.npz)."""
+    from csa_amd.data import relation_planes
+    z = golden("ast_relations")
+    L, T, Lm, Tm = relation_planes(z["parents"], z["n_nodes"], 150)
+    np.testing.assert_array_equal(L, z["L"])
+    np.testing.assert_array_equal(T, z["T"])
+    np.testing.assert_array_equal(Lm, z["L_mask"])
+    np.testing.assert_array_equal(Tm, z["T_mask"])
+
+
+def test_native_collect_fn_matches_reference_encoding(golden):
+    """csa_amd.data.collect_fn (native csa_collate_relations) on raw L / T matrices rebuilt from the
+    fixture's trees reproduces the reference collate output bit for bit."""
+    from csa_amd.data import collect_fn, random_tree, relation_matrices  # noqa: F401
+    z = golden("ast_relations")
+    batch = []
+    for b in range(len(z["n_nodes"])):
+        n = int(z["n_nodes"][b])
+        par = z["parents"][b, :n].astype(np.int64)
+        kids = [[] for _ in range(n)]
+        for v in range(1, n):
+            kids[par[v]].append(v)
+        rl, rt = relation_matrices(par, kids, 150)
+        batch.append(({"L": torch.from_numpy(rl), "T": torch.from_numpy(rt), "src_seq": torch.zeros(150, dtype=torch.long),
+                       "tgt_seq": torch.zeros(49, dtype=torch.long), "target": torch.zeros(49, dtype=torch.long),
+                       "num_node": n}, None))
+    data, target = collect_fn(batch)
+    np.testing.assert_array_equal(data.L.numpy(), z["L"])
+    np.testing.assert_array_equal(data.T.numpy(), z["T"])
+    np.testing.assert_array_equal(data.L_mask.numpy(), z["L_mask"])
+    np.testing.assert_array_equal(data.T_mask.numpy(), z["T_mask"])
+    assert data.num_node.tolist() == z["n_nodes"].tolist() and target.shape == (len(batch), 49)
+    # the clamp edges: raw distances beyond +-74 saturate to 0 / 149
+    raw = torch.tensor([[-200.0, -75.0, -74.0, 0.0], [1.0, 74.0, 75.0, 300.0]])
+    d2, _ = collect_fn([({"L": raw, "T": -raw, "src_seq": torch.zeros(1), "tgt_seq": torch.zeros(1),
+                          "target": torch.zeros(1), "num_node": 1}, None)])
+    assert d2.L.tolist() == [[[0, 0, 1, 75], [76, 149, 149, 149]]]
+    assert d2.L_mask.tolist() == [[[False, False, False, True], [False] * 4]]
+
+
+from hypothesis import given, settings  # noqa: E402
+from hypothesis import strategies as st  # noqa: E402
+
+
+@settings(max_examples=40, deadline=None, derandomize=True)
+@given(sizes=st.lists(st.integers(1, 150), min_size=1, max_size=4), max_children=st.integers(1, 9),
+       seed=st.integers(0, 2 ** 31 - 1))
+def test_native_relation_planes_property(sizes, max_children, seed):
+    """csa_ast_relations vs the Python restatement of my_ast.py:198-273 + collate on random trees (any
+    branching, sizes 1..150): bit-exact; L antisymmetric around 75 away from the clamp (|raw| >= 75
+    saturates to 0 / 149, dataset/base_data_set.py:35), diagonal masked."""
+    from csa_amd.data import collate_relations, random_tree, relation_matrices, relation_planes
+    rng = np.random.default_rng(seed)
+    B, N = len(sizes), 150
+    parents = np.full((B, N), -1, np.int32)
+    want = []
+    for b, n in enumerate(sizes):
+        par, kids = random_tree(n, rng, max_children=max_children)
+        parents[b, :n] = par
+        rl, rt = relation_matrices(par, kids, N)
+        want.append((collate_relations(rl), collate_relations(rt)))
+    L, T, Lm, Tm = relation_planes(parents, np.array(sizes, np.int32), N)
+    for b in range(B):
+        (wl, wlm), (wt, wtm) = want[b]
+        np.testing.assert_array_equal(L[b], wl)
+        np.testing.assert_array_equal(T[b], wt)
+        np.testing.assert_array_equal(Lm[b], wlm)
+        np.testing.assert_array_equal(Tm[b], wtm)
+        assert np.all(np.diag(Lm[b])) and np.all(np.diag(Tm[b]))
+        li = L[b].astype(int) - 75
+        inner = (np.abs(li) < 74) & (np.abs(li.T) < 74)
+        np.testing.assert_array_equal(li[inner], -li.T[inner])

@@ -441,6 +441,15 @@ def csatrans_java_case(name):
     for k, p in model.named_parameters():
         if any(k.startswith(t) for t in gi.JAVA_GRAD_KEYS):
             res["g:" + k] = np32(p.grad)
+    # one optimizer step of the train step (script/train.py:80,110: the reference AdamW, lr 1e-4 from
+    # config/java.py:49, correct_bias=False; the GradScaler's power-of-two scale cancels exactly)
+    so = importlib.util.spec_from_file_location("ref_optimizer", f"{REF}/script/optimizer.py")
+    om = importlib.util.module_from_spec(so)
+    so.loader.exec_module(om)
+    om.AdamW(model.parameters(), lr=1e-4, correct_bias=False).step()
+    for k, p in model.named_parameters():
+        if any(k.startswith(t) for t in gi.JAVA_GRAD_KEYS):
+            res["p1:" + k] = np32(p)
     np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **res)
     print(f"{name}: loss={loss.item():.5f} sparsity={sparsity.item():.5f} nudged={[len(n[0]) for n in nudges]}"
           f" grads={sum(k.startswith('g:') for k in res)}")
@@ -484,12 +493,53 @@ def greedy_tiny_case(name, seed, max_tgt_len=7):
     print(f"{name}: ys={ys.tolist()}")
 
 
+def ast_relations_case(name, seed, max_size=150):
+    """F2 host data path pinned to the reference: random pre-order trees -> my_ast.Node trees ->
+    MyAst.__sub_tree (the max_size truncation of __process_treesitter) -> MyAst.__get_matrices
+    (my_ast.py:198-273) -> BaseASTDataSet.collect_fn's L/T encoding (dataset/base_data_set.py:33-36).
+    Stores the parent arrays of the kept pre-order prefix and the collated uint8/bool planes."""
+    refmod, Data = load_full_reference_package()
+    import my_ast
+    from dataset.base_data_set import BaseASTDataSet
+    from csa_amd.data import random_tree
+    rng = np.random.default_rng(seed)
+    sizes = [1, 2, 3, 17, 60, 149, 150, 151, 230, 150, 90, 400]
+    parents = np.full((len(sizes), max_size), -1, np.int32)
+    n_nodes = np.zeros(len(sizes), np.int32)
+    batch = []
+    for b, n in enumerate(sizes):
+        par, kids = random_tree(n, rng, max_children=int(rng.integers(2, 9)))
+        nodes = [my_ast.Node(label=f"nont:n{v}", children=[]) for v in range(n)]
+        for v in range(1, n):
+            nodes[v].parent = nodes[par[v]]
+        for v in range(n):
+            for ci, c in enumerate(kids[v]):
+                nodes[v].children.append(nodes[c])
+                nodes[c].child_idx = ci
+        my_ast.MyAst._MyAst__sub_tree(nodes[0], max_size)
+        _, L, T, *_ = my_ast.MyAst._MyAst__get_matrices(nodes[0], "python", max_size)
+        keep = min(n, max_size)
+        parents[b, :keep] = par[:keep]
+        n_nodes[b] = keep
+        z = torch.zeros(1)
+        batch.append(({"L": L, "T": T, "src_seq": z, "tgt_seq": z, "target": z, "num_node": keep, "adj": z,
+                       "tree_pos": torch.zeros(keep, 2), "triplet": z}, None))
+    data, _ = BaseASTDataSet.collect_fn(None, batch)
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), parents=parents, n_nodes=n_nodes,
+                        L=data.L.numpy().astype(np.uint8), T=data.T.numpy().astype(np.uint8),
+                        L_mask=data.L_mask.numpy(), T_mask=data.T_mask.numpy(), sizes=np.array(sizes, np.int64))
+    print(f"{name}: {len(sizes)} trees, L range {int(data.L.min())}..{int(data.L.max())}")
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     torch.set_num_threads(8)
     eq = verify_bernoulli_equivalence()
     print("bernoulli == rand<p (CPU):", eq)
     assert eq, "host-uniform recipe does not reproduce torch.bernoulli"
+    if sys.argv[1:] == ["ast"]:
+        ast_relations_case("ast_relations", seed=91)
+        return
     if sys.argv[1:] == ["large"]:  # only the round-2 production-shape fixtures
         rel_attn_large_case("rel_attn_n150_dk64", B=1, N=150, dk=64, L=150, seed=44)
         greedy_tiny_case("greedy_tiny", seed=72)
@@ -517,6 +567,7 @@ def main():
     adamw_case("adamw_nobias", seed=62)
     csatrans_case("csatrans_tiny", seed=71)
     if True:
+        ast_relations_case("ast_relations", seed=91)
         rel_attn_large_case("rel_attn_n150_dk64", B=1, N=150, dk=64, L=150, seed=44)
         greedy_tiny_case("greedy_tiny", seed=72)
         csatrans_java_case("csatrans_java")
