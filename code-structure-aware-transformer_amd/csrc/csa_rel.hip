@@ -168,11 +168,31 @@ struct RelArgs {
   // backward
   const float* dout;
   float *dq, *G, *P;
+  // fused path (d_k = 64): prepared planes, plane count, padded size, bins layout, gather-backward output
+  const uint16_t *RM, *RT; int P_, NP, KB2, LB; int64_t ldx;
+  const float* RB;  // tile-major relation bias (written by k_rel_fwd_f)
+  float *dk, *dv, *gc2p, *gp2ct, *qstat;
+  const float *lq, *lk;
 };
 
 __device__ __forceinline__ int64_t plane_off(const RelArgs& p, int b, int hd, int64_t sb, int64_t sh) {
   if (p.group > 0) return b * sb + (hd >= p.group ? 1 : 0) * sh;
   return b * sb + hd * sh;
+}
+
+// A lane's accumulator tiles (rows 32 t + crow(r, h) of one output row) -> out[0 .. 32 DT)
+template <int DT>
+__device__ __forceinline__ void store_rows_f(float* __restrict__ out, const f32x16 (&a)[DT]) {
+  const int h = lane_id() >> 5;
+#pragma unroll
+  for (int t = 0; t < DT; ++t)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      f32x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = a[t][4 * g4 + e];
+      *reinterpret_cast<f32x4*>(out + 32 * t + 8 * g4 + 4 * h) = v;
+    }
 }
 
 // Score of one (x, y) element; returns NEG_INF outside the matrix.
@@ -408,6 +428,560 @@ __global__ __launch_bounds__(64) void k_rel_scatter(const RelArgs p, float* __re
   }
 }
 
+
+// ------------------------------------------------------------------------------------
+// Fused path (d_k = 64): prepared relation planes, LDS-DMA tile images, in-kernel gather backward
+// ------------------------------------------------------------------------------------
+// Prepared planes per (batch element, relation plane), NP = 32 ceil(N/32) rows and columns, uint16:
+//   RM[a][tile_pos(b)] = rel[a][b] | mask[a][b] << 8      RT[a][tile_pos(b)] = rel[b][a] | mask[b][a] << 8
+// Columns are permuted inside each 32-wide tile so that the 16 elements a lane holds in MFMA
+// accumulator registers r = 0..15 of half h (column crow(r, h)) sit at positions 16 h + r: a lane's
+// codes for one tile are 32 contiguous bytes (two dwordx4 loads) of ITS OWN row. The forward (lane =
+// query x) reads rel[x][y] + mask[x][y] from RM and rel[y][x] from RT for its two logit gathers; the
+// query-side backward reads rel[x][y] (its c2p bin) from RM, the key-side backward (lane = key y)
+// rel[y][x] (its p2c bin) from RM -- no byte-wise or transposed access anywhere, and a general
+// (asymmetric) mask stays exact. Entries outside [0,N)^2 hold 0x0100.
+__host__ __device__ constexpr int tile_pos(int j) { return 16 * ((j >> 2) & 1) + (j & 3) + 4 * (j >> 3); }
+
+__global__ __launch_bounds__(256) void k_rel_prep(const RelArgs p, uint16_t* __restrict__ RM, uint16_t* __restrict__ RT) {
+  __shared__ uint16_t tile[32][33];
+  const int NT = p.NP / 32, at = (int)blockIdx.x / NT, bt = (int)blockIdx.x % NT;
+  const int bp = blockIdx.y, b = bp / p.P_, pl = bp % p.P_;
+  const int hd = p.group > 0 ? (pl == 0 ? 0 : p.group) : pl;  // a head that reads plane pl
+  const uint8_t* rp = p.rel + plane_off(p, b, hd, p.rel_sb, p.rel_sh);
+  const uint8_t* mp = p.mask + plane_off(p, b, hd, p.mask_sb, p.mask_sh);
+  uint16_t* rm = RM + (size_t)bp * p.NP * p.NP;
+  uint16_t* rt = RT + (size_t)bp * p.NP * p.NP;
+  for (int e = threadIdx.x; e < 1024; e += 256) {
+    const int al = e >> 5, bl = e & 31, a = at * 32 + al, bb = bt * 32 + bl;
+    uint16_t code = 0x0100;
+    if (a < p.N && bb < p.N) {
+      int r = rp[(int64_t)a * p.N + bb];
+      r = r < p.L ? r : p.L - 1;  // memory safety; the reference requires rel < L
+      code = (uint16_t)(r | (mp[(int64_t)a * p.N + bb] ? 0x100 : 0));
+    }
+    rm[(size_t)a * p.NP + bt * 32 + tile_pos(bl)] = code;
+    tile[al][bl] = code;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < 1024; e += 256) {
+    const int bl = e >> 5, al = e & 31;
+    rt[(size_t)(bt * 32 + bl) * p.NP + at * 32 + tile_pos(al)] = tile[al][bl];
+  }
+}
+
+struct Codes { uint32_t w[8]; };
+// a lane's 16 codes of one tile (32 B of its own prepared row)
+__device__ __forceinline__ Codes load_codes(const uint16_t* __restrict__ row, int tile) {
+  Codes k;
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(row + 32 * tile + 16 * (lane_id() >> 5));
+  const u32x4 a = *reinterpret_cast<const u32x4*>(q), bq = *reinterpret_cast<const u32x4*>(q + 4);
+  k.w[0] = a.x; k.w[1] = a.y; k.w[2] = a.z; k.w[3] = a.w; k.w[4] = bq.x; k.w[5] = bq.y; k.w[6] = bq.z; k.w[7] = bq.w;
+  return k;
+}
+__device__ __forceinline__ uint32_t code_of(const Codes& k, int r) { return (k.w[r >> 1] >> (16 * (r & 1))) & 0xffffu; }
+
+__device__ __forceinline__ const uint16_t* prep_row(const RelArgs& p, const uint16_t* plane, int b, int hd, int row) {
+  const int pl = p.group > 0 ? (hd >= p.group ? 1 : 0) : (p.P_ == 1 ? 0 : hd);
+  return plane + ((size_t)(b * p.P_ + pl) * p.NP + row) * p.NP;
+}
+
+// bins (32 rows x LB floats, LB / 4 odd: the 16 rows of a ds_read_b128 lane group hit 16 distinct
+// 16-B bank slots) += g at column rel, the two lane halves one after the other (they share rows),
+// lanes of a half own distinct rows: no two lanes ever add to one address in the same instruction and
+// a row's additions happen in a fixed order -> deterministic.
+__device__ __forceinline__ void bins_scatter(float* bins, int LB, const float (&g)[16], const uint32_t (&col)[16]) {
+  const int c = lane_id() & 31, h = lane_id() >> 5;
+  float* row = bins + c * LB;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    if (h == pass) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (g[r] != 0.f) atomicAdd(row + col[r], g[r]);
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): pass 0's adds land before pass 1's
+  }
+}
+
+// acc[t] (rows d = 32 t + crow(r,h), lanes = the bins' rows) += sum_r Lmat[r][d] * bins[lane row][r]
+// (dq_rel = G_c2p LK or dk_rel = G_p2cT LQ), K = 2 KB2 (lin perm: k = s + KB2 h), Lmat rows >= L read 0.
+template <int DT>
+__device__ __forceinline__ void bins_times(f32x16 (&acc)[DT], const float* bins, int LB, int KB2,
+                                           const float* __restrict__ Lmat, int L, int D) {
+  const int c = lane_id() & 31, h = lane_id() >> 5;
+  const float* brow = bins + c * LB + KB2 * h;
+  auto lmat = [&](int s4, float (&v)[4][DT]) {  // Lmat rows s4 + e + KB2 h (0 beyond L), columns 32 t + c
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int r = s4 + e + KB2 * h;
+      const float* lr = Lmat + (int64_t)(r < L ? r : 0) * D;
+#pragma unroll
+      for (int t = 0; t < DT; ++t) {
+        const float lv = lr[32 * t + c];
+        v[e][t] = r < L ? lv : 0.f;
+      }
+    }
+  };
+  float lv[2][4][DT];
+  lmat(0, lv[0]);
+  for (int s4 = 0; s4 < KB2; s4 += 8) {  // two groups of 4 K-steps per trip: group g+1's loads fly under g
+    if (s4 + 4 < KB2) lmat(s4 + 4, lv[1]);
+    {
+      const f32x4 bv = *reinterpret_cast<const f32x4*>(brow + s4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int t = 0; t < DT; ++t) acc[t] = mfma(lv[0][e][t], bv[e], acc[t]);
+    }
+    if (s4 + 4 < KB2) {
+      if (s4 + 8 < KB2) lmat(s4 + 8, lv[0]);
+      const f32x4 bv = *reinterpret_cast<const f32x4*>(brow + s4 + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int t = 0; t < DT; ++t) acc[t] = mfma(lv[1][e][t], bv[e], acc[t]);
+    }
+  }
+}
+
+// bins row of this lane (row = lane & 31, the half's columns [KB2 h, KB2 h + KB2) clipped to Lp) -> column
+// `row` of a transposed (Lp, ldx) table: for each bin r the 32 lanes of a half store 32 consecutive
+// floats (coalesced), and the dlq / dlk GEMMs then read it with x contiguous (dwordx4 operand loads).
+__device__ __forceinline__ void bins_store_t(float* __restrict__ outT, int64_t ldx, int row, const float* bins, int LB,
+                                             int KB2, int Lp, bool valid) {
+  if (!valid) return;
+  const int c = lane_id() & 31, h = lane_id() >> 5;
+  const float* brow = bins + c * LB;
+  const int r1 = imin(KB2 * h + KB2, Lp);
+  for (int r = KB2 * h; r < r1; ++r) outT[(int64_t)r * ldx + row] = brow[r];
+}
+
+// Relation logits C2P = Q LK_h^T and P2CT = K LQ_h^T, (B,H,N,Lp) each: one wave per (b,h, 32 rows,
+// table). The wave's 32 rows stay in registers; the 32-row slabs of LK / LQ (L2-resident, shared by
+// the whole batch) come in by LDS-DMA into two SW_ROW images, slab lt+1 in flight while slab lt's 32
+// MFMAs run (per-lane row loads from global would touch 64 cache lines per instruction); stores are
+// coalesced along the relation index.
+template <int D>
+__global__ __launch_bounds__(64) void k_rel_logits(const RelArgs p, float* __restrict__ c2p, float* __restrict__ p2ct) {
+  constexpr int NS = D / 2, IMG = 32 * D * 4;
+  static_assert(D == 64, "fused CSE path is d_k = 64");
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const uint32_t L0 = lds_offset(lds);
+  const int lane = lane_id(), c = lane & 31, h = lane >> 5;
+  const BhBlock xb = xcd_block(2 * p.NQB, p.B * p.H);
+  if (!xb.valid) return;
+  const int which = xb.blk & 1, rb = xb.blk >> 1, bh = xb.bh, b = bh / p.H, hd = bh % p.H;
+  const int x = rb * 32 + c;
+  const int xc = imin(x, p.N - 1);
+  const float* X = which ? p.k + b * p.k_sb + hd * p.k_sh + (int64_t)xc * p.k_sn
+                         : p.q + b * p.q_sb + hd * p.q_sh + (int64_t)xc * p.q_sn;
+  const float* Lm = (which ? p.lq : p.lk) + (int64_t)hd * p.L * D;
+  const __amdgpu_buffer_rsrc_t lr = make_rsrc(Lm, p.L * D * 4);
+  lds_zero<2 * IMG / 4>(lds);
+  const DmaPat pat = dma_pat(SW_ROW, D * 4);
+  dma64(L0, lr, pat, D * 4, 0);
+  float xr[NS];
+  load_run<NS>(xr, X + h * NS, x < p.N);
+  float* out = (which ? p2ct : c2p) + (int64_t)bh * p.N * p.Lp;
+  const int NLT = (p.L + 31) / 32;
+  const int rbase = row_base64(c, h);
+  for (int lt = 0; lt < NLT; ++lt) {
+    const int l = lt * 32 + c;
+    const int cur = lt & 1;
+    wait_vm_all();
+    if (lt + 1 < NLT) dma64(L0 + IMG * (cur ^ 1), lr, pat, D * 4, (lt + 1) * 32);
+    f32x16 acc = zero16();
+#pragma unroll
+    for (int j = 0; j < NS / 4; ++j) {
+      const f32x4 lv = lds_f4(lds, IMG * cur + (rbase ^ (16 * j)));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc = mfma(xr[4 * j + e], lv[e], acc);  // D[x][l]
+    }
+    if (l < p.L) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int xx = rb * 32 + crow(r, h);
+        if (xx < p.N) out[(int64_t)xx * p.Lp + l] = acc[r];
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slab lt read out before it is refilled
+  }
+}
+
+// Tile-major relation bias, written by the forward for the two backward kernels: RB[b,h][qb][kt] is the
+// 32 x 32 tile (query rows x, key columns y) of
+//   c2p[x][rel[x][y]] + p2ct[y][rel[y][x]]      (the reference's two gathers, disentangled_attn.py:55-58)
+// or -inf where mask[x][y] (the -1e9 masked_fill), 0 outside [0,N)^2. Inside a tile, column y sits at
+// tile_pos(y) and the 16-B chunks of row x are XOR-swizzled by (x >> 1) & 7, so a 4 KB tile DMA'd to
+// LDS serves both orientations conflict-free: a query lane's 16 columns (4 ds_read_b128) and a key
+// lane's 16 rows (ds_read_b32).
+__host__ __device__ constexpr int rb_off(int x, int pos) { return x * 32 + 4 * ((pos >> 2) ^ ((x >> 1) & 7)) + (pos & 3); }
+
+// Forward, one wave per (b,h, 32 queries), S^T orientation (keys = accumulator rows, queries = lanes):
+// K (SW_ROW) and V (SW_COL) tile images by LDS-DMA one tile ahead; the relation codes of the next tile
+// prefetched with it; the two logit gathers per element from the L2-resident C2P / P2CT tables.
+template <int D>
+__global__ __launch_bounds__(64, 2) void k_rel_fwd_f(const RelArgs p) {
+  constexpr int DT = D / 32, NS = D / 2, IMG = 32 * D * 4;
+  static_assert(D == 64, "fused CSE path is d_k = 64");
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const uint32_t Kl = lds_offset(lds), Vl = Kl + IMG;
+  const int lane = lane_id(), c = lane & 31, h = lane >> 5;
+  const BhBlock xb = xcd_block(p.NQB, p.B * p.H);
+  if (!xb.valid) return;
+  const int qb = xb.blk, bh = xb.bh, b = bh / p.H, hd = bh % p.H;
+  const int i = qb * 32 + c;
+  const bool iv = i < p.N;
+  const int ic = imin(i, p.N - 1);
+  const int kld = (int)p.k_sn * 4, vld = (int)p.v_sn * 4;
+  const __amdgpu_buffer_rsrc_t kr = make_rsrc(p.k + b * p.k_sb + hd * p.k_sh, (p.N - 1) * kld + D * 4);
+  const __amdgpu_buffer_rsrc_t vr = make_rsrc(p.v + b * p.v_sb + hd * p.v_sh, (p.N - 1) * vld + D * 4);
+  lds_zero<2 * IMG / 4>(lds);
+  const DmaPat kpat = dma_pat(SW_ROW, kld), vpat = dma_pat(SW_COL, vld);
+  const uint16_t* rmrow = prep_row(p, p.RM, b, hd, ic);
+  const uint16_t* rtrow = prep_row(p, p.RT, b, hd, ic);
+  Codes cm = load_codes(rmrow, 0), ct = load_codes(rtrow, 0);
+  float q[NS];
+  load_run<NS>(q, p.q + b * p.q_sb + hd * p.q_sh + (int64_t)ic * p.q_sn + h * NS, iv);
+  dma64(Kl, kr, kpat, kld, 0);
+  dma64(Vl, vr, vpat, vld, 0);
+  const float* c2prow = p.c2p + ((int64_t)bh * p.N + ic) * p.Lp;
+  const float* p2ct = p.p2ct + (int64_t)bh * p.N * p.Lp;
+  // this lane's 16 bias columns of tile kt: row c of the tile, chunk j at byte rboff ^ 16 j
+  char* rbase_g = reinterpret_cast<char*>(const_cast<float*>(p.RB) + ((int64_t)bh * p.NQB + qb) * p.NKB * 1024);
+  const int rboff = 4 * rb_off(c, 16 * h);
+  const int kbase = row_base64(c, h);
+  int vb[DT];
+#pragma unroll
+  for (int t = 0; t < DT; ++t) vb[t] = IMG + col_base64(t, c, h);
+  float m_run = NEG_INF, zp = 0.f;
+  f32x16 o[DT];
+#pragma unroll
+  for (int t = 0; t < DT; ++t) o[t] = zero16();
+  for (int kt = 0; kt < p.NKB; ++kt) {
+    const int j0 = kt * 32;
+    wait_vm_all();  // tile kt's K / V images and its codes have landed
+    // the 32 logit gathers (disentangled_attn.py:55-58) first: their latency runs under the QK^T MFMAs
+    float gl[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const uint32_t a = code_of(cm, r), t2 = code_of(ct, r);
+      const int y = imin(j0 + crow(r, h), p.N - 1);
+      const float v = c2prow[a & 0xffu] + p2ct[(int64_t)y * p.Lp + (t2 & 0xffu)];
+      gl[r] = (a & 0x100u) ? NEG_INF : v;  // the bias table marks masked entries -inf
+    }
+    f32x16 sacc = zero16();
+#pragma unroll
+    for (int j = 0; j < NS / 4; ++j) {
+      const f32x4 kv = lds_f4(lds, kbase ^ (16 * j));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) sacc = mfma(kv[e], q[4 * j + e], sacc);
+    }
+    float vt[DT][16];
+#pragma unroll
+    for (int t = 0; t < DT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) vt[t][r] = lds_f1(lds, vb[t] + 256 * crow(r, 0));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (kt + 1 < p.NKB) {
+      dma64(Kl, kr, kpat, kld, j0 + 32);
+      dma64(Vl, vr, vpat, vld, j0 + 32);
+      cm = load_codes(rmrow, kt + 1);
+      ct = load_codes(rtrow, kt + 1);
+    }
+    // save the gathered bias for the backward kernels (tile-major, 4 x 16 B per lane)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      f32x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = (iv && j0 + crow(4 * j + e, h) < p.N) ? gl[4 * j + e] : 0.f;
+      *reinterpret_cast<f32x4*>(rbase_g + kt * 4096 + (rboff ^ (16 * j))) = v;
+    }
+    float sv[16];
+    float tmax = NEG_INF;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const bool inside = j0 + crow(r, h) < p.N;
+      const float v = (sacc[r] + gl[r]) * p.inv_scale;
+      // masked_fill(mask == 1, -1e9) (disentangled_attn.py:62)
+      sv[r] = !inside ? NEG_INF : (gl[r] == NEG_INF) ? -1e9f : v;
+      tmax = fmaxf(tmax, sv[r]);
+    }
+    tmax = xhalf_max(tmax);
+    const float m_new = fmaxf(m_run, tmax);
+    const float alpha = (m_new == NEG_INF) ? 1.f : __expf(m_run - m_new);
+    zp *= alpha;
+#pragma unroll
+    for (int t = 0; t < DT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
+    float w[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      w[r] = (sv[r] == NEG_INF) ? 0.f : __expf(sv[r] - m_new);
+      zp += w[r];
+    }
+    m_run = m_new;
+#pragma unroll
+    for (int t = 0; t < DT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[t] = mfma(vt[t][r], w[r], o[t]);
+  }
+  const float Z = xhalf_sum(zp);
+  if (iv) {
+    const float inv = 1.f / Z;
+#pragma unroll
+    for (int t = 0; t < DT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[t][r] *= inv;
+    store_rows_f<DT>(p.out + ((int64_t)bh * p.N + i) * D, o);
+    if (h == 0) {
+      p.stats[((int64_t)bh * p.N + i) * 2] = m_run;
+      p.stats[((int64_t)bh * p.N + i) * 2 + 1] = inv;
+    }
+  }
+}
+
+// Backward, query side: one wave per (b,h, 32 queries), S^T orientation. Recomputes P and dP = dO V^T,
+// g = P (dP - delta) / sqrt(3 d) (0 where masked); dq = g K + G_c2p LK with G_c2p[x][r] = sum over y
+// with rel[x][y] = r of g[x][y] accumulated in LDS bins (the gather backward of disentangled_attn.py:58);
+// writes dq, the G_c2p rows (for dlk) and (row max, 1/row sum, delta) per query for the key side.
+template <int D>
+__global__ __launch_bounds__(64, 1) void k_rel_bwd_qf(const RelArgs p) {
+  constexpr int DT = D / 32, NS = D / 2, IMG = 32 * D * 4;
+  static_assert(D == 64, "fused CSE path is d_k = 64");
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const uint32_t Kl = lds_offset(lds), Vl = Kl + IMG, Rl = Kl + 2 * IMG;
+  float* bins = lds + (2 * IMG + 4096) / 4;
+  const int lane = lane_id(), c = lane & 31, h = lane >> 5;
+  const BhBlock xb = xcd_block(p.NQB, p.B * p.H);
+  if (!xb.valid) return;
+  const int qb = xb.blk, bh = xb.bh, b = bh / p.H, hd = bh % p.H;
+  const int i = qb * 32 + c;
+  const bool iv = i < p.N;
+  const int ic = imin(i, p.N - 1);
+  const int kld = (int)p.k_sn * 4, vld = (int)p.v_sn * 4;
+  const __amdgpu_buffer_rsrc_t kr = make_rsrc(p.k + b * p.k_sb + hd * p.k_sh, (p.N - 1) * kld + D * 4);
+  const __amdgpu_buffer_rsrc_t vr = make_rsrc(p.v + b * p.v_sb + hd * p.v_sh, (p.N - 1) * vld + D * 4);
+  const __amdgpu_buffer_rsrc_t rbr = make_rsrc(p.RB + ((int64_t)bh * p.NQB + qb) * p.NKB * 1024, p.NKB * 4096);
+  lds_zero<2 * IMG / 4>(lds);
+  for (int e = lane; e < 32 * p.LB; e += 64) bins[e] = 0.f;
+  const DmaPat kpat = dma_pat(SW_BOTH, kld), vpat = dma_pat(SW_ROW, vld);
+  const uint16_t* rmrow = prep_row(p, p.RM, b, hd, ic);
+  Codes cm = load_codes(rmrow, 0);
+  float q[NS], dO[NS];
+  load_run<NS>(q, p.q + b * p.q_sb + hd * p.q_sh + (int64_t)ic * p.q_sn + h * NS, iv);
+  load_run<NS>(dO, p.dout + ((int64_t)bh * p.N + ic) * D + h * NS, iv);
+  dma64(Kl, kr, kpat, kld, 0);
+  dma64(Vl, vr, vpat, vld, 0);
+  dma_block16<4096>(Rl, rbr, 0);
+  const int rbase = 2 * IMG + rb_off(c, 16 * h) * 4;
+  float dp = 0.f;
+  {
+    float o[NS];
+    load_run<NS>(o, p.out + ((int64_t)bh * p.N + ic) * D + h * NS, iv);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) dp = fmaf(dO[s], o[s], dp);
+  }
+  const float delta = xhalf_sum(dp);
+  const float rmax = p.stats[((int64_t)bh * p.N + ic) * 2];
+  const float rinv = p.stats[((int64_t)bh * p.N + ic) * 2 + 1];
+  f32x16 dq[DT];
+#pragma unroll
+  for (int t = 0; t < DT; ++t) dq[t] = zero16();
+  for (int kt = 0; kt < p.NKB; ++kt) {
+    int ln = threadIdx.x;  // opaque per iteration: keeps the per-row LDS addresses out of the prologue
+    asm volatile("" : "+v"(ln));
+    const int c = ln & 31, h = (ln >> 5) & 1;
+    const int j0 = kt * 32;
+    wait_vm_all();
+    float gl[16];
+    uint32_t col[16];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const f32x4 v = lds_f4(lds, rbase ^ (16 * j));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) gl[4 * j + e] = v[e];
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) col[r] = code_of(cm, r) & 0xffu;  // rel[x][y]: the c2p gather's column
+    f32x16 sacc = zero16(), dpacc = zero16();
+    const int kb = row_base64(c, h, SW_BOTH);
+    const int vbb = IMG + row_base64(c, h, SW_ROW);
+#pragma unroll
+    for (int j = 0; j < NS / 4; ++j) {
+      const f32x4 kv = lds_f4(lds, kb ^ (16 * j));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) sacc = mfma(kv[e], q[4 * j + e], sacc);
+    }
+#pragma unroll
+    for (int j = 0; j < NS / 4; ++j) {
+      const f32x4 vv = lds_f4(lds, vbb ^ (16 * j));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dpacc = mfma(vv[e], dO[4 * j + e], dpacc);
+    }
+    float kT[DT][16];
+#pragma unroll
+    for (int t = 0; t < DT; ++t) {
+      const int tb = both_base64(t, c, h);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) kT[t][r] = both_read(lds, tb, r, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (kt + 1 < p.NKB) {
+      dma64(Kl, kr, kpat, kld, j0 + 32);
+      dma64(Vl, vr, vpat, vld, j0 + 32);
+      dma_block16<4096>(Rl, rbr, (kt + 1) * 4096);
+      cm = load_codes(rmrow, kt + 1);
+    }
+    float gv[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const bool inside = iv && (j0 + crow(r, h) < p.N);
+      const bool msk = gl[r] == NEG_INF;
+      const float s = msk ? -1e9f : (sacc[r] + gl[r]) * p.inv_scale;
+      const float P = inside ? __expf(s - rmax) * rinv : 0.f;
+      gv[r] = (inside && !msk) ? P * (dpacc[r] - delta) * p.inv_scale : 0.f;
+    }
+#pragma unroll
+    for (int t = 0; t < DT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dq[t] = mfma(kT[t][r], gv[r], dq[t]);
+#ifndef CSA_EXP_NOSCATTER
+    bins_scatter(bins, p.LB, gv, col);
+#endif
+  }
+  __syncthreads();
+#ifndef CSA_EXP_NOBT
+  bins_times<DT>(dq, bins, p.LB, p.KB2, p.lk + (int64_t)hd * p.L * D, p.L, D);
+#endif
+  if (iv) {
+    store_rows_f<DT>(p.dq + ((int64_t)bh * p.N + i) * D, dq);
+    if (h == 0) {
+      f32x4 st;
+      st[0] = rmax; st[1] = rinv; st[2] = delta; st[3] = 0.f;
+      *reinterpret_cast<f32x4*>(p.qstat + ((int64_t)bh * p.N + i) * 4) = st;
+    }
+  }
+  bins_store_t(p.gc2p + (int64_t)bh * p.Lp * p.ldx, p.ldx, i, bins, p.LB, p.KB2, p.Lp, iv);
+}
+
+// Backward, key side: one wave per (b,h, 32 keys), S orientation (queries = accumulator rows, keys =
+// lanes); Q and dO tile images (SW_BOTH) and the per-query (max, 1/sum, delta) by LDS-DMA. dv = P^T dO,
+// dk = g^T q + G_p2cT LQ with G_p2cT[y][r] = sum over x with rel[y][x] = r of g[x][y] in LDS bins
+// (the gather backward of disentangled_attn.py:55); writes dk, dv and the G_p2cT rows (for dlq).
+template <int D>
+__global__ __launch_bounds__(64, 1) void k_rel_bwd_kf(const RelArgs p) {
+  constexpr int DT = D / 32, NS = D / 2, IMG = 32 * D * 4;
+  static_assert(D == 64, "fused CSE path is d_k = 64");
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const uint32_t L0 = lds_offset(lds), Ql = L0, Xl = L0 + IMG, Sl = L0 + 2 * IMG, Rl = L0 + 2 * IMG + 512;
+  float* bins = lds + (2 * IMG + 512 + 4096) / 4;
+  const int lane = lane_id(), c = lane & 31, h = lane >> 5;
+  const BhBlock xb = xcd_block(p.NKB, p.B * p.H);
+  if (!xb.valid) return;
+  const int kbi = xb.blk, bh = xb.bh, b = bh / p.H, hd = bh % p.H;
+  const int j = kbi * 32 + c;
+  const bool jv = j < p.N;
+  const int jc = imin(j, p.N - 1);
+  const int qld = (int)p.q_sn * 4;
+  const __amdgpu_buffer_rsrc_t qr_ = make_rsrc(p.q + b * p.q_sb + hd * p.q_sh, (p.N - 1) * qld + D * 4);
+  const __amdgpu_buffer_rsrc_t xr_ = make_rsrc(p.dout + (int64_t)bh * p.N * D, p.N * D * 4);
+  const __amdgpu_buffer_rsrc_t sr_ = make_rsrc(p.qstat + (int64_t)bh * p.N * 4, p.N * 16);
+  // bias tiles (qb, kbi) for qb = 0.. are NKB tiles apart: descriptor over the whole (b,h) table
+  const __amdgpu_buffer_rsrc_t rbr = make_rsrc(p.RB + (int64_t)bh * p.NQB * p.NKB * 1024, p.NQB * p.NKB * 4096);
+  lds_zero<(2 * IMG + 512) / 4>(lds);
+  for (int e = lane; e < 32 * p.LB; e += 64) bins[e] = 0.f;
+  const DmaPat qpat = dma_pat(SW_BOTH, qld), xpat = dma_pat(SW_BOTH, 4 * D);
+  const uint16_t* rmrow = prep_row(p, p.RM, b, hd, jc);
+  Codes cm = load_codes(rmrow, 0);
+  float kr[NS], vr[NS];
+  load_run<NS>(kr, p.k + b * p.k_sb + hd * p.k_sh + (int64_t)jc * p.k_sn + h * NS, jv);
+  load_run<NS>(vr, p.v + b * p.v_sb + hd * p.v_sh + (int64_t)jc * p.v_sn + h * NS, jv);
+  dma64(Ql, qr_, qpat, qld, 0);
+  dma64(Xl, xr_, xpat, 4 * D, 0);
+  dma_tile_contig<4>(Sl, sr_, 0);
+  dma_block16<4096>(Rl, rbr, kbi * 4096);
+  const int rcol = 2 * IMG + 512 + 4 * rb_off(0, tile_pos(c));  // + 128 row: this key's bias in row `row`
+  f32x16 dv[DT], dk[DT];
+#pragma unroll
+  for (int t = 0; t < DT; ++t) { dv[t] = zero16(); dk[t] = zero16(); }
+  for (int qb = 0; qb < p.NQB; ++qb) {
+    int ln = threadIdx.x;
+    asm volatile("" : "+v"(ln));
+    const int c = ln & 31, h = (ln >> 5) & 1;
+    const int i0 = qb * 32;
+    wait_vm_all();
+    float gl[16];
+    uint32_t col[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int x = crow(r, h);  // the row's chunk swizzle depends on x: fold it into the column offset
+      gl[r] = lds_f1(lds, 2 * IMG + 512 + 4 * rb_off(x, tile_pos(c)));
+      col[r] = code_of(cm, r) & 0xffu;  // rel[y][x]: the p2c gather's column
+    }
+    (void)rcol;
+    f32x16 sacc = zero16(), dpacc = zero16();
+    const int qrb = row_base64(c, h, SW_BOTH);
+#pragma unroll
+    for (int s4 = 0; s4 < NS / 4; ++s4) {
+      const f32x4 qv = lds_f4(lds, qrb ^ (16 * s4));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) sacc = mfma(qv[e], kr[4 * s4 + e], sacc);
+    }
+#pragma unroll
+    for (int s4 = 0; s4 < NS / 4; ++s4) {
+      const f32x4 xv = lds_f4(lds, IMG + (qrb ^ (16 * s4)));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dpacc = mfma(xv[e], vr[4 * s4 + e], dpacc);
+    }
+    float Pv[16], gv[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int x = i0 + crow(r, h);
+      const bool inside = (x < p.N) && jv;
+      const f32x4 st = lds_f4(lds, 2 * IMG + 16 * crow(r, h));
+      const bool msk = gl[r] == NEG_INF;
+      const float s = msk ? -1e9f : (sacc[r] + gl[r]) * p.inv_scale;
+      const float P = inside ? __expf(s - st[0]) * st[1] : 0.f;
+      Pv[r] = P;
+      gv[r] = (inside && !msk) ? P * (dpacc[r] - st[2]) * p.inv_scale : 0.f;
+    }
+    int cb[DT];
+#pragma unroll
+    for (int t = 0; t < DT; ++t) cb[t] = both_base64(t, c, h);
+#pragma unroll
+    for (int t = 0; t < DT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dv[t] = mfma(both_read(lds, cb[t], r, IMG), Pv[r], dv[t]);
+#pragma unroll
+    for (int t = 0; t < DT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dk[t] = mfma(both_read(lds, cb[t], r, 0), gv[r], dk[t]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (qb + 1 < p.NQB) {
+      dma64(Ql, qr_, qpat, qld, i0 + 32);
+      dma64(Xl, xr_, xpat, 4 * D, i0 + 32);
+      dma_tile_contig<4>(Sl, sr_, i0 + 32);
+      dma_block16<4096>(Rl, rbr, ((qb + 1) * p.NKB + kbi) * 4096);
+      cm = load_codes(rmrow, qb + 1);
+    }
+#ifndef CSA_EXP_NOSCATTER
+    bins_scatter(bins, p.LB, gv, col);
+#endif
+  }
+  __syncthreads();
+#ifndef CSA_EXP_NOBT
+  bins_times<DT>(dk, bins, p.LB, p.KB2, p.lq + (int64_t)hd * p.L * D, p.L, D);
+#endif
+  if (jv) {
+    store_rows_f<DT>(p.dk + ((int64_t)bh * p.N + j) * D, dk);
+    store_rows_f<DT>(p.dv + ((int64_t)bh * p.N + j) * D, dv);
+  }
+  bins_store_t(p.gp2ct + (int64_t)bh * p.Lp * p.ldx, p.ldx, j, bins, p.LB, p.KB2, p.Lp, jv);
+}
+
 csa_status rfail(csa_status s, const char* m) {
   csa::set_error("%s", m);
   return s;
@@ -436,10 +1010,11 @@ void gemm(hipStream_t st, const GemmArgs& g, int nbat) {
 }
 
 struct RelLayout {
-  int64_t Lp, ldg;
+  int64_t Lp, ldg, NP, ldx;
   int RS;                                    // batch splits of the dlq / dlk reductions
-  size_t c2p, p2ct, state_total;             // forward state
-  size_t G, P, gc2p, gp2ct, part, ws_total;  // backward workspace
+  bool fused;                                // d_k = 64: prepared planes + in-kernel gather backward
+  size_t c2p, p2ct, RM, RT, RB, state_total;  // forward state
+  size_t G, P, gc2p, gp2ct, part, qstat, ws_total;  // backward workspace
 };
 
 inline size_t ral(size_t x) { return (x + 255) & ~size_t(255); }
@@ -452,16 +1027,24 @@ RelLayout rel_layout(int64_t B, int64_t H, int64_t N, int64_t L, int64_t d) {
   R.RS = (int)(B < 16 ? B : 16);
   size_t o = 0;
   auto take = [&](size_t bytes) { size_t r = o; o += ral(bytes); return r; };
+  R.fused = (d == 64);
+  R.NP = ((N + 31) / 32) * 32;
   R.c2p = take(sizeof(float) * B * H * N * R.Lp);
   R.p2ct = take(sizeof(float) * B * H * N * R.Lp);
+  // prepared planes: at most one per head (fewer when heads share planes, e.g. the CSE's 2)
+  R.RM = take(R.fused ? sizeof(uint16_t) * B * H * R.NP * R.NP : 0);
+  R.RT = take(R.fused ? sizeof(uint16_t) * B * H * R.NP * R.NP : 0);
+  R.RB = take(R.fused ? sizeof(float) * B * H * R.NP * R.NP : 0);  // tile-major relation bias
   R.state_total = o;
   o = 0;
   R.ldg = ((N + 3) / 4) * 4;
-  R.G = take(sizeof(float) * B * H * N * R.ldg);
-  R.P = take(sizeof(float) * B * H * N * R.ldg);
-  R.gc2p = take(sizeof(float) * B * H * N * R.Lp);
-  R.gp2ct = take(sizeof(float) * B * H * N * R.Lp);
+  R.G = take(R.fused ? 0 : sizeof(float) * B * H * N * R.ldg);
+  R.P = take(R.fused ? 0 : sizeof(float) * B * H * N * R.ldg);
+  R.ldx = ((N + 3) / 4) * 4;  // fused: G tables stored transposed (B,H,Lp,ldx)
+  R.gc2p = take(R.fused ? sizeof(float) * B * H * R.Lp * R.ldx : sizeof(float) * B * H * N * R.Lp);
+  R.gp2ct = take(R.fused ? sizeof(float) * B * H * R.Lp * R.ldx : sizeof(float) * B * H * N * R.Lp);
   R.part = take(sizeof(float) * R.RS * H * L * d);
+  R.qstat = take(R.fused ? sizeof(float) * B * H * N * 4 : 0);
   R.ws_total = o;
   return R;
 }
@@ -500,8 +1083,21 @@ RelArgs make_rel(const csa_rel_attn_args* a, const RelLayout& R) {
   p.p2ct = (const float*)((char*)ws + R.p2ct);
   p.out = a->out; p.stats = a->row_stats;
   p.inv_scale = 1.f / sqrtf(3.f * (float)a->d);
+  p.lq = a->lq; p.lk = a->lk;
+  if (R.fused) {
+    p.NP = (int)R.NP;
+    p.P_ = a->rel_head_group > 0 ? 2 : (a->rel_sh == 0 && a->mask_sh == 0 ? 1 : (int)a->H);
+    p.RM = (const uint16_t*)((char*)ws + R.RM);
+    p.RT = (const uint16_t*)((char*)ws + R.RT);
+    p.RB = (const float*)((char*)ws + R.RB);
+    p.ldx = R.ldx;
+    p.KB2 = (int)(((a->L + 7) / 8) * 4);  // bins K loop: 2 KB2 >= L, KB2 a multiple of 4
+    p.LB = 2 * p.KB2 + (((2 * p.KB2 / 4) % 2 == 0) ? 4 : 0);  // LB / 4 odd (conflict-free b128 rows)
+  }
   return p;
 }
+
+size_t bins_lds_bytes(const RelArgs& p) { return sizeof(float) * 32 * (size_t)p.LB; }
 
 // relation logits: C2P[b,h] = Q LK_h^T (N x L), P2CT[b,h] = K LQ_h^T (N x L)
 void rel_logits(const csa_rel_attn_args* a, const RelLayout& R, hipStream_t st) {
@@ -517,6 +1113,38 @@ void rel_logits(const csa_rel_attn_args* a, const RelLayout& R, hipStream_t st) 
     g.c_m = R.Lp; g.c_n = 1; g.c_b1 = a->H * a->N * R.Lp; g.c_b2 = a->N * R.Lp;
     g.M = (int)a->N; g.N = (int)a->L; g.K = (int)a->d; g.H2 = (int)a->H; g.R = 1; g.alpha = 1.f; g.accumulate = 0;
     gemm(st, g, (int)(a->B * a->H));
+  }
+}
+
+void rel_param_grads(const csa_rel_attn_args* a, const csa_rel_attn_bwd_args* b, const RelLayout& R, float* gc2p,
+                     float* gp2ct, hipStream_t st) {
+  void* ws = b->workspace;
+  const int B = (int)a->B, H = (int)a->H, N = (int)a->N, L = (int)a->L, D = (int)a->d;
+  const int64_t Lp = R.Lp;
+  // dlk_h = sum_b G_c2p^T Q ; dlq_h = sum_b G_p2cT^T K    (C(m=r, n=dd) = sum_b sum_x G(x,r) X(x,dd))
+  for (int which = 0; which < 2; ++which) {
+    GemmArgs g;
+    memset(&g, 0, sizeof(g));
+    g.A = which == 0 ? gc2p : gp2ct;
+    if (R.fused) {  // (B,H,Lp,ldx): x contiguous
+      g.a_m = R.ldx; g.a_k = 1; g.a_b1 = 0; g.a_b2 = Lp * R.ldx; g.a_r = (int64_t)H * Lp * R.ldx;
+    } else {
+      g.a_m = 1; g.a_k = Lp; g.a_b1 = 0; g.a_b2 = (int64_t)N * Lp; g.a_r = (int64_t)H * N * Lp;
+    }
+    const float* X = which == 0 ? a->q : a->k;
+    g.B = X; g.b_n = 1; g.b_k = which == 0 ? a->q_sn : a->k_sn; g.b_b1 = 0;
+    g.b_b2 = which == 0 ? a->q_sh : a->k_sh; g.b_r = which == 0 ? a->q_sb : a->k_sb;
+    float* part = (float*)((char*)ws + R.part);
+    g.C = R.RS > 1 ? part : (which == 0 ? b->dlk : b->dlq);
+    g.c_m = D; g.c_n = 1; g.c_b1 = 0; g.c_b2 = (int64_t)L * D;
+    g.M = L; g.N = D; g.K = N; g.H2 = H; g.R = B; g.alpha = 1.f; g.accumulate = 0;
+    g.rsplit = R.RS; g.nbat = H; g.c_split = (int64_t)H * L * D;
+    gemm(st, g, H);
+    if (R.RS > 1) {
+      const int64_t n = (int64_t)H * L * D;
+      hipLaunchKernelGGL(k_sum_splits, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part,
+                         which == 0 ? b->dlk : b->dlq, n, R.RS, g.c_split);
+    }
   }
 }
 
@@ -537,9 +1165,18 @@ csa_status csa_rel_attn_fwd(const csa_rel_attn_args* a, void* stream) {
   if (s != CSA_OK) return s;
   const RelLayout R = rel_layout(a->B, a->H, a->N, a->L, a->d);
   hipStream_t st = (hipStream_t)stream;
-  rel_logits(a, R, st);
   RelArgs p = make_rel(a, R);
   const dim3 grid(xcd_grid(p.NQB, (int)(a->B * a->H)));
+  if (R.fused) {
+    hipLaunchKernelGGL(k_rel_logits<64>, dim3(xcd_grid(2 * p.NQB, (int)(a->B * a->H))), dim3(64), 2 * 32 * 64 * 4,
+                       st, p, (float*)p.c2p, (float*)p.p2ct);
+    const int NT = (int)(R.NP / 32);
+    hipLaunchKernelGGL(k_rel_prep, dim3((unsigned)(NT * NT), (unsigned)(a->B * p.P_)), dim3(256), 0, st, p,
+                       (uint16_t*)p.RM, (uint16_t*)p.RT);
+    hipLaunchKernelGGL(k_rel_fwd_f<64>, grid, dim3(64), 2 * 32 * 64 * 4, st, p);
+    return rcheck("csa_rel_attn_fwd");
+  }
+  rel_logits(a, R, st);
   if (a->d == 64) hipLaunchKernelGGL(k_rel_fwd<64>, grid, dim3(64), 0, st, p);
   else if (a->d == 32) hipLaunchKernelGGL(k_rel_fwd<32>, grid, dim3(64), 0, st, p);
   else if (a->d == 16) hipLaunchKernelGGL(k_rel_fwd<16>, grid, dim3(64), 0, st, p);
@@ -563,6 +1200,22 @@ csa_status csa_rel_attn_bwd(const csa_rel_attn_bwd_args* b, void* stream) {
   p.P = (float*)((char*)ws + R.P);
   const int B = (int)a->B, H = (int)a->H, N = (int)a->N, L = (int)a->L, D = (int)a->d;
   const int64_t Lp = R.Lp;
+  float* gc2p = (float*)((char*)ws + R.gc2p);
+  float* gp2ct = (float*)((char*)ws + R.gp2ct);
+  if (R.fused) {
+    p.dk = b->dk; p.dv = b->dv; p.gc2p = gc2p; p.gp2ct = gp2ct;
+    p.qstat = (float*)((char*)ws + R.qstat);
+    const size_t lq_bytes = 2 * 32 * 64 * 4 + 4096 + bins_lds_bytes(p);
+    const size_t lk_bytes = 2 * 32 * 64 * 4 + 512 + 4096 + bins_lds_bytes(p);
+    if (lk_bytes > 64 * 1024) {
+      (void)hipFuncSetAttribute((const void*)k_rel_bwd_qf<64>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lq_bytes);
+      (void)hipFuncSetAttribute((const void*)k_rel_bwd_kf<64>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lk_bytes);
+    }
+    hipLaunchKernelGGL(k_rel_bwd_qf<64>, dim3(xcd_grid(p.NQB, B * H)), dim3(64), lq_bytes, st, p);
+    hipLaunchKernelGGL(k_rel_bwd_kf<64>, dim3(xcd_grid(p.NKB, B * H)), dim3(64), lk_bytes, st, p);
+    rel_param_grads(a, b, R, gc2p, gp2ct, st);
+    return rcheck("csa_rel_attn_bwd");
+  }
   // G^T / P^T: columns x >= N of each row are never written; the GEMMs select zeros there
   const dim3 grid(xcd_grid(p.NQB, B * H));
   if (D == 64) hipLaunchKernelGGL(k_rel_bwd_q<64>, grid, dim3(64), 0, st, p);
@@ -582,8 +1235,6 @@ csa_status csa_rel_attn_bwd(const csa_rel_attn_bwd_args* b, void* stream) {
     gemm(st, g, B * H);
   }
   // gather backward
-  float* gc2p = (float*)((char*)ws + R.gc2p);
-  float* gp2ct = (float*)((char*)ws + R.gp2ct);
   const unsigned nrow = (unsigned)(((int64_t)B * H * N + 63) / 64);
   const size_t lds = sizeof(float) * 64 * Lp;
   (void)hipFuncSetAttribute((const void*)k_rel_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -599,27 +1250,7 @@ csa_status csa_rel_attn_bwd(const csa_rel_attn_bwd_args* b, void* stream) {
     g.M = N; g.N = D; g.K = L; g.H2 = H; g.R = 1; g.alpha = 1.f; g.accumulate = 1;
     gemm(st, g, B * H);
   }
-  // dlk_h = sum_b G_c2p^T Q ; dlq_h = sum_b G_p2cT^T K    (C(m=r, n=dd) = sum_b sum_x G(x,r) X(x,dd))
-  for (int which = 0; which < 2; ++which) {
-    GemmArgs g;
-    memset(&g, 0, sizeof(g));
-    g.A = which == 0 ? gc2p : gp2ct; g.a_m = 1; g.a_k = Lp; g.a_b1 = 0; g.a_b2 = (int64_t)N * Lp;
-    g.a_r = (int64_t)H * N * Lp;
-    const float* X = which == 0 ? a->q : a->k;
-    g.B = X; g.b_n = 1; g.b_k = which == 0 ? a->q_sn : a->k_sn; g.b_b1 = 0;
-    g.b_b2 = which == 0 ? a->q_sh : a->k_sh; g.b_r = which == 0 ? a->q_sb : a->k_sb;
-    float* part = (float*)((char*)ws + R.part);
-    g.C = R.RS > 1 ? part : (which == 0 ? b->dlk : b->dlq);
-    g.c_m = D; g.c_n = 1; g.c_b1 = 0; g.c_b2 = (int64_t)L * D;
-    g.M = L; g.N = D; g.K = N; g.H2 = H; g.R = B; g.alpha = 1.f; g.accumulate = 0;
-    g.rsplit = R.RS; g.nbat = H; g.c_split = (int64_t)H * L * D;
-    gemm(st, g, H);
-    if (R.RS > 1) {
-      const int64_t n = (int64_t)H * L * D;
-      hipLaunchKernelGGL(k_sum_splits, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part,
-                         which == 0 ? b->dlk : b->dlq, n, R.RS, g.c_split);
-    }
-  }
+  rel_param_grads(a, b, R, gc2p, gp2ct, st);
   return rcheck("csa_rel_attn_bwd");
 }
 
