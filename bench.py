@@ -324,6 +324,9 @@ def main():
     ap.add_argument("--clusters", type=int, default=10, help="SBM clusters k (config 5 sweep: 16..128)")
     ap.add_argument("--dense", action="store_true", help="FullAttention ablation (config/python_full_att.py)")
     ap.add_argument("--eval", action="store_true", help="eval mode (no dropout)")
+    ap.add_argument("--precision", choices=("fp32", "bf16"), default="fp32",
+                    help="operand precision of the attention contractions (fp32 = the reference's)")
+    ap.add_argument("--no-bf16-leg", action="store_true", help="skip the bf16-mode side measurement")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cpu-config1", action="store_true", help="skip the config-1 CPU CSATrans protocol")
@@ -351,7 +354,8 @@ def main():
 
     B, H, N, d, k = args.batch, 8, args.seq_len, 64, args.clusters
     torch.manual_seed(1234 + rank)
-    cfg = {"attention_dropout": 0.2, "head_dim": d, "num_head": H, "num_clusters": [k], "return_maps": False}
+    cfg = {"attention_dropout": 0.2, "head_dim": d, "num_head": H, "num_clusters": [k], "return_maps": False,
+           "attn_precision": args.precision}
     mod = (FullAttention(cfg, 0) if args.dense else SBMAttention(cfg, 0)).to(dev)
     for p in mod.parameters():
         if p.dim() > 1:
@@ -459,7 +463,8 @@ def main():
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "ASTs/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "f32", "data": f"synthetic (N(0,1) Q/K/V, {N}-node ASTs, no padding)",
+        "vs_baseline": None, "dtype": "f32" if args.precision == "fp32" else "bf16 MFMA operands, f32 storage/accumulation",
+        "data": f"synthetic (N(0,1) Q/K/V, {N}-node ASTs, no padding)",
         "config": {"workload": "SBMAttention fwd+bwd (config/python.py dims) " + ("dense FullAttention" if args.dense
                    else "SBM") + ("" if N == 150 else f", long-AST stress N={N} k={k}"), "global_batch": B * world, "per_gpu_batch": B, "seq_len": N, "heads": H,
                    "head_dim": d, "clusters": 0 if args.dense else k, "mode": "eval" if args.eval else "train",
@@ -472,6 +477,16 @@ def main():
         "stage_ms": {s: round(v, 4) for s, v in stage_ms.items()},  # untimed profiling pass, all stages
 
     }
+    if args.precision == "fp32" and not args.no_bf16_leg and not args.dense and N <= 150:
+        # the same layer with CSA_DTYPE_BF16 (north_star's bf16 variant): side measurement, same step
+        mod.attn_precision = "bf16"
+        for _ in range(args.warmup):
+            step()
+        el_bf = timed_region(world, dev, args.steps, lambda i: step())
+        mod.attn_precision = "fp32"
+        out["bf16_mode"] = {"value": round(world * B * args.steps / el_bf, 1), "unit": "ASTs/s",
+                            "ms_per_step": round(el_bf * 1000.0 / args.steps, 4),
+                            "note": "QK^T/PV/dP/dQ/dK/dV on bf16 MFMA; projection MLP, expA, sampling fp32"}
     if not args.no_train:
         out["train"] = train_step_bench(world, rank, dev, args.train_steps, args.train_warmup)
         if world == 1:

@@ -11,8 +11,9 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CSA_HIP_LIB", os.path.join(_HERE, "lib", "libcsa_hip.so"))
 
-CSA_ABI_VERSION = 1
+CSA_ABI_VERSION = 2
 CSA_FLAG_DENSE = 1
+CSA_DTYPE_F32, CSA_DTYPE_BF16 = 0, 1
 STATUS = {0: "CSA_OK", 1: "CSA_INVALID_ARG", 2: "CSA_UNSUPPORTED_SHAPE", 3: "CSA_LAUNCH_FAILED"}
 
 i64, u64, u32, f32, vp = ctypes.c_int64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_float, ctypes.c_void_p
@@ -40,7 +41,7 @@ class SbmFwdArgs(ctypes.Structure):
         ("uniforms", vp),
         ("seed", u64), ("offset", u64),
         ("attn_dropout", f32), ("proj_dropout", f32),
-        ("flags", u32),
+        ("flags", u32), ("dtype", u32),
         ("X", vp), ("sparsity", vp), ("state", vp),
         ("prof", ctypes.POINTER(CsaProf)),
     ]
@@ -66,7 +67,7 @@ class RelAttnArgs(ctypes.Structure):
         ("lq", vp), ("lk", vp),
         ("rel", vp), ("rel_sb", i64), ("rel_sh", i64),
         ("mask", vp), ("mask_sb", i64), ("mask_sh", i64),
-        ("rel_head_group", i64),
+        ("rel_head_group", i64), ("dtype", u32),
         ("out", vp), ("row_stats", vp),
         ("state", vp),
     ]

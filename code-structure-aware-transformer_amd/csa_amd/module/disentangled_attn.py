@@ -1,5 +1,7 @@
 """Drop-in DisentangledAttn (module/disentangled_attn.py:11-65): same constructor, forward signature,
-return tuple and state_dict keys; the relation attention runs in torch.ops.csa.rel_attn_*."""
+return tuple and state_dict keys; the relation attention runs in torch.ops.csa.rel_attn_*.
+``module.attn_precision = "bf16"`` runs its c2c / PV contractions and their gradients on bf16 MFMA
+(d_k = 64; default "fp32", the reference's precision)."""
 import copy
 
 import torch
@@ -34,6 +36,7 @@ class DisentangledAttn(nn.Module):
         self.dropout = nn.Dropout(p=dropout)  # unused, as in the reference
         self.l_linear = _get_clones(Linear(d_model, self.d_k * 4), 2)
         self.t_linear = _get_clones(Linear(d_model, self.d_k * 4), 2)
+        self.attn_precision = "fp32"
 
     def forward(self, query, key, value, rel_emb, rel, mask):
         if query is key and key is value:  # self-attention (CSE_layer, csa_trans.py:231-233): one QKV GEMM
@@ -51,7 +54,10 @@ class DisentangledAttn(nn.Module):
         tq, tk = [transpose_for_scores(lin(x), 4) for lin, x in zip(self.t_linear, (t, t))]
         lq = torch.cat([lq, tq], dim=1)  # 1, 8, L, d
         lk = torch.cat([lk, tk], dim=1)
-        output = self.rel_attn(query, key, value, lq, lk, rel, mask)
+        if self.attn_precision == "bf16":
+            output = rel_ops.rel_attn(query, key, value, lq, lk, rel, mask, bf16=True)
+        else:
+            output = self.rel_attn(query, key, value, lq, lk, rel, mask)
         output = output.permute(0, 2, 1, 3).contiguous()
         output = output.view(*(output.size()[:-2] + (-1,)))
         output = self.linear_layers[-1](output)

@@ -10,6 +10,9 @@ Extensions (all default to the reference behaviour):
     False and skip materialising two fp32 N x M tensors per layer.
   * ``module.uniforms``: optional (B,H,N,M) uniforms for the next forward's Bernoulli draws
     (host-supplied-draw parity mode, bit-identical to torch.bernoulli given the same draws).
+  * ``config["attn_precision"]`` / ``module.attn_precision`` (default "fp32", the reference's
+    forced precision, sbm_attn.py:120-126): "bf16" runs QK^T, PV and their gradients on bf16 MFMA
+    (fp32 accumulation; the cluster projection, expA and the sampled graph stay fp32).
 """
 import torch
 import torch.nn as nn
@@ -41,6 +44,7 @@ class SBMAttention(nn.Module):
             nn.Linear(self.head_dim, self.head_dim),
         )
         self.return_maps = config.get("return_maps", True)
+        self.attn_precision = config.get("attn_precision", "fp32")
         self.uniforms = None
 
     def forward(self, Q, K, V, mask):
@@ -54,7 +58,8 @@ class SBMAttention(nn.Module):
             Q, K, V, mask, self.layer.weight,
             [self.proj[0].weight, self.proj[0].bias, self.proj[3].weight, self.proj[3].bias,
              self.proj[6].weight, self.proj[6].bias],
-            k, uniforms=u, attn_p=attn_p, proj_p=proj_p, want_maps=self.return_maps)
+            k, uniforms=u, attn_p=attn_p, proj_p=proj_p, want_maps=self.return_maps,
+            bf16=self.attn_precision == "bf16")
         return X, sparsity, graph, attn
 
 
@@ -66,10 +71,12 @@ class FullAttention(nn.Module):
         self.num_head = config["num_head"]
         self.dropout = nn.Dropout(0.2)
         self.return_maps = config.get("return_maps", True)
+        self.attn_precision = config.get("attn_precision", "fp32")
 
     def forward(self, Q, K, V, mask):
         attn_p = self.drop_attn.p if self.training else 0.0
-        X, _, _, attn = ops.dense_attention(Q, K, V, mask, attn_p=attn_p, want_maps=self.return_maps)
+        X, _, _, attn = ops.dense_attention(Q, K, V, mask, attn_p=attn_p, want_maps=self.return_maps,
+                                            bf16=self.attn_precision == "bf16")
         return X, None, mask, attn  # sbm_attn.py:84-87
 
 

@@ -17,7 +17,7 @@ from typing import List, Optional, Tuple
 import torch
 
 from . import _lib
-from ._lib import CSA_FLAG_DENSE, SbmBwdArgs, SbmFwdArgs, check, lib
+from ._lib import CSA_DTYPE_BF16, CSA_DTYPE_F32, CSA_FLAG_DENSE, SbmBwdArgs, SbmFwdArgs, check, lib
 
 __all__ = ["sbm_attention", "dense_attention", "ste_sample", "ste_backward", "rel_attn", "SBMAttentionFunction"]
 
@@ -54,7 +54,8 @@ def _bhnd(t: torch.Tensor) -> torch.Tensor:
     return t if ok else t.contiguous()
 
 
-def _fwd_struct(Q, K, V, mask, cluster_w, pw, pb, u, seed, offset, attn_p, proj_p, dense, X, sp, state, k):
+def _fwd_struct(Q, K, V, mask, cluster_w, pw, pb, u, seed, offset, attn_p, proj_p, dense, X, sp, state, k,
+                bf16=False):
     B, H, N, d = Q.shape
     M = K.shape[2]
     a = SbmFwdArgs()
@@ -75,6 +76,7 @@ def _fwd_struct(Q, K, V, mask, cluster_w, pw, pb, u, seed, offset, attn_p, proj_
     a.seed, a.offset = seed & (2 ** 64 - 1), offset & (2 ** 64 - 1)
     a.attn_dropout, a.proj_dropout = attn_p, proj_p
     a.flags = CSA_FLAG_DENSE if dense else 0
+    a.dtype = CSA_DTYPE_BF16 if bf16 else CSA_DTYPE_F32
     a.X = X.data_ptr()
     a.state = state.data_ptr()
     return a
@@ -100,9 +102,10 @@ def _prep(Q, K, V, mask, cluster_w, pw, pb, u):
 def sbm_fwd_op(Q: torch.Tensor, K: torch.Tensor, V: torch.Tensor, mask: Optional[torch.Tensor],
                cluster_w: Optional[torch.Tensor], proj_w: List[torch.Tensor], proj_b: List[torch.Tensor],
                uniforms: Optional[torch.Tensor], k: int, seed: int, offset: int, attn_p: float, proj_p: float,
-               dense: bool) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+               dense: bool, bf16: bool = False) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     """Forward of SBMAttention (module/sbm_attn.py:32-66) or FullAttention (:77-87, dense=True).
-    Returns (X (B,H,N,d), sparsity (H,) [empty if dense], state (uint8, saved for backward))."""
+    Returns (X (B,H,N,d), sparsity (H,) [empty if dense], state (uint8, saved for backward)).
+    bf16=True: the N^2 contractions on bf16 MFMA (CSA_DTYPE_BF16; fp32 storage, fp32 expA / sampling)."""
     Q, K, V, mask, cw, pw, pb, u = _prep(Q, K, V, mask, cluster_w, proj_w, proj_b, uniforms)
     B, H, N, d = Q.shape
     M = K.shape[2]
@@ -113,7 +116,7 @@ def sbm_fwd_op(Q: torch.Tensor, K: torch.Tensor, V: torch.Tensor, mask: Optional
     X = torch.empty(B, H, N, d, device=Q.device, dtype=torch.float32)
     sp = torch.empty(0 if dense else H, device=Q.device, dtype=torch.float32)
     state = torch.empty(L.csa_sbm_state_bytes(B, H, N, M, d, k, flags), device=Q.device, dtype=torch.uint8)
-    a = _fwd_struct(Q, K, V, mask, cw, pw, pb, u, seed, offset, attn_p, proj_p, dense, X, sp, state, k)
+    a = _fwd_struct(Q, K, V, mask, cw, pw, pb, u, seed, offset, attn_p, proj_p, dense, X, sp, state, k, bf16)
     if _PROF["fwd"] is not None:
         a.prof = ctypes.pointer(_PROF["fwd"])
     check(L.csa_sbm_fwd(ctypes.byref(a), _stream(Q.device)), "csa_sbm_fwd")
@@ -121,7 +124,7 @@ def sbm_fwd_op(Q: torch.Tensor, K: torch.Tensor, V: torch.Tensor, mask: Optional
 
 
 @sbm_fwd_op.register_fake
-def _(Q, K, V, mask, cluster_w, proj_w, proj_b, uniforms, k, seed, offset, attn_p, proj_p, dense):
+def _(Q, K, V, mask, cluster_w, proj_w, proj_b, uniforms, k, seed, offset, attn_p, proj_p, dense, bf16=False):
     B, H, N, d = Q.shape
     return (Q.new_empty(B, H, N, d), Q.new_empty(0 if dense else H),
             Q.new_empty(lib().csa_sbm_state_bytes(B, H, N, K.shape[2], d, k, CSA_FLAG_DENSE if dense else 0),
@@ -163,7 +166,7 @@ def sbm_bwd_op(Q: torch.Tensor, K: torch.Tensor, V: torch.Tensor, mask: Optional
                cluster_w: Optional[torch.Tensor], proj_w: List[torch.Tensor], proj_b: List[torch.Tensor],
                k: int, attn_p: float, proj_p: float, seed: int, offset: int, dense: bool, state: torch.Tensor,
                X: torch.Tensor, dX: torch.Tensor, dsparsity: Optional[torch.Tensor],
-               dgraph: Optional[torch.Tensor]) -> List[torch.Tensor]:
+               dgraph: Optional[torch.Tensor], bf16: bool = False) -> List[torch.Tensor]:
     """Backward of csa::sbm_fwd. Returns [dQ, dK, dV] (+ [dcluster_w, dW0, db0, dW1, db1, dW2, db2] if not dense)."""
     Q, K, V, mask, cw, pw, pb, _ = _prep(Q, K, V, mask, cluster_w, proj_w, proj_b, None)
     B, H, N, d = Q.shape
@@ -171,7 +174,7 @@ def sbm_bwd_op(Q: torch.Tensor, K: torch.Tensor, V: torch.Tensor, mask: Optional
     L = lib()
     flags = CSA_FLAG_DENSE if dense else 0
     sp = torch.empty(0 if dense else H, device=Q.device, dtype=torch.float32)
-    a = _fwd_struct(Q, K, V, mask, cw, pw, pb, None, seed, offset, attn_p, proj_p, dense, X, sp, state, k)
+    a = _fwd_struct(Q, K, V, mask, cw, pw, pb, None, seed, offset, attn_p, proj_p, dense, X, sp, state, k, bf16)
     dX = dX.float().contiguous()
     dQ = torch.empty(B, H, N, d, device=Q.device, dtype=torch.float32)
     dK = torch.empty(B, H, M, d, device=Q.device, dtype=torch.float32)
@@ -206,7 +209,7 @@ def sbm_bwd_op(Q: torch.Tensor, K: torch.Tensor, V: torch.Tensor, mask: Optional
 
 @sbm_bwd_op.register_fake
 def _(Q, K, V, mask, cluster_w, proj_w, proj_b, k, attn_p, proj_p, seed, offset, dense, state, X, dX, dsparsity,
-      dgraph):
+      dgraph, bf16=False):
     outs = [torch.empty_like(Q), torch.empty_like(K), torch.empty_like(V)]
     if not dense:
         outs.append(torch.empty_like(cluster_w))
@@ -260,24 +263,24 @@ class SBMAttentionFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, Q, K, V, mask, cluster_w, w0, b0, w1, b1, w2, b2, uniforms, k, attn_p, proj_p, dense,
-                want_maps):
+                want_maps, bf16=False):
         seed = _draw_seed()
         pw = [] if dense else [w0, w1, w2]
         pb = [] if dense else [b0, b1, b2]
         X, sp, state = torch.ops.csa.sbm_fwd(Q, K, V, mask, None if dense else cluster_w, pw, pb, uniforms, k, seed, 0,
-                                            attn_p, proj_p, dense)
+                                            attn_p, proj_p, dense, bf16)
         graph = attn = None
         if want_maps:
             graph, attn = torch.ops.csa.sbm_maps(Q, K, V, mask, state, k, dense)
         ctx.save_for_backward(Q, K, V, mask, cluster_w, w0, b0, w1, b1, w2, b2, state, X)
-        ctx.cfg = (k, attn_p, proj_p, seed, dense)
+        ctx.cfg = (k, attn_p, proj_p, seed, dense, bf16)
         ctx.set_materialize_grads(False)
         return X, (sp if not dense else None), graph, attn
 
     @staticmethod
     def backward(ctx, dX, dsp, dgraph, dattn):
         Q, K, V, mask, cluster_w, w0, b0, w1, b1, w2, b2, state, X = ctx.saved_tensors
-        k, attn_p, proj_p, seed, dense = ctx.cfg
+        k, attn_p, proj_p, seed, dense, bf16 = ctx.cfg
         if dattn is not None and bool(torch.any(dattn != 0)):
             raise NotImplementedError("csa: gradients through the returned attn map are not supported; "
                                       "train through X / sparsity (as script/train.py does)")
@@ -286,28 +289,30 @@ class SBMAttentionFunction(torch.autograd.Function):
         pw = [] if dense else [w0, w1, w2]
         pb = [] if dense else [b0, b1, b2]
         g = torch.ops.csa.sbm_bwd(Q, K, V, mask, None if dense else cluster_w, pw, pb, k, attn_p, proj_p, seed, 0,
-                                  dense, state, X, dX, dsp, None if dense else dgraph)
+                                  dense, state, X, dX, dsp, None if dense else dgraph, bf16)
         dQ, dK, dV = g[:3]
         if dense:
-            return dQ, dK, dV, None, None, None, None, None, None, None, None, None, None, None, None, None, None
+            return (dQ, dK, dV) + (None,) * 15
         dC, dw0, db0, dw1, db1, dw2, db2 = g[3:]
-        return dQ, dK, dV, None, dC, dw0, db0, dw1, db1, dw2, db2, None, None, None, None, None, None
+        return dQ, dK, dV, None, dC, dw0, db0, dw1, db1, dw2, db2, None, None, None, None, None, None, None
 
 
-def sbm_attention(Q, K, V, mask, cluster_w, proj, k, uniforms=None, attn_p=0.0, proj_p=0.0, want_maps=True):
+def sbm_attention(Q, K, V, mask, cluster_w, proj, k, uniforms=None, attn_p=0.0, proj_p=0.0, want_maps=True,
+                  bf16=False):
     """Fused SBMAttention.forward (module/sbm_attn.py:32-66) -> (X, sparsity, graph, attn).
 
     proj: [w0, b0, w1, b1, w2, b2] (proj.0/.3/.6). uniforms: optional (B,H,N,M) host-supplied draws
-    (bit-exact parity mode); otherwise in-kernel Philox. graph/attn are None when want_maps=False."""
+    (bit-exact parity mode); otherwise in-kernel Philox. graph/attn are None when want_maps=False.
+    bf16: bf16-MFMA attention contractions (the maps, if requested, are still computed in fp32)."""
     w0, b0, w1, b1, w2, b2 = proj
     return SBMAttentionFunction.apply(Q, K, V, mask, cluster_w, w0, b0, w1, b1, w2, b2, uniforms, int(k),
-                                      float(attn_p), float(proj_p), False, bool(want_maps))
+                                      float(attn_p), float(proj_p), False, bool(want_maps), bool(bf16))
 
 
-def dense_attention(Q, K, V, mask, attn_p=0.0, want_maps=True):
+def dense_attention(Q, K, V, mask, attn_p=0.0, want_maps=True, bf16=False):
     """Fused FullAttention.forward (module/sbm_attn.py:77-87) -> (X, None, graph(unused), attn)."""
     return SBMAttentionFunction.apply(Q, K, V, mask, None, None, None, None, None, None, None, None, 0,
-                                      float(attn_p), 0.0, True, bool(want_maps))
+                                      float(attn_p), 0.0, True, bool(want_maps), bool(bf16))
 
 
 class _STEFunction(torch.autograd.Function):

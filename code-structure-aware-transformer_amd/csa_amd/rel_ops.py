@@ -5,7 +5,7 @@ from typing import List
 
 import torch
 
-from ._lib import RelAttnArgs, RelAttnBwdArgs, check, lib
+from ._lib import CSA_DTYPE_BF16, CSA_DTYPE_F32, RelAttnArgs, RelAttnBwdArgs, check, lib
 from .ops import _bhnd, _require_gpu, _stream
 
 
@@ -28,7 +28,7 @@ def _planes(rel: torch.Tensor, mask: torch.Tensor, H: int):
     return rel, mask, group
 
 
-def _fwd_args(q, k, v, lq, lk, rel, mask, group, out, lse, state):
+def _fwd_args(q, k, v, lq, lk, rel, mask, group, out, lse, state, bf16=False):
     B, H, N, d = q.shape
     a = RelAttnArgs()
     a.B, a.H, a.N, a.L, a.d = B, H, N, lq.shape[1], d
@@ -39,14 +39,15 @@ def _fwd_args(q, k, v, lq, lk, rel, mask, group, out, lse, state):
     a.rel, a.rel_sb, a.rel_sh = rel.data_ptr(), rel.stride(0), rel.stride(1)
     a.mask, a.mask_sb, a.mask_sh = mask.data_ptr(), mask.stride(0), mask.stride(1)
     a.rel_head_group = group
+    a.dtype = CSA_DTYPE_BF16 if bf16 else CSA_DTYPE_F32
     a.out, a.row_stats, a.state = out.data_ptr(), lse.data_ptr(), state.data_ptr()
     return a
 
 
 @torch.library.custom_op("csa::rel_attn_fwd", mutates_args=())
 def rel_attn_fwd_op(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, lq: torch.Tensor, lk: torch.Tensor,
-                    rel: torch.Tensor, mask: torch.Tensor, group: int) -> List[torch.Tensor]:
-    """Returns [out (B,H,N,d), row_stats (B,H,N,2), state (uint8)]."""
+                    rel: torch.Tensor, mask: torch.Tensor, group: int, bf16: bool = False) -> List[torch.Tensor]:
+    """Returns [out (B,H,N,d), row_stats (B,H,N,2), state (uint8)]; bf16 = CSA_DTYPE_BF16 (d_k = 64)."""
     _require_gpu(q, k, v, lq, lk, rel, mask)
     q, k, v = _bhnd(q), _bhnd(k), _bhnd(v)
     lq, lk = lq.float().contiguous(), lk.float().contiguous()
@@ -55,13 +56,13 @@ def rel_attn_fwd_op(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, lq: torch
     out = torch.empty(B, H, N, d, device=q.device, dtype=torch.float32)
     lse = torch.empty(B, H, N, 2, device=q.device, dtype=torch.float32)  # (row max, 1/row sum)
     state = torch.empty(lib().csa_rel_attn_state_bytes(B, H, N, L, d), device=q.device, dtype=torch.uint8)
-    a = _fwd_args(q, k, v, lq, lk, rel, mask, group, out, lse, state)
+    a = _fwd_args(q, k, v, lq, lk, rel, mask, group, out, lse, state, bf16)
     check(lib().csa_rel_attn_fwd(ctypes.byref(a), _stream(q.device)), "csa_rel_attn_fwd")
     return [out, lse, state]
 
 
 @rel_attn_fwd_op.register_fake
-def _(q, k, v, lq, lk, rel, mask, group):
+def _(q, k, v, lq, lk, rel, mask, group, bf16=False):
     B, H, N, d = q.shape
     return [q.new_empty(B, H, N, d), q.new_empty(B, H, N, 2),
             q.new_empty(lib().csa_rel_attn_state_bytes(B, H, N, lq.shape[1], d), dtype=torch.uint8)]
@@ -70,14 +71,14 @@ def _(q, k, v, lq, lk, rel, mask, group):
 @torch.library.custom_op("csa::rel_attn_bwd", mutates_args=())
 def rel_attn_bwd_op(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, lq: torch.Tensor, lk: torch.Tensor,
                     rel: torch.Tensor, mask: torch.Tensor, group: int, out: torch.Tensor, lse: torch.Tensor,
-                    state: torch.Tensor, dout: torch.Tensor) -> List[torch.Tensor]:
+                    state: torch.Tensor, dout: torch.Tensor, bf16: bool = False) -> List[torch.Tensor]:
     """Returns [dq, dk, dv, dlq (H,L,d), dlk (H,L,d)]."""
     q, k, v = _bhnd(q), _bhnd(k), _bhnd(v)
     lq, lk = lq.float().contiguous(), lk.float().contiguous()
     dout = dout.float().contiguous()
     B, H, N, d = q.shape
     L = lq.shape[1]
-    a = _fwd_args(q, k, v, lq, lk, rel, mask, group, out, lse, state)
+    a = _fwd_args(q, k, v, lq, lk, rel, mask, group, out, lse, state, bf16)
     dq, dk, dv = (torch.empty(B, H, N, d, device=q.device, dtype=torch.float32) for _ in range(3))
     dlq, dlk = torch.empty_like(lq), torch.empty_like(lk)
     ws = torch.empty(lib().csa_rel_attn_bwd_workspace_bytes(B, H, N, L, d), device=q.device, dtype=torch.uint8)
@@ -90,26 +91,27 @@ def rel_attn_bwd_op(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, lq: torch
 
 
 @rel_attn_bwd_op.register_fake
-def _(q, k, v, lq, lk, rel, mask, group, out, lse, state, dout):
+def _(q, k, v, lq, lk, rel, mask, group, out, lse, state, dout, bf16=False):
     return [torch.empty_like(q), torch.empty_like(k), torch.empty_like(v), torch.empty_like(lq), torch.empty_like(lk)]
 
 
 class RelAttnFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, q, k, v, lq, lk, rel, mask, group):
-        out, lse, state = torch.ops.csa.rel_attn_fwd(q, k, v, lq, lk, rel, mask, group)
+    def forward(ctx, q, k, v, lq, lk, rel, mask, group, bf16=False):
+        out, lse, state = torch.ops.csa.rel_attn_fwd(q, k, v, lq, lk, rel, mask, group, bf16)
         ctx.save_for_backward(q, k, v, lq, lk, rel, mask, out, lse, state)
-        ctx.group = group
+        ctx.group, ctx.bf16 = group, bf16
         return out
 
     @staticmethod
     def backward(ctx, dout):
         q, k, v, lq, lk, rel, mask, out, lse, state = ctx.saved_tensors
-        dq, dk, dv, dlq, dlk = torch.ops.csa.rel_attn_bwd(q, k, v, lq, lk, rel, mask, ctx.group, out, lse, state, dout)
-        return dq, dk, dv, dlq, dlk, None, None, None
+        dq, dk, dv, dlq, dlk = torch.ops.csa.rel_attn_bwd(q, k, v, lq, lk, rel, mask, ctx.group, out, lse, state, dout,
+                                                          ctx.bf16)
+        return dq, dk, dv, dlq, dlk, None, None, None, None
 
 
-def rel_attn(q, k, v, lq, lk, rel, mask):
+def rel_attn(q, k, v, lq, lk, rel, mask, bf16=False):
     """DisentangledAttn.rel_attn (module/disentangled_attn.py:44-65) on the GPU.
 
     q,k,v (B,H,N,d) (strided views fine); lq,lk (1,H,L,d) or (H,L,d); rel/mask (B,H,N,N) (reference
@@ -118,4 +120,4 @@ def rel_attn(q, k, v, lq, lk, rel, mask):
     rel, mask, group = _planes(rel, mask, H)
     if lq.dim() == 4:
         lq, lk = lq[0], lk[0]
-    return RelAttnFunction.apply(q, k, v, lq, lk, rel, mask, group)
+    return RelAttnFunction.apply(q, k, v, lq, lk, rel, mask, group, bool(bf16))

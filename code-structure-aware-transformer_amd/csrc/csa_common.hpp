@@ -36,6 +36,28 @@ __device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 acc) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
 }
 
+// bf16 mode (CSA_DTYPE_BF16): the N^2 contractions run on v_mfma_f32_32x32x16_bf16 (16x the f32 MFMA
+// rate, fp32 accumulation). One instruction takes 8 consecutive K-steps of the f32 chains above from
+// each lane (lane half h, element j <-> K-step 8 s + j), so a chain keeps its K permutation and both
+// operands stay consistent: f32 operands are rounded to bf16 (RNE, v_cvt_pk_bf16_f32) when packed.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ f32x16 mfma_bf(bf16x8 a, bf16x8 b, f32x16 acc) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+}
+__device__ __forceinline__ bf16x8 pack8(const float* v) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (__bf16)v[j];
+  return r;
+}
+__device__ __forceinline__ bf16x8 pack8(f32x4 a, f32x4 b) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { r[j] = (__bf16)a[j]; r[4 + j] = (__bf16)b[j]; }
+  return r;
+}
+
 __device__ __forceinline__ f32x16 zero16() {
   f32x16 z;
 #pragma unroll

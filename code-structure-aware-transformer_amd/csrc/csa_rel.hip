@@ -171,6 +171,7 @@ struct RelArgs {
   // fused path (d_k = 64): prepared planes, plane count, padded size, bins layout, gather-backward output
   const uint16_t *RM, *RT; int P_, NP, KB2, LB; int64_t ldx;
   const float* RB;  // tile-major relation bias (written by k_rel_fwd_f)
+  int bf16;         // CSA_DTYPE_BF16: bf16 MFMA for c2c, PV and their gradients
   float *dk, *dv, *gc2p, *gp2ct, *qstat;
   const float *lq, *lk;
 };
@@ -621,7 +622,7 @@ __host__ __device__ constexpr int rb_off(int x, int pos) { return x * 32 + 4 * (
 // Forward, one wave per (b,h, 32 queries), S^T orientation (keys = accumulator rows, queries = lanes):
 // K (SW_ROW) and V (SW_COL) tile images by LDS-DMA one tile ahead; the relation codes of the next tile
 // prefetched with it; the two logit gathers per element from the L2-resident C2P / P2CT tables.
-template <int D>
+template <int D, bool BF>
 __global__ __launch_bounds__(64, 2) void k_rel_fwd_f(const RelArgs p) {
   constexpr int DT = D / 32, NS = D / 2, IMG = 32 * D * 4;
   static_assert(D == 64, "fused CSE path is d_k = 64");
@@ -672,11 +673,18 @@ __global__ __launch_bounds__(64, 2) void k_rel_fwd_f(const RelArgs p) {
       gl[r] = (a & 0x100u) ? NEG_INF : v;  // the bias table marks masked entries -inf
     }
     f32x16 sacc = zero16();
+    if constexpr (BF) {
 #pragma unroll
-    for (int j = 0; j < NS / 4; ++j) {
-      const f32x4 kv = lds_f4(lds, kbase ^ (16 * j));
+      for (int j2 = 0; j2 < NS / 8; ++j2)
+        sacc = mfma_bf(pack8(lds_f4(lds, kbase ^ (32 * j2)), lds_f4(lds, kbase ^ (32 * j2 + 16))), pack8(&q[8 * j2]),
+                       sacc);
+    } else {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) sacc = mfma(kv[e], q[4 * j + e], sacc);
+      for (int j = 0; j < NS / 4; ++j) {
+        const f32x4 kv = lds_f4(lds, kbase ^ (16 * j));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sacc = mfma(kv[e], q[4 * j + e], sacc);
+      }
     }
     float vt[DT][16];
 #pragma unroll
@@ -723,10 +731,19 @@ __global__ __launch_bounds__(64, 2) void k_rel_fwd_f(const RelArgs p) {
       zp += w[r];
     }
     m_run = m_new;
+    if constexpr (BF) {
+      const bf16x8 w0 = pack8(&w[0]), w1 = pack8(&w[8]);
 #pragma unroll
-    for (int t = 0; t < DT; ++t)
+      for (int t = 0; t < DT; ++t) {
+        o[t] = mfma_bf(pack8(&vt[t][0]), w0, o[t]);
+        o[t] = mfma_bf(pack8(&vt[t][8]), w1, o[t]);
+      }
+    } else {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) o[t] = mfma(vt[t][r], w[r], o[t]);
+      for (int t = 0; t < DT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[t] = mfma(vt[t][r], w[r], o[t]);
+    }
   }
   const float Z = xhalf_sum(zp);
   if (iv) {
@@ -747,7 +764,7 @@ __global__ __launch_bounds__(64, 2) void k_rel_fwd_f(const RelArgs p) {
 // g = P (dP - delta) / sqrt(3 d) (0 where masked); dq = g K + G_c2p LK with G_c2p[x][r] = sum over y
 // with rel[x][y] = r of g[x][y] accumulated in LDS bins (the gather backward of disentangled_attn.py:58);
 // writes dq, the G_c2p rows (for dlk) and (row max, 1/row sum, delta) per query for the key side.
-template <int D>
+template <int D, bool BF>
 __global__ __launch_bounds__(64, 1) void k_rel_bwd_qf(const RelArgs p) {
   constexpr int DT = D / 32, NS = D / 2, IMG = 32 * D * 4;
   static_assert(D == 64, "fused CSE path is d_k = 64");
@@ -809,17 +826,26 @@ __global__ __launch_bounds__(64, 1) void k_rel_bwd_qf(const RelArgs p) {
     f32x16 sacc = zero16(), dpacc = zero16();
     const int kb = row_base64(c, h, SW_BOTH);
     const int vbb = IMG + row_base64(c, h, SW_ROW);
+    if constexpr (BF) {
 #pragma unroll
-    for (int j = 0; j < NS / 4; ++j) {
-      const f32x4 kv = lds_f4(lds, kb ^ (16 * j));
+      for (int j2 = 0; j2 < NS / 8; ++j2) {
+        sacc = mfma_bf(pack8(lds_f4(lds, kb ^ (32 * j2)), lds_f4(lds, kb ^ (32 * j2 + 16))), pack8(&q[8 * j2]), sacc);
+        dpacc = mfma_bf(pack8(lds_f4(lds, vbb ^ (32 * j2)), lds_f4(lds, vbb ^ (32 * j2 + 16))), pack8(&dO[8 * j2]),
+                        dpacc);
+      }
+    } else {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) sacc = mfma(kv[e], q[4 * j + e], sacc);
-    }
+      for (int j = 0; j < NS / 4; ++j) {
+        const f32x4 kv = lds_f4(lds, kb ^ (16 * j));
 #pragma unroll
-    for (int j = 0; j < NS / 4; ++j) {
-      const f32x4 vv = lds_f4(lds, vbb ^ (16 * j));
+        for (int e = 0; e < 4; ++e) sacc = mfma(kv[e], q[4 * j + e], sacc);
+      }
 #pragma unroll
-      for (int e = 0; e < 4; ++e) dpacc = mfma(vv[e], dO[4 * j + e], dpacc);
+      for (int j = 0; j < NS / 4; ++j) {
+        const f32x4 vv = lds_f4(lds, vbb ^ (16 * j));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dpacc = mfma(vv[e], dO[4 * j + e], dpacc);
+      }
     }
     float kT[DT][16];
 #pragma unroll
@@ -844,10 +870,19 @@ __global__ __launch_bounds__(64, 1) void k_rel_bwd_qf(const RelArgs p) {
       const float P = inside ? __expf(s - rmax) * rinv : 0.f;
       gv[r] = (inside && !msk) ? P * (dpacc[r] - delta) * p.inv_scale : 0.f;
     }
+    if constexpr (BF) {
+      const bf16x8 g0 = pack8(&gv[0]), g1 = pack8(&gv[8]);
 #pragma unroll
-    for (int t = 0; t < DT; ++t)
+      for (int t = 0; t < DT; ++t) {
+        dq[t] = mfma_bf(pack8(&kT[t][0]), g0, dq[t]);
+        dq[t] = mfma_bf(pack8(&kT[t][8]), g1, dq[t]);
+      }
+    } else {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) dq[t] = mfma(kT[t][r], gv[r], dq[t]);
+      for (int t = 0; t < DT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dq[t] = mfma(kT[t][r], gv[r], dq[t]);
+    }
 #ifndef CSA_EXP_NOSCATTER
     bins_scatter(bins, p.LB, gv, col);
 #endif
@@ -871,7 +906,7 @@ __global__ __launch_bounds__(64, 1) void k_rel_bwd_qf(const RelArgs p) {
 // lanes); Q and dO tile images (SW_BOTH) and the per-query (max, 1/sum, delta) by LDS-DMA. dv = P^T dO,
 // dk = g^T q + G_p2cT LQ with G_p2cT[y][r] = sum over x with rel[y][x] = r of g[x][y] in LDS bins
 // (the gather backward of disentangled_attn.py:55); writes dk, dv and the G_p2cT rows (for dlq).
-template <int D>
+template <int D, bool BF>
 __global__ __launch_bounds__(64, 1) void k_rel_bwd_kf(const RelArgs p) {
   constexpr int DT = D / 32, NS = D / 2, IMG = 32 * D * 4;
   static_assert(D == 64, "fused CSE path is d_k = 64");
@@ -924,17 +959,27 @@ __global__ __launch_bounds__(64, 1) void k_rel_bwd_kf(const RelArgs p) {
     (void)rcol;
     f32x16 sacc = zero16(), dpacc = zero16();
     const int qrb = row_base64(c, h, SW_BOTH);
+    if constexpr (BF) {
 #pragma unroll
-    for (int s4 = 0; s4 < NS / 4; ++s4) {
-      const f32x4 qv = lds_f4(lds, qrb ^ (16 * s4));
+      for (int j2 = 0; j2 < NS / 8; ++j2) {
+        sacc = mfma_bf(pack8(lds_f4(lds, qrb ^ (32 * j2)), lds_f4(lds, qrb ^ (32 * j2 + 16))), pack8(&kr[8 * j2]),
+                       sacc);
+        dpacc = mfma_bf(pack8(lds_f4(lds, IMG + (qrb ^ (32 * j2))), lds_f4(lds, IMG + (qrb ^ (32 * j2 + 16)))),
+                        pack8(&vr[8 * j2]), dpacc);
+      }
+    } else {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) sacc = mfma(qv[e], kr[4 * s4 + e], sacc);
-    }
+      for (int s4 = 0; s4 < NS / 4; ++s4) {
+        const f32x4 qv = lds_f4(lds, qrb ^ (16 * s4));
 #pragma unroll
-    for (int s4 = 0; s4 < NS / 4; ++s4) {
-      const f32x4 xv = lds_f4(lds, IMG + (qrb ^ (16 * s4)));
+        for (int e = 0; e < 4; ++e) sacc = mfma(qv[e], kr[4 * s4 + e], sacc);
+      }
 #pragma unroll
-      for (int e = 0; e < 4; ++e) dpacc = mfma(xv[e], vr[4 * s4 + e], dpacc);
+      for (int s4 = 0; s4 < NS / 4; ++s4) {
+        const f32x4 xv = lds_f4(lds, IMG + (qrb ^ (16 * s4)));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dpacc = mfma(xv[e], vr[4 * s4 + e], dpacc);
+      }
     }
     float Pv[16], gv[16];
 #pragma unroll
@@ -951,14 +996,28 @@ __global__ __launch_bounds__(64, 1) void k_rel_bwd_kf(const RelArgs p) {
     int cb[DT];
 #pragma unroll
     for (int t = 0; t < DT; ++t) cb[t] = both_base64(t, c, h);
+    if constexpr (BF) {
+      const bf16x8 p0 = pack8(&Pv[0]), p1 = pack8(&Pv[8]), g0 = pack8(&gv[0]), g1 = pack8(&gv[8]);
 #pragma unroll
-    for (int t = 0; t < DT; ++t)
+      for (int t = 0; t < DT; ++t) {
+        float xc[16], qc[16];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) dv[t] = mfma(both_read(lds, cb[t], r, IMG), Pv[r], dv[t]);
+        for (int r = 0; r < 16; ++r) { xc[r] = both_read(lds, cb[t], r, IMG); qc[r] = both_read(lds, cb[t], r, 0); }
+        dv[t] = mfma_bf(pack8(&xc[0]), p0, dv[t]);
+        dv[t] = mfma_bf(pack8(&xc[8]), p1, dv[t]);
+        dk[t] = mfma_bf(pack8(&qc[0]), g0, dk[t]);
+        dk[t] = mfma_bf(pack8(&qc[8]), g1, dk[t]);
+      }
+    } else {
 #pragma unroll
-    for (int t = 0; t < DT; ++t)
+      for (int t = 0; t < DT; ++t)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) dk[t] = mfma(both_read(lds, cb[t], r, 0), gv[r], dk[t]);
+        for (int r = 0; r < 16; ++r) dv[t] = mfma(both_read(lds, cb[t], r, IMG), Pv[r], dv[t]);
+#pragma unroll
+      for (int t = 0; t < DT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dk[t] = mfma(both_read(lds, cb[t], r, 0), gv[r], dk[t]);
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (qb + 1 < p.NQB) {
       dma64(Ql, qr_, qpat, qld, i0 + 32);
@@ -1058,6 +1117,8 @@ csa_status validate_rel(const csa_rel_attn_args* a) {
   if (!a->q || !a->k || !a->v || !a->lq || !a->lk || !a->rel || !a->mask || !a->out || !a->row_stats || !a->state)
     return rfail(CSA_INVALID_ARG, "null pointer");
   if (a->rel_head_group < 0 || a->rel_head_group > a->H) return rfail(CSA_INVALID_ARG, "bad rel_head_group");
+  if (a->dtype != CSA_DTYPE_F32 && a->dtype != CSA_DTYPE_BF16) return rfail(CSA_INVALID_ARG, "bad dtype");
+  if (a->dtype == CSA_DTYPE_BF16 && a->d != 64) return rfail(CSA_UNSUPPORTED_SHAPE, "bf16 CSE needs d_k = 64");
   auto al16 = [](const void* ptr, int64_t sb, int64_t sh, int64_t sn) {
     return (((uintptr_t)ptr) % 16 == 0) && sb % 4 == 0 && sh % 4 == 0 && sn % 4 == 0;
   };
@@ -1084,6 +1145,7 @@ RelArgs make_rel(const csa_rel_attn_args* a, const RelLayout& R) {
   p.out = a->out; p.stats = a->row_stats;
   p.inv_scale = 1.f / sqrtf(3.f * (float)a->d);
   p.lq = a->lq; p.lk = a->lk;
+  p.bf16 = a->dtype == CSA_DTYPE_BF16;
   if (R.fused) {
     p.NP = (int)R.NP;
     p.P_ = a->rel_head_group > 0 ? 2 : (a->rel_sh == 0 && a->mask_sh == 0 ? 1 : (int)a->H);
@@ -1173,7 +1235,8 @@ csa_status csa_rel_attn_fwd(const csa_rel_attn_args* a, void* stream) {
     const int NT = (int)(R.NP / 32);
     hipLaunchKernelGGL(k_rel_prep, dim3((unsigned)(NT * NT), (unsigned)(a->B * p.P_)), dim3(256), 0, st, p,
                        (uint16_t*)p.RM, (uint16_t*)p.RT);
-    hipLaunchKernelGGL(k_rel_fwd_f<64>, grid, dim3(64), 2 * 32 * 64 * 4, st, p);
+    if (p.bf16) hipLaunchKernelGGL((k_rel_fwd_f<64, true>), grid, dim3(64), 2 * 32 * 64 * 4, st, p);
+    else hipLaunchKernelGGL((k_rel_fwd_f<64, false>), grid, dim3(64), 2 * 32 * 64 * 4, st, p);
     return rcheck("csa_rel_attn_fwd");
   }
   rel_logits(a, R, st);
@@ -1207,12 +1270,14 @@ csa_status csa_rel_attn_bwd(const csa_rel_attn_bwd_args* b, void* stream) {
     p.qstat = (float*)((char*)ws + R.qstat);
     const size_t lq_bytes = 2 * 32 * 64 * 4 + 4096 + bins_lds_bytes(p);
     const size_t lk_bytes = 2 * 32 * 64 * 4 + 512 + 4096 + bins_lds_bytes(p);
-    if (lk_bytes > 64 * 1024) {
-      (void)hipFuncSetAttribute((const void*)k_rel_bwd_qf<64>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lq_bytes);
-      (void)hipFuncSetAttribute((const void*)k_rel_bwd_kf<64>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lk_bytes);
+    const dim3 gq(xcd_grid(p.NQB, B * H)), gk(xcd_grid(p.NKB, B * H));
+    if (p.bf16) {
+      hipLaunchKernelGGL((k_rel_bwd_qf<64, true>), gq, dim3(64), lq_bytes, st, p);
+      hipLaunchKernelGGL((k_rel_bwd_kf<64, true>), gk, dim3(64), lk_bytes, st, p);
+    } else {
+      hipLaunchKernelGGL((k_rel_bwd_qf<64, false>), gq, dim3(64), lq_bytes, st, p);
+      hipLaunchKernelGGL((k_rel_bwd_kf<64, false>), gk, dim3(64), lk_bytes, st, p);
     }
-    hipLaunchKernelGGL(k_rel_bwd_qf<64>, dim3(xcd_grid(p.NQB, B * H)), dim3(64), lq_bytes, st, p);
-    hipLaunchKernelGGL(k_rel_bwd_kf<64>, dim3(xcd_grid(p.NKB, B * H)), dim3(64), lk_bytes, st, p);
     rel_param_grads(a, b, R, gc2p, gp2ct, st);
     return rcheck("csa_rel_attn_bwd");
   }

@@ -256,6 +256,7 @@ struct KArgs {
   uint32_t seed_lo, seed_hi, off;
   float attn_p, proj_p, scale;
   uint32_t drop_thr, pdrop_thr;  // 16-bit keep thresholds: keep <=> u16 >= thr (thr = ceil(p * 65536))
+  int bf16;                      // CSA_DTYPE_BF16: bf16 MFMA for the N^2 contractions (wave-uniform branch)
   // outputs
   float* X;
   // backward
@@ -590,7 +591,7 @@ __device__ __forceinline__ void key_bias_store(float* bias, const KArgs& p, int 
 // DROP: attention dropout on (keep <=> 16-bit uniform >= drop_thr). HAS_U: STE uniforms supplied by
 // the caller (bit-exact parity path, fp32 compare as torch.bernoulli); otherwise 16-bit Philox
 // uniforms u16 / 65536 (STE.py:13 draws u < p with p = clamp(expA, .01, .99)).
-template <int D, int KPH, bool DENSE, bool HAS_U, bool DROP>
+template <int D, int KPH, bool DENSE, bool HAS_U, bool DROP, bool BF>
 __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd(const KArgs p) {
   using LY = AttnFwdLds<D, KPH>;
   constexpr int DT = D / 32, NS = D / 2, DP = LY::DP, KP = LY::KP;
@@ -654,11 +655,20 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd
     wait_vm_all();  // tile kt's K/V/T images have landed
     // S^T = K Q^T : A operand = K rows from the image (row c, lin-perm chunks of half h)
     f32x16 sacc = zero16();
+    if constexpr (BF) {
 #pragma unroll
-    for (int j = 0; j < NS / 4; ++j) {
-      const f32x4 kv = lds_f4(lds, SWZ ? (kbase ^ (16 * j)) : kbase + 16 * j);
+      for (int j2 = 0; j2 < NS / 8; ++j2) {
+        const f32x4 k0 = lds_f4(lds, SWZ ? (kbase ^ (32 * j2)) : kbase + 32 * j2);
+        const f32x4 k1 = lds_f4(lds, SWZ ? (kbase ^ (32 * j2 + 16)) : kbase + 32 * j2 + 16);
+        sacc = mfma_bf(pack8(k0, k1), pack8(&q[8 * j2]), sacc);
+      }
+    } else {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) sacc = mfma(kv[e], q[4 * j + e], sacc);
+      for (int j = 0; j < NS / 4; ++j) {
+        const f32x4 kv = lds_f4(lds, SWZ ? (kbase ^ (16 * j)) : kbase + 16 * j);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sacc = mfma(kv[e], q[4 * j + e], sacc);
+      }
     }
     f32x16 eacc;
     if constexpr (!DENSE) {  // expA^T = T Qh^T (sbm_attn.py:55)
@@ -758,10 +768,19 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd
     }
     m_run = m_new;
     // O^T += V^T W^T (keys beyond M carry w = 0)
+    if constexpr (BF) {
+      const bf16x8 w0 = pack8(&w[0]), w1 = pack8(&w[8]);
 #pragma unroll
-    for (int t = 0; t < DT; ++t)
+      for (int t = 0; t < DT; ++t) {
+        o[t] = mfma_bf(pack8(&vt[t][0]), w0, o[t]);
+        o[t] = mfma_bf(pack8(&vt[t][8]), w1, o[t]);
+      }
+    } else {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) o[t] = mfma(vt[t][r], w[r], o[t]);
+      for (int t = 0; t < DT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[t] = mfma(vt[t][r], w[r], o[t]);
+    }
   }
   const float Z = xhalf_sum(zp), Zg = xhalf_sum(zgp);
   const float n = Zg / Z;
@@ -899,7 +918,7 @@ struct AttnBwdShape {
 // B2: per (b,h, query block), S^T orientation: dQ (attention path), dQh, gamma
 // ------------------------------------------------------------------------------------
 // DG: an upstream gradient of the graph output is present (p.dgraph)
-template <int D, int KPH, bool DENSE, bool DROP, bool DG>
+template <int D, int KPH, bool DENSE, bool DROP, bool DG, bool BF>
 __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd_q(const KArgs p) {
   using SH = AttnBwdShape<D, KPH>;
   constexpr int DT = D / 32, NS = D / 2, DP = SH::DP, KP = SH::KP, KPN = SH::KPN, KTA = SH::KTA;
@@ -969,17 +988,29 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
     f32x16 sacc = zero16(), dpacc = zero16();
     const int kb = SWZ ? row_base64(c, h, SW_BOTH) : 4 * (c * DP + NS * h);
     const int vb = SH::QV + (SWZ ? row_base64(c, h, SW_ROW) : 4 * (c * DP + NS * h));
+    if constexpr (BF) {
 #pragma unroll
-    for (int j = 0; j < NS / 4; ++j) {
-      const f32x4 kv = lds_f4(lds, SWZ ? (kb ^ (16 * j)) : kb + 16 * j);
+      for (int j2 = 0; j2 < NS / 8; ++j2) {
+        const f32x4 k0 = lds_f4(lds, SWZ ? (kb ^ (32 * j2)) : kb + 32 * j2);
+        const f32x4 k1 = lds_f4(lds, SWZ ? (kb ^ (32 * j2 + 16)) : kb + 32 * j2 + 16);
+        sacc = mfma_bf(pack8(k0, k1), pack8(&q[8 * j2]), sacc);
+        const f32x4 v0 = lds_f4(lds, SWZ ? (vb ^ (32 * j2)) : vb + 32 * j2);
+        const f32x4 v1 = lds_f4(lds, SWZ ? (vb ^ (32 * j2 + 16)) : vb + 32 * j2 + 16);
+        dpacc = mfma_bf(pack8(v0, v1), pack8(&dx[8 * j2]), dpacc);
+      }
+    } else {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) sacc = mfma(kv[e], q[4 * j + e], sacc);
-    }
+      for (int j = 0; j < NS / 4; ++j) {
+        const f32x4 kv = lds_f4(lds, SWZ ? (kb ^ (16 * j)) : kb + 16 * j);
 #pragma unroll
-    for (int j = 0; j < NS / 4; ++j) {
-      const f32x4 vv = lds_f4(lds, SWZ ? (vb ^ (16 * j)) : vb + 16 * j);
+        for (int e = 0; e < 4; ++e) sacc = mfma(kv[e], q[4 * j + e], sacc);
+      }
 #pragma unroll
-      for (int e = 0; e < 4; ++e) dpacc = mfma(vv[e], dx[4 * j + e], dpacc);
+      for (int j = 0; j < NS / 4; ++j) {
+        const f32x4 vv = lds_f4(lds, SWZ ? (vb ^ (16 * j)) : vb + 16 * j);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dpacc = mfma(vv[e], dx[4 * j + e], dpacc);
+      }
     }
     // transposed operands of this tile's dQ / dQh products (lane d holds K[key crow(r,h)][d])
     float kT[DT][16], tT[KTA][16];
@@ -1024,10 +1055,19 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
       gv[r] = e.g;
     }
     // dQ^T += K^T ds^T ; dQh^T += T^T G^T  (keys beyond M carry ds = G = 0)
+    if constexpr (BF) {
+      const bf16x8 s0 = pack8(&dsv[0]), s1 = pack8(&dsv[8]);
 #pragma unroll
-    for (int t = 0; t < DT; ++t)
+      for (int t = 0; t < DT; ++t) {
+        dq[t] = mfma_bf(pack8(&kT[t][0]), s0, dq[t]);
+        dq[t] = mfma_bf(pack8(&kT[t][8]), s1, dq[t]);
+      }
+    } else {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) dq[t] = mfma(kT[t][r], dsv[r], dq[t]);
+      for (int t = 0; t < DT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dq[t] = mfma(kT[t][r], dsv[r], dq[t]);
+    }
     if constexpr (!DENSE) {
 #pragma unroll
       for (int at = 0; at < KTA; ++at)
@@ -1043,7 +1083,7 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
 // ------------------------------------------------------------------------------------
 // B1: per (b,h, key block), S orientation (queries = acc rows, keys = lanes): dK, dV, dT
 // ------------------------------------------------------------------------------------
-template <int D, int KPH, bool DENSE, bool DROP, bool DG>
+template <int D, int KPH, bool DENSE, bool DROP, bool DG, bool BF>
 __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd_kv(const KArgs p) {
   using SH = AttnBwdShape<D, KPH>;
   constexpr int DT = D / 32, NS = D / 2, DP = SH::DP, KP = SH::KP, KPN = SH::KPN, KTA = SH::KTA;
@@ -1105,17 +1145,29 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
     }
     f32x16 sacc = zero16(), dpacc = zero16();
     const int qrb = SWZ ? row_base64(c, h, SW_BOTH) : 4 * (c * DP + NS * h);
+    if constexpr (BF) {
 #pragma unroll
-    for (int s4 = 0; s4 < NS / 4; ++s4) {
-      const f32x4 qv = lds_f4(lds, SH::KQ + (SWZ ? (qrb ^ (16 * s4)) : qrb + 16 * s4));
+      for (int j2 = 0; j2 < NS / 8; ++j2) {
+        const f32x4 q0 = lds_f4(lds, SH::KQ + (SWZ ? (qrb ^ (32 * j2)) : qrb + 32 * j2));
+        const f32x4 q1 = lds_f4(lds, SH::KQ + (SWZ ? (qrb ^ (32 * j2 + 16)) : qrb + 32 * j2 + 16));
+        sacc = mfma_bf(pack8(q0, q1), pack8(&kr[8 * j2]), sacc);
+        const f32x4 x0 = lds_f4(lds, SH::KX + (SWZ ? (qrb ^ (32 * j2)) : qrb + 32 * j2));
+        const f32x4 x1 = lds_f4(lds, SH::KX + (SWZ ? (qrb ^ (32 * j2 + 16)) : qrb + 32 * j2 + 16));
+        dpacc = mfma_bf(pack8(x0, x1), pack8(&vr[8 * j2]), dpacc);
+      }
+    } else {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) sacc = mfma(qv[e], kr[4 * s4 + e], sacc);
-    }
+      for (int s4 = 0; s4 < NS / 4; ++s4) {
+        const f32x4 qv = lds_f4(lds, SH::KQ + (SWZ ? (qrb ^ (16 * s4)) : qrb + 16 * s4));
 #pragma unroll
-    for (int s4 = 0; s4 < NS / 4; ++s4) {
-      const f32x4 xv = lds_f4(lds, SH::KX + (SWZ ? (qrb ^ (16 * s4)) : qrb + 16 * s4));
+        for (int e = 0; e < 4; ++e) sacc = mfma(qv[e], kr[4 * s4 + e], sacc);
+      }
 #pragma unroll
-      for (int e = 0; e < 4; ++e) dpacc = mfma(xv[e], vr[4 * s4 + e], dpacc);
+      for (int s4 = 0; s4 < NS / 4; ++s4) {
+        const f32x4 xv = lds_f4(lds, SH::KX + (SWZ ? (qrb ^ (16 * s4)) : qrb + 16 * s4));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dpacc = mfma(xv[e], vr[4 * s4 + e], dpacc);
+      }
     }
     // column read of element (query crow(r,h), d = 32t + c) of the Q / dX image at byte offset off
     int cb[DT];
@@ -1146,14 +1198,26 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
         awv[rr] = e.attw;
       }
       // dV^T += dX^T attw ; dK^T += Q^T ds ; dT^T += Qh^T G  (queries beyond N carry zeros)
+      if constexpr (BF) {
+        const bf16x8 aw8 = pack8(awv), ds8 = pack8(dsv);
 #pragma unroll
-      for (int t = 0; t < DT; ++t)
+        for (int t = 0; t < DT; ++t) {
+          float xc[8], qc[8];
 #pragma unroll
-        for (int rr = 0; rr < 8; ++rr) dv[t] = mfma(colv(SH::KX, t, 8 * half + rr), awv[rr], dv[t]);
+          for (int rr = 0; rr < 8; ++rr) { xc[rr] = colv(SH::KX, t, 8 * half + rr); qc[rr] = colv(SH::KQ, t, 8 * half + rr); }
+          dv[t] = mfma_bf(pack8(xc), aw8, dv[t]);
+          dk[t] = mfma_bf(pack8(qc), ds8, dk[t]);
+        }
+      } else {
 #pragma unroll
-      for (int t = 0; t < DT; ++t)
+        for (int t = 0; t < DT; ++t)
 #pragma unroll
-        for (int rr = 0; rr < 8; ++rr) dk[t] = mfma(colv(SH::KQ, t, 8 * half + rr), dsv[rr], dk[t]);
+          for (int rr = 0; rr < 8; ++rr) dv[t] = mfma(colv(SH::KX, t, 8 * half + rr), awv[rr], dv[t]);
+#pragma unroll
+        for (int t = 0; t < DT; ++t)
+#pragma unroll
+          for (int rr = 0; rr < 8; ++rr) dk[t] = mfma(colv(SH::KQ, t, 8 * half + rr), dsv[rr], dk[t]);
+      }
       if constexpr (!DENSE) {
 #pragma unroll
         for (int at = 0; at < KTA; ++at)
@@ -1970,6 +2034,7 @@ KArgs make_kargs(const csa_sbm_fwd_args* a, const Layout& L) {
   p.k_sb = a->k_sb; p.k_sh = a->k_sh; p.k_sn = a->k_sn;
   p.v_sb = a->v_sb; p.v_sh = a->v_sh; p.v_sn = a->v_sn;
   p.mask = a->key_mask; p.mask_sb = a->mask_sb;
+  p.bf16 = a->dtype == CSA_DTYPE_BF16;
   for (int l = 0; l < 3; ++l) p.pb[l] = a->proj_b[l];
   void* st = a->state;
   for (int l = 0; l < 3; ++l) {
@@ -1996,6 +2061,9 @@ KArgs make_kargs(const csa_sbm_fwd_args* a, const Layout& L) {
 
 csa_status validate_fwd(const csa_sbm_fwd_args* a) {
   if (!a) return fail(CSA_INVALID_ARG, "null args");
+  if (a->dtype != CSA_DTYPE_F32 && a->dtype != CSA_DTYPE_BF16) return fail(CSA_INVALID_ARG, "dtype must be CSA_DTYPE_F32 or CSA_DTYPE_BF16");
+  if (a->dtype == CSA_DTYPE_BF16 && !(a->flags & CSA_FLAG_DENSE) && a->k > 16)
+    return fail(CSA_UNSUPPORTED_SHAPE, "bf16 SBM attention is instantiated for k <= 16");
   const bool dense = a->flags & CSA_FLAG_DENSE;
   if (a->B < 1 || a->H < 1 || a->N < 1 || a->M < 1) return fail(CSA_INVALID_ARG, "B, H, N, M must be >= 1");
   if (!a->Q || !a->K || !a->V || !a->X || !a->state) return fail(CSA_INVALID_ARG, "null Q/K/V/X/state");
@@ -2017,27 +2085,36 @@ csa_status validate_fwd(const csa_sbm_fwd_args* a) {
   return CSA_OK;
 }
 
-template <int D, int KPH, bool DENSE>
+template <int D, int KPH, bool DENSE, bool BF>
 void launch_attn_fwd(const KArgs& p, int BH, const Layout& L, bool has_u, bool drop, hipStream_t st) {
   const size_t lds_bytes = AttnFwdLds<D, KPH>::bytes((int)L.Mpad);
   const dim3 grid(xcd_grid((int)L.NQB, BH));
   if (lds_bytes > 64 * 1024) {
-    (void)hipFuncSetAttribute((const void*)k_attn_fwd<D, KPH, DENSE, false, false>,
+    (void)hipFuncSetAttribute((const void*)k_attn_fwd<D, KPH, DENSE, false, false, BF>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
-    (void)hipFuncSetAttribute((const void*)k_attn_fwd<D, KPH, DENSE, false, true>,
+    (void)hipFuncSetAttribute((const void*)k_attn_fwd<D, KPH, DENSE, false, true, BF>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
-    (void)hipFuncSetAttribute((const void*)k_attn_fwd<D, KPH, DENSE, !DENSE, false>,
+    (void)hipFuncSetAttribute((const void*)k_attn_fwd<D, KPH, DENSE, !DENSE, false, BF>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
-    (void)hipFuncSetAttribute((const void*)k_attn_fwd<D, KPH, DENSE, !DENSE, true>,
+    (void)hipFuncSetAttribute((const void*)k_attn_fwd<D, KPH, DENSE, !DENSE, true, BF>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
   }
   if (!DENSE && has_u) {
-    if (drop) hipLaunchKernelGGL((k_attn_fwd<D, KPH, DENSE, !DENSE, true>), grid, dim3(64), lds_bytes, st, p);
-    else hipLaunchKernelGGL((k_attn_fwd<D, KPH, DENSE, !DENSE, false>), grid, dim3(64), lds_bytes, st, p);
+    if (drop) hipLaunchKernelGGL((k_attn_fwd<D, KPH, DENSE, !DENSE, true, BF>), grid, dim3(64), lds_bytes, st, p);
+    else hipLaunchKernelGGL((k_attn_fwd<D, KPH, DENSE, !DENSE, false, BF>), grid, dim3(64), lds_bytes, st, p);
   } else {
-    if (drop) hipLaunchKernelGGL((k_attn_fwd<D, KPH, DENSE, false, true>), grid, dim3(64), lds_bytes, st, p);
-    else hipLaunchKernelGGL((k_attn_fwd<D, KPH, DENSE, false, false>), grid, dim3(64), lds_bytes, st, p);
+    if (drop) hipLaunchKernelGGL((k_attn_fwd<D, KPH, DENSE, false, true, BF>), grid, dim3(64), lds_bytes, st, p);
+    else hipLaunchKernelGGL((k_attn_fwd<D, KPH, DENSE, false, false, BF>), grid, dim3(64), lds_bytes, st, p);
   }
+}
+
+// bf16 instantiations exist for the shapes BASELINE runs (k <= 16, and the dense ablation) only
+template <int D, int KPH, bool DENSE>
+void launch_attn_fwd_any(const KArgs& p, int BH, const Layout& L, bool has_u, bool drop, hipStream_t st) {
+  if constexpr (KPH <= 8) {
+    if (p.bf16) return launch_attn_fwd<D, KPH, DENSE, true>(p, BH, L, has_u, drop, st);
+  }
+  launch_attn_fwd<D, KPH, DENSE, false>(p, BH, L, has_u, drop, st);
 }
 
 template <int D, int KPH, int KT>
@@ -2081,44 +2158,52 @@ csa_status launch_fwd(const csa_sbm_fwd_args* a, const Layout& L, hipStream_t st
     }
     {
       Stage sg(a->prof, CSA_STAGE_ATTN_FWD, st);
-      launch_attn_fwd<D, KPH, false>(p, BH, L, a->uniforms != nullptr, a->attn_dropout > 0.f, st);
+      launch_attn_fwd_any<D, KPH, false>(p, BH, L, a->uniforms != nullptr, a->attn_dropout > 0.f, st);
     }
     hipLaunchKernelGGL(k_sparsity_finish, dim3(1), dim3(64), 0, st, (const unsigned long long*)p.cnt, a->sparsity,
                        (int)a->H, (float)a->B * (float)a->N * (float)a->M);
   } else {
     Stage sg(a->prof, CSA_STAGE_ATTN_FWD, st);
-    launch_attn_fwd<D, 0, true>(p, BH, L, false, a->attn_dropout > 0.f, st);
+    launch_attn_fwd_any<D, 0, true>(p, BH, L, false, a->attn_dropout > 0.f, st);
   }
   return check_launch("csa_sbm_fwd");
 }
 
-template <int D, int KPH, bool DENSE, bool DROP, bool DG>
+template <int D, int KPH, bool DENSE, bool DROP, bool DG, bool BF>
 void launch_attn_bwd_v(const KArgs& p, int BH, const Layout& L, const csa_prof* pf, hipStream_t st) {
   using SH = AttnBwdShape<D, KPH>;
   {
     Stage sg(pf, CSA_STAGE_ATTN_BWD_Q, st);
     const size_t lds_bytes = SH::q_bytes((int)L.Mpad);
     if (lds_bytes > 64 * 1024)
-      (void)hipFuncSetAttribute((const void*)k_attn_bwd_q<D, KPH, DENSE, DROP, DG>,
+      (void)hipFuncSetAttribute((const void*)k_attn_bwd_q<D, KPH, DENSE, DROP, DG, BF>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
-    hipLaunchKernelGGL((k_attn_bwd_q<D, KPH, DENSE, DROP, DG>), dim3(xcd_grid((int)L.NQB, BH)), dim3(64), lds_bytes,
-                       st, p);
+    hipLaunchKernelGGL((k_attn_bwd_q<D, KPH, DENSE, DROP, DG, BF>), dim3(xcd_grid((int)L.NQB, BH)), dim3(64),
+                       lds_bytes, st, p);
   }
   Stage sg(pf, CSA_STAGE_ATTN_BWD_KV, st);
-  hipLaunchKernelGGL((k_attn_bwd_kv<D, KPH, DENSE, DROP, DG>), dim3(xcd_grid((int)L.NKB, BH)), dim3(64), SH::KV_BYTES,
-                     st, p);
+  hipLaunchKernelGGL((k_attn_bwd_kv<D, KPH, DENSE, DROP, DG, BF>), dim3(xcd_grid((int)L.NKB, BH)), dim3(64),
+                     SH::KV_BYTES, st, p);
+}
+
+template <int D, int KPH, bool DENSE, bool BF>
+void launch_attn_bwd_b(const KArgs& p, int BH, const Layout& L, bool drop, const csa_prof* pf, hipStream_t st) {
+  const bool dg = p.dgraph != nullptr;
+  if (drop) {
+    if (dg) launch_attn_bwd_v<D, KPH, DENSE, true, true, BF>(p, BH, L, pf, st);
+    else launch_attn_bwd_v<D, KPH, DENSE, true, false, BF>(p, BH, L, pf, st);
+  } else {
+    if (dg) launch_attn_bwd_v<D, KPH, DENSE, false, true, BF>(p, BH, L, pf, st);
+    else launch_attn_bwd_v<D, KPH, DENSE, false, false, BF>(p, BH, L, pf, st);
+  }
 }
 
 template <int D, int KPH, bool DENSE>
 void launch_attn_bwd(const KArgs& p, int BH, const Layout& L, bool drop, const csa_prof* pf, hipStream_t st) {
-  const bool dg = p.dgraph != nullptr;
-  if (drop) {
-    if (dg) launch_attn_bwd_v<D, KPH, DENSE, true, true>(p, BH, L, pf, st);
-    else launch_attn_bwd_v<D, KPH, DENSE, true, false>(p, BH, L, pf, st);
-  } else {
-    if (dg) launch_attn_bwd_v<D, KPH, DENSE, false, true>(p, BH, L, pf, st);
-    else launch_attn_bwd_v<D, KPH, DENSE, false, false>(p, BH, L, pf, st);
+  if constexpr (KPH <= 8) {
+    if (p.bf16) return launch_attn_bwd_b<D, KPH, DENSE, true>(p, BH, L, drop, pf, st);
   }
+  launch_attn_bwd_b<D, KPH, DENSE, false>(p, BH, L, drop, pf, st);
 }
 
 template <int D, int KPH, int KT>

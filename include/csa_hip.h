@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define CSA_ABI_VERSION 1
+#define CSA_ABI_VERSION 2
 
 typedef enum csa_status {
   CSA_OK = 0,
@@ -49,6 +49,15 @@ typedef enum csa_status {
 
 /* flags */
 #define CSA_FLAG_DENSE 1u /* FullAttention (graph == 1, no cluster projection, no sampling) */
+
+/* operand precision of the N^2 attention contractions (dtype field of the args structs). Storage is
+ * fp32 either way. CSA_DTYPE_F32 is the reference's precision (sbm_attn.py:120-126 forces fp32) and
+ * the parity mode (rtol 1e-4 / atol 1e-5). CSA_DTYPE_BF16 rounds the operands of QK^T, dX V^T, PV, dQ,
+ * dK, dV (SBM) and of the CSE's c2c, PV and their gradients to bf16 for v_mfma_f32_32x32x16_bf16
+ * (fp32 accumulation; north_star tolerance 2e-2). The cluster projection, expA (so the sampled graph)
+ * and every softmax / normalisation stay fp32. */
+#define CSA_DTYPE_F32 0
+#define CSA_DTYPE_BF16 1
 
 /* Optional per-stage timing: caller-created hipEvent_t handles; when start[s] and stop[s] are
  * non-NULL the library records them on `stream` around stage s (no library-side state). */
@@ -80,6 +89,7 @@ typedef struct csa_sbm_fwd_args {
   float attn_dropout;         /* drop_attn p (0 in eval) — sbm_attn.py:14,63 */
   float proj_dropout;         /* proj Dropout p (0 in eval) — sbm_attn.py:24,27 */
   uint32_t flags;
+  uint32_t dtype;             /* CSA_DTYPE_F32 or CSA_DTYPE_BF16 */
   float* X;                   /* out (B,H,N,d) contiguous */
   float* sparsity;            /* out (H,) head-wise sparsity (sbm_attn.py:64); NULL if DENSE */
   void* state;                /* csa_sbm_state_bytes(): saved for backward and csa_sbm_maps */
@@ -129,6 +139,7 @@ typedef struct csa_rel_attn_args {
   const uint8_t* rel;  int64_t rel_sb, rel_sh;  /* (B,*,N,N) relation index < L; head stride may be 0 */
   const uint8_t* mask; int64_t mask_sb, mask_sh;/* (B,*,N,N) 1 = masked (-1e9); head stride may be 0 */
   int64_t rel_head_group; /* heads [0,g) read plane 0, heads [g,H) plane 1 (CSE: 4); 0 = use rel_sh */
+  uint32_t dtype;          /* CSA_DTYPE_F32 or CSA_DTYPE_BF16 (bf16: d = 64 only) */
   float* out;          /* (B,H,N,d) contiguous */
   float* row_stats;    /* (B,H,N,2) saved (row max, 1/row sum) for backward; kept separate because
                           fully masked rows sit at -1e9 where max + log(sum) is not representable */
