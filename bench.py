@@ -322,6 +322,8 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--seq-len", type=int, default=150, help="AST nodes N (config 5 long-AST stress: 1024)")
     ap.add_argument("--clusters", type=int, default=10, help="SBM clusters k (config 5 sweep: 16..128)")
+    ap.add_argument("--head-dim", type=int, choices=(64, 96), default=64,
+                    help="SBM head dim d (config/python.py: 64; config/java.py sbm_enc_dim 768 / 8 heads: 96)")
     ap.add_argument("--dense", action="store_true", help="FullAttention ablation (config/python_full_att.py)")
     ap.add_argument("--eval", action="store_true", help="eval mode (no dropout)")
     ap.add_argument("--precision", choices=("fp32", "bf16"), default="fp32",
@@ -352,7 +354,7 @@ def main():
     from csa_amd._lib import STAGES, CsaProf, KERNEL_OF_STAGE
     from csa_amd.module.sbm_attn import FullAttention, SBMAttention
 
-    B, H, N, d, k = args.batch, 8, args.seq_len, 64, args.clusters
+    B, H, N, d, k = args.batch, 8, args.seq_len, args.head_dim, args.clusters
     torch.manual_seed(1234 + rank)
     cfg = {"attention_dropout": 0.2, "head_dim": d, "num_head": H, "num_clusters": [k], "return_maps": False,
            "attn_precision": args.precision}
@@ -429,7 +431,7 @@ def main():
     timed = {s: v for s, v in stage_ms.items() if s in flops}
     dom = max(timed, key=timed.get) if timed else None
     kernel_of = dict(KERNEL_OF_STAGE)
-    if not args.dense and d == 64 and k <= 16:
+    if not args.dense and d in (64, 96) and k <= 16:
         kernel_of["proj_bwd"] = "k_proj_bwd_s"  # the k <= 16 projection-backward variant
 
     # 2) timed region: events only around the dominant kernel (its live average launch duration)

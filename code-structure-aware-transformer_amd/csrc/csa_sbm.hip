@@ -19,6 +19,8 @@
 #include "csa_common.hpp"
 #include "../../include/csa_hip.h"
 
+#include <algorithm>
+#include <stdint.h>
 #include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
@@ -55,6 +57,22 @@ struct Layout {
 
 inline size_t al(size_t x) { return (x + 255) & ~size_t(255); }
 
+// Projection-backward workgroups per head. The head's I = B * items_per_b items (32-row Q / K blocks)
+// are split evenly over G workgroups of 4 waves (one item per wave per group of 4). G minimises
+// (dispatch rounds over the 256 CUs) x (groups of 4 items per workgroup); the smallest G wins ties
+// (fewer slabs to reduce). java B = 64, H = 8, 10 items per AST, 1 workgroup per CU: G = 32, one round
+// of 5 full groups (a whole-batch split, G = 64, ran two rounds of 3 groups, the last half empty).
+int64_t proj_bwd_groups(int64_t B, int64_t H, int64_t items_per_b, int wg_per_cu) {
+  const int64_t I = B * items_per_b, slots = 256LL * wg_per_cu;
+  const int64_t gmax = std::min<int64_t>(I, std::max<int64_t>(1, 4 * slots / H));
+  int64_t best = 1, best_cost = INT64_MAX;
+  for (int64_t G = 1; G <= gmax; ++G) {
+    const int64_t cost = ((H * G + slots - 1) / slots) * (((I + G - 1) / G + 3) / 4);
+    if (cost < best_cost) { best_cost = cost; best = G; }
+  }
+  return best;
+}
+
 Layout make_layout(int64_t B, int64_t H, int64_t N, int64_t M, int64_t D, int64_t k, bool dense) {
   Layout L;
   L.B = B; L.H = H; L.N = N; L.M = M; L.D = D; L.k = dense ? 0 : k;
@@ -83,7 +101,8 @@ Layout make_layout(int64_t B, int64_t H, int64_t N, int64_t M, int64_t D, int64_
   L.Act = take(sizeof(float) * (dense ? 0 : B * H * (L.NQB + L.NKB) * (3 * D + KP32) * 32));
   L.total = o;
   // backward workspace
-  L.G = dense ? 0 : (B < 64 ? B : 64);
+  // two workgroups per CU for d = 64 with KT = 1 (k_proj_bwd_s / k_proj_bwd<64, 1>: 80 / 64 KiB LDS)
+  L.G = dense ? 0 : proj_bwd_groups(B, H, L.NQB + L.NKB, (D == 64 && L.KT == 1) ? 2 : 1);
   L.slab_floats = dense ? 0 : (3 * D * D + 3 * D + KP32 * D + KP32 * KP32);
   o = 0;
   L.w_dQh = take(sizeof(float) * B * H * N * L.kp);
@@ -118,20 +137,26 @@ __device__ __forceinline__ f32x4 frag4(const float* __restrict__ f, int it, int 
 // out[t] += sum_{s < 4 S4N} frag(t)[s] * bval(s) for t < NTO, fragments fetched LA K-groups (4 steps
 // each) ahead: LA = 1 covers the L2 latency when the 4 NTO MFMAs of a group (>= 256 cycles) and other
 // waves fill the gap; the sched fence keeps the lookahead (and its registers) at LA groups.
-template <int NTO, int S4N, int LA = 1, typename BF>
+// The same fragment layout copied into LDS (FL): one ds_read_b128 per lane per K-group and tile.
+__device__ __forceinline__ f32x4 frag4_lds(const float* __restrict__ f, int it, int nsteps, int s4) {
+  return *reinterpret_cast<const f32x4*>(f + ((it * (nsteps >> 2) + s4) * 64 + lane_id()) * 4);
+}
+
+template <int NTO, int S4N, int LA = 1, bool FL = false, typename BF>
 __device__ __forceinline__ void frag_chain(const float* __restrict__ frag, int nsteps, f32x16 (&out)[NTO], BF bval) {
   static_assert(LA == 1 || LA == 2, "lookahead of one or two K-groups");
+  auto ld = [&](int t, int s4) { return FL ? frag4_lds(frag, t, nsteps, s4) : frag4(frag, t, nsteps, s4); };
   f32x4 wq[LA + 1][NTO];
 #pragma unroll
   for (int a = 0; a < LA; ++a)
     if (a < S4N)
 #pragma unroll
-      for (int t = 0; t < NTO; ++t) wq[a][t] = frag4(frag, t, nsteps, a);
+      for (int t = 0; t < NTO; ++t) wq[a][t] = ld(t, a);
 #pragma unroll
   for (int s4 = 0; s4 < S4N; ++s4) {
     if (s4 + LA < S4N) {
 #pragma unroll
-      for (int t = 0; t < NTO; ++t) wq[(s4 + LA) % (LA + 1)][t] = frag4(frag, t, nsteps, s4 + LA);
+      for (int t = 0; t < NTO; ++t) wq[(s4 + LA) % (LA + 1)][t] = ld(t, s4 + LA);
     }
 #pragma unroll
     for (int t = 0; t < NTO; ++t)
@@ -459,7 +484,7 @@ __global__ __launch_bounds__(64) void k_proj_fwd(const KArgs p) {
     store_act<D / 32>(blk, h1);
     store_act<D / 32>(blk + 32 * D, h2);
     store_act<D / 32>(blk + 64 * D, po);
-    if (D == 64 && p.kp <= 16) {  // clusters >= 16 are zero and never read back (k_proj_bwd_s: features 0..15)
+    if ((D == 64 || D == 96) && p.kp <= 16) {  // clusters >= 16 are zero, never read back (k_proj_bwd_s)
       const int cl = lane_id() & 31, hl = lane_id() >> 5;
 #pragma unroll
       for (int r = 0; r < 8; ++r) __builtin_nontemporal_store(hat[0][r], blk + 96 * D + act_off(crow(r, hl), cl));
@@ -1258,7 +1283,7 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
 // reduce over the group's 128 rows. Both operands are staged in LDS in the activation-block
 // layout (one 32-row region per wave): DS from the wave's registers, IN by LDS-DMA of the saved
 // block, issued as soon as the region is free so it lands under the chain MFMAs. The output tiles
-// are dealt round-robin to the waves (tile g -> wave g % 4). When they fit (REGACC: <= 4 tiles per
+// are dealt round-robin to the waves (tile g -> wave g % 4). When they fit (REGACC: <= 8 tiles per
 // wave) each wave accumulates its tiles in registers over all its items and writes its part of
 // the WG's slab exactly once. Otherwise it read-modify-writes the slab once per group. Neither
 // path uses atomics, so the result is deterministic.
@@ -1274,7 +1299,10 @@ struct ProjBwdShape {
   static constexpr int G_S = 0, G_C = KT * KT, G_W2 = G_C + KT * DT, G_W1 = G_W2 + DT * DT, G_W0 = G_W1 + DT * DT,
                        NTILE = G_W0 + DT * DT;
   static constexpr int NACC = (NTILE + 3) / 4;
-  static constexpr bool REGACC = NACC <= 4;
+  // up to 8 accumulator tiles per wave (128 registers: the kernel runs one wave per SIMD for d = 96 or
+  // KT > 1, so the unified VGPR/AGPR file has room); d = 96 has 31 tiles = 8 per wave. Beyond that the
+  // slab is read-modify-written once per group.
+  static constexpr bool REGACC = NACC <= 8;
 };
 
 // act_off(32t + crow(r,h), c) split into a lane base and a compile-time offset: for these features
@@ -1421,6 +1449,15 @@ __device__ __forceinline__ void mm_acc(const float* __restrict__ frag, const f32
   frag_chain<NTO, S4MAX, LA>(frag, 16 * NTI, out, [&](int s) { return in[s / 16][s % 16]; });
 }
 
+// mm_acc over fragments held in LDS (FL) or global memory; NSTEP = the K-steps of the stored layout
+// (8 for the compacted k <= 16 cluster fragments: only K-groups 0 and 1 of each tile are copied).
+template <int NTO, int NTI, int S4MAX, int NSTEP, bool FL>
+__device__ __forceinline__ void mm_acc_f(const float* __restrict__ frag, const f32x16 (&in)[NTI], f32x16 (&out)[NTO]) {
+#pragma unroll
+  for (int t = 0; t < NTO; ++t) out[t] = zero16();
+  frag_chain<NTO, S4MAX, 1, FL>(frag, NSTEP, out, [&](int s) { return in[s / 16][s % 16]; });
+}
+
 template <int D, int KT>
 __global__ __launch_bounds__(256, (D <= 64 && KT <= 1 ? 2 : 1)) void k_proj_bwd(const KArgs p) {
   using Sh = ProjBwdShape<D, KT>;
@@ -1431,9 +1468,9 @@ __global__ __launch_bounds__(256, (D <= 64 && KT <= 1 ? 2 : 1)) void k_proj_bwd(
   const int lane = lane_id(), c = lane & 31, h = lane >> 5;
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int hd = blockIdx.y, g = blockIdx.x, G = gridDim.x;
-  const int b_lo = (int)((int64_t)g * p.B / G), b_hi = (int)((int64_t)(g + 1) * p.B / G);
   const int per_b = p.NQB + p.NKB;
-  const int n_items = (b_hi - b_lo) * per_b;
+  const int i_lo = (int)((int64_t)g * p.B * per_b / G), i_hi = (int)((int64_t)(g + 1) * p.B * per_b / G);
+  const int n_items = i_hi - i_lo;  // this workgroup's items: i_lo .. i_hi - 1 of the head
   float* slab = p.slab + ((int64_t)hd * G + g) * p.slab_floats;
   const float ks = p.proj_p > 0.f ? 1.f / (1.f - p.proj_p) : 1.f;
   const float* CfT = p.CfT + (size_t)hd * KP32 * D;
@@ -1452,8 +1489,8 @@ __global__ __launch_bounds__(256, (D <= 64 && KT <= 1 ? 2 : 1)) void k_proj_bwd(
     Item it;
     const int item = grp * 4 + w;
     it.has = item < n_items;
-    it.b = b_lo + (it.has ? item / per_b : 0);
-    it.r = it.has ? item % per_b : 0;
+    it.b = it.has ? (i_lo + item) / per_b : 0;
+    it.r = it.has ? (i_lo + item) % per_b : 0;
     it.isK = it.r >= p.NQB;
     it.rb = it.isK ? it.r - p.NQB : it.r;
     it.nrows = it.isK ? p.M : p.N;
@@ -1616,65 +1653,161 @@ __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 acc) {
 }
 
 // ------------------------------------------------------------------------------------
-// B3s: projection backward for k <= 16 clusters and d = 64 (config/python.py and java sizes of k).
+// B3s: projection backward for k <= 16 clusters and d = 64 or 96 (config/python.py and config/java.py).
 // Same math and slab layout as k_proj_bwd. Differences:
 //  * dS_h and dC_h are k x k and k x d: each wave accumulates them over its OWN items with 16x16x4
 //    MFMAs (dT^T Kh from a global-load operand and the hat block; dZ^T po through a wave-private
 //    transpose), so these two small products need no barriers; the 4 wave partials are summed in a
 //    fixed order once per workgroup.
-//  * only the three d x d products dW2, dW1, dW0 go through the shared staging (one 32x32 tile per
-//    wave per stage), and each wave's next chain product runs between the two barriers of a stage:
+//  * only the three d x d products dW2, dW1, dW0 go through the shared staging, split evenly over the
+//    4 waves (d = 64: one 32x32 tile each; d = 96: 9 tiles x 4 K-quarters = 36 units, 9 per wave, see
+//    outer_stage96), and each wave's next chain product runs between the two barriers of a stage:
 //    6 barriers per group of 4 items instead of 10, no idle waves.
+//  * bias sums: each wave sums its own staged rows (8 LDS reads per feature), the 4 wave partials are
+//    combined once at the end.
 //  * chain products over the cluster index stop at K = 16.
 // ------------------------------------------------------------------------------------
 template <int D>
 struct ProjBwdSmallShape {
   static constexpr int DT = D / 32, NS = D / 2, REG = D * 32;
+  static constexpr int NSL = D == 64 ? 1 : 3;               // dW tile slots per wave per stage
   static constexpr int HATF = 16 * 32;                       // hat block: 16 features x 32 rows
   static constexpr int GINF = 32 * 16;                       // dT / dQh rows of the item: 32 rows x 16
-  static constexpr size_t LDS_BYTES = sizeof(float) * (8 * REG + 4 * HATF + 4 * GINF);  // 80 KiB: 2 per CU
+  static constexpr int PARTF = 256 + 16 * D + 3 * D;         // end-of-kernel wave partial: dS | dC | db
+  // d = 96 (one workgroup per CU anyway): weight fragments in LDS. WF holds the d x d layer of the next
+  // chain product (W2, W1, W0 in turn, DMA'd a stage ahead); CF / SF the head's cluster fragments
+  // (K-groups 0, 1 only: k <= 16), loaded once.
+  // (d = 64 with LW, one workgroup per CU instead of two, measured no faster: 0.404 vs 0.402 ms)
+  static constexpr bool LW = D == 96;
+  static constexpr int WF = 8 * REG + 4 * HATF + 4 * GINF, WFF = LW ? D * D : 0;
+  static constexpr int CF = WF + WFF, CFF = LW ? D / 32 * 512 : 0, SF = CF + CFF, SFF = LW ? 512 : 0;
+  // d = 64: 80 KiB (2 workgroups per CU); d = 96: 156 KiB
+  static constexpr size_t LDS_BYTES = sizeof(float) * (SF + SFF);
+  static_assert(4 * PARTF + (D == 96 ? 9 * 1024 : 0) <= 8 * REG, "end-of-kernel partials fit the staging");
 };
 
+// One K-quarter (s4 = 4q .. 4q+3: 32 of the 128 staged rows, 16 MFMAs) of a staged outer product:
+// operand reads and the MFMAs, split so the next quarter's reads can be issued first.
+template <int REG>
+__device__ __forceinline__ void quarter_load(const float* __restrict__ a, const float* __restrict__ b, int q, int sw,
+                                             f32x4 (&av)[4], f32x4 (&bv)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int off = (q >> 1) * REG + 4 * ((4 * (q & 1) + i) ^ sw);
+    av[i] = *reinterpret_cast<const f32x4*>(a + off);
+    bv[i] = *reinterpret_cast<const f32x4*>(b + off);
+  }
+}
+
+// d = 96 stage: the 9 output tiles x 4 K-quarters are 36 units; wave w takes units 9w .. 9w+8 in
+// tile-major order, i.e. tiles t = 2w + j (ot = t / 3, it = t % 3) over the quarters [w, 4), [0, 4),
+// [0, w] for j = 0, 1, 2. Slot 0 of wave w > 0 and slot 2 of wave w < 3 are the two halves of one tile,
+// combined in a fixed order at the end. The operand reads of the next position are issued before the
+// current position's MFMAs (unconditionally: every read is in bounds), so only the MFMA blocks sit
+// under the wave-uniform activity branches.
+template <int REG>
+__device__ __forceinline__ void outer_stage96(const float* __restrict__ ds, const float* __restrict__ in,
+                                              f32x16 (&acc)[3], int w, int lane) {
+  asm volatile("" : "+v"(lane));
+  const int c = lane & 31, h = lane >> 5, sw = (c >> 1) & 7;
+  const float* a[3];
+  const float* b[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int t = 2 * w + j, ot = t / 3, it = t - 3 * ot;
+    a[j] = ds + 2 * h * REG + (32 * ot + c) * 32;
+    b[j] = in + 2 * h * REG + (32 * it + c) * 32;
+  }
+  f32x4 av[2][4], bv[2][4];
+  quarter_load<REG>(a[0], b[0], 0, sw, av[0], bv[0]);
+#pragma unroll
+  for (int P = 0; P < 12; ++P) {
+    const int j = P >> 2, q = P & 3;
+    if (P + 1 < 12) quarter_load<REG>(a[(P + 1) >> 2], b[(P + 1) >> 2], (P + 1) & 3, sw, av[(P + 1) & 1], bv[(P + 1) & 1]);
+    if (j == 1 || (j == 0 ? q >= w : q <= w)) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[j] = mfma(av[P & 1][i][e], bv[P & 1][i][e], acc[j]);
+    }
+    fence_sched();
+  }
+}
+
 template <int D>
-__global__ __launch_bounds__(256, 2) void k_proj_bwd_s(const KArgs p) {
-  static_assert(D == 64, "4 d x d tiles per stage = one per wave");
+__device__ __forceinline__ void outer_stage_s(const float* __restrict__ ds, const float* __restrict__ in,
+                                              f32x16 (&acc)[ProjBwdSmallShape<D>::NSL], int w, int lane) {
+  if constexpr (D == 64) acc[0] = outer_tile<ProjBwdSmallShape<D>::REG>(ds, in, w >> 1, w & 1, acc[0], lane);
+  else outer_stage96<ProjBwdSmallShape<D>::REG>(ds, in, acc, w, lane);
+}
+
+// bias-gradient partial of this wave: sums of its own staged rows, feature lane (and lane + 64 for d = 96).
+// (Batching the reads, or moving them under the chain / outer MFMAs as side work, pushed d = 96 into
+// spills or measured no faster on one box: tools/ab_multi.sh.)
+template <int D>
+__device__ __forceinline__ void own_rowsum(const float* __restrict__ dsw, float (&db)[2], int lane) {
+  asm volatile("" : "+v"(lane));
+#pragma unroll
+  for (int u = 0; u < (D + 63) / 64; ++u) {
+    const int f = lane + 64 * u;
+    if (f < D) {
+      float s = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(dsw + act_off(f, 4 * k));
+        s += (v[0] + v[1]) + (v[2] + v[3]);
+      }
+      db[u] += s;
+    }
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(256, ProjBwdSmallShape<D>::LW ? 1 : 2) void k_proj_bwd_s(const KArgs p) {
+  static_assert(D == 64 || D == 96, "d x d stages split over 4 waves for d = 64 and 96");
   using Sh = ProjBwdSmallShape<D>;
   using Sf = ProjBwdShape<D, 1>;  // slab layout
-  constexpr int DT = Sh::DT, NS = Sh::NS, REG = Sh::REG, ABLK = Sf::ABLK;
+  constexpr int DT = Sh::DT, NS = Sh::NS, REG = Sh::REG, NSL = Sh::NSL, ABLK = Sf::ABLK;
+  constexpr bool LW = Sh::LW;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* DS = lds;
   float* IN = lds + 4 * REG;
   const int lane = lane_id(), c = lane & 31, h = lane >> 5, c16 = lane & 15, g4 = lane >> 4;
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int hd = blockIdx.y, g = blockIdx.x, G = gridDim.x;
-  const int b_lo = (int)((int64_t)g * p.B / G), b_hi = (int)((int64_t)(g + 1) * p.B / G);
   const int per_b = p.NQB + p.NKB;
-  const int n_items = (b_hi - b_lo) * per_b;
+  const int i_lo = (int)((int64_t)g * p.B * per_b / G), i_hi = (int)((int64_t)(g + 1) * p.B * per_b / G);
+  const int n_items = i_hi - i_lo;  // this workgroup's items: i_lo .. i_hi - 1 of the head
   float* slab = p.slab + ((int64_t)hd * G + g) * p.slab_floats;
   const float ks = p.proj_p > 0.f ? 1.f / (1.f - p.proj_p) : 1.f;
   const float* CfT = p.CfT + (size_t)hd * 32 * D;
   const float* SfT = p.SfT + (size_t)hd * 32 * 32;
+  const float* WFs = lds + Sh::WF;  // LW: weight fragments of the next chain product
+  const float* CFs = lds + Sh::CF;  // LW: cluster fragments (K-groups 0, 1)
+  const float* SFs = lds + Sh::SF;
   float* DSw = DS + w * REG;
   float* INw = IN + w * REG;
   float* HATw = lds + 8 * REG + w * Sh::HATF;
   const uint32_t INl = lds_offset(IN) + 4 * REG * w, HATl = lds_offset(lds) + 4 * (8 * REG + w * Sh::HATF);
   const float* GINw = lds + 8 * REG + 4 * Sh::HATF + w * Sh::GINF;
   const uint32_t GINl = lds_offset(lds) + 4 * (8 * REG + 4 * Sh::HATF + w * Sh::GINF);
-  f32x16 acc[3];  // this wave's tile (ot = w >> 1, it = w & 1) of dW2, dW1, dW0
+  f32x16 acc[3][NSL];  // this wave's dW2 | dW1 | dW0 tile slots (outer_stage_s)
 #pragma unroll
-  for (int i = 0; i < 3; ++i) acc[i] = zero16();
-  f32x4 accS = {0.f, 0.f, 0.f, 0.f}, accC[4];
+  for (int l = 0; l < 3; ++l)
 #pragma unroll
-  for (int t = 0; t < 4; ++t) accC[t] = accS;
-  float dbacc[3] = {0.f, 0.f, 0.f};
+    for (int j = 0; j < NSL; ++j) acc[l][j] = zero16();
+  f32x4 accS = {0.f, 0.f, 0.f, 0.f}, accC[D / 16];
+#pragma unroll
+  for (int t = 0; t < D / 16; ++t) accC[t] = accS;
+  float dbp[3][2] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};  // db0 | db1 | db2 partials (own_rowsum)
 
   struct Item { int b, r, isK, rb, nrows; bool has; };
   auto item_of = [&](int grp) {
     Item it;
     const int item = grp * 4 + w;
     it.has = item < n_items;
-    it.b = b_lo + (it.has ? item / per_b : 0);
-    it.r = it.has ? item % per_b : 0;
+    it.b = it.has ? (i_lo + item) / per_b : 0;
+    it.r = it.has ? (i_lo + item) % per_b : 0;
     it.isK = it.r >= p.NQB;
     it.rb = it.isK ? it.r - p.NQB : it.r;
     it.nrows = it.isK ? p.M : p.N;
@@ -1693,8 +1826,25 @@ __global__ __launch_bounds__(256, 2) void k_proj_bwd_s(const KArgs p) {
     // rows past the item's last row are outside the descriptor: not fetched (values masked below)
     dma_block16<2048>(GINl, make_rsrc(src, imin(32, it.nrows - row0) * p.kp * 4), 0);
   };
+  // LW: layer l's d x d fragments (36 KiB) -> WF, a quarter per wave (visible after a vmcnt wait + barrier)
+  auto load_wf = [&](int l) {
+    dma_block16<D * D>(lds_offset(lds) + 4 * Sh::WF + D * D * w, make_rsrc(p.WfT[l], 4 * D * D), D * D * w);
+  };
+  if constexpr (LW) {  // the head's cluster fragments, K-groups 0 and 1 of each tile (2 KiB pieces)
+    if (w < DT) dma_block16<2048>(lds_offset(lds) + 4 * (Sh::CF + 512 * w), make_rsrc(CfT, 4 * 32 * D), 4096 * w);
+    else if (w == 3) dma_block16<2048>(lds_offset(lds) + 4 * Sh::SF, make_rsrc(SfT, 4 * 32 * 32), 0);
+    wait_vm_all();
+    __syncthreads();
+  }
   prefetch_hat(item_of(0));
   prefetch(item_of(0));
+  if constexpr (LW) load_wf(2);
+#ifdef CSA_PHASES  // dev instrumentation: per-wave cycles by phase of workgroup (0, 0), printed at exit
+  unsigned long long ph_t = __builtin_amdgcn_s_memtime(), ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define PHASE(i) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); ph[i] += t_ - ph_t; ph_t = t_; }
+#else
+#define PHASE(i)
+#endif
 
   for (int grp = 0; grp * 4 < n_items; ++grp) {
     int tid = threadIdx.x;  // opaque: per-lane addresses are recomputed in the loop, not hoisted
@@ -1706,7 +1856,10 @@ __global__ __launch_bounds__(256, 2) void k_proj_bwd_s(const KArgs p) {
     const int rowc = imin(row, it.nrows - 1);
     const int bh = it.b * p.H + hd;
     const __amdgpu_buffer_rsrc_t ar = act_rsrc(it);
-    wait_vm_all();  // hat block, gin, dTt
+    // hat block, gin, dTt (LW: the W2 fragments, D*D/1024 DMAs issued after them, may be in flight)
+    if constexpr (LW) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D * D / 1024) : "memory");
+    else wait_vm_all();
+    PHASE(0);
     dma_block16<D * 128>(INl, ar, 64 * D * 4);  // po -> own IN region (free since B6), lands under dS / dZ / dp
     f32x16 gin[1];
     float dTt[8];
@@ -1734,7 +1887,7 @@ __global__ __launch_bounds__(256, 2) void k_proj_bwd_s(const KArgs p) {
     for (int r = 0; r < 16; ++r) hat[r] = r < 8 ? HATw[act_off(crow(r, h), c)] : 0.f;
     f32x16 dz[1];
     if (it.isK) {
-      mm_acc<1, 1, 2>(SfT, gin, dz);  // dKh^T = S^T dT^T (clusters < 16)
+      mm_acc_f<1, 1, 2, LW ? 8 : 16, LW>(LW ? SFs : SfT, gin, dz);  // dKh^T = S^T dT^T (clusters < 16)
     } else {
       dz[0] = gin[0];
     }
@@ -1750,25 +1903,30 @@ __global__ __launch_bounds__(256, 2) void k_proj_bwd_s(const KArgs p) {
     }
     // ---- dp^T = C^T dZ^T (clusters < 16)
     f32x16 dcur[DT];
-    mm_acc<DT, 1, 2>(CfT, dz, dcur);
-    wait_vm_all();  // po
+    mm_acc_f<DT, 1, 2, LW ? 8 : 16, LW>(LW ? CFs : CfT, dz, dcur);
+    wait_vm_all();  // po (LW: and the W2 fragments)
     // ---- dC_h += dZ^T po, private 16x16x4: A = dZ[row 4s + g4][cluster c16], B = po[row 4s + g4][16t + c16]
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
       const float a = DSw[(4 * s + g4) * 16 + c16];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) accC[t] = mfma16(a, INw[act_off(16 * t + c16, 4 * s + g4)], accC[t]);
+      for (int t = 0; t < D / 16; ++t) accC[t] = mfma16(a, INw[act_off(16 * t + c16, 4 * s + g4)], accC[t]);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    PHASE(1);
     // ---- layer 2 (proj.6): stage dp, h2 -> IN; dh2_pre = W2^T dp under the DMA
     stage_ds<DT>(DSw, dcur, D, ln);
+    if constexpr (LW) __syncthreads();  // B0: every wave's quarter of the W2 fragments landed
     dma_block16<D * 128>(INl, ar, 32 * D * 4);  // h2
     f32x16 dh[DT];
-    mm_acc<DT, DT>(p.WfT[2], dcur, dh);
+    mm_acc_f<DT, DT, 4 * DT, 16 * DT, LW>(LW ? WFs : p.WfT[2], dcur, dh);
     wait_vm_all();
+    PHASE(7);
     __syncthreads();  // B1: dp, h2 of every wave staged
-    acc[0] = outer_tile<REG>(DS, IN, w >> 1, w & 1, acc[0], ln);
-    if (tid < D) dbacc[2] += region_rowsum<REG>(DS, tid);
+    PHASE(2);
+    if constexpr (LW) load_wf(1);  // every wave is past its W2 chain
+    outer_stage_s<D>(DS, IN, acc[0], w, ln);
+    own_rowsum<D>(DSw, dbp[2], ln);
     {
       f32x16 hv[DT];
       read_act<DT>(hv, INw, ln);  // own h2 (relu mask)
@@ -1777,7 +1935,10 @@ __global__ __launch_bounds__(256, 2) void k_proj_bwd_s(const KArgs p) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) dcur[t][r] = (hv[t][r] > 0.f) ? dh[t][r] * ks : 0.f;
     }
+    if constexpr (LW) wait_vm_all();  // W1 fragments
+    PHASE(3);
     __syncthreads();  // B2: stage dW2 read out
+    PHASE(2);
     // ---- layer 1 (proj.3): stage dh2, h1 -> IN and x rows under dh1_pre = W1^T dh2
     stage_ds<DT>(DSw, dcur, D, ln);
     dma_block16<D * 128>(INl, ar, 0);  // h1
@@ -1788,11 +1949,14 @@ __global__ __launch_bounds__(256, 2) void k_proj_bwd_s(const KArgs p) {
 #pragma unroll
       for (int j = 0; j < NS / 4; ++j) x4[j] = *reinterpret_cast<const f32x4*>(X + h * NS + 4 * j);
     }
-    mm_acc<DT, DT>(p.WfT[1], dcur, dh);
+    mm_acc_f<DT, DT, 4 * DT, 16 * DT, LW>(LW ? WFs : p.WfT[1], dcur, dh);
     wait_vm_all();
+    PHASE(4);
     __syncthreads();  // B3
-    acc[1] = outer_tile<REG>(DS, IN, w >> 1, w & 1, acc[1], ln);
-    if (tid < D) dbacc[1] += region_rowsum<REG>(DS, tid);
+    PHASE(2);
+    if constexpr (LW) load_wf(0);  // every wave is past its W1 chain
+    outer_stage_s<D>(DS, IN, acc[1], w, ln);
+    own_rowsum<D>(DSw, dbp[1], ln);
     {
       f32x16 hv[DT];
       read_act<DT>(hv, INw, ln);  // own h1 (relu mask)
@@ -1801,32 +1965,48 @@ __global__ __launch_bounds__(256, 2) void k_proj_bwd_s(const KArgs p) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) dcur[t][r] = (hv[t][r] > 0.f) ? dh[t][r] * ks : 0.f;
     }
+    PHASE(3);
     __syncthreads();  // B4
+    PHASE(2);
     // ---- layer 0 (proj.0): stage dh1, x -> IN; this item's dQ / dK rows load under the last stage
     stage_ds<DT>(DSw, dcur, D, ln);
 #pragma unroll
     for (int s = 0; s < NS; ++s) INw[act_off(s + NS * h, c)] = rv ? x4[s >> 2][s & 3] : 0.f;
     float* dst = it.isK ? p.dK + ((int64_t)bh * p.M + rowc) * D : p.dQ + ((int64_t)bh * p.N + rowc) * D;
-    f32x4 old[2 * DT];
-#pragma unroll
-    for (int t = 0; t < DT; ++t)
-#pragma unroll
-      for (int g2 = 0; g2 < 4; g2 += 2) old[2 * t + g2 / 2] = *reinterpret_cast<const f32x4*>(dst + 32 * t + 8 * g2 + 4 * h);
-    f32x4 old2[2 * DT];
-#pragma unroll
-    for (int t = 0; t < DT; ++t)
-#pragma unroll
-      for (int g2 = 1; g2 < 4; g2 += 2) old2[2 * t + g2 / 2] = *reinterpret_cast<const f32x4*>(dst + 32 * t + 8 * g2 + 4 * h);
+    f32x4 old[2 * DT], old2[2 * DT];
     const bool more = (grp + 1) * 4 < n_items;
-    if (more) {  // private hat / gin regions are free again: next group's operands stream in now
-      prefetch_hat(item_of(grp + 1));
-      prefetch(item_of(grp + 1));
+    auto load_old = [&]() {
+#pragma unroll
+      for (int t = 0; t < DT; ++t)
+#pragma unroll
+        for (int g2 = 0; g2 < 4; g2 += 2) old[2 * t + g2 / 2] = *reinterpret_cast<const f32x4*>(dst + 32 * t + 8 * g2 + 4 * h);
+#pragma unroll
+      for (int t = 0; t < DT; ++t)
+#pragma unroll
+        for (int g2 = 1; g2 < 4; g2 += 2) old2[2 * t + g2 / 2] = *reinterpret_cast<const f32x4*>(dst + 32 * t + 8 * g2 + 4 * h);
+    };
+    auto prefetch_next = [&]() {
+      if (more) {  // private hat / gin regions are free again: next group's operands stream in now
+        prefetch_hat(item_of(grp + 1));
+        prefetch(item_of(grp + 1));
+      }
+    };
+    if constexpr (LW) {
+      wait_vm_all();  // W0 fragments
+    } else {
+      load_old();
+      prefetch_next();
     }
+    PHASE(5);
     __syncthreads();  // B5
-    acc[2] = outer_tile<REG>(DS, IN, w >> 1, w & 1, acc[2], ln);
-    if (tid < D) dbacc[0] += region_rowsum<REG>(DS, tid);
+    PHASE(2);
+    if constexpr (LW) prefetch_next();  // (after the W0 wait above)
+    outer_stage_s<D>(DS, IN, acc[2], w, ln);
+    own_rowsum<D>(DSw, dbp[0], ln);
+    if constexpr (LW) load_old();  // LW: the dQ / dK rows load under the dx chain (fewer live registers)
+    PHASE(3);
     f32x16 dxm[DT];
-    mm_acc<DT, DT>(p.WfT[0], dcur, dxm);  // second-path dx = W0^T dh1
+    mm_acc_f<DT, DT, 4 * DT, 16 * DT, LW>(LW ? WFs : p.WfT[0], dcur, dxm);  // second-path dx = W0^T dh1
     if (rv) {  // dQ / dK += MLP backward
 #pragma unroll
       for (int t = 0; t < DT; ++t)
@@ -1838,28 +2018,71 @@ __global__ __launch_bounds__(256, 2) void k_proj_bwd_s(const KArgs p) {
           *reinterpret_cast<f32x4*>(dst + 32 * t + 8 * g2 + 4 * h) = v;
         }
     }
-    __syncthreads();  // B6: DS / IN free for the next group
+    PHASE(6);
+    __syncthreads();  // B6: DS / IN free for the next group (LW: WF too)
+    PHASE(2);
+    if constexpr (LW) {
+      if (more) load_wf(2);
+    }
   }
-  // ---- slab: dW tiles and bias sums (written once), dS / dC summed over the 4 waves in a fixed order
-#pragma unroll
-  for (int l = 0; l < 3; ++l) {
-    const TileDst<D, 1> t = tile_dst<D, 1>(slab, (l == 0 ? Sf::G_W2 : l == 1 ? Sf::G_W1 : Sf::G_W0) + w);
-    tile_store<0>(t.base, t.ldo, t.orows, t.icols, t.ot, t.it, acc[l], false, lane);
-  }
-  const int tid = threadIdx.x;
-  if (tid < D) {
-    slab[3 * D * D + tid] = dbacc[0];
-    slab[3 * D * D + D + tid] = dbacc[1];
-    slab[3 * D * D + 2 * D + tid] = dbacc[2];
-  }
-  float* part = lds + w * (16 * 16 + 16 * D);  // [dS 16 x 16 | dC 16 x D] of this wave
+#ifdef CSA_PHASES
+  if (blockIdx.x == 0 && blockIdx.y == 0 && lane == 0)
+    printf("PHASES d=%d w=%d prefetch %llu preB1 %llu chainW2 %llu barrier %llu outer %llu chainW1 %llu stageX %llu dx %llu\n",
+           D, w, ph[0], ph[1], ph[7], ph[2], ph[3], ph[4], ph[5], ph[6]);
+#endif
+#undef PHASE
+  // ---- slab, written once: dW tiles, bias sums and dS / dC, wave partials combined in a fixed order
+  float* part = lds + w * Sh::PARTF;  // [dS 16 x 16 | dC 16 x D | db0 | db1 | db2] of this wave
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     part[(4 * g4 + e) * 16 + c16] = accS[e];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) part[256 + (4 * g4 + e) * D + 16 * t + c16] = accC[t][e];
+    for (int t = 0; t < D / 16; ++t) part[256 + (4 * g4 + e) * D + 16 * t + c16] = accC[t][e];
+  }
+#pragma unroll
+  for (int l = 0; l < 3; ++l)
+#pragma unroll
+    for (int u = 0; u < (D + 63) / 64; ++u)
+      if (lane + 64 * u < D) part[256 + 16 * D + l * D + lane + 64 * u] = dbp[l][u];
+  float* shr = lds + 4 * Sh::PARTF;  // d = 96: slot-2 halves of the shared tiles, [stage][wave < 3]
+  if constexpr (NSL == 3) {
+    if (w < 3) {
+#pragma unroll
+      for (int l = 0; l < 3; ++l)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) shr[(3 * l + w) * 1024 + 64 * r + lane] = acc[l][2][r];
+    }
   }
   __syncthreads();
+#pragma unroll
+  for (int l = 0; l < 3; ++l) {
+    const int g0 = l == 0 ? Sf::G_W2 : l == 1 ? Sf::G_W1 : Sf::G_W0;
+    if constexpr (NSL == 1) {
+      const TileDst<D, 1> t = tile_dst<D, 1>(slab, g0 + w);
+      tile_store<0>(t.base, t.ldo, t.orows, t.icols, t.ot, t.it, acc[l][0], false, lane);
+    } else {
+      f32x16 v = acc[l][0];
+      if (w > 0) {  // tile 2w: quarters [0, w) from wave w - 1, then [w, 4) from this wave
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = shr[(3 * l + w - 1) * 1024 + 64 * r + lane] + v[r];
+      }
+      const TileDst<D, 1> t0 = tile_dst<D, 1>(slab, g0 + 2 * w);
+      tile_store<0>(t0.base, t0.ldo, t0.orows, t0.icols, t0.ot, t0.it, v, false, lane);
+      const TileDst<D, 1> t1 = tile_dst<D, 1>(slab, g0 + 2 * w + 1);
+      tile_store<0>(t1.base, t1.ldo, t1.orows, t1.icols, t1.ot, t1.it, acc[l][1], false, lane);
+      if (w == 3) {
+        const TileDst<D, 1> t2 = tile_dst<D, 1>(slab, g0 + 8);
+        tile_store<0>(t2.base, t2.ldo, t2.orows, t2.icols, t2.ot, t2.it, acc[l][2], false, lane);
+      }
+    }
+  }
+  const int tid = threadIdx.x;
+  for (int e = tid; e < 3 * D; e += 256) {
+    float v = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) v += lds[ww * Sh::PARTF + 256 + 16 * D + e];
+    slab[3 * D * D + e] = v;  // db0 | db1 | db2
+  }
   float* sC = slab + 3 * D * D + 3 * D;  // (32 x D), rows >= 16 zero
   float* sS = sC + 32 * D;               // (32 x 32), rows / cols >= 16 zero
   for (int e = tid; e < 32 * D + 32 * 32; e += 256) {
@@ -1868,14 +2091,14 @@ __global__ __launch_bounds__(256, 2) void k_proj_bwd_s(const KArgs p) {
       const int a = e / D, f = e % D;
       if (a < 16) {
 #pragma unroll
-        for (int ww = 0; ww < 4; ++ww) v += lds[ww * (256 + 16 * D) + 256 + a * D + f];
+        for (int ww = 0; ww < 4; ++ww) v += lds[ww * Sh::PARTF + 256 + a * D + f];
       }
       sC[e] = v;
     } else {
       const int q = e - 32 * D, a = q / 32, bb = q % 32;
       if (a < 16 && bb < 16) {
 #pragma unroll
-        for (int ww = 0; ww < 4; ++ww) v += lds[ww * (256 + 16 * D) + a * 16 + bb];
+        for (int ww = 0; ww < 4; ++ww) v += lds[ww * Sh::PARTF + a * 16 + bb];
       }
       sS[q] = v;
     }
@@ -2227,7 +2450,7 @@ csa_status launch_bwd(const csa_sbm_bwd_args* b, const Layout& L, hipStream_t st
       return check_launch("memset slabs");
     {
       Stage sg(pf, CSA_STAGE_PROJ_BWD, st);
-      if constexpr (D == 64 && KPH == 8) {  // k <= 16
+      if constexpr ((D == 64 || D == 96) && KPH == 8) {  // k <= 16
         using Ss = ProjBwdSmallShape<D>;
         (void)hipFuncSetAttribute((const void*)k_proj_bwd_s<D>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)Ss::LDS_BYTES);

@@ -4,7 +4,7 @@ set -o pipefail
 export TMPDIR=/tmp
 OUT=${1:-gpurun_out/pmc}
 mkdir -p "$OUT"
-CMD="python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-train"
+CMD=${PMC_CMD:-"python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-train"}
 i=0
 for grp in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES" \
            "SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES" \
