@@ -51,6 +51,74 @@ def linear(x, w, b=None):
     return _LinearFn.apply(x, w, b)
 
 
+def _packed(ts):
+    """The tensor spanning three same-shape contiguous tensors stored back to back in one storage
+    (pack_adjacent_), or None."""
+    a = ts[0]
+    n = a.numel()
+    for i, t in enumerate(ts):
+        if (not t.is_contiguous() or t.shape != a.shape or t.dtype != a.dtype or t.device != a.device
+                or t.untyped_storage().data_ptr() != a.untyped_storage().data_ptr()
+                or t.storage_offset() != a.storage_offset() + i * n):
+            return None
+    return a.detach().as_strided((len(ts) * a.shape[0],) + tuple(a.shape[1:]), a.stride())
+
+
+def pack_adjacent_(params):
+    """Move the data of same-shape parameters into one buffer, back to back (each keeps its own
+    Parameter object, shape and state_dict key). Returns True when they are (now) packed."""
+    if _packed(params) is not None:
+        return True
+    a = params[0]
+    if any(p.shape != a.shape or p.dtype != a.dtype or p.device != a.device for p in params):
+        return False
+    with torch.no_grad():
+        buf = torch.cat([p.detach() for p in params], 0)
+        n = a.shape[0]
+        for i, p in enumerate(params):
+            p.data = buf[i * n:(i + 1) * n]
+    return True
+
+
+class _LinearPackedFn(torch.autograd.Function):
+    """y = x [W_0; W_1; W_2]^T + [b_0; b_1; b_2] for weights / biases packed back to back: one GEMM
+    over the packed memory, no per-forward concatenation; the backward's single dW / db GEMM is
+    handed back as three views."""
+
+    @staticmethod
+    def forward(ctx, x, w0, w1, w2, b0, b1, b2):
+        W, B = _packed((w0, w1, w2)), _packed((b0, b1, b2))
+        ctx.save_for_backward(x, W)
+        ctx.n = w0.shape[0]
+        return F.linear(x, W, B)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, W = ctx.saved_tensors
+        n = ctx.n
+        gy2 = gy.reshape(-1, gy.shape[-1])
+        dx = gy @ W if ctx.needs_input_grad[0] else None
+        dw = gy2.t() @ x.reshape(-1, x.shape[-1])
+        g = gy2 if gy2.is_contiguous() and gy2.dtype == torch.float32 else gy2.float().contiguous()
+        db = bias_grad(g).to(gy.dtype)
+        return (dx,) + tuple(dw[i * n:(i + 1) * n] for i in range(3)) + tuple(db[i * n:(i + 1) * n] for i in range(3))
+
+
+def linear3(x, linears):
+    """The three nn.Linear layers `linears` applied to the same x as one GEMM, outputs concatenated on
+    the last dim: (..., 3 out). Their parameters are packed back to back on first use (and again after
+    a device move), so no per-forward weight concatenation happens."""
+    ws, bs = [l.weight for l in linears], [l.bias for l in linears]
+    if (x.is_cuda and x.dtype == torch.float32 and all(b is not None for b in bs)
+            and pack_adjacent_(ws) and pack_adjacent_(bs)):
+        if _batch_major(x):
+            return _LinearPackedFn.apply(x.transpose(0, 1), *ws, *bs).transpose(0, 1)
+        return _LinearPackedFn.apply(x, *ws, *bs)
+    w = torch.cat(ws, 0)
+    b = torch.cat(bs, 0) if all(b is not None for b in bs) else None
+    return linear(x, w, b)
+
+
 class Linear(nn.Linear):
     def forward(self, x):
         return linear(x, self.weight, self.bias)

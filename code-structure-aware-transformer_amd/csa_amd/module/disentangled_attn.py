@@ -9,7 +9,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import rel_ops
-from ..glue import Linear, linear, split_heads3
+from ..glue import Linear, linear3, split_heads3
 
 __all__ = ["DisentangledAttn", "transpose_for_scores", "_get_clones"]
 
@@ -40,10 +40,7 @@ class DisentangledAttn(nn.Module):
 
     def forward(self, query, key, value, rel_emb, rel, mask):
         if query is key and key is value:  # self-attention (CSE_layer, csa_trans.py:231-233): one QKV GEMM
-            qkv = self.linear_layers[:3]
-            w = torch.cat([l.weight for l in qkv], 0)
-            b = torch.cat([l.bias for l in qkv], 0)
-            query, key, value = split_heads3(linear(query, w, b), self.h)
+            query, key, value = split_heads3(linear3(query, self.linear_layers[:3]), self.h)
         else:
             query, key, value = [transpose_for_scores(l(x), self.h)
                                  for l, x in zip(self.linear_layers, (query, key, value))]

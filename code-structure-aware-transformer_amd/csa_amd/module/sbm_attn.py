@@ -19,7 +19,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
-from ..glue import Linear, linear, split_heads3
+from ..glue import Linear, linear3, split_heads3
 
 __all__ = ["SBMAttention", "FullAttention", "Attention"]
 
@@ -101,9 +101,7 @@ class Attention(nn.Module):
         X, mask, deliver = inputs
         # W_q / W_k / W_v as ONE (3 H d x dim) GEMM (parameters and state_dict keys unchanged); Q, K, V
         # are strided (B, H, N, d) views of its output, consumed in place by the kernels
-        w = torch.cat([self.W_q.weight, self.W_k.weight, self.W_v.weight], 0)
-        b = torch.cat([self.W_q.bias, self.W_k.bias, self.W_v.bias], 0)
-        Q, K, V = split_heads3(linear(X, w, b), self.num_head)
+        Q, K, V = split_heads3(linear3(X, (self.W_q, self.W_k, self.W_v)), self.num_head)
         with torch.autocast(device_type="cuda", enabled=False):  # sbm_attn.py:120
             attn_out, sparsity, graph, attn = self.attn(Q.float(), K.float(), V.float(), mask.float())
         attn_out = self.combine_heads(attn_out)
