@@ -11,7 +11,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CSA_HIP_LIB", os.path.join(_HERE, "lib", "libcsa_hip.so"))
 
-CSA_ABI_VERSION = 2
+CSA_ABI_VERSION = 3
 CSA_FLAG_DENSE = 1
 CSA_DTYPE_F32, CSA_DTYPE_BF16 = 0, 1
 STATUS = {0: "CSA_OK", 1: "CSA_INVALID_ARG", 2: "CSA_UNSUPPORTED_SHAPE", 3: "CSA_LAUNCH_FAILED"}
@@ -44,6 +44,7 @@ class SbmFwdArgs(ctypes.Structure):
         ("flags", u32), ("dtype", u32),
         ("X", vp), ("sparsity", vp), ("state", vp),
         ("prof", ctypes.POINTER(CsaProf)),
+        ("x_sb", i64), ("x_sh", i64), ("x_sn", i64),  # ABI v3: 0,0,0 = (B,H,N,d) contiguous
     ]
 
 
@@ -55,6 +56,8 @@ class SbmBwdArgs(ctypes.Structure):
         ("dcluster_w", vp), ("dproj_w", vp * 3), ("dproj_b", vp * 3),
         ("workspace", vp),
         ("prof", ctypes.POINTER(CsaProf)),
+        ("dx_sb", i64), ("dx_sh", i64), ("dx_sn", i64), ("dq_sb", i64), ("dq_sh", i64), ("dq_sn", i64),
+        ("dk_sb", i64), ("dk_sh", i64), ("dk_sn", i64), ("dv_sb", i64), ("dv_sh", i64), ("dv_sn", i64),
     ]
 
 
@@ -70,6 +73,7 @@ class RelAttnArgs(ctypes.Structure):
         ("rel_head_group", i64), ("dtype", u32),
         ("out", vp), ("row_stats", vp),
         ("state", vp),
+        ("o_sb", i64), ("o_sh", i64), ("o_sn", i64),  # ABI v3: 0,0,0 = contiguous
     ]
 
 
@@ -80,6 +84,8 @@ class RelAttnBwdArgs(ctypes.Structure):
         ("dq", vp), ("dk", vp), ("dv", vp),
         ("dlq", vp), ("dlk", vp),
         ("workspace", vp),
+        ("do_sb", i64), ("do_sh", i64), ("do_sn", i64), ("dq_sb", i64), ("dq_sh", i64), ("dq_sn", i64),
+        ("dk_sb", i64), ("dk_sh", i64), ("dk_sn", i64), ("dv_sb", i64), ("dv_sh", i64), ("dv_sn", i64),
     ]
 
 

@@ -245,6 +245,10 @@ class _SplitHeads3(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dq, dk, dv):
         B, N, C = ctx.shape
+        if dq is not None and dk is not None and dv is not None:
+            from .ops import packed_qkv
+            if packed_qkv(dq, dk, dv):  # the kernels wrote the packed layout already (ops.packed_grads)
+                return dq.as_strided((B, N, C), (N * C, C, 1), dq.storage_offset()), None
         ref = next(g for g in (dq, dk, dv) if g is not None)
         out = torch.empty(B, N, C, device=ref.device, dtype=ref.dtype)
         ov = out.view(B, N, 3, ref.shape[1], C // (3 * ref.shape[1]))

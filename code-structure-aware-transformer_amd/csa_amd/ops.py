@@ -54,6 +54,31 @@ def _bhnd(t: torch.Tensor) -> torch.Tensor:
     return t if ok else t.contiguous()
 
 
+def packed_qkv(Q, K, V) -> bool:
+    """Q, K, V are the three head-major views of one packed (B, N, 3, H, d) projection output
+    (glue.split_heads3): same storage, K / V offset by H*d / 2*H*d elements."""
+    if not (Q.shape == K.shape == V.shape and Q.stride() == K.stride() == V.stride() and Q.dim() == 4):
+        return False
+    B, H, N, d = Q.shape
+    if Q.stride() != (N * 3 * H * d, d, 3 * H * d, 1) or Q.dtype != torch.float32:
+        return False
+    st = Q.untyped_storage().data_ptr()
+    return (K.untyped_storage().data_ptr() == st and V.untyped_storage().data_ptr() == st
+            and K.storage_offset() == Q.storage_offset() + H * d and V.storage_offset() == Q.storage_offset() + 2 * H * d)
+
+
+def packed_grads(B, H, N, d, device):
+    """A packed (B, N, 3, H, d) gradient buffer and its three head-major (B, H, N, d) views."""
+    P = torch.empty(B, N, 3, H, d, device=device, dtype=torch.float32)
+    return P, [P[:, :, i].transpose(1, 2) for i in range(3)]
+
+
+def head_major_out(B, H, N, d, device):
+    """(B, H, N, d) view of a (B, N, H, d) buffer: combine_heads (sbm_attn.py:143-146,
+    disentangled_attn.py:63) of it is a free view."""
+    return torch.empty(B, N, H, d, device=device, dtype=torch.float32).transpose(1, 2)
+
+
 def _fwd_struct(Q, K, V, mask, cluster_w, pw, pb, u, seed, offset, attn_p, proj_p, dense, X, sp, state, k,
                 bf16=False):
     B, H, N, d = Q.shape
@@ -78,6 +103,8 @@ def _fwd_struct(Q, K, V, mask, cluster_w, pw, pb, u, seed, offset, attn_p, proj_
     a.flags = CSA_FLAG_DENSE if dense else 0
     a.dtype = CSA_DTYPE_BF16 if bf16 else CSA_DTYPE_F32
     a.X = X.data_ptr()
+    if X.dim() == 4:
+        a.x_sb, a.x_sh, a.x_sn = X.stride()[:3]
     a.state = state.data_ptr()
     return a
 
@@ -113,7 +140,7 @@ def sbm_fwd_op(Q: torch.Tensor, K: torch.Tensor, V: torch.Tensor, mask: Optional
     flags = CSA_FLAG_DENSE if dense else 0
     if not L.csa_sbm_supported(d, k, flags):
         raise RuntimeError(f"csa::sbm_fwd: unsupported head_dim={d} / num_clusters={k}")
-    X = torch.empty(B, H, N, d, device=Q.device, dtype=torch.float32)
+    X = head_major_out(B, H, N, d, Q.device)
     sp = torch.empty(0 if dense else H, device=Q.device, dtype=torch.float32)
     state = torch.empty(L.csa_sbm_state_bytes(B, H, N, M, d, k, flags), device=Q.device, dtype=torch.uint8)
     a = _fwd_struct(Q, K, V, mask, cw, pw, pb, u, seed, offset, attn_p, proj_p, dense, X, sp, state, k, bf16)
@@ -126,7 +153,7 @@ def sbm_fwd_op(Q: torch.Tensor, K: torch.Tensor, V: torch.Tensor, mask: Optional
 @sbm_fwd_op.register_fake
 def _(Q, K, V, mask, cluster_w, proj_w, proj_b, uniforms, k, seed, offset, attn_p, proj_p, dense, bf16=False):
     B, H, N, d = Q.shape
-    return (Q.new_empty(B, H, N, d), Q.new_empty(0 if dense else H),
+    return (Q.new_empty(B, N, H, d).transpose(1, 2), Q.new_empty(0 if dense else H),
             Q.new_empty(lib().csa_sbm_state_bytes(B, H, N, K.shape[2], d, k, CSA_FLAG_DENSE if dense else 0),
                         dtype=torch.uint8))
 
@@ -144,6 +171,7 @@ def sbm_maps_op(Q: torch.Tensor, K: torch.Tensor, V: torch.Tensor, mask: Optiona
     a.flags = CSA_FLAG_DENSE if dense else 0
     a.k = 0 if dense else k
     a.X = Q.data_ptr()  # unused by maps; must be a valid aligned pointer for validation
+    a.x_sb = a.x_sh = a.x_sn = 0
     if not dense:  # validation of non-dense args needs these non-null (unused by the maps kernel)
         a.cluster_w = a.Q
         a.sparsity = a.Q
@@ -166,8 +194,10 @@ def sbm_bwd_op(Q: torch.Tensor, K: torch.Tensor, V: torch.Tensor, mask: Optional
                cluster_w: Optional[torch.Tensor], proj_w: List[torch.Tensor], proj_b: List[torch.Tensor],
                k: int, attn_p: float, proj_p: float, seed: int, offset: int, dense: bool, state: torch.Tensor,
                X: torch.Tensor, dX: torch.Tensor, dsparsity: Optional[torch.Tensor],
-               dgraph: Optional[torch.Tensor], bf16: bool = False) -> List[torch.Tensor]:
-    """Backward of csa::sbm_fwd. Returns [dQ, dK, dV] (+ [dcluster_w, dW0, db0, dW1, db1, dW2, db2] if not dense)."""
+               dgraph: Optional[torch.Tensor], bf16: bool = False, packed: bool = False) -> List[torch.Tensor]:
+    """Backward of csa::sbm_fwd. Returns [dQ, dK, dV] (+ [dcluster_w, dW0, db0, dW1, db1, dW2, db2] if not dense).
+    packed: [dQ, dK, dV] is replaced by ONE packed (B, N, 3, H, d) tensor (the gradient of a fused QKV
+    projection, written in place by the kernels; see packed_qkv)."""
     Q, K, V, mask, cw, pw, pb, _ = _prep(Q, K, V, mask, cluster_w, proj_w, proj_b, None)
     B, H, N, d = Q.shape
     M = K.shape[2]
@@ -175,14 +205,22 @@ def sbm_bwd_op(Q: torch.Tensor, K: torch.Tensor, V: torch.Tensor, mask: Optional
     flags = CSA_FLAG_DENSE if dense else 0
     sp = torch.empty(0 if dense else H, device=Q.device, dtype=torch.float32)
     a = _fwd_struct(Q, K, V, mask, cw, pw, pb, None, seed, offset, attn_p, proj_p, dense, X, sp, state, k, bf16)
-    dX = dX.float().contiguous()
-    dQ = torch.empty(B, H, N, d, device=Q.device, dtype=torch.float32)
-    dK = torch.empty(B, H, M, d, device=Q.device, dtype=torch.float32)
-    dV = torch.empty_like(dK)
+    dX = _bhnd(dX)  # strided (e.g. the combine_heads view's gradient) without a copy
+    if packed:
+        P, (dQ, dK, dV) = packed_grads(B, H, N, d, Q.device)
+        outs = [P]
+    else:
+        dQ = torch.empty(B, H, N, d, device=Q.device, dtype=torch.float32)
+        dK = torch.empty(B, H, M, d, device=Q.device, dtype=torch.float32)
+        dV = torch.empty_like(dK)
+        outs = [dQ, dK, dV]
     b = SbmBwdArgs()
     b.fwd = ctypes.pointer(a)
     b.dX, b.dQ, b.dK, b.dV = dX.data_ptr(), dQ.data_ptr(), dK.data_ptr(), dV.data_ptr()
-    outs = [dQ, dK, dV]
+    b.dx_sb, b.dx_sh, b.dx_sn = dX.stride()[:3]
+    b.dq_sb, b.dq_sh, b.dq_sn = dQ.stride()[:3]
+    b.dk_sb, b.dk_sh, b.dk_sn = dK.stride()[:3]
+    b.dv_sb, b.dv_sh, b.dv_sn = dV.stride()[:3]
     keep = []
     if not dense:
         if dsparsity is not None:
@@ -209,8 +247,9 @@ def sbm_bwd_op(Q: torch.Tensor, K: torch.Tensor, V: torch.Tensor, mask: Optional
 
 @sbm_bwd_op.register_fake
 def _(Q, K, V, mask, cluster_w, proj_w, proj_b, k, attn_p, proj_p, seed, offset, dense, state, X, dX, dsparsity,
-      dgraph, bf16=False):
-    outs = [torch.empty_like(Q), torch.empty_like(K), torch.empty_like(V)]
+      dgraph, bf16=False, packed=False):
+    B, H, N, d = Q.shape
+    outs = [Q.new_empty(B, N, 3, H, d)] if packed else [torch.empty_like(Q), torch.empty_like(K), torch.empty_like(V)]
     if not dense:
         outs.append(torch.empty_like(cluster_w))
         for i in range(3):
@@ -274,6 +313,7 @@ class SBMAttentionFunction(torch.autograd.Function):
             graph, attn = torch.ops.csa.sbm_maps(Q, K, V, mask, state, k, dense)
         ctx.save_for_backward(Q, K, V, mask, cluster_w, w0, b0, w1, b1, w2, b2, state, X)
         ctx.cfg = (k, attn_p, proj_p, seed, dense, bf16)
+        ctx.packed = packed_qkv(Q, K, V)
         ctx.set_materialize_grads(False)
         return X, (sp if not dense else None), graph, attn
 
@@ -289,8 +329,12 @@ class SBMAttentionFunction(torch.autograd.Function):
         pw = [] if dense else [w0, w1, w2]
         pb = [] if dense else [b0, b1, b2]
         g = torch.ops.csa.sbm_bwd(Q, K, V, mask, None if dense else cluster_w, pw, pb, k, attn_p, proj_p, seed, 0,
-                                  dense, state, X, dX, dsp, None if dense else dgraph, bf16)
-        dQ, dK, dV = g[:3]
+                                  dense, state, X, dX, dsp, None if dense else dgraph, bf16, ctx.packed)
+        if ctx.packed:  # the three head-major views of the packed gradient (split_heads3's backward takes it whole)
+            dQ, dK, dV = (g[0][:, :, i].transpose(1, 2) for i in range(3))
+            g = [None, None] + list(g)
+        else:
+            dQ, dK, dV = g[:3]
         if dense:
             return (dQ, dK, dV) + (None,) * 15
         dC, dw0, db0, dw1, db1, dw2, db2 = g[3:]

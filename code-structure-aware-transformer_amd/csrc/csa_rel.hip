@@ -164,9 +164,11 @@ struct RelArgs {
   const uint8_t *rel, *mask; int64_t rel_sb, rel_sh, mask_sb, mask_sh;
   const float *c2p, *p2ct;  // (B,H,N,Lp), (B,H,N,Lp)
   float *out, *stats;
+  int64_t o_sb, o_sh, o_sn;  // element strides of out (fused path; contiguous otherwise)
   float inv_scale;
   // backward
   const float* dout;
+  int64_t do_sb, do_sh, do_sn, dq_sb, dq_sh, dq_sn, dk_sb, dk_sh, dk_sn, dv_sb, dv_sh, dv_sn;
   float *dq, *G, *P;
   // fused path (d_k = 64): prepared planes, plane count, padded size, bins layout, gather-backward output
   const uint16_t *RM, *RT; int P_, NP, KB2, LB; int64_t ldx;
@@ -752,7 +754,7 @@ __global__ __launch_bounds__(64, 2) void k_rel_fwd_f(const RelArgs p) {
     for (int t = 0; t < DT; ++t)
 #pragma unroll
       for (int r = 0; r < 16; ++r) o[t][r] *= inv;
-    store_rows_f<DT>(p.out + ((int64_t)bh * p.N + i) * D, o);
+    store_rows_f<DT>(p.out + b * p.o_sb + hd * p.o_sh + (int64_t)i * p.o_sn, o);
     if (h == 0) {
       p.stats[((int64_t)bh * p.N + i) * 2] = m_run;
       p.stats[((int64_t)bh * p.N + i) * 2 + 1] = inv;
@@ -789,7 +791,7 @@ __global__ __launch_bounds__(64, 1) void k_rel_bwd_qf(const RelArgs p) {
   Codes cm = load_codes(rmrow, 0);
   float q[NS], dO[NS];
   load_run<NS>(q, p.q + b * p.q_sb + hd * p.q_sh + (int64_t)ic * p.q_sn + h * NS, iv);
-  load_run<NS>(dO, p.dout + ((int64_t)bh * p.N + ic) * D + h * NS, iv);
+  load_run<NS>(dO, p.dout + b * p.do_sb + hd * p.do_sh + (int64_t)ic * p.do_sn + h * NS, iv);
   dma64(Kl, kr, kpat, kld, 0);
   dma64(Vl, vr, vpat, vld, 0);
   dma_block16<4096>(Rl, rbr, 0);
@@ -797,7 +799,7 @@ __global__ __launch_bounds__(64, 1) void k_rel_bwd_qf(const RelArgs p) {
   float dp = 0.f;
   {
     float o[NS];
-    load_run<NS>(o, p.out + ((int64_t)bh * p.N + ic) * D + h * NS, iv);
+    load_run<NS>(o, p.out + b * p.o_sb + hd * p.o_sh + (int64_t)ic * p.o_sn + h * NS, iv);
 #pragma unroll
     for (int s = 0; s < NS; ++s) dp = fmaf(dO[s], o[s], dp);
   }
@@ -892,7 +894,7 @@ __global__ __launch_bounds__(64, 1) void k_rel_bwd_qf(const RelArgs p) {
   bins_times<DT>(dq, bins, p.LB, p.KB2, p.lk + (int64_t)hd * p.L * D, p.L, D);
 #endif
   if (iv) {
-    store_rows_f<DT>(p.dq + ((int64_t)bh * p.N + i) * D, dq);
+    store_rows_f<DT>(p.dq + b * p.dq_sb + hd * p.dq_sh + (int64_t)i * p.dq_sn, dq);
     if (h == 0) {
       f32x4 st;
       st[0] = rmax; st[1] = rinv; st[2] = delta; st[3] = 0.f;
@@ -922,20 +924,21 @@ __global__ __launch_bounds__(64, 1) void k_rel_bwd_kf(const RelArgs p) {
   const int jc = imin(j, p.N - 1);
   const int qld = (int)p.q_sn * 4;
   const __amdgpu_buffer_rsrc_t qr_ = make_rsrc(p.q + b * p.q_sb + hd * p.q_sh, (p.N - 1) * qld + D * 4);
-  const __amdgpu_buffer_rsrc_t xr_ = make_rsrc(p.dout + (int64_t)bh * p.N * D, p.N * D * 4);
+  const int xld = (int)p.do_sn * 4;
+  const __amdgpu_buffer_rsrc_t xr_ = make_rsrc(p.dout + b * p.do_sb + hd * p.do_sh, (p.N - 1) * xld + D * 4);
   const __amdgpu_buffer_rsrc_t sr_ = make_rsrc(p.qstat + (int64_t)bh * p.N * 4, p.N * 16);
   // bias tiles (qb, kbi) for qb = 0.. are NKB tiles apart: descriptor over the whole (b,h) table
   const __amdgpu_buffer_rsrc_t rbr = make_rsrc(p.RB + (int64_t)bh * p.NQB * p.NKB * 1024, p.NQB * p.NKB * 4096);
   lds_zero<(2 * IMG + 512) / 4>(lds);
   for (int e = lane; e < 32 * p.LB; e += 64) bins[e] = 0.f;
-  const DmaPat qpat = dma_pat(SW_BOTH, qld), xpat = dma_pat(SW_BOTH, 4 * D);
+  const DmaPat qpat = dma_pat(SW_BOTH, qld), xpat = dma_pat(SW_BOTH, xld);
   const uint16_t* rmrow = prep_row(p, p.RM, b, hd, jc);
   Codes cm = load_codes(rmrow, 0);
   float kr[NS], vr[NS];
   load_run<NS>(kr, p.k + b * p.k_sb + hd * p.k_sh + (int64_t)jc * p.k_sn + h * NS, jv);
   load_run<NS>(vr, p.v + b * p.v_sb + hd * p.v_sh + (int64_t)jc * p.v_sn + h * NS, jv);
   dma64(Ql, qr_, qpat, qld, 0);
-  dma64(Xl, xr_, xpat, 4 * D, 0);
+  dma64(Xl, xr_, xpat, xld, 0);
   dma_tile_contig<4>(Sl, sr_, 0);
   dma_block16<4096>(Rl, rbr, kbi * 4096);
   const int rcol = 2 * IMG + 512 + 4 * rb_off(0, tile_pos(c));  // + 128 row: this key's bias in row `row`
@@ -1021,7 +1024,7 @@ __global__ __launch_bounds__(64, 1) void k_rel_bwd_kf(const RelArgs p) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (qb + 1 < p.NQB) {
       dma64(Ql, qr_, qpat, qld, i0 + 32);
-      dma64(Xl, xr_, xpat, 4 * D, i0 + 32);
+      dma64(Xl, xr_, xpat, xld, i0 + 32);
       dma_tile_contig<4>(Sl, sr_, i0 + 32);
       dma_block16<4096>(Rl, rbr, ((qb + 1) * p.NKB + kbi) * 4096);
       cm = load_codes(rmrow, qb + 1);
@@ -1035,8 +1038,8 @@ __global__ __launch_bounds__(64, 1) void k_rel_bwd_kf(const RelArgs p) {
   bins_times<DT>(dk, bins, p.LB, p.KB2, p.lq + (int64_t)hd * p.L * D, p.L, D);
 #endif
   if (jv) {
-    store_rows_f<DT>(p.dk + ((int64_t)bh * p.N + j) * D, dk);
-    store_rows_f<DT>(p.dv + ((int64_t)bh * p.N + j) * D, dv);
+    store_rows_f<DT>(p.dk + b * p.dk_sb + hd * p.dk_sh + (int64_t)j * p.dk_sn, dk);
+    store_rows_f<DT>(p.dv + b * p.dv_sb + hd * p.dv_sh + (int64_t)j * p.dv_sn, dv);
   }
   bins_store_t(p.gp2ct + (int64_t)bh * p.Lp * p.ldx, p.ldx, j, bins, p.LB, p.KB2, p.Lp, jv);
 }
@@ -1108,6 +1111,11 @@ RelLayout rel_layout(int64_t B, int64_t H, int64_t N, int64_t L, int64_t d) {
   return R;
 }
 
+// a zero stride triple, or the (B,H,N,d)-contiguous one
+inline bool contig3(int64_t sb, int64_t sh, int64_t sn, int64_t H, int64_t N, int64_t d) {
+  return (sb == 0 && sh == 0 && sn == 0) || (sb == H * N * d && sh == N * d && sn == d);
+}
+
 csa_status validate_rel(const csa_rel_attn_args* a) {
   if (!a) return rfail(CSA_INVALID_ARG, "null args");
   if (a->B < 1 || a->H < 1 || a->N < 1 || a->L < 1) return rfail(CSA_INVALID_ARG, "B, H, N, L must be >= 1");
@@ -1123,8 +1131,10 @@ csa_status validate_rel(const csa_rel_attn_args* a) {
     return (((uintptr_t)ptr) % 16 == 0) && sb % 4 == 0 && sh % 4 == 0 && sn % 4 == 0;
   };
   if (!al16(a->q, a->q_sb, a->q_sh, a->q_sn) || !al16(a->k, a->k_sb, a->k_sh, a->k_sn) ||
-      !al16(a->v, a->v_sb, a->v_sh, a->v_sn) || ((uintptr_t)a->out) % 16)
+      !al16(a->v, a->v_sb, a->v_sh, a->v_sn) || !al16(a->out, a->o_sb, a->o_sh, a->o_sn))
     return rfail(CSA_INVALID_ARG, "q/k/v/out must be 16-byte aligned with strides multiple of 4 elements");
+  if (a->d != 64 && !contig3(a->o_sb, a->o_sh, a->o_sn, a->H, a->N, a->d))
+    return rfail(CSA_UNSUPPORTED_SHAPE, "a strided out needs d_k = 64");
   return CSA_OK;
 }
 
@@ -1143,6 +1153,12 @@ RelArgs make_rel(const csa_rel_attn_args* a, const RelLayout& R) {
   p.c2p = (const float*)((char*)ws + R.c2p);
   p.p2ct = (const float*)((char*)ws + R.p2ct);
   p.out = a->out; p.stats = a->row_stats;
+  {
+    const bool oc = a->o_sb == 0 && a->o_sh == 0 && a->o_sn == 0;  // zero triple: contiguous
+    p.o_sb = oc ? a->H * a->N * a->d : a->o_sb;
+    p.o_sh = oc ? a->N * a->d : a->o_sh;
+    p.o_sn = oc ? a->d : a->o_sn;
+  }
   p.inv_scale = 1.f / sqrtf(3.f * (float)a->d);
   p.lq = a->lq; p.lk = a->lk;
   p.bf16 = a->dtype == CSA_DTYPE_BF16;
@@ -1259,6 +1275,26 @@ csa_status csa_rel_attn_bwd(const csa_rel_attn_bwd_args* b, void* stream) {
   void* ws = b->workspace;
   RelArgs p = make_rel(a, R);
   p.dout = b->dout; p.dq = b->dq;
+  {
+    auto al16 = [](const void* ptr, int64_t sb, int64_t sh, int64_t sn) {
+      return (((uintptr_t)ptr) % 16 == 0) && sb % 4 == 0 && sh % 4 == 0 && sn % 4 == 0;
+    };
+    const int64_t t[4][3] = {{b->do_sb, b->do_sh, b->do_sn}, {b->dq_sb, b->dq_sh, b->dq_sn},
+                             {b->dk_sb, b->dk_sh, b->dk_sn}, {b->dv_sb, b->dv_sh, b->dv_sn}};
+    const void* ptrs[4] = {b->dout, b->dq, b->dk, b->dv};
+    int64_t* dst[4][3] = {{&p.do_sb, &p.do_sh, &p.do_sn}, {&p.dq_sb, &p.dq_sh, &p.dq_sn},
+                          {&p.dk_sb, &p.dk_sh, &p.dk_sn}, {&p.dv_sb, &p.dv_sh, &p.dv_sn}};
+    for (int u = 0; u < 4; ++u) {
+      const bool c = t[u][0] == 0 && t[u][1] == 0 && t[u][2] == 0;
+      if (!R.fused && !contig3(t[u][0], t[u][1], t[u][2], a->H, a->N, a->d))
+        return rfail(CSA_UNSUPPORTED_SHAPE, "strided dout/dq/dk/dv need d_k = 64");
+      if (!al16(ptrs[u], t[u][0], t[u][1], t[u][2]))
+        return rfail(CSA_INVALID_ARG, "dout/dq/dk/dv must be 16-byte aligned with strides multiple of 4 elements");
+      *dst[u][0] = c ? a->H * a->N * a->d : t[u][0];
+      *dst[u][1] = c ? a->N * a->d : t[u][1];
+      *dst[u][2] = c ? a->d : t[u][2];
+    }
+  }
   p.G = (float*)((char*)ws + R.G);
   p.P = (float*)((char*)ws + R.P);
   const int B = (int)a->B, H = (int)a->H, N = (int)a->N, L = (int)a->L, D = (int)a->d;

@@ -283,10 +283,11 @@ struct KArgs {
   uint32_t drop_thr, pdrop_thr;  // 16-bit keep thresholds: keep <=> u16 >= thr (thr = ceil(p * 65536))
   int bf16;                      // CSA_DTYPE_BF16: bf16 MFMA for the N^2 contractions (wave-uniform branch)
   // outputs
-  float* X;
+  float* X; int64_t x_sb, x_sh, x_sn;
   // backward
   const float *dX, *dsp, *dgraph;
   float *dQ, *dK, *dV, *dQh, *dT, *slab;
+  int64_t dx_sb, dx_sh, dx_sn, dq_sb, dq_sh, dq_sn, dk_sb, dk_sh, dk_sn, dv_sb, dv_sh, dv_sn;
   int G; int64_t slab_floats;
 };
 
@@ -813,7 +814,7 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd
   const float dscale = DROP ? 1.f / (1.f - p.attn_p) : 1.f;  // dropout's 1/(1-p), applied once per row
   const float inv = dscale / (Z * Dn);
   if (iv) {
-    float* xo = p.X + ((int64_t)bh * p.N + i) * D;
+    float* xo = p.X + b * p.x_sb + hd * p.x_sh + (int64_t)i * p.x_sn;
 #pragma unroll
     for (int t = 0; t < DT; ++t) {
       f32x16 v = o[t];
@@ -984,11 +985,11 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
   uint32_t wRn = DROP ? p.Rbits[wrow] : 0xffffffffu;
   float q[NS], dx[NS];
   load_run<NS>(q, p.Q + b * p.q_sb + hd * p.q_sh + (int64_t)ic * p.q_sn + h * NS, iv);
-  load_run<NS>(dx, p.dX + ((int64_t)bh * p.N + ic) * D + h * NS, iv);
+  load_run<NS>(dx, p.dX + b * p.dx_sb + hd * p.dx_sh + (int64_t)ic * p.dx_sn + h * NS, iv);
   float gp = 0.f;
   {
     float xr[NS];
-    load_run<NS>(xr, p.X + ((int64_t)bh * p.N + ic) * D + h * NS, iv);
+    load_run<NS>(xr, p.X + b * p.x_sb + hd * p.x_sh + (int64_t)ic * p.x_sn + h * NS, iv);
 #pragma unroll
     for (int s = 0; s < NS; ++s) gp = fmaf(dx[s], xr[s], gp);
   }
@@ -1101,7 +1102,7 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
     }
   }
 #undef CSA_ISSUE_BQ
-  store_rows<DT>(p.dQ + ((int64_t)bh * p.N + i) * D, D, D, dq, iv);
+  store_rows<DT>(p.dQ + b * p.dq_sb + hd * p.dq_sh + (int64_t)i * p.dq_sn, D, D, dq, iv);
   if constexpr (!DENSE) store_rows<KTA>(p.dQh + ((int64_t)bh * p.N + i) * p.kp, p.kp, p.kp, dqh, iv);
 }
 
@@ -1122,21 +1123,21 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
   const int j = kbi * 32 + c;
   const bool jv = j < p.M;
   const int jc = imin(j, p.M - 1);
-  const int qld = (int)p.q_sn * 4;
+  const int qld = (int)p.q_sn * 4, xld = (int)p.dx_sn * 4;
   const __amdgpu_buffer_rsrc_t qr_ = make_rsrc(p.Q + b * p.q_sb + hd * p.q_sh, SWZ ? (p.N - 1) * qld + D * 4 : 0x7fffffff);
-  const __amdgpu_buffer_rsrc_t xr_ = make_rsrc(p.dX + (int64_t)bh * p.N * D, SWZ ? p.N * D * 4 : 0x7fffffff);
+  const __amdgpu_buffer_rsrc_t xr_ = make_rsrc(p.dX + b * p.dx_sb + hd * p.dx_sh, SWZ ? (p.N - 1) * xld + D * 4 : 0x7fffffff);
   const __amdgpu_buffer_rsrc_t hr_ = make_rsrc(DENSE ? p.dX : p.Qh + (int64_t)bh * p.N * p.kp, p.N * p.kp * 4);
   const __amdgpu_buffer_rsrc_t sr_ = make_rsrc(p.stats + (int64_t)bh * p.N * 4, p.N * 16);
   // rows past N are never fetched: zero the images once so they only ever hold finite data
   if constexpr (SWZ) lds_zero<(int)(SH::KV_BYTES / 4)>(lds);
   else lds_zero<(SH::NIMG + 512) / 4>(lds + SH::KH / 4);
-  const DmaPat qpat = dma_pat(SW_BOTH, qld), xpat = dma_pat(SW_BOTH, 4 * D);
+  const DmaPat qpat = dma_pat(SW_BOTH, qld), xpat = dma_pat(SW_BOTH, xld);
   if constexpr (SWZ) {
     dma64(Ql, qr_, qpat, qld, 0);
-    dma64(Xl, xr_, xpat, 4 * D, 0);
+    dma64(Xl, xr_, xpat, xld, 0);
   } else {
     dma_rows<D>(Ql, qr_, qld, 0, p.N);
-    dma_rows<D>(Xl, xr_, 4 * D, 0, p.N);
+    dma_rows<D>(Xl, xr_, xld, 0, p.N);
   }
   if constexpr (!DENSE) dma_narrow(Hl, hr_, 0, KPN);
   dma_tile_contig<4>(Sl, sr_, 0);
@@ -1256,13 +1257,13 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
       if (more) {
         if constexpr (SWZ) {  // rows 16 half .. 16 half + 15 of every image are free again
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          dma64(Xl, xr_, xpat, 4 * D, i0 + 32, 4 * half, 4 * half + 4);
+          dma64(Xl, xr_, xpat, xld, i0 + 32, 4 * half, 4 * half + 4);
           dma64(Ql, qr_, qpat, qld, i0 + 32, 4 * half, 4 * half + 4);
           if constexpr (!DENSE) dma_narrow(Hl, hr_, i0 + 32, KPN, half, half + 1);
           dma_tile_contig<4>(Sl, sr_, i0 + 32, half, half + 1);
         } else if (half == 1) {
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          dma_rows<D>(Xl, xr_, 4 * D, i0 + 32, p.N);
+          dma_rows<D>(Xl, xr_, xld, i0 + 32, p.N);
           dma_rows<D>(Ql, qr_, qld, i0 + 32, p.N);
           if constexpr (!DENSE) dma_narrow(Hl, hr_, i0 + 32, KPN);
           dma_tile_contig<4>(Sl, sr_, i0 + 32);
@@ -1270,8 +1271,8 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
       }
     }
   }
-  store_rows<DT>(p.dK + ((int64_t)bh * p.M + j) * D, D, D, dk, jv);
-  store_rows<DT>(p.dV + ((int64_t)bh * p.M + j) * D, D, D, dv, jv);
+  store_rows<DT>(p.dK + b * p.dk_sb + hd * p.dk_sh + (int64_t)j * p.dk_sn, D, D, dk, jv);
+  store_rows<DT>(p.dV + b * p.dv_sb + hd * p.dv_sh + (int64_t)j * p.dv_sn, D, D, dv, jv);
   if constexpr (!DENSE) store_rows<KTA>(p.dT + ((int64_t)bh * p.M + j) * p.kp, p.kp, p.kp, dtt, jv);
 }
 
@@ -1618,7 +1619,8 @@ __global__ __launch_bounds__(256, (D <= 64 && KT <= 1 ? 2 : 1)) void k_proj_bwd(
       f32x16 dxm[DT];
       mm_acc<DT, DT>(p.WfT[0], dcur, dxm);
       if (rv) {  // second-path gradient: dQ/dK += MLP backward
-        float* dst = it.isK ? p.dK + ((int64_t)bh * p.M + row) * D : p.dQ + ((int64_t)bh * p.N + row) * D;
+        float* dst = it.isK ? p.dK + it.b * p.dk_sb + hd * p.dk_sh + (int64_t)row * p.dk_sn
+                            : p.dQ + it.b * p.dq_sb + hd * p.dq_sh + (int64_t)row * p.dq_sn;
 #pragma unroll
         for (int t = 0; t < DT; ++t)
 #pragma unroll
@@ -1972,7 +1974,8 @@ __global__ __launch_bounds__(256, ProjBwdSmallShape<D>::LW ? 1 : 2) void k_proj_
     stage_ds<DT>(DSw, dcur, D, ln);
 #pragma unroll
     for (int s = 0; s < NS; ++s) INw[act_off(s + NS * h, c)] = rv ? x4[s >> 2][s & 3] : 0.f;
-    float* dst = it.isK ? p.dK + ((int64_t)bh * p.M + rowc) * D : p.dQ + ((int64_t)bh * p.N + rowc) * D;
+    float* dst = it.isK ? p.dK + it.b * p.dk_sb + hd * p.dk_sh + (int64_t)rowc * p.dk_sn
+                        : p.dQ + it.b * p.dq_sb + hd * p.dq_sh + (int64_t)rowc * p.dq_sn;
     f32x4 old[2 * DT], old2[2 * DT];
     const bool more = (grp + 1) * 4 < n_items;
     auto load_old = [&]() {
@@ -2279,7 +2282,18 @@ KArgs make_kargs(const csa_sbm_fwd_args* a, const Layout& L) {
   p.pdrop_thr = (uint32_t)ceil((double)a->proj_dropout * 65536.0);
   p.scale = 1.f / sqrtf((float)a->d);
   p.X = a->X;
+  const bool xc = a->x_sb == 0 && a->x_sh == 0 && a->x_sn == 0;  // zero triple: (B,H,N,d) contiguous
+  p.x_sb = xc ? a->H * a->N * a->d : a->x_sb;
+  p.x_sh = xc ? a->N * a->d : a->x_sh;
+  p.x_sn = xc ? a->d : a->x_sn;
   return p;
+}
+
+// (b, h, row) element strides of a (B,H,R,d) operand; the zero triple means contiguous
+struct Str3 { int64_t sb, sh, sn; };
+inline Str3 strides_or_contig(int64_t sb, int64_t sh, int64_t sn, int64_t H, int64_t R, int64_t d) {
+  if (sb == 0 && sh == 0 && sn == 0) return Str3{H * R * d, R * d, d};
+  return Str3{sb, sh, sn};
 }
 
 csa_status validate_fwd(const csa_sbm_fwd_args* a) {
@@ -2304,7 +2318,8 @@ csa_status validate_fwd(const csa_sbm_fwd_args* a) {
   if (!al16(a->Q, a->q_sb, a->q_sh, a->q_sn) || !al16(a->K, a->k_sb, a->k_sh, a->k_sn) ||
       !al16(a->V, a->v_sb, a->v_sh, a->v_sn))
     return fail(CSA_INVALID_ARG, "Q/K/V must be 16-byte aligned with strides multiple of 4 elements");
-  if (((uintptr_t)a->X) % 16) return fail(CSA_INVALID_ARG, "X must be 16-byte aligned");
+  if (!al16(a->X, a->x_sb, a->x_sh, a->x_sn))
+    return fail(CSA_INVALID_ARG, "X must be 16-byte aligned with strides multiple of 4 elements");
   return CSA_OK;
 }
 
@@ -2436,6 +2451,16 @@ csa_status launch_bwd(const csa_sbm_bwd_args* b, const Layout& L, hipStream_t st
   const bool dense = a->flags & CSA_FLAG_DENSE;
   p.dX = b->dX; p.dsp = b->dsparsity; p.dgraph = b->dgraph;
   p.dQ = b->dQ; p.dK = b->dK; p.dV = b->dV;
+  {
+    const Str3 x = strides_or_contig(b->dx_sb, b->dx_sh, b->dx_sn, a->H, a->N, a->d);
+    const Str3 q = strides_or_contig(b->dq_sb, b->dq_sh, b->dq_sn, a->H, a->N, a->d);
+    const Str3 k = strides_or_contig(b->dk_sb, b->dk_sh, b->dk_sn, a->H, a->M, a->d);
+    const Str3 v = strides_or_contig(b->dv_sb, b->dv_sh, b->dv_sn, a->H, a->M, a->d);
+    p.dx_sb = x.sb; p.dx_sh = x.sh; p.dx_sn = x.sn;
+    p.dq_sb = q.sb; p.dq_sh = q.sh; p.dq_sn = q.sn;
+    p.dk_sb = k.sb; p.dk_sh = k.sh; p.dk_sn = k.sn;
+    p.dv_sb = v.sb; p.dv_sh = v.sh; p.dv_sn = v.sn;
+  }
   p.dQh = (float*)((char*)b->workspace + L.w_dQh);
   p.dT = (float*)((char*)b->workspace + L.w_dT);
   p.slab = (float*)((char*)b->workspace + L.w_slab);
@@ -2551,6 +2576,14 @@ csa_status csa_sbm_bwd(const csa_sbm_bwd_args* b, void* stream) {
   const bool dense = a->flags & CSA_FLAG_DENSE;
   if (!b->dX || !b->dQ || !b->dK || !b->dV || (!dense && !b->workspace))
     return fail(CSA_INVALID_ARG, "null dX/dQ/dK/dV/workspace");
+  {
+    auto al16 = [](const void* ptr, int64_t sb, int64_t sh, int64_t sn) {
+      return (((uintptr_t)ptr) % 16 == 0) && sb % 4 == 0 && sh % 4 == 0 && sn % 4 == 0;
+    };
+    if (!al16(b->dX, b->dx_sb, b->dx_sh, b->dx_sn) || !al16(b->dQ, b->dq_sb, b->dq_sh, b->dq_sn) ||
+        !al16(b->dK, b->dk_sb, b->dk_sh, b->dk_sn) || !al16(b->dV, b->dv_sb, b->dv_sh, b->dv_sn))
+      return fail(CSA_INVALID_ARG, "dX/dQ/dK/dV must be 16-byte aligned with strides multiple of 4 elements");
+  }
   if (!dense && (!b->dcluster_w || !b->dproj_w[0] || !b->dproj_w[1] || !b->dproj_w[2] || !b->dproj_b[0] ||
                  !b->dproj_b[1] || !b->dproj_b[2]))
     return fail(CSA_INVALID_ARG, "null parameter-gradient output");

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define CSA_ABI_VERSION 2
+#define CSA_ABI_VERSION 3
 
 typedef enum csa_status {
   CSA_OK = 0,
@@ -90,22 +90,29 @@ typedef struct csa_sbm_fwd_args {
   float proj_dropout;         /* proj Dropout p (0 in eval) — sbm_attn.py:24,27 */
   uint32_t flags;
   uint32_t dtype;             /* CSA_DTYPE_F32 or CSA_DTYPE_BF16 */
-  float* X;                   /* out (B,H,N,d) contiguous */
+  float* X;                   /* out (B,H,N,d), strides x_* below */
   float* sparsity;            /* out (H,) head-wise sparsity (sbm_attn.py:64); NULL if DENSE */
   void* state;                /* csa_sbm_state_bytes(): saved for backward and csa_sbm_maps */
   const csa_prof* prof;       /* optional stage timing (NULL = off) */
+  /* ABI v3: element strides of X; all three 0 = (B,H,N,d) contiguous. d stays contiguous; like
+   * Q/K/V, X must be 16-byte aligned with strides multiple of 4 elements. A (B,N,H,d) buffer read
+   * as (B,H,N,d) makes combine_heads (sbm_attn.py:143-146) a free view. */
+  int64_t x_sb, x_sh, x_sn;
 } csa_sbm_fwd_args;
 
 typedef struct csa_sbm_bwd_args {
   const csa_sbm_fwd_args* fwd; /* the forward's arguments (same inputs and the filled state) */
-  const float* dX;             /* (B,H,N,d) contiguous */
+  const float* dX;             /* (B,H,N,d), strides dx_* below */
   const float* dsparsity;      /* (H,) or NULL */
   const float* dgraph;         /* (B,H,N,M) grad of the returned graph map, or NULL */
-  float* dQ; float* dK; float* dV; /* out (B,H,N|M,d) contiguous */
+  float* dQ; float* dK; float* dV; /* out (B,H,N|M,d), strides dq_* / dk_* / dv_* below */
   float* dcluster_w;           /* out (H*k, d); NULL if DENSE */
   float* dproj_w[3]; float* dproj_b[3]; /* out; NULL if DENSE */
   void* workspace;             /* csa_sbm_bwd_workspace_bytes() */
   const csa_prof* prof;        /* optional stage timing (NULL = off) */
+  /* ABI v3: element strides (b, h, row) of dX, dQ, dK, dV; a zero triple = contiguous. E.g. dQ/dK/dV
+   * as the three head-major views of one packed (B,N,3,H,d) gradient of a fused QKV projection. */
+  int64_t dx_sb, dx_sh, dx_sn, dq_sb, dq_sh, dq_sn, dk_sb, dk_sh, dk_sn, dv_sb, dv_sh, dv_sn;
 } csa_sbm_bwd_args;
 
 int csa_abi_version(void);
@@ -140,18 +147,23 @@ typedef struct csa_rel_attn_args {
   const uint8_t* mask; int64_t mask_sb, mask_sh;/* (B,*,N,N) 1 = masked (-1e9); head stride may be 0 */
   int64_t rel_head_group; /* heads [0,g) read plane 0, heads [g,H) plane 1 (CSE: 4); 0 = use rel_sh */
   uint32_t dtype;          /* CSA_DTYPE_F32 or CSA_DTYPE_BF16 (bf16: d = 64 only) */
-  float* out;          /* (B,H,N,d) contiguous */
+  float* out;          /* (B,H,N,d), strides o_* below */
   float* row_stats;    /* (B,H,N,2) saved (row max, 1/row sum) for backward; kept separate because
                           fully masked rows sit at -1e9 where max + log(sum) is not representable */
   void* state;         /* csa_rel_attn_state_bytes(): relation logits q.lk^T, k.lq^T, kept for backward */
+  /* ABI v3: element strides (b, h, row) of out; zero triple = (B,H,N,d) contiguous. Non-contiguous
+   * layouts need d = 64 (the fused path); 16-byte aligned, strides multiple of 4 elements. */
+  int64_t o_sb, o_sh, o_sn;
 } csa_rel_attn_args;
 
 typedef struct csa_rel_attn_bwd_args {
   const csa_rel_attn_args* fwd;
-  const float* dout;   /* (B,H,N,d) contiguous */
-  float* dq; float* dk; float* dv; /* (B,H,N,d) contiguous */
+  const float* dout;   /* (B,H,N,d), strides do_* below */
+  float* dq; float* dk; float* dv; /* (B,H,N,d), strides dq_* / dk_* / dv_* below */
   float* dlq; float* dlk;          /* (H,L,d) */
   void* workspace;
+  /* ABI v3: element strides (b, h, row); a zero triple = contiguous; non-contiguous needs d = 64 */
+  int64_t do_sb, do_sh, do_sn, dq_sb, dq_sh, dq_sn, dk_sb, dk_sh, dk_sn, dv_sb, dv_sh, dv_sn;
 } csa_rel_attn_bwd_args;
 
 size_t csa_rel_attn_state_bytes(int64_t B, int64_t H, int64_t N, int64_t L, int64_t d);
