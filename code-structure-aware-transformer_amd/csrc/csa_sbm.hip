@@ -25,6 +25,7 @@
 #include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
+#include <stdlib.h>
 
 using namespace csa;
 
@@ -130,7 +131,13 @@ __device__ __forceinline__ void fence_sched() { __builtin_amdgcn_sched_barrier(0
 __device__ __forceinline__ f32x4 frag4(const float* __restrict__ f, int it, int nsteps, int s4) {
   const __amdgpu_buffer_rsrc_t r =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(f), (short)0, 0x7fffffff, 0x00020000);
+#ifdef CSA_EXP_FRAG_L1
+  const int soff = 0 * (it + s4 + nsteps);
+#elif defined(CSA_EXP_FRAG_SPREAD)
+  const int soff = (it * (nsteps >> 2) + s4) * 1024 + (int)((blockIdx.x + blockIdx.y) & 15) * 69632;
+#else
   const int soff = (it * (nsteps >> 2) + s4) * 1024;
+#endif
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, lane_id() * 16, soff, 0));
 }
 
@@ -343,50 +350,53 @@ __device__ __forceinline__ void add_bias(const float (&ba)[D / 32], f32x16 (&a)[
   for (int ot = 0; ot < D / 32; ++ot) a[ot] = mfma(ba[ot], one, a[ot]);
 }
 
+// Fragment sources of the projection forward: global (L2-resident) or the workgroup's LDS copy (FL).
+struct FwdFrags { const float* W[3]; const float* C; const float* S; const float* b[3]; };
+
 // h1 = relu(drop(W0 x + b0)) from lin-perm input rows
-template <int D>
-__device__ __forceinline__ void mlp_layer0(const KArgs& p, const float (&x)[D / 2], f32x16 (&h1)[D / 32], int row,
-                                           int bh, int isK) {
+template <int D, bool FL>
+__device__ __forceinline__ void mlp_layer0(const KArgs& p, const float* W0, const float* b0, const float (&x)[D / 2],
+                                           f32x16 (&h1)[D / 32], int row, int bh, int isK) {
   constexpr int DT = D / 32, NS = D / 2;
   float ba[DT];
-  bias_operand<D>(p.pb[0], ba);
+  bias_operand<D>(b0, ba);
 #pragma unroll
   for (int ot = 0; ot < DT; ++ot) h1[ot] = zero16();
-  frag_chain<DT, NS / 4, MLP_LA>(p.Wf[0], NS, h1, [&](int s) { return x[s]; });
+  frag_chain<DT, NS / 4, FL ? 1 : MLP_LA, FL>(W0, NS, h1, [&](int s) { return x[s]; });
   add_bias<D>(ba, h1);
   mlp_act<D>(p, h1, 0, row, bh, isK);
 }
 
 // out = W_l in + b_l  (acc-perm input), l = 1, 2
-template <int D>
-__device__ __forceinline__ void mlp_layer(const KArgs& p, const f32x16 (&in)[D / 32], f32x16 (&out)[D / 32], int l) {
+template <int D, bool FL>
+__device__ __forceinline__ void mlp_layer(const float* Wl, const float* bl, const f32x16 (&in)[D / 32],
+                                          f32x16 (&out)[D / 32]) {
   constexpr int DT = D / 32, NS = D / 2;
   float ba[DT];
-  bias_operand<D>(p.pb[l], ba);
+  bias_operand<D>(bl, ba);
 #pragma unroll
   for (int ot = 0; ot < DT; ++ot) out[ot] = zero16();
-  frag_chain<DT, NS / 4, MLP_LA>(p.Wf[l], NS, out, [&](int s) { return in[s / 16][s % 16]; });
+  frag_chain<DT, NS / 4, FL ? 1 : MLP_LA, FL>(Wl, NS, out, [&](int s) { return in[s / 16][s % 16]; });
   add_bias<D>(ba, out);
 }
 
-template <int D>
-__device__ __forceinline__ void mlp_fwd(const KArgs& p, const float (&x)[D / 2], f32x16 (&h1)[D / 32],
+template <int D, bool FL>
+__device__ __forceinline__ void mlp_fwd(const KArgs& p, const FwdFrags& F, const float (&x)[D / 2], f32x16 (&h1)[D / 32],
                                         f32x16 (&h2)[D / 32], f32x16 (&po)[D / 32], int row, int bh, int isK) {
-  mlp_layer0<D>(p, x, h1, row, bh, isK);
-  mlp_layer<D>(p, h1, h2, 1);
+  mlp_layer0<D, FL>(p, F.W[0], F.b[0], x, h1, row, bh, isK);
+  mlp_layer<D, FL>(F.W[1], F.b[1], h1, h2);
   mlp_act<D>(p, h2, 1, row, bh, isK);
-  mlp_layer<D>(p, h2, po, 2);
+  mlp_layer<D, FL>(F.W[2], F.b[2], h2, po);
 }
 
-// hat^T = sigmoid(C_h p^T), rows (clusters) >= k zeroed.
-template <int D, int KT>
-__device__ __forceinline__ void cluster_hat(const KArgs& p, const f32x16 (&po)[D / 32], f32x16 (&hat)[KT], int hd) {
+// hat^T = sigmoid(C_h p^T), rows (clusters) >= k zeroed. Cf: the head's cluster fragments.
+template <int D, int KT, bool FL>
+__device__ __forceinline__ void cluster_hat(const KArgs& p, const float* Cf, const f32x16 (&po)[D / 32], f32x16 (&hat)[KT]) {
   constexpr int NS = D / 2;
   const int h = lane_id() >> 5;
-  const float* Cf = p.Cf + (size_t)hd * 32 * KT * D;
 #pragma unroll
   for (int kt = 0; kt < KT; ++kt) hat[kt] = zero16();
-  frag_chain<KT, NS / 4>(Cf, NS, hat, [&](int s) { return po[s / 16][s % 16]; });
+  frag_chain<KT, NS / 4, 1, FL>(Cf, NS, hat, [&](int s) { return po[s / 16][s % 16]; });
 #pragma unroll
   for (int kt = 0; kt < KT; ++kt) {
 #pragma unroll
@@ -399,11 +409,11 @@ __device__ __forceinline__ void cluster_hat(const KArgs& p, const f32x16 (&po)[D
 }
 
 // out^T = Sfrag * in^T (K = 32 KT clusters, acc-perm input)
-template <int KT>
+template <int KT, bool FL = false>
 __device__ __forceinline__ void small_mm(const float* __restrict__ frag, const f32x16 (&in)[KT], f32x16 (&out)[KT]) {
 #pragma unroll
   for (int at = 0; at < KT; ++at) out[at] = zero16();
-  frag_chain<KT, 4 * KT>(frag, 16 * KT, out, [&](int s) { return in[s / 16][s % 16]; });
+  frag_chain<KT, 4 * KT, 1, FL>(frag, 16 * KT, out, [&](int s) { return in[s / 16][s % 16]; });
 }
 
 // Store an accumulator tile set (feature rows, data row = lane) to out[row][0..ncols) (row-major, ld)
@@ -458,48 +468,166 @@ __device__ __forceinline__ void store_act(float* __restrict__ blk, const f32x16 
     for (int r = 0; r < 16; ++r) __builtin_nontemporal_store(a[t][r], blk + act_off(32 * t + crow(r, h), c));
 }
 
-// ------------------------------------------------------------------------------------
-// F2: per 32-row block of Q or K: Qh = sigmoid(MLP(Q) C^T); Kh likewise and T = Kh S^T.
-// grid (NQB + NKB, B*H), one wave per block.
-// ------------------------------------------------------------------------------------
-template <int D, int KT>
-__global__ __launch_bounds__(64) void k_proj_fwd(const KArgs p) {
+// The same through a wave-private 4 KiB LDS scratch: each 32-feature tile is written to the scratch in the
+// block layout (16 ds_write_b32 per lane, conflict-free: a lane half writes one feature row) and leaves
+// as 4 x 1 KiB contiguous dwordx4 stores (4x fewer store instructions, half the VGPR traffic per byte).
+// NF = features of the tile set (<= 32 NT; a partial last tile stores only its first NF - 32 (NT - 1)).
+template <int NT, int NF = 32 * NT>
+__device__ __forceinline__ void store_act_lds(float* __restrict__ blk, const f32x16 (&a)[NT], float* __restrict__ scr) {
   const int lane = lane_id(), c = lane & 31, h = lane >> 5;
-  const int bh = blockIdx.y, b = bh / p.H, hd = bh % p.H;
-  const int isK = blockIdx.x >= p.NQB;
-  const int rb = isK ? blockIdx.x - p.NQB : blockIdx.x;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int nf = NF - 32 * t < 32 ? NF - 32 * t : 32;
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      if (crow(r, 0) < nf) scr[act_off(crow(r, h), c)] = a[t][r];
+#pragma unroll
+    for (int k = 0; k < nf / 8; ++k) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(scr + 4 * (lane + 64 * k));
+      __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(blk + 1024 * t + 4 * (lane + 64 * k)));
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// F2 body: one 32-row item (block rb of Q, or of K when isK) of batch element b, head hd.
+// ------------------------------------------------------------------------------------
+// x rows (lin-perm half rows) of item r of (b, hd)
+template <int D>
+__device__ __forceinline__ void load_item_x(const KArgs& p, int b, int hd, int r, float (&x)[D / 2]) {
+  const int c = lane_id() & 31, h = lane_id() >> 5;
+  const int isK = r >= p.NQB;
   const int nrows = isK ? p.M : p.N;
-  const int row = rb * 32 + c;
-  const bool rv = row < nrows;
+  const int row = (isK ? r - p.NQB : r) * 32 + c;
   const int rowc = imin(row, nrows - 1);
   const float* X = isK ? p.K + b * p.k_sb + hd * p.k_sh + (int64_t)rowc * p.k_sn
                        : p.Q + b * p.q_sb + hd * p.q_sh + (int64_t)rowc * p.q_sn;
-  float x[D / 2];
-  load_run<D / 2>(x, X + h * (D / 2), rv);
-  f32x16 h1[D / 32], h2[D / 32], po[D / 32], hat[KT];
-  mlp_fwd<D>(p, x, h1, h2, po, row, bh, isK);
-  cluster_hat<D, KT>(p, po, hat, hd);
-  {  // save the activations for k_proj_bwd (item blockIdx.x of this (b,h): Q blocks, then K blocks)
-    constexpr int ABLK = (3 * D + 32 * KT) * 32;
-    float* blk = p.Act + ((int64_t)bh * (p.NQB + p.NKB) + blockIdx.x) * ABLK;
-    store_act<D / 32>(blk, h1);
-    store_act<D / 32>(blk + 32 * D, h2);
-    store_act<D / 32>(blk + 64 * D, po);
-    if ((D == 64 || D == 96) && p.kp <= 16) {  // clusters >= 16 are zero, never read back (k_proj_bwd_s)
-      const int cl = lane_id() & 31, hl = lane_id() >> 5;
+  // raw loads (rows past the end re-read the last row): nothing consumes them here, so no wait is
+  // placed before the caller's stores; proj_fwd_item zeroes the padding rows when it uses them
 #pragma unroll
-      for (int r = 0; r < 8; ++r) __builtin_nontemporal_store(hat[0][r], blk + 96 * D + act_off(crow(r, hl), cl));
-    } else {
-      store_act<KT>(blk + 96 * D, hat);
-    }
+  for (int i = 0; i < D / 2; i += 4) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(X + h * (D / 2) + i);
+    x[i] = v[0]; x[i + 1] = v[1]; x[i + 2] = v[2]; x[i + 3] = v[3];
   }
+}
+
+// F2 body: item r of (b, hd) from its x rows. `next` runs once every product is done and x is dead,
+// before the stores (the persistent kernel issues the next item's x loads there: a later vmcnt wait
+// for them then does not also wait for this item's stores, which drain under the next item).
+template <int D, int KT, bool FL, typename NEXT>
+__device__ __forceinline__ void proj_fwd_item(const KArgs& p, const FwdFrags& F, int b, int hd, int r, float (&x)[D / 2],
+                                              float* scr, NEXT next) {
+  const int lane = lane_id(), c = lane & 31, h = lane >> 5;
+  const int bh = b * p.H + hd;
+  const int isK = r >= p.NQB;
+  const int rb = isK ? r - p.NQB : r;
+  const int nrows = isK ? p.M : p.N;
+  const int row = rb * 32 + c;
+  const bool rv = row < nrows;
+  f32x16 h1[D / 32], h2[D / 32], po[D / 32], hat[KT], t[KT];
+#pragma unroll
+  for (int i = 0; i < D / 2; ++i) x[i] = rv ? x[i] : 0.f;
+  mlp_fwd<D, FL>(p, F, x, h1, h2, po, row, bh, isK);
+  cluster_hat<D, KT, FL>(p, F.C, po, hat);
+  if (isK) small_mm<KT, FL>(F.S, hat, t);
+  next();
+#ifndef CSA_EXP_NO_ACT
+  {  // save the activations for k_proj_bwd (item r of this (b,h): Q blocks, then K blocks)
+    constexpr int ABLK = (3 * D + 32 * KT) * 32;
+    float* blk = p.Act + ((int64_t)bh * (p.NQB + p.NKB) + r) * ABLK;
+    store_act_lds<D / 32>(blk, h1, scr);
+    store_act_lds<D / 32>(blk + 32 * D, h2, scr);
+    store_act_lds<D / 32>(blk + 64 * D, po, scr);
+    bool hat16 = false;
+    if constexpr (KT == 1) {
+      if ((D == 64 || D == 96) && p.kp <= 16) {  // clusters >= 16 are zero, never read back (k_proj_bwd_s)
+        store_act_lds<1, 16>(blk + 96 * D, hat, scr);
+        hat16 = true;
+      }
+    }
+    if (!hat16) store_act_lds<KT>(blk + 96 * D, hat, scr);
+  }
+#endif
   if (!isK) {
     store_rows<KT>(p.Qh + ((int64_t)bh * p.N + row) * p.kp, p.kp, p.kp, hat, rv);
   } else {
     store_rows<KT>(p.Kh + ((int64_t)bh * p.M + row) * p.kp, p.kp, p.kp, hat, rv);
-    f32x16 t[KT];
-    small_mm<KT>(p.Sf + (size_t)hd * 1024 * KT * KT, hat, t);
     store_rows<KT>(p.T + ((int64_t)bh * p.M + row) * p.kp, p.kp, p.kp, t, rv);
+  }
+  (void)lane; (void)h;
+}
+
+// ------------------------------------------------------------------------------------
+// F2: per 32-row block of Q or K: Qh = sigmoid(MLP(Q) C^T); Kh likewise and T = Kh S^T.
+// grid (NQB + NKB, B*H), one wave per block; weight fragments read from L2.
+// ------------------------------------------------------------------------------------
+template <int D, int KT>
+__global__ __launch_bounds__(64) void k_proj_fwd(const KArgs p) {
+  __shared__ __attribute__((aligned(16))) float scr[1024];  // activation store staging (store_act_lds)
+  const int bh = blockIdx.y, hd = bh % p.H;
+  const FwdFrags F{{p.Wf[0], p.Wf[1], p.Wf[2]}, p.Cf + (size_t)hd * 32 * KT * D, p.Sf + (size_t)hd * 1024 * KT * KT,
+                   {p.pb[0], p.pb[1], p.pb[2]}};
+  float x[D / 2];
+  load_item_x<D>(p, bh / p.H, hd, blockIdx.x, x);
+  proj_fwd_item<D, KT, false>(p, F, bh / p.H, hd, blockIdx.x, x, scr, [] {});
+}
+
+// F2 with the weight fragments in LDS: grid (G, H), NW waves per workgroup. The workgroup copies the three
+// d x d layers and head hd's cluster / S fragments (operand-major, unchanged) into LDS once, then its waves
+// run the head's items i_lo + w, i_lo + w + NW, ... of [i_lo, i_hi) (item = b * (NQB + NKB) + block).
+// Same results as k_proj_fwd (identical MFMA chains); one L2 fragment fetch per workgroup instead of
+// one per item.
+template <int D, int KT>
+struct ProjFwdLds {
+  static constexpr int WB = D * D * 4, CB = 32 * KT * D * 4, SB = 1024 * KT * KT * 4;  // bytes
+#ifdef CSA_EXP_PF6
+  static constexpr int NW = D == 64 ? 6 : 8;
+#else
+  static constexpr int NW = D == 64 ? 4 : 8;  // d = 64: two workgroups per CU; d = 96: one of 8 waves
+#endif
+  static constexpr int PIECES = (3 * WB + CB + SB) / 1024;
+  static constexpr size_t FBYTES = 3 * WB + CB + SB;
+  static constexpr size_t BBYTES = (3 * D * 4 + 15) / 16 * 16;  // the three biases
+  static constexpr size_t BYTES = FBYTES + NW * 4096 + BBYTES;   // + a 4 KiB activation staging scratch per wave
+  static_assert((3 * WB + CB + SB) % 1024 == 0, "whole 1 KiB DMA pieces");
+};
+
+template <int D, int KT>
+#ifdef CSA_EXP_PF6
+__global__ __launch_bounds__((64 * ProjFwdLds<D, KT>::NW), (D == 64 ? 3 : 2)) void k_proj_fwd_l(const KArgs p) {
+#else
+__global__ __launch_bounds__((64 * ProjFwdLds<D, KT>::NW)) void k_proj_fwd_l(const KArgs p) {
+#endif
+  using LY = ProjFwdLds<D, KT>;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int hd = blockIdx.y, g = blockIdx.x, G = gridDim.x;
+  const uint32_t L0 = lds_offset(lds);
+  for (int pc = w; pc < LY::PIECES; pc += LY::NW) {  // 1 KiB pieces: W0 | W1 | W2 | C_hd | S_hd
+    const int byte = pc * 1024;
+    const float* src;
+    int off;
+    if (byte < 3 * LY::WB) { src = p.Wf[byte / LY::WB]; off = byte % LY::WB; }
+    else if (byte < 3 * LY::WB + LY::CB) { src = p.Cf + (size_t)hd * 32 * KT * D; off = byte - 3 * LY::WB; }
+    else { src = p.Sf + (size_t)hd * 1024 * KT * KT; off = byte - 3 * LY::WB - LY::CB; }
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(make_rsrc(src, 0x7fffffff), lds_at(L0 + byte), 16, lane_id() * 16, off, 0, 0);
+  }
+  float* bias = lds + (LY::FBYTES + LY::NW * 4096) / 4;
+  for (int e = threadIdx.x; e < 3 * D; e += 64 * LY::NW) bias[e] = p.pb[e / D][e % D];
+  const int per_b = p.NQB + p.NKB;
+  const int i_lo = (int)((int64_t)g * p.B * per_b / G), i_hi = (int)((int64_t)(g + 1) * p.B * per_b / G);
+  float x[D / 2];
+  if (i_lo + w < i_hi) load_item_x<D>(p, (i_lo + w) / per_b, hd, (i_lo + w) % per_b, x);
+  wait_vm_all();
+  __syncthreads();
+  const FwdFrags F{{lds, lds + D * D, lds + 2 * D * D}, lds + 3 * D * D, lds + 3 * D * D + 32 * KT * D,
+                   {bias, bias + D, bias + 2 * D}};
+  float* scr = lds + LY::FBYTES / 4 + 1024 * w;
+  for (int it = i_lo + w; it < i_hi; it += LY::NW) {
+    const int nx = it + LY::NW;
+    proj_fwd_item<D, KT, true>(p, F, it / per_b, hd, it % per_b, x, scr, [&] {
+      if (nx < i_hi) load_item_x<D>(p, nx / per_b, hd, nx % per_b, x);
+    });
   }
 }
 
@@ -1069,8 +1197,13 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int jj = crow(r, h), j = j0 + jj;
+#ifdef CSA_EXP_NO_SHFL
+      const uint32_t a_w = DENSE ? 0xffffffffu : wA ^ jj;
+      const uint32_t r_w = DROP ? wR ^ jj : 0xffffffffu;
+#else
       const uint32_t a_w = DENSE ? 0xffffffffu : (uint32_t)__shfl((int)wA, jj, 64);
       const uint32_t r_w = DROP ? (uint32_t)__shfl((int)wR, jj, 64) : 0xffffffffu;
+#endif
       const bool a = (a_w >> c) & 1u;
       const bool keep = (r_w >> c) & 1u;
       const bool inside = iv && (j < p.M);
@@ -2244,6 +2377,12 @@ csa_status check_launch(const char* what) {
   return CSA_OK;
 }
 
+// LDS-resident weight fragments for the projection forward (CSA_PROJ_FWD_L=0 selects the L2 variant: A/B)
+bool proj_fwd_lds() {
+  static const bool on = [] { const char* e = getenv("CSA_PROJ_FWD_L"); return !(e && e[0] == '0'); }();
+  return on;
+}
+
 bool supported(int64_t d, int64_t k, uint32_t flags) {
   if (d != 64 && d != 96) return false;
   if (flags & CSA_FLAG_DENSE) return true;
@@ -2392,7 +2531,19 @@ csa_status launch_fwd(const csa_sbm_fwd_args* a, const Layout& L, hipStream_t st
     }
     {
       Stage sg(a->prof, CSA_STAGE_PROJ_FWD, st);
-      hipLaunchKernelGGL((k_proj_fwd<D, KT>), dim3(L.NQB + L.NKB, BH), dim3(64), 0, st, p);
+      bool done = false;
+      if constexpr (KT == 1) {  // k <= 32: weight fragments in LDS
+        using PL = ProjFwdLds<D, KT>;
+        if (proj_fwd_lds()) {
+          const int64_t items = a->B * (L.NQB + L.NKB), slots = (D == 64 ? 2 : 1) * 256LL;
+          const int G = (int)std::max<int64_t>(1, std::min<int64_t>(slots / a->H, (items + PL::NW - 1) / PL::NW));
+          (void)hipFuncSetAttribute((const void*)k_proj_fwd_l<D, KT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)PL::BYTES);
+          hipLaunchKernelGGL((k_proj_fwd_l<D, KT>), dim3(G, a->H), dim3(64 * PL::NW), PL::BYTES, st, p);
+          done = true;
+        }
+      }
+      if (!done) hipLaunchKernelGGL((k_proj_fwd<D, KT>), dim3(L.NQB + L.NKB, BH), dim3(64), 0, st, p);
     }
     {
       Stage sg(a->prof, CSA_STAGE_ATTN_FWD, st);
