@@ -16,6 +16,7 @@
 // Relation planes are uint8 (B,P,N,N) with a head->plane map (heads 0-3 parent plane L, 4-7 sibling
 // plane T; module/csa_trans.py:206-211), replacing the reference's repeated int64 (B,8,N,N) copies.
 #include "csa_common.hpp"
+#include <algorithm>
 #include "../../include/csa_hip.h"
 
 #include <math.h>
@@ -901,7 +902,7 @@ __global__ __launch_bounds__(64, 1) void k_rel_bwd_qf(const RelArgs p) {
       *reinterpret_cast<f32x4*>(p.qstat + ((int64_t)bh * p.N + i) * 4) = st;
     }
   }
-  bins_store_t(p.gc2p + (int64_t)bh * p.Lp * p.ldx, p.ldx, i, bins, p.LB, p.KB2, p.Lp, iv);
+  bins_store_t(p.gc2p + ((int64_t)hd * p.B + b) * p.Lp * p.ldx, p.ldx, i, bins, p.LB, p.KB2, p.Lp, iv);
 }
 
 // Backward, key side: one wave per (b,h, 32 keys), S orientation (queries = accumulator rows, keys =
@@ -1041,7 +1042,83 @@ __global__ __launch_bounds__(64, 1) void k_rel_bwd_kf(const RelArgs p) {
     store_rows_f<DT>(p.dk + b * p.dk_sb + hd * p.dk_sh + (int64_t)j * p.dk_sn, dk);
     store_rows_f<DT>(p.dv + b * p.dv_sb + hd * p.dv_sh + (int64_t)j * p.dv_sn, dv);
   }
-  bins_store_t(p.gp2ct + (int64_t)bh * p.Lp * p.ldx, p.ldx, j, bins, p.LB, p.KB2, p.Lp, jv);
+  bins_store_t(p.gp2ct + ((int64_t)hd * p.B + b) * p.Lp * p.ldx, p.ldx, j, bins, p.LB, p.KB2, p.Lp, jv);
+}
+
+// Relation-embedding gradients of the fused path, split over the batch (deterministic):
+//   part[s][h](l, dd) = sum over the chunks of split s of G_h[l][x] X_h[x][dd]
+// (dlk: G = G_c2p, X = Q; dlq: G = G_p2cT, X = K; disentangled_attn.py:51-52 backward). The G tables are
+// (H, B, Lp, NP), x = n (written by bins_store_t; columns n >= N are never written and masked here).
+// One wave per (32-row l tile, head, split) computes both 32-column halves of dd: A = G rows (dwordx4 runs
+// of x in the acc K-permutation), B = the chunk's 32 X rows by LDS-DMA into a double-buffered SW_COL image
+// (column reads conflict-free); chunk c + 1 lands while chunk c's 32 MFMAs run. k_sum_splits adds the
+// splits in order.
+struct LgradArgs {
+  const float* G[2];   // G_c2p, G_p2cT tables (H, Lp, ldx)
+  const float* X[2];   // Q, K
+  int64_t x_sb[2], x_sh[2], x_sn[2];
+  float* part[2];      // (nsplit, H, L, 64) partials of dlk, dlq
+  int64_t ldx; int Lp, L, NP, B, N, H, nsplit;
+};
+// Workgroup = one wave per 32-row l tile (all of L), grid (H, 2 splits-sets): the chunk's X image is shared
+// by the waves (each DMAs some of its eight 1 KiB pieces; a barrier per chunk publishes it).
+__global__ __launch_bounds__(512) void k_rel_lgrad(const LgradArgs g) {
+  constexpr int D = 64, IMG = 32 * D * 4;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const uint32_t L0 = lds_offset(lds);
+  const int lane = lane_id(), c = lane & 31, h = lane >> 5;
+  const int lt = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), NW = (int)(blockDim.x >> 6);
+  const int hd = blockIdx.x, which = (int)blockIdx.y / g.nsplit, sp = (int)blockIdx.y % g.nsplit;
+  const int cpb = g.NP / 32, nch = g.B * cpb;  // 32-row chunks per batch element / in all
+  const int c0 = (int)((int64_t)sp * nch / g.nsplit), c1 = (int)((int64_t)(sp + 1) * nch / g.nsplit);
+  const int l = lt * 32 + c;
+  const float* arow = g.G[which] + ((int64_t)hd * g.B * g.Lp + imin(l, g.L - 1)) * g.ldx;  // + b Lp ldx per chunk
+  const float* X = g.X[which] + hd * g.x_sh[which];
+  const int64_t x_sb = g.x_sb[which];
+  const int ld = (int)g.x_sn[which] * 4, N = g.N;
+  const DmaPat pat = dma_pat(SW_COL, ld);
+  for (int e = threadIdx.x; e < 2 * IMG / 16; e += blockDim.x)  // rows >= N are never fetched: finite zeros
+    reinterpret_cast<f32x4*>(lds)[e] = f32x4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
+  // chunk ch: this wave's pieces of rows n0 .. n0 + 31 of batch element b into image buf, and its G runs
+  // G[l][x0 + 8 q + 4 h + e] = the A operand of K-step r = 4 q + e (acc perm: x = x0 + crow(r, h))
+  auto issue = [&](int ch, int buf, f32x4 (&a4)[4]) {
+    const int b = ch / cpb, n0 = (ch % cpb) * 32;
+    const __amdgpu_buffer_rsrc_t xr = make_rsrc(X + b * x_sb, (N - 1) * ld + D * 4);
+    for (int q = lt; q < 8; q += NW) dma64(L0 + IMG * buf, xr, pat, ld, n0, q, q + 1);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      a4[q] = *reinterpret_cast<const f32x4*>(arow + (int64_t)b * g.Lp * g.ldx + n0 + 8 * q + 4 * h);
+  };
+  int vb[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) vb[t] = col_base64(t, c, h);
+  f32x16 acc[2] = {zero16(), zero16()};
+  f32x4 a4[4], an[4];
+  if (c0 < c1) issue(c0, 0, a4);
+  for (int ch = c0; ch < c1; ++ch) {
+    const int cur = (ch - c0) & 1, n0 = (ch % cpb) * 32;
+    wait_vm_all();     // this wave's pieces of chunk ch and its G runs have landed
+    __syncthreads();   // every wave's pieces landed; every wave read out image cur ^ 1 (chunk ch - 1)
+    if (ch + 1 < c1) issue(ch + 1, cur ^ 1, an);
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float a = (n0 + crow(r, h) < N) ? a4[r >> 2][r & 3] : 0.f;
+        acc[t] = mfma(a, lds_f1(lds, IMG * cur + vb[t] + 256 * crow(r, 0)), acc[t]);
+      }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) a4[q] = an[q];
+  }
+  float* out = g.part[which] + ((int64_t)sp * g.H + hd) * g.L * D;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int ll = lt * 32 + crow(r, h);
+      if (ll < g.L) out[(int64_t)ll * D + 32 * t + c] = acc[t][r];
+    }
 }
 
 csa_status rfail(csa_status s, const char* m) {
@@ -1086,11 +1163,13 @@ RelLayout rel_layout(int64_t B, int64_t H, int64_t N, int64_t L, int64_t d) {
   R.Lp = ((L + 3) / 4) * 4;
   // dlq / dlk sum over the whole batch: RS partial sums of B / RS elements each fill the GPU
   // (a single reduction chain per output tile left only H * 10 waves)
-  R.RS = (int)(B < 16 ? B : 16);
-  size_t o = 0;
-  auto take = [&](size_t bytes) { size_t r = o; o += ral(bytes); return r; };
   R.fused = (d == 64);
   R.NP = ((N + 31) / 32) * 32;
+  // fused: k_rel_lgrad splits the B * NP / 32 chunks of x over RS waves per (l tile, head); otherwise the
+  // k_bgemm R-split sums RS partials of B / RS elements each (one chain per tile left only H * 10 waves)
+  R.RS = R.fused ? (int)std::min<int64_t>(32, B * R.NP / 32) : (int)(B < 16 ? B : 16);
+  size_t o = 0;
+  auto take = [&](size_t bytes) { size_t r = o; o += ral(bytes); return r; };
   R.c2p = take(sizeof(float) * B * H * N * R.Lp);
   R.p2ct = take(sizeof(float) * B * H * N * R.Lp);
   // prepared planes: at most one per head (fewer when heads share planes, e.g. the CSE's 2)
@@ -1102,10 +1181,10 @@ RelLayout rel_layout(int64_t B, int64_t H, int64_t N, int64_t L, int64_t d) {
   R.ldg = ((N + 3) / 4) * 4;
   R.G = take(R.fused ? 0 : sizeof(float) * B * H * N * R.ldg);
   R.P = take(R.fused ? 0 : sizeof(float) * B * H * N * R.ldg);
-  R.ldx = ((N + 3) / 4) * 4;  // fused: G tables stored transposed (B,H,Lp,ldx)
-  R.gc2p = take(R.fused ? sizeof(float) * B * H * R.Lp * R.ldx : sizeof(float) * B * H * N * R.Lp);
-  R.gp2ct = take(R.fused ? sizeof(float) * B * H * R.Lp * R.ldx : sizeof(float) * B * H * N * R.Lp);
-  R.part = take(sizeof(float) * R.RS * H * L * d);
+  R.ldx = R.NP;  // fused: G tables stored transposed (H, B, Lp, ldx), x = n
+  R.gc2p = take(R.fused ? sizeof(float) * H * B * R.Lp * R.ldx : sizeof(float) * B * H * N * R.Lp);
+  R.gp2ct = take(R.fused ? sizeof(float) * H * B * R.Lp * R.ldx : sizeof(float) * B * H * N * R.Lp);
+  R.part = take(sizeof(float) * (R.fused ? 2 : 1) * R.RS * H * L * d);  // fused: dlk and dlq partials
   R.qstat = take(R.fused ? sizeof(float) * B * H * N * 4 : 0);
   R.ws_total = o;
   return R;
@@ -1200,15 +1279,27 @@ void rel_param_grads(const csa_rel_attn_args* a, const csa_rel_attn_bwd_args* b,
   const int B = (int)a->B, H = (int)a->H, N = (int)a->N, L = (int)a->L, D = (int)a->d;
   const int64_t Lp = R.Lp;
   // dlk_h = sum_b G_c2p^T Q ; dlq_h = sum_b G_p2cT^T K    (C(m=r, n=dd) = sum_b sum_x G(x,r) X(x,dd))
+  if (R.fused) {
+    float* part = (float*)((char*)ws + R.part);
+    const int64_t n = (int64_t)H * L * D;
+    LgradArgs g;
+    g.G[0] = gc2p; g.G[1] = gp2ct; g.X[0] = a->q; g.X[1] = a->k;
+    g.x_sb[0] = a->q_sb; g.x_sh[0] = a->q_sh; g.x_sn[0] = a->q_sn;
+    g.x_sb[1] = a->k_sb; g.x_sh[1] = a->k_sh; g.x_sn[1] = a->k_sn;
+    g.part[0] = part; g.part[1] = part + (int64_t)R.RS * n;
+    g.ldx = R.ldx; g.Lp = (int)Lp; g.L = L; g.NP = (int)R.NP; g.B = B; g.N = N; g.H = H; g.nsplit = R.RS;
+    hipLaunchKernelGGL(k_rel_lgrad, dim3((unsigned)H, (unsigned)(2 * R.RS)), dim3(64 * (unsigned)((L + 31) / 32)),
+                       2 * 32 * 64 * 4, st, g);
+    for (int which = 0; which < 2; ++which)
+      hipLaunchKernelGGL(k_sum_splits, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, g.part[which],
+                         which == 0 ? b->dlk : b->dlq, n, R.RS, n);
+    return;
+  }
   for (int which = 0; which < 2; ++which) {
     GemmArgs g;
     memset(&g, 0, sizeof(g));
     g.A = which == 0 ? gc2p : gp2ct;
-    if (R.fused) {  // (B,H,Lp,ldx): x contiguous
-      g.a_m = R.ldx; g.a_k = 1; g.a_b1 = 0; g.a_b2 = Lp * R.ldx; g.a_r = (int64_t)H * Lp * R.ldx;
-    } else {
-      g.a_m = 1; g.a_k = Lp; g.a_b1 = 0; g.a_b2 = (int64_t)N * Lp; g.a_r = (int64_t)H * N * Lp;
-    }
+    g.a_m = 1; g.a_k = Lp; g.a_b1 = 0; g.a_b2 = (int64_t)N * Lp; g.a_r = (int64_t)H * N * Lp;
     const float* X = which == 0 ? a->q : a->k;
     g.B = X; g.b_n = 1; g.b_k = which == 0 ? a->q_sn : a->k_sn; g.b_b1 = 0;
     g.b_b2 = which == 0 ? a->q_sh : a->k_sh; g.b_r = which == 0 ? a->q_sb : a->k_sb;
