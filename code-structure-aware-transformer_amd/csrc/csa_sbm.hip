@@ -1589,7 +1589,8 @@ template <int NTO, int NTI, int S4MAX, int NSTEP, bool FL>
 __device__ __forceinline__ void mm_acc_f(const float* __restrict__ frag, const f32x16 (&in)[NTI], f32x16 (&out)[NTO]) {
 #pragma unroll
   for (int t = 0; t < NTO; ++t) out[t] = zero16();
-  frag_chain<NTO, S4MAX, 1, FL>(frag, NSTEP, out, [&](int s) { return in[s / 16][s % 16]; });
+  // L2 fragments two K-groups ahead (measured 2% faster k_proj_bwd_s<64> than one), LDS fragments one
+  frag_chain<NTO, S4MAX, (FL || S4MAX < 4) ? 1 : 2, FL>(frag, NSTEP, out, [&](int s) { return in[s / 16][s % 16]; });
 }
 
 template <int D, int KT>
