@@ -1813,11 +1813,15 @@ struct ProjBwdSmallShape {
   // d = 96 (one workgroup per CU anyway): weight fragments in LDS. WF holds the d x d layer of the next
   // chain product (W2, W1, W0 in turn, DMA'd a stage ahead); CF / SF the head's cluster fragments
   // (K-groups 0, 1 only: k <= 16), loaded once.
-  // (d = 64 with LW, one workgroup per CU instead of two, measured no faster: 0.404 vs 0.402 ms)
-  static constexpr bool LW = D == 96;
-  static constexpr int WF = 8 * REG + 4 * HATF + 4 * GINF, WFF = LW ? D * D : 0;
-  static constexpr int CF = WF + WFF, CFF = LW ? D / 32 * 512 : 0, SF = CF + CFF, SFF = LW ? 512 : 0;
+  // d = 64 keeps two workgroups per CU within 80 KiB: the hat / gin blocks go into the wave's own DS region
+  // (free from B6 to the stage of layer 2, so they are DMA'd right after B6) and the small cluster chains
+  // read their fragments from L2 (LCS = 0). (Round 1's d = 64 LW with the d = 96 layout, 102 KiB, one
+  // workgroup per CU, measured no faster: 0.404 vs 0.402 ms.)
+  static constexpr bool LW = true, LCS = D == 96, HIN_DS = D == 64;
+  static constexpr int WF = 8 * REG + (HIN_DS ? 0 : 4 * HATF + 4 * GINF), WFF = LW ? D * D : 0;
+  static constexpr int CF = WF + WFF, CFF = LCS ? D / 32 * 512 : 0, SF = CF + CFF, SFF = LCS ? 512 : 0;
   // d = 64: 80 KiB (2 workgroups per CU); d = 96: 156 KiB
+  static_assert(!HIN_DS || 512 + HATF + GINF <= REG, "dZ scratch | hat | gin fit the wave's DS region");
   static constexpr size_t LDS_BYTES = sizeof(float) * (SF + SFF);
   static_assert(4 * PARTF + (D == 96 ? 9 * 1024 : 0) <= 8 * REG, "end-of-kernel partials fit the staging");
 };
@@ -1899,12 +1903,12 @@ __device__ __forceinline__ void own_rowsum(const float* __restrict__ dsw, float 
 }
 
 template <int D>
-__global__ __launch_bounds__(256, ProjBwdSmallShape<D>::LW ? 1 : 2) void k_proj_bwd_s(const KArgs p) {
+__global__ __launch_bounds__(256, ProjBwdSmallShape<D>::LCS ? 1 : 2) void k_proj_bwd_s(const KArgs p) {
   static_assert(D == 64 || D == 96, "d x d stages split over 4 waves for d = 64 and 96");
   using Sh = ProjBwdSmallShape<D>;
   using Sf = ProjBwdShape<D, 1>;  // slab layout
   constexpr int DT = Sh::DT, NS = Sh::NS, REG = Sh::REG, NSL = Sh::NSL, ABLK = Sf::ABLK;
-  constexpr bool LW = Sh::LW;
+  constexpr bool LW = Sh::LW, LCS = Sh::LCS, HIN_DS = Sh::HIN_DS;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* DS = lds;
   float* IN = lds + 4 * REG;
@@ -1923,10 +1927,13 @@ __global__ __launch_bounds__(256, ProjBwdSmallShape<D>::LW ? 1 : 2) void k_proj_
   const float* SFs = lds + Sh::SF;
   float* DSw = DS + w * REG;
   float* INw = IN + w * REG;
-  float* HATw = lds + 8 * REG + w * Sh::HATF;
-  const uint32_t INl = lds_offset(IN) + 4 * REG * w, HATl = lds_offset(lds) + 4 * (8 * REG + w * Sh::HATF);
-  const float* GINw = lds + 8 * REG + 4 * Sh::HATF + w * Sh::GINF;
-  const uint32_t GINl = lds_offset(lds) + 4 * (8 * REG + 4 * Sh::HATF + w * Sh::GINF);
+  // hat / gin blocks: HIN_DS: floats [512, 1536) of the wave's DS region (after the dZ scratch)
+  const int hat_f = HIN_DS ? w * REG + 512 : 8 * REG + w * Sh::HATF;
+  const int gin_f = HIN_DS ? w * REG + 512 + Sh::HATF : 8 * REG + 4 * Sh::HATF + w * Sh::GINF;
+  float* HATw = lds + hat_f;
+  const uint32_t INl = lds_offset(IN) + 4 * REG * w, HATl = lds_offset(lds) + 4 * hat_f;
+  const float* GINw = lds + gin_f;
+  const uint32_t GINl = lds_offset(lds) + 4 * gin_f;
   f32x16 acc[3][NSL];  // this wave's dW2 | dW1 | dW0 tile slots (outer_stage_s)
 #pragma unroll
   for (int l = 0; l < 3; ++l)
@@ -1966,7 +1973,7 @@ __global__ __launch_bounds__(256, ProjBwdSmallShape<D>::LW ? 1 : 2) void k_proj_
   auto load_wf = [&](int l) {
     dma_block16<D * D>(lds_offset(lds) + 4 * Sh::WF + D * D * w, make_rsrc(p.WfT[l], 4 * D * D), D * D * w);
   };
-  if constexpr (LW) {  // the head's cluster fragments, K-groups 0 and 1 of each tile (2 KiB pieces)
+  if constexpr (LCS) {  // the head's cluster fragments, K-groups 0 and 1 of each tile (2 KiB pieces)
     if (w < DT) dma_block16<2048>(lds_offset(lds) + 4 * (Sh::CF + 512 * w), make_rsrc(CfT, 4 * 32 * D), 4096 * w);
     else if (w == 3) dma_block16<2048>(lds_offset(lds) + 4 * Sh::SF, make_rsrc(SfT, 4 * 32 * 32), 0);
     wait_vm_all();
@@ -2023,7 +2030,7 @@ __global__ __launch_bounds__(256, ProjBwdSmallShape<D>::LW ? 1 : 2) void k_proj_
     for (int r = 0; r < 16; ++r) hat[r] = r < 8 ? HATw[act_off(crow(r, h), c)] : 0.f;
     f32x16 dz[1];
     if (it.isK) {
-      mm_acc_f<1, 1, 2, LW ? 8 : 16, LW>(LW ? SFs : SfT, gin, dz);  // dKh^T = S^T dT^T (clusters < 16)
+      mm_acc_f<1, 1, 2, LCS ? 8 : 16, LCS>(LCS ? SFs : SfT, gin, dz);  // dKh^T = S^T dT^T (clusters < 16)
     } else {
       dz[0] = gin[0];
     }
@@ -2039,7 +2046,7 @@ __global__ __launch_bounds__(256, ProjBwdSmallShape<D>::LW ? 1 : 2) void k_proj_
     }
     // ---- dp^T = C^T dZ^T (clusters < 16)
     f32x16 dcur[DT];
-    mm_acc_f<DT, 1, 2, LW ? 8 : 16, LW>(LW ? CFs : CfT, dz, dcur);
+    mm_acc_f<DT, 1, 2, LCS ? 8 : 16, LCS>(LCS ? CFs : CfT, dz, dcur);
     wait_vm_all();  // po (LW: and the W2 fragments)
     // ---- dC_h += dZ^T po, private 16x16x4: A = dZ[row 4s + g4][cluster c16], B = po[row 4s + g4][16t + c16]
 #pragma unroll
@@ -2137,7 +2144,7 @@ __global__ __launch_bounds__(256, ProjBwdSmallShape<D>::LW ? 1 : 2) void k_proj_
     PHASE(5);
     __syncthreads();  // B5
     PHASE(2);
-    if constexpr (LW) prefetch_next();  // (after the W0 wait above)
+    if constexpr (LW && !HIN_DS) prefetch_next();  // (after the W0 wait above)
     outer_stage_s<D>(DS, IN, acc[2], w, ln);
     own_rowsum<D>(DSw, dbp[0], ln);
     if constexpr (LW) load_old();  // LW: the dQ / dK rows load under the dx chain (fewer live registers)
@@ -2159,7 +2166,8 @@ __global__ __launch_bounds__(256, ProjBwdSmallShape<D>::LW ? 1 : 2) void k_proj_
     __syncthreads();  // B6: DS / IN free for the next group (LW: WF too)
     PHASE(2);
     if constexpr (LW) {
-      if (more) load_wf(2);
+      if constexpr (HIN_DS) prefetch_next();  // DS regions are free: hat / gin first (the next group top
+      if (more) load_wf(2);                   // waits for them with the W2 fragments still in flight)
     }
   }
 #ifdef CSA_PHASES
