@@ -510,9 +510,14 @@ __device__ __forceinline__ void bins_scatter(float* bins, int LB, const float (&
 
 // acc[t] (rows d = 32 t + crow(r,h), lanes = the bins' rows) += sum_r Lmat[r][d] * bins[lane row][r]
 // (dq_rel = G_c2p LK or dk_rel = G_p2cT LQ), K = 2 KB2 (lin perm: k = s + KB2 h), Lmat rows >= L read 0.
+// The Lmat operand comes from L2 (the head's L x d matrix): a ring of RING groups of 4 K-steps is kept in
+// flight (RING - 1 groups ahead, ~1500 MFMA cycles), which covers the L2 latency at one wave per SIMD;
+// a lookahead of one group left this phase latency-bound. The chunks of RING groups run unguarded
+// (a prefetch past the end loads a clamped, never-used row); the < RING leftover groups follow.
 template <int DT>
 __device__ __forceinline__ void bins_times(f32x16 (&acc)[DT], const float* bins, int LB, int KB2,
                                            const float* __restrict__ Lmat, int L, int D) {
+  constexpr int RING = 4;
   const int c = lane_id() & 31, h = lane_id() >> 5;
   const float* brow = bins + c * LB + KB2 * h;
   auto lmat = [&](int s4, float (&v)[4][DT]) {  // Lmat rows s4 + e + KB2 h (0 beyond L), columns 32 t + c
@@ -527,26 +532,27 @@ __device__ __forceinline__ void bins_times(f32x16 (&acc)[DT], const float* bins,
       }
     }
   };
-  float lv[2][4][DT];
-  lmat(0, lv[0]);
-  for (int s4 = 0; s4 < KB2; s4 += 8) {  // two groups of 4 K-steps per trip: group g+1's loads fly under g
-    if (s4 + 4 < KB2) lmat(s4 + 4, lv[1]);
-    {
-      const f32x4 bv = *reinterpret_cast<const f32x4*>(brow + s4);
+  auto group = [&](int g, const float (&v)[4][DT]) {
+    const f32x4 bv = *reinterpret_cast<const f32x4*>(brow + 4 * g);
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
+    for (int e = 0; e < 4; ++e)
 #pragma unroll
-        for (int t = 0; t < DT; ++t) acc[t] = mfma(lv[0][e][t], bv[e], acc[t]);
-    }
-    if (s4 + 4 < KB2) {
-      if (s4 + 8 < KB2) lmat(s4 + 8, lv[0]);
-      const f32x4 bv = *reinterpret_cast<const f32x4*>(brow + s4 + 4);
+      for (int t = 0; t < DT; ++t) acc[t] = mfma(v[e][t], bv[e], acc[t]);
+  };
+  const int ng = KB2 / 4, ngf = ng / RING * RING;  // groups of 4 K-steps per half; in whole chunks
+  float lv[RING][4][DT];
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
+  for (int u = 0; u < RING - 1; ++u) lmat(4 * u, lv[u]);
+  for (int g0 = 0; g0 < ngf; g0 += RING) {
 #pragma unroll
-        for (int t = 0; t < DT; ++t) acc[t] = mfma(lv[1][e][t], bv[e], acc[t]);
+    for (int u = 0; u < RING; ++u) {
+      lmat(4 * (g0 + u + RING - 1), lv[(u + RING - 1) % RING]);
+      group(g0 + u, lv[u]);
     }
   }
+#pragma unroll
+  for (int u = 0; u < RING - 1; ++u)  // leftover groups ngf + u < ng: already in ring slot u
+    if (ngf + u < ng) group(ngf + u, lv[u]);
 }
 
 // bins row of this lane (row = lane & 31, the half's columns [KB2 h, KB2 h + KB2) clipped to Lp) -> column

@@ -581,7 +581,7 @@ template <int D, int KT>
 struct ProjFwdLds {
   static constexpr int WB = D * D * 4, CB = 32 * KT * D * 4, SB = 1024 * KT * KT * 4;  // bytes
 #ifdef CSA_EXP_PF6
-  static constexpr int NW = D == 64 ? 6 : 8;
+  static constexpr int NW = D == 64 ? 12 : 8;  // d = 64: one workgroup of 12 waves per CU (3 per SIMD)
 #else
   static constexpr int NW = D == 64 ? 4 : 8;  // d = 64: two workgroups per CU; d = 96: one of 8 waves
 #endif
@@ -594,7 +594,7 @@ struct ProjFwdLds {
 
 template <int D, int KT>
 #ifdef CSA_EXP_PF6
-__global__ __launch_bounds__((64 * ProjFwdLds<D, KT>::NW), (D == 64 ? 3 : 2)) void k_proj_fwd_l(const KArgs p) {
+__global__ __launch_bounds__((64 * ProjFwdLds<D, KT>::NW)) void k_proj_fwd_l(const KArgs p) {
 #else
 __global__ __launch_bounds__((64 * ProjFwdLds<D, KT>::NW)) void k_proj_fwd_l(const KArgs p) {
 #endif
@@ -2544,7 +2544,7 @@ csa_status launch_fwd(const csa_sbm_fwd_args* a, const Layout& L, hipStream_t st
       if constexpr (KT == 1) {  // k <= 32: weight fragments in LDS
         using PL = ProjFwdLds<D, KT>;
         if (proj_fwd_lds()) {
-          const int64_t items = a->B * (L.NQB + L.NKB), slots = (D == 64 ? 2 : 1) * 256LL;
+          const int64_t items = a->B * (L.NQB + L.NKB), slots = (D == 64 && PL::NW == 4 ? 2 : 1) * 256LL;
           const int G = (int)std::max<int64_t>(1, std::min<int64_t>(slots / a->H, (items + PL::NW - 1) / PL::NW));
           (void)hipFuncSetAttribute((const void*)k_proj_fwd_l<D, KT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)PL::BYTES);
