@@ -807,6 +807,22 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd
   for (int kt = 0; kt < p.NKB; ++kt) {
     const int j0 = kt * 32;
     wait_vm_all();  // tile kt's K/V/T images have landed
+    // the tile's Philox words depend only on (query, tile, head): computed first, so their VALU work can
+    // interleave with the S / expA MFMA chains below instead of waiting behind them
+    u32x4 r_ste[2], r_drop[2];
+    {
+      uint32_t sk0 = p.seed_lo, sk1 = p.seed_hi;  // opaque per tile: round keys are not held across the loop
+      asm volatile("" : "+s"(sk0), "+s"(sk1));
+#pragma unroll
+      for (int gp = 0; gp < 2; ++gp) {
+        if constexpr (!DENSE && !HAS_U)
+          r_ste[gp] = philox4x32(u32x4{(uint32_t)i, (uint32_t)(8 * kt + 4 * gp + h), (uint32_t)bh,
+                                       (RNG_STE << 28) ^ p.off}, sk0, sk1);
+        if constexpr (DROP)
+          r_drop[gp] = philox4x32(u32x4{(uint32_t)i, (uint32_t)(8 * kt + 4 * gp + h), (uint32_t)bh,
+                                        (RNG_ATTN_DROP << 28) ^ p.off}, sk0, sk1);
+      }
+    }
     // S^T = K Q^T : A operand = K rows from the image (row c, lin-perm chunks of half h)
     f32x16 sacc = zero16();
     if constexpr (BF) {
@@ -853,8 +869,6 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd
       s[r] = fmaf(sacc[r], p.scale, bz[r >> 2][r & 3]);
       tmax = fmaxf(tmax, s[r]);
     }
-    uint32_t sk0 = p.seed_lo, sk1 = p.seed_hi;  // opaque per tile: round keys are not held across the loop
-    asm volatile("" : "+s"(sk0), "+s"(sk1));
     bool av[16], keep[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) { av[r] = true; keep[r] = true; }
@@ -870,8 +884,7 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd
       } else {
 #pragma unroll
         for (int gp = 0; gp < 2; ++gp) {
-          const u32x4 rr = philox4x32(u32x4{(uint32_t)i, (uint32_t)(8 * kt + 4 * gp + h), (uint32_t)bh,
-                                            (RNG_STE << 28) ^ p.off}, sk0, sk1);
+          const u32x4 rr = r_ste[gp];
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             const int r = 8 * gp + e;
@@ -883,8 +896,7 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd
     if constexpr (DROP) {
 #pragma unroll
       for (int gp = 0; gp < 2; ++gp) {
-        const u32x4 rr = philox4x32(u32x4{(uint32_t)i, (uint32_t)(8 * kt + 4 * gp + h), (uint32_t)bh,
-                                          (RNG_ATTN_DROP << 28) ^ p.off}, sk0, sk1);
+        const u32x4 rr = r_drop[gp];
 #pragma unroll
         for (int e = 0; e < 8; ++e) keep[8 * gp + e] = u16_of(rr, e) >= p.drop_thr;
       }
