@@ -11,7 +11,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CSA_HIP_LIB", os.path.join(_HERE, "lib", "libcsa_hip.so"))
 
-CSA_ABI_VERSION = 3
+CSA_ABI_VERSION = 4
 CSA_FLAG_DENSE = 1
 CSA_DTYPE_F32, CSA_DTYPE_BF16 = 0, 1
 STATUS = {0: "CSA_OK", 1: "CSA_INVALID_ARG", 2: "CSA_UNSUPPORTED_SHAPE", 3: "CSA_LAUNCH_FAILED"}
@@ -58,6 +58,7 @@ class SbmBwdArgs(ctypes.Structure):
         ("prof", ctypes.POINTER(CsaProf)),
         ("dx_sb", i64), ("dx_sh", i64), ("dx_sn", i64), ("dq_sb", i64), ("dq_sh", i64), ("dq_sn", i64),
         ("dk_sb", i64), ("dk_sh", i64), ("dk_sn", i64), ("dv_sb", i64), ("dv_sh", i64), ("dv_sn", i64),
+        ("dattn", vp),  # ABI v4
     ]
 
 

@@ -194,8 +194,10 @@ def sbm_bwd_op(Q: torch.Tensor, K: torch.Tensor, V: torch.Tensor, mask: Optional
                cluster_w: Optional[torch.Tensor], proj_w: List[torch.Tensor], proj_b: List[torch.Tensor],
                k: int, attn_p: float, proj_p: float, seed: int, offset: int, dense: bool, state: torch.Tensor,
                X: torch.Tensor, dX: torch.Tensor, dsparsity: Optional[torch.Tensor],
-               dgraph: Optional[torch.Tensor], bf16: bool = False, packed: bool = False) -> List[torch.Tensor]:
+               dgraph: Optional[torch.Tensor], bf16: bool = False, packed: bool = False,
+               dattn: Optional[torch.Tensor] = None) -> List[torch.Tensor]:
     """Backward of csa::sbm_fwd. Returns [dQ, dK, dV] (+ [dcluster_w, dW0, db0, dW1, db1, dW2, db2] if not dense).
+    dgraph / dattn: upstream gradients of the returned graph / attn maps (sbm_attn.py:66), or None.
     packed: [dQ, dK, dV] is replaced by ONE packed (B, N, 3, H, d) tensor (the gradient of a fused QKV
     projection, written in place by the kernels; see packed_qkv)."""
     Q, K, V, mask, cw, pw, pb, _ = _prep(Q, K, V, mask, cluster_w, proj_w, proj_b, None)
@@ -222,6 +224,14 @@ def sbm_bwd_op(Q: torch.Tensor, K: torch.Tensor, V: torch.Tensor, mask: Optional
     b.dk_sb, b.dk_sh, b.dk_sn = dK.stride()[:3]
     b.dv_sb, b.dv_sh, b.dv_sn = dV.stride()[:3]
     keep = []
+    ws = None
+    if dattn is not None or not dense:
+        ws = torch.empty(L.csa_sbm_bwd_workspace_bytes(B, H, N, M, d, k, flags), device=Q.device, dtype=torch.uint8)
+        b.workspace = ws.data_ptr()
+        keep.append(ws)
+    if dattn is not None:
+        dattn = dattn.float().contiguous()
+        b.dattn = dattn.data_ptr()
     if not dense:
         if dsparsity is not None:
             dsparsity = dsparsity.float().contiguous()
@@ -236,9 +246,6 @@ def sbm_bwd_op(Q: torch.Tensor, K: torch.Tensor, V: torch.Tensor, mask: Optional
             dw, db = torch.empty_like(pw[i]), torch.empty_like(pb[i])
             b.dproj_w[i], b.dproj_b[i] = dw.data_ptr(), db.data_ptr()
             outs += [dw, db]
-        ws = torch.empty(L.csa_sbm_bwd_workspace_bytes(B, H, N, M, d, k, flags), device=Q.device, dtype=torch.uint8)
-        b.workspace = ws.data_ptr()
-        keep.append(ws)
     if _PROF["bwd"] is not None:
         b.prof = ctypes.pointer(_PROF["bwd"])
     check(L.csa_sbm_bwd(ctypes.byref(b), _stream(Q.device)), "csa_sbm_bwd")
@@ -247,7 +254,7 @@ def sbm_bwd_op(Q: torch.Tensor, K: torch.Tensor, V: torch.Tensor, mask: Optional
 
 @sbm_bwd_op.register_fake
 def _(Q, K, V, mask, cluster_w, proj_w, proj_b, k, attn_p, proj_p, seed, offset, dense, state, X, dX, dsparsity,
-      dgraph, bf16=False, packed=False):
+      dgraph, bf16=False, packed=False, dattn=None):
     B, H, N, d = Q.shape
     outs = [Q.new_empty(B, N, 3, H, d)] if packed else [torch.empty_like(Q), torch.empty_like(K), torch.empty_like(V)]
     if not dense:
@@ -321,15 +328,12 @@ class SBMAttentionFunction(torch.autograd.Function):
     def backward(ctx, dX, dsp, dgraph, dattn):
         Q, K, V, mask, cluster_w, w0, b0, w1, b1, w2, b2, state, X = ctx.saved_tensors
         k, attn_p, proj_p, seed, dense, bf16 = ctx.cfg
-        if dattn is not None:  # device-side check: no host sync in the backward
-            torch._assert_async(torch.all(dattn == 0), "csa: gradients through the returned attn map are not "
-                                "supported; train through X / sparsity (as script/train.py does)")
         if dX is None:
             dX = torch.zeros_like(X)
         pw = [] if dense else [w0, w1, w2]
         pb = [] if dense else [b0, b1, b2]
         g = torch.ops.csa.sbm_bwd(Q, K, V, mask, None if dense else cluster_w, pw, pb, k, attn_p, proj_p, seed, 0,
-                                  dense, state, X, dX, dsp, None if dense else dgraph, bf16, ctx.packed)
+                                  dense, state, X, dX, dsp, None if dense else dgraph, bf16, ctx.packed, dattn)
         if ctx.packed:  # the three head-major views of the packed gradient (split_heads3's backward takes it whole)
             dQ, dK, dV = (g[0][:, :, i].transpose(1, 2) for i in range(3))
             g = [None, None] + list(g)

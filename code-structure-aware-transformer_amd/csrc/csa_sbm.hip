@@ -52,7 +52,7 @@ struct Layout {
   int64_t B, H, N, M, D, k, kp, KT, NQB, NKB, Mpad;
   size_t S, Qh, Kh, T, stats, Abits, Rbits, cnt, Wf[3], WfT[3], Cf, CfT, Sf, SfT, Act, total;
   // bwd workspace
-  size_t w_dQh, w_dT, w_slab, w_dS, w_dC, w_total;
+  size_t w_dQh, w_dT, w_slab, w_dS, w_dC, w_gx, w_total;
   int64_t G, slab_floats;
 };
 
@@ -111,6 +111,7 @@ Layout make_layout(int64_t B, int64_t H, int64_t N, int64_t M, int64_t D, int64_
   L.w_slab = take(sizeof(float) * H * L.G * L.slab_floats);
   L.w_dS = take(sizeof(float) * H * KP32 * KP32);
   L.w_dC = take(sizeof(float) * H * KP32 * D);
+  L.w_gx = take(sizeof(float) * B * H * N);  // used only when an attn-map gradient is passed
   L.w_total = o;
   return L;
 }
@@ -292,7 +293,8 @@ struct KArgs {
   // outputs
   float* X; int64_t x_sb, x_sh, x_sn;
   // backward
-  const float *dX, *dsp, *dgraph;
+  const float *dX, *dsp, *dgraph, *dattn;  // dgraph / dattn: upstream grads of the returned maps (or null)
+  float* gx;                               // dattn: per query row sum_j dattn_ij attn_ij (k_attn_gx)
   float *dQ, *dK, *dV, *dQh, *dT, *slab;
   int64_t dx_sb, dx_sh, dx_sn, dq_sb, dq_sh, dq_sn, dk_sb, dk_sh, dk_sn, dv_sb, dv_sh, dv_sn;
   int G; int64_t slab_floats;
@@ -1034,6 +1036,60 @@ __global__ __launch_bounds__(64) void k_maps(const KArgs p, float* __restrict__ 
   }
 }
 
+// gx[b,h,i] = sum_j dattn[b,h,i,j] * attn[b,h,i,j] for an upstream gradient of the returned attn map
+// (sbm_attn.py:62 F.normalize backward needs sum_j G_ij attn_ij over the TOTAL gradient G of attn; the
+// dX V^T part is rowsum(dX * X), computed by k_attn_bwd_q). Recomputes attn like k_maps (S orientation:
+// keys on lanes, queries in registers), one wave per (b, h, 32 queries); lane sums, then one reduction.
+template <int D, bool DENSE>
+__global__ __launch_bounds__(64) void k_attn_gx(const KArgs p) {
+  constexpr int NS = D / 2;
+  const int lane = lane_id(), c = lane & 31, h = lane >> 5;
+  const BhBlock xb = xcd_block(p.NQB, p.B * p.H);
+  if (!xb.valid) return;
+  const int qb = xb.blk, bh = xb.bh, b = bh / p.H, hd = bh % p.H;
+  const int i0 = qb * 32;
+  float q[NS];
+  load_run<NS>(q, p.Q + b * p.q_sb + hd * p.q_sh + (int64_t)imin(i0 + c, p.N - 1) * p.q_sn + h * NS, i0 + c < p.N);
+  float lse[16], invD[16], acc[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int ii = imin(i0 + crow(r, h), p.N - 1);
+    lse[r] = p.stats[((int64_t)bh * p.N + ii) * 4 + 0];
+    invD[r] = p.stats[((int64_t)bh * p.N + ii) * 4 + 1];
+    acc[r] = 0.f;
+  }
+  const float* kb = p.K + b * p.k_sb + hd * p.k_sh;
+  const float* mk = p.mask ? p.mask + b * p.mask_sb : nullptr;
+  for (int kt = 0; kt < p.NKB; ++kt) {
+    const int j = kt * 32 + c;
+    const bool jv = j < p.M;
+    const int jc = imin(j, p.M - 1);
+    float kr[NS];
+    load_run<NS>(kr, kb + (int64_t)jc * p.k_sn + h * NS, jv);
+    f32x16 sacc = zero16();
+#pragma unroll
+    for (int s2 = 0; s2 < NS; ++s2) sacc = mfma(q[s2], kr[s2], sacc);
+    const float mval = mk ? mk[jc] : 0.f;
+    const bool kval = jv && mval == 0.f;
+    const uint32_t word = DENSE ? 0xffffffffu : p.Abits[((int64_t)bh * p.NQB + qb) * p.Mpad + j];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int ii = i0 + crow(r, h);
+      const bool in = ii < p.N && jv;
+      const bool a = (word >> crow(r, h)) & 1u;
+      const float pv = kval ? __expf(sacc[r] * p.scale - lse[r]) : 0.f;
+      const float at = (a && in) ? pv * invD[r] : 0.f;
+      acc[r] = fmaf(ldz(p.dattn, ((int64_t)bh * p.N + imin(ii, p.N - 1)) * p.M + jc, INT64_MAX, in), at, acc[r]);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const float v = half_sum32(acc[r]);
+    const int ii = i0 + crow(r, h);
+    if (c == 0 && ii < p.N) p.gx[(int64_t)bh * p.N + ii] = v;
+  }
+}
+
 // ------------------------------------------------------------------------------------
 // Backward elementwise core for one (query i, key j) element (see oracle/closed_form.py)
 // ------------------------------------------------------------------------------------
@@ -1043,11 +1099,11 @@ struct Elem { float ds, g, attw; };
 // elements outside [0,N) x [0,M) are computed from finite stand-in operands and selected to zero.
 __device__ __forceinline__ Elem bwd_elem(float s_raw, float kbias, float dpp, bool a, bool keep, bool inside,
                                          float lse, float invD, float big, float gamma, float scale, float dscale,
-                                         float csp, float dgr) {
+                                         float csp, float dgr, float dam) {
   Elem r;
   const float P = __expf(fmaf(s_raw, scale, kbias) - lse);
   const float rm = keep ? dscale : 0.f;
-  const float dattn = dpp * rm;
+  const float dattn = dpp * rm + dam;  // dropout backward of dX V^T, plus the attn map's own gradient
   const bool mpos = a && (P > 0.f);
   const float dM = (dattn - ((big != 0.f && mpos) ? gamma : 0.f)) * invD;
   const float dPm = a ? dM : 0.f;
@@ -1083,7 +1139,7 @@ struct AttnBwdShape {
 // ------------------------------------------------------------------------------------
 // B2: per (b,h, query block), S^T orientation: dQ (attention path), dQh, gamma
 // ------------------------------------------------------------------------------------
-// DG: an upstream gradient of the graph output is present (p.dgraph)
+// DG: an upstream gradient of the graph and / or attn output is present (p.dgraph, p.dattn)
 template <int D, int KPH, bool DENSE, bool DROP, bool DG, bool BF>
 __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd_q(const KArgs p) {
   using SH = AttnBwdShape<D, KPH>;
@@ -1133,7 +1189,9 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
 #pragma unroll
     for (int s = 0; s < NS; ++s) gp = fmaf(dx[s], xr[s], gp);
   }
-  const float gamma = xhalf_sum(gp);
+  // gamma = sum_j G_ij attn_ij with G the total upstream gradient of attn: rowsum(dX * X) plus, with an
+  // attn-map gradient, sum_j dattn_ij attn_ij (k_attn_gx)
+  const float gamma = xhalf_sum(gp) + ((DG && p.dattn) ? p.gx[(int64_t)bh * p.N + ic] : 0.f);
   f32x4 st = *reinterpret_cast<const f32x4*>(p.stats + ((int64_t)bh * p.N + ic) * 4);
   if (iv && h == 0) p.stats[((int64_t)bh * p.N + i) * 4 + 3] = gamma;
   const float lse = st[0], invD = st[1], big = st[2];
@@ -1219,9 +1277,11 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
       const bool a = (a_w >> c) & 1u;
       const bool keep = (r_w >> c) & 1u;
       const bool inside = iv && (j < p.M);
-      const float dgr = DG ? ldz(p.dgraph, ((int64_t)bh * p.N + ic) * p.M + imin(j, p.M - 1), INT64_MAX, inside) : 0.f;
+      const int64_t me = ((int64_t)bh * p.N + ic) * p.M + imin(j, p.M - 1);
+      const float dgr = (DG && p.dgraph) ? ldz(p.dgraph, me, INT64_MAX, inside) : 0.f;
+      const float dam = (DG && p.dattn) ? ldz(p.dattn, me, INT64_MAX, inside) : 0.f;
       const Elem e = bwd_elem(sacc[r], bz[r >> 2][r & 3], dpacc[r], DENSE ? inside : a, keep, inside, lse, invD, big,
-                              gamma, p.scale, dscale, csp, dgr);
+                              gamma, p.scale, dscale, csp, dgr, dam);
       dsv[r] = e.ds;
       gv[r] = e.g;
     }
@@ -1361,9 +1421,11 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
         const f32x4 st = lds_f4(lds, SH::KS + 16 * crow(r, h));
         const bool a = DENSE ? inside : ((wA >> crow(r, h)) & 1u);
         const bool keep = (wR >> crow(r, h)) & 1u;
-        const float dgr = DG ? ldz(p.dgraph, ((int64_t)bh * p.N + imin(ii, p.N - 1)) * p.M + jc, INT64_MAX, inside) : 0.f;
+        const int64_t me = ((int64_t)bh * p.N + imin(ii, p.N - 1)) * p.M + jc;
+        const float dgr = (DG && p.dgraph) ? ldz(p.dgraph, me, INT64_MAX, inside) : 0.f;
+        const float dam = (DG && p.dattn) ? ldz(p.dattn, me, INT64_MAX, inside) : 0.f;
         const Elem e = bwd_elem(sacc[r], kbias, dpacc[r], a, keep, inside, st[0], st[1], st[2], st[3], p.scale, dscale,
-                                csp, dgr);
+                                csp, dgr, dam);
         dsv[rr] = e.ds;
         gv[rr] = e.g;
         awv[rr] = e.attw;
@@ -2598,7 +2660,9 @@ void launch_attn_bwd_v(const KArgs& p, int BH, const Layout& L, const csa_prof* 
 
 template <int D, int KPH, bool DENSE, bool BF>
 void launch_attn_bwd_b(const KArgs& p, int BH, const Layout& L, bool drop, const csa_prof* pf, hipStream_t st) {
-  const bool dg = p.dgraph != nullptr;
+  const bool dg = p.dgraph != nullptr || p.dattn != nullptr;
+  if (p.dattn)  // sum_j dattn_ij attn_ij per query row, read by k_attn_bwd_q's gamma
+    hipLaunchKernelGGL((k_attn_gx<D, DENSE>), dim3(xcd_grid((int)L.NQB, BH)), dim3(64), 0, st, p);
   if (drop) {
     if (dg) launch_attn_bwd_v<D, KPH, DENSE, true, true, BF>(p, BH, L, pf, st);
     else launch_attn_bwd_v<D, KPH, DENSE, true, false, BF>(p, BH, L, pf, st);
@@ -2621,7 +2685,8 @@ csa_status launch_bwd(const csa_sbm_bwd_args* b, const Layout& L, hipStream_t st
   const csa_sbm_fwd_args* a = b->fwd;
   KArgs p = make_kargs(a, L);
   const bool dense = a->flags & CSA_FLAG_DENSE;
-  p.dX = b->dX; p.dsp = b->dsparsity; p.dgraph = b->dgraph;
+  p.dX = b->dX; p.dsp = b->dsparsity; p.dgraph = b->dgraph; p.dattn = b->dattn;
+  p.gx = b->workspace ? (float*)((char*)b->workspace + L.w_gx) : nullptr;
   p.dQ = b->dQ; p.dK = b->dK; p.dV = b->dV;
   {
     const Str3 x = strides_or_contig(b->dx_sb, b->dx_sh, b->dx_sn, a->H, a->N, a->d);
@@ -2746,8 +2811,8 @@ csa_status csa_sbm_bwd(const csa_sbm_bwd_args* b, void* stream) {
   if (s != CSA_OK) return s;
   const csa_sbm_fwd_args* a = b->fwd;
   const bool dense = a->flags & CSA_FLAG_DENSE;
-  if (!b->dX || !b->dQ || !b->dK || !b->dV || (!dense && !b->workspace))
-    return fail(CSA_INVALID_ARG, "null dX/dQ/dK/dV/workspace");
+  if (!b->dX || !b->dQ || !b->dK || !b->dV || ((!dense || b->dattn) && !b->workspace))
+    return fail(CSA_INVALID_ARG, "null dX/dQ/dK/dV/workspace (the workspace is required unless DENSE without dattn)");
   {
     auto al16 = [](const void* ptr, int64_t sb, int64_t sh, int64_t sn) {
       return (((uintptr_t)ptr) % 16 == 0) && sb % 4 == 0 && sh % 4 == 0 && sn % 4 == 0;

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define CSA_ABI_VERSION 3
+#define CSA_ABI_VERSION 4
 
 typedef enum csa_status {
   CSA_OK = 0,
@@ -113,6 +113,9 @@ typedef struct csa_sbm_bwd_args {
   /* ABI v3: element strides (b, h, row) of dX, dQ, dK, dV; a zero triple = contiguous. E.g. dQ/dK/dV
    * as the three head-major views of one packed (B,N,3,H,d) gradient of a fused QKV projection. */
   int64_t dx_sb, dx_sh, dx_sn, dq_sb, dq_sh, dq_sn, dk_sb, dk_sh, dk_sn, dv_sb, dv_sh, dv_sn;
+  /* ABI v4: (B,H,N,M) contiguous upstream gradient of the returned attn map (sbm_attn.py:62, the tensor the
+   * reference returns), or NULL. Needs the workspace, also for DENSE. */
+  const float* dattn;
 } csa_sbm_bwd_args;
 
 int csa_abi_version(void);

@@ -38,6 +38,24 @@ def test_sbm_oracle_matches_reference(golden, case):
         np.testing.assert_allclose(p.grad.numpy(), z["g:" + pk], rtol=1e-4, atol=1e-5, err_msg=pk)
 
 
+@pytest.mark.parametrize("case", ["sbm_n37_mapgrad", "sbm_n33_d96_mapgrad"])
+def test_sbm_oracle_map_gradients(golden, case):
+    """Upstream gradients of the returned graph and attn maps (sbm_attn.py:66) flow like the reference's."""
+    z = golden(case)
+    B, H, N, d, k = z["meta"]
+    Q, K, V = t(z["Q"], True), t(z["K"], True), t(z["V"], True)
+    params = sbm_params(z)
+    X, sp, graph, attn = sbm_ref.sbm_attention(Q, K, V, t(z["mask"]), params, t(z["u"]), int(k))
+    assert np.array_equal(graph.detach().numpy().astype(np.uint8), z["graph"])
+    loss = ((X * t(z["dX"])).sum() + (sp * t(z["dsparsity"])).sum() + (graph * t(z["dgraph"])).sum()
+            + (attn * t(z["dattn"])).sum())
+    loss.backward()
+    for name, g in (("dQ", Q.grad), ("dK", K.grad), ("dV", V.grad)):
+        np.testing.assert_allclose(g.numpy(), z[name], rtol=1e-4, atol=1e-5, err_msg=name)
+    for pk, p in params.items():
+        np.testing.assert_allclose(p.grad.numpy(), z["g:" + pk], rtol=1e-4, atol=1e-5, err_msg=pk)
+
+
 @pytest.mark.parametrize("case", SBM_CASES)
 def test_sampler_bit_exact_on_reference_expA(golden, case):
     """STE.py:10-15: A = u < clamp(expA, .01, .99) — bit-exact given the reference's own expA."""
@@ -64,14 +82,17 @@ def test_closed_form_matches_reference(golden, case):
         np.testing.assert_allclose(g[pk].numpy(), z["g:" + pk], rtol=1e-4, atol=1e-5, err_msg=pk)
 
 
-@pytest.mark.parametrize("case", ["full_n37", "full_n150"])
+@pytest.mark.parametrize("case", ["full_n37", "full_n150", "full_n37_mapgrad"])
 def test_full_attention_oracle(golden, case):
     z = golden(case)
     Q, K, V = t(z["Q"], True), t(z["K"], True), t(z["V"], True)
     X, sp, graph, attn = sbm_ref.full_attention(Q, K, V, t(z["mask"]))
     np.testing.assert_allclose(X.detach().numpy(), z["X"], rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(attn.detach().numpy(), z["attn"], rtol=1e-5, atol=1e-6)
-    (X * t(z["dX"])).sum().backward()
+    loss = (X * t(z["dX"])).sum()
+    if "dattn" in z:
+        loss = loss + (attn * t(z["dattn"])).sum()
+    loss.backward()
     for name, gg in (("dQ", Q.grad), ("dK", K.grad), ("dV", V.grad)):
         np.testing.assert_allclose(gg.numpy(), z[name], rtol=1e-4, atol=1e-5)
 

@@ -70,6 +70,56 @@ def test_sbm_forward_backward_matches_reference(golden, case):
 
 
 @pytest.mark.skipif(not has_gpu(), reason="needs GPU")
+@pytest.mark.parametrize("case", ["sbm_n37_mapgrad", "sbm_n33_d96_mapgrad"])
+def test_sbm_map_gradients_match_reference(golden, case):
+    """Gradients through the returned graph and attn maps (sbm_attn.py:66; ABI v4 dattn) as the reference's.
+    A graph flip at a near-tie (flips_allowed) is pinned by re-running the CPU oracle with u nudged to the
+    GPU's side of the tie."""
+    from oracle import sbm_ref
+    z = golden(case)
+    B, H, N, d, k = (int(v) for v in z["meta"])
+    m = make_module(z, k)
+    Q, K, V = dev(z["Q"], True), dev(z["K"], True), dev(z["V"], True)
+    m.uniforms = dev(z["u"])
+    X, sp, graph, attn = m(Q, K, V, dev(z["mask"]))
+    g = graph.detach().cpu().numpy().astype(np.uint8)
+    nflip = flips_allowed(g, z)
+    loss = ((X * dev(z["dX"])).sum() + (sp * dev(z["dsparsity"])).sum() + (graph * dev(z["dgraph"])).sum()
+            + (attn * dev(z["dattn"])).sum())
+    loss.backward()
+    if nflip == 0:
+        ref = {n: z[n] for n in ("dQ", "dK", "dV")}
+        ref.update({pn: z["g:" + pn] for pn, _ in m.named_parameters()})
+    else:
+        u = z["u"].copy()
+        u[g != z["graph"]] = np.where(g[g != z["graph"]] == 1, 0.0, 1.0)  # force the GPU's samples
+        tq, tk, tv = (torch.from_numpy(z[n]).requires_grad_(True) for n in ("Q", "K", "V"))
+        params = {kk[2:]: torch.from_numpy(v).requires_grad_(True) for kk, v in z.items() if kk.startswith("p:")}
+        Xr, spr, gr, ar = sbm_ref.sbm_attention(tq, tk, tv, torch.from_numpy(z["mask"]), params, torch.from_numpy(u), k)
+        ((Xr * torch.from_numpy(z["dX"])).sum() + (spr * torch.from_numpy(z["dsparsity"])).sum()
+         + (gr * torch.from_numpy(z["dgraph"])).sum() + (ar * torch.from_numpy(z["dattn"])).sum()).backward()
+        ref = {"dQ": tq.grad.numpy(), "dK": tk.grad.numpy(), "dV": tv.grad.numpy()}
+        ref.update({pn: params[pn].grad.numpy() for pn in params})
+    for name, t in (("dQ", Q), ("dK", K), ("dV", V)):
+        np.testing.assert_allclose(t.grad.cpu().numpy(), ref[name], rtol=RTOL, atol=ATOL, err_msg=name)
+    for pn, p in m.named_parameters():
+        np.testing.assert_allclose(p.grad.cpu().numpy(), ref[pn], rtol=RTOL, atol=ATOL, err_msg=pn)
+
+
+@pytest.mark.skipif(not has_gpu(), reason="needs GPU")
+def test_full_attention_attn_gradient_matches_reference(golden):
+    from csa_amd.module.sbm_attn import FullAttention
+    z = golden("full_n37_mapgrad")
+    B, H, N, d = (int(v) for v in z["meta"])
+    m = FullAttention({"attention_dropout": 0.2, "head_dim": d, "num_head": H}, 0).cuda().eval()
+    Q, K, V = dev(z["Q"], True), dev(z["K"], True), dev(z["V"], True)
+    X, sp, graph, attn = m(Q, K, V, dev(z["mask"]))
+    ((X * dev(z["dX"])).sum() + (attn * dev(z["dattn"])).sum()).backward()
+    for name, t in (("dQ", Q), ("dK", K), ("dV", V)):
+        np.testing.assert_allclose(t.grad.cpu().numpy(), z[name], rtol=RTOL, atol=ATOL, err_msg=name)
+
+
+@pytest.mark.skipif(not has_gpu(), reason="needs GPU")
 @pytest.mark.parametrize("case", SBM_CASES)
 def test_ste_sample_bit_exact(golden, case):
     """STE.py:10-15 on the reference's own expA and uniforms: bit-exact."""

@@ -78,7 +78,7 @@ def np32(t):
     return t.detach().cpu().numpy().astype(np.float32)
 
 
-def sbm_case(name, B, H, N, d, k, pad_counts, seed, zero_row=None, noncontig=False):
+def sbm_case(name, B, H, N, d, k, pad_counts, seed, zero_row=None, noncontig=False, map_grads=False):
     g = torch.Generator().manual_seed(seed)
     torch.manual_seed(seed)
     mod = SA.SBMAttention({"attention_dropout": 0.2, "head_dim": d, "num_head": H, "num_clusters": [k]}, 0)
@@ -113,11 +113,17 @@ def sbm_case(name, B, H, N, d, k, pad_counts, seed, zero_row=None, noncontig=Fal
         Kh = torch.sigmoid(torch.matmul(mod.proj(K), c.transpose(-1, -2)))
         expA = torch.matmul(Qh, torch.matmul(S, Kh.transpose(-1, -2)))
     loss = (X * dX).sum() + (sparsity * dsp).sum()
+    extra = {}
+    if map_grads:  # upstream gradients of the returned graph and attn maps too (sbm_attn.py:66)
+        dgraph = 0.1 * torch.randn(B, H, N, N, generator=g)
+        dattn = torch.randn(B, H, N, N, generator=g)
+        loss = loss + (graph * dgraph).sum() + (attn * dattn).sum()
+        extra = dict(dgraph=np32(dgraph), dattn=np32(dattn))
     loss.backward()
     out = dict(Q=np32(Q), K=np32(K), V=np32(V), mask=np32(mask), u=np32(u), dX=np32(dX), dsparsity=np32(dsp),
                X=np32(X), sparsity=np32(sparsity), graph=graph.detach().numpy().astype(np.uint8), attn=np32(attn),
                expA=np32(expA), dQ=np32(Q.grad), dK=np32(K.grad), dV=np32(V.grad),
-               meta=np.array([B, H, N, d, k], np.int64))
+               meta=np.array([B, H, N, d, k], np.int64), **extra)
     for n_, p in mod.named_parameters():
         out["p:" + n_] = np32(p)
         out["g:" + n_] = np32(p.grad)
@@ -125,7 +131,7 @@ def sbm_case(name, B, H, N, d, k, pad_counts, seed, zero_row=None, noncontig=Fal
     print(f"{name}: sparsity={sparsity.detach().numpy()} |X|={X.abs().max().item():.3g}")
 
 
-def full_case(name, B, H, N, d, pad_counts, seed):
+def full_case(name, B, H, N, d, pad_counts, seed, map_grads=False):
     g = torch.Generator().manual_seed(seed)
     mod = SA.FullAttention({"attention_dropout": 0.2, "head_dim": d, "num_head": H}, 0).eval()
     Q, K, V = (torch.randn(B, H, N, d, generator=g).requires_grad_(True) for _ in range(3))
@@ -136,10 +142,16 @@ def full_case(name, B, H, N, d, pad_counts, seed):
     dX = torch.randn(B, H, N, d, generator=g)
     X, sp, graph, attn = mod(Q, K, V, mask)
     assert sp is None and graph is mask
-    (X * dX).sum().backward()
+    loss = (X * dX).sum()
+    extra = {}
+    if map_grads:  # upstream gradient of the returned attn map too (sbm_attn.py:87)
+        dattn = torch.randn(B, H, N, N, generator=g)
+        loss = loss + (attn * dattn).sum()
+        extra = dict(dattn=np32(dattn))
+    loss.backward()
     np.savez_compressed(os.path.join(OUT, f"{name}.npz"), Q=np32(Q), K=np32(K), V=np32(V), mask=np32(mask),
                         dX=np32(dX), X=np32(X), attn=np32(attn), dQ=np32(Q.grad), dK=np32(K.grad),
-                        dV=np32(V.grad), meta=np.array([B, H, N, d], np.int64))
+                        dV=np32(V.grad), meta=np.array([B, H, N, d], np.int64), **extra)
     print(f"{name}: ok")
 
 
@@ -540,6 +552,11 @@ def main():
     if sys.argv[1:] == ["ast"]:
         ast_relations_case("ast_relations", seed=91)
         return
+    if sys.argv[1:] == ["mapgrad"]:  # only the round-2 map-gradient fixtures
+        sbm_case("sbm_n37_mapgrad", B=2, H=2, N=37, d=64, k=10, pad_counts=[0, 7], seed=17, map_grads=True)
+        sbm_case("sbm_n33_d96_mapgrad", B=1, H=2, N=33, d=96, k=10, pad_counts=[1], seed=18, map_grads=True)
+        full_case("full_n37_mapgrad", B=2, H=2, N=37, d=64, pad_counts=[0, 5], seed=23, map_grads=True)
+        return
     if sys.argv[1:] == ["large"]:  # only the round-2 production-shape fixtures
         rel_attn_large_case("rel_attn_n150_dk64", B=1, N=150, dk=64, L=150, seed=44)
         greedy_tiny_case("greedy_tiny", seed=72)
@@ -567,6 +584,9 @@ def main():
     adamw_case("adamw_nobias", seed=62)
     csatrans_case("csatrans_tiny", seed=71)
     if True:
+        sbm_case("sbm_n37_mapgrad", B=2, H=2, N=37, d=64, k=10, pad_counts=[0, 7], seed=17, map_grads=True)
+        sbm_case("sbm_n33_d96_mapgrad", B=1, H=2, N=33, d=96, k=10, pad_counts=[1], seed=18, map_grads=True)
+        full_case("full_n37_mapgrad", B=2, H=2, N=37, d=64, pad_counts=[0, 5], seed=23, map_grads=True)
         ast_relations_case("ast_relations", seed=91)
         rel_attn_large_case("rel_attn_n150_dk64", B=1, N=150, dk=64, L=150, seed=44)
         greedy_tiny_case("greedy_tiny", seed=72)
