@@ -3,16 +3,21 @@
 //   s[x,y] = (q_x.k_y + lq[rel[y,x]].k_y + q_x.lk[rel[x,y]]) / sqrt(3 d);  s[mask] = -1e9;
 //   out = softmax(s) v
 //
-// Forward:  k_bgemm   C2P  = Q LK^T   (B,H,N,Lp)   p2c/c2p relation logits, as the reference's
-//           k_bgemm   P2CT = K LQ^T   (B,H,M,Lp)   lq @ k^T / q @ lk^T (disentangled_attn.py:53-58)
-//           k_rel_fwd one wave per (b,h,32 queries): c2c by MFMA + per-element gathers of the two
-//                     relation logits, -1e9 masking, online softmax, PV; saves (row max, 1/row sum).
-// Backward: k_rel_bwd_q    recompute P, dP = dO V^T (MFMA), g = P (dP - dO.O)/sqrt(3d) (0 where masked);
-//                          dq += g K (MFMA); materialises g and P (B,H,N,N) once.
-//           k_bgemm        dv = P^T dO, dk = g^T Q
-//           k_rel_scatter  G_c2p[x][r] = sum_{y: rel[x,y]=r} g[x,y];  G_p2cT[y][r] = sum_{x: rel[y,x]=r} g[x,y]
-//                          (the gather backward; one thread per row/column, fixed order => deterministic)
-//           k_bgemm        dq += G_c2p LK ; dk += G_p2cT LQ ; dlk = sum_b G_c2p^T Q ; dlq = sum_b G_p2cT^T K
+// Fused path (d_k = 64, every config; below): k_rel_logits (C2P = Q LK^T, P2CT = K LQ^T), k_rel_prep
+// (permuted uint16 relation/mask code planes), k_rel_fwd_f (c2c MFMA + the two logit gathers, online
+// softmax, PV; saves the gathered bias tile-major), k_rel_bwd_qf / k_rel_bwd_kf (query / key side
+// backward, the gather backward as LDS bin histograms, no g/P materialised), k_rel_lgrad (dlk, dlq).
+// Generic path (d_k = 16 / 32 / 96, tests only):
+//   Forward:  k_bgemm   C2P  = Q LK^T   (B,H,N,Lp)   p2c/c2p relation logits, as the reference's
+//             k_bgemm   P2CT = K LQ^T   (B,H,M,Lp)   lq @ k^T / q @ lk^T (disentangled_attn.py:53-58)
+//             k_rel_fwd one wave per (b,h,32 queries): c2c by MFMA + per-element gathers of the two
+//                       relation logits, -1e9 masking, online softmax, PV; saves (row max, 1/row sum).
+//   Backward: k_rel_bwd_q    recompute P, dP = dO V^T (MFMA), g = P (dP - dO.O)/sqrt(3d) (0 where masked);
+//                            dq += g K (MFMA); materialises g and P (B,H,N,N) once.
+//             k_bgemm        dv = P^T dO, dk = g^T Q
+//             k_rel_scatter  G_c2p[x][r] = sum_{y: rel[x,y]=r} g[x,y];  G_p2cT[y][r] = sum_{x: rel[y,x]=r} g[x,y]
+//                            (the gather backward; one thread per row/column, fixed order => deterministic)
+//             k_bgemm        dq += G_c2p LK ; dk += G_p2cT LQ ; dlk = sum_b G_c2p^T Q ; dlq = sum_b G_p2cT^T K
 // Relation planes are uint8 (B,P,N,N) with a head->plane map (heads 0-3 parent plane L, 4-7 sibling
 // plane T; module/csa_trans.py:206-211), replacing the reference's repeated int64 (B,8,N,N) copies.
 #include "csa_common.hpp"

@@ -1,5 +1,7 @@
 // SBM attention (module/sbm_attn.py:11-87 + module/STE.py) as gfx950 HIP kernels.
 //
+// CSA_EXP_* macros select throw-away experiment builds (tools/build_variant.py);
+// the shipped library is built without them.
 // Pipeline (one forward + one backward = 9 launches, all stream-ordered, no host sync):
 //   fwd: k_cluster_softmax   S_h = softmax_{k^2}(C_h C_h^T)                      sbm_attn.py:37-39
 //        k_frag_prep         weights -> MFMA-operand-major fragments (L2-resident)
@@ -460,17 +462,9 @@ __device__ __forceinline__ void load_rows(f32x16 (&a)[NT], const float* __restri
 // ------------------------------------------------------------------------------------
 __device__ __forceinline__ int act_off(int f, int row) { return f * 32 + 4 * ((row >> 2) ^ ((f >> 1) & 7)) + (row & 3); }
 
-// accumulator tiles (feature rows 32t + crow(r,h), data row = lane c) -> block slice (features from 0)
-template <int NT>
-__device__ __forceinline__ void store_act(float* __restrict__ blk, const f32x16 (&a)[NT]) {
-  const int lane = lane_id(), c = lane & 31, h = lane >> 5;
-#pragma unroll
-  for (int t = 0; t < NT; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) __builtin_nontemporal_store(a[t][r], blk + act_off(32 * t + crow(r, h), c));
-}
 
-// The same through a wave-private 4 KiB LDS scratch: each 32-feature tile is written to the scratch in the
+// Accumulator tiles (feature rows 32t + crow(r,h), data row = lane c) -> block slice (features from 0),
+// through a wave-private 4 KiB LDS scratch: each 32-feature tile is written to the scratch in the
 // block layout (16 ds_write_b32 per lane, conflict-free: a lane half writes one feature row) and leaves
 // as 4 x 1 KiB contiguous dwordx4 stores (4x fewer store instructions, half the VGPR traffic per byte).
 // NF = features of the tile set (<= 32 NT; a partial last tile stores only its first NF - 32 (NT - 1)).
