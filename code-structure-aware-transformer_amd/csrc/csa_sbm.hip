@@ -337,6 +337,11 @@ __device__ __forceinline__ void mlp_act(const KArgs& p, f32x16 (&a)[D / 32], int
 }
 
 constexpr int MLP_LA = 2;  // forward MLP chains: fragments two K-groups ahead
+#ifdef CSA_EXP_FL2
+constexpr int FL_LA = 2;   // LDS fragment chains: lookahead (experiment)
+#else
+constexpr int FL_LA = 1;   // LDS fragment chains: one K-group ahead covers the LDS latency
+#endif
 
 // Linear bias as one more MFMA K-step after the weight chain (x W^T + b, summed last like addmm):
 // A = b[32 ot + c] on every lane (raw load issued before the chain, no select on it), B = 1 on the
@@ -366,7 +371,7 @@ __device__ __forceinline__ void mlp_layer0(const KArgs& p, const float* W0, cons
   bias_operand<D>(b0, ba);
 #pragma unroll
   for (int ot = 0; ot < DT; ++ot) h1[ot] = zero16();
-  frag_chain<DT, NS / 4, FL ? 1 : MLP_LA, FL>(W0, NS, h1, [&](int s) { return x[s]; });
+  frag_chain<DT, NS / 4, FL ? FL_LA : MLP_LA, FL>(W0, NS, h1, [&](int s) { return x[s]; });
   add_bias<D>(ba, h1);
   mlp_act<D>(p, h1, 0, row, bh, isK);
 }
@@ -380,7 +385,7 @@ __device__ __forceinline__ void mlp_layer(const float* Wl, const float* bl, cons
   bias_operand<D>(bl, ba);
 #pragma unroll
   for (int ot = 0; ot < DT; ++ot) out[ot] = zero16();
-  frag_chain<DT, NS / 4, FL ? 1 : MLP_LA, FL>(Wl, NS, out, [&](int s) { return in[s / 16][s % 16]; });
+  frag_chain<DT, NS / 4, FL ? FL_LA : MLP_LA, FL>(Wl, NS, out, [&](int s) { return in[s / 16][s % 16]; });
   add_bias<D>(ba, out);
 }
 
@@ -1658,7 +1663,7 @@ __device__ __forceinline__ void mm_acc_f(const float* __restrict__ frag, const f
 #pragma unroll
   for (int t = 0; t < NTO; ++t) out[t] = zero16();
   // L2 fragments two K-groups ahead (measured 2% faster k_proj_bwd_s<64> than one), LDS fragments one
-  frag_chain<NTO, S4MAX, (FL || S4MAX < 4) ? 1 : 2, FL>(frag, NSTEP, out, [&](int s) { return in[s / 16][s % 16]; });
+  frag_chain<NTO, S4MAX, S4MAX < 4 ? 1 : (FL ? FL_LA : 2), FL>(frag, NSTEP, out, [&](int s) { return in[s / 16][s % 16]; });
 }
 
 template <int D, int KT>
