@@ -46,6 +46,8 @@ namespace {
 
 constexpr float NEG_INF = -__builtin_inff();
 constexpr float NORM_EPS = 1e-12f;  // F.normalize default eps (sbm_attn.py:62)
+constexpr float LOG2E = 1.4426950408889634f;
+typedef float f2 __attribute__((ext_vector_type(2)));  // register pairs for packed fp32 (v_pk_*)
 
 // ------------------------------------------------------------------------------------
 // Layout of the saved forward state (caller-allocated, csa_sbm_state_bytes)
@@ -1356,6 +1358,7 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
   load_run<NS>(vr, p.V + b * p.v_sb + hd * p.v_sh + (int64_t)jc * p.v_sn + h * NS, jv);
   const float dscale = DROP ? 1.f / (1.f - p.attn_p) : 1.f;
   const float csp = (!DENSE && p.dsp) ? p.dsp[hd] / ((float)p.B * (float)p.N * (float)p.M) : 0.f;
+  const float c1 = p.scale * LOG2E;
   f32x16 dv[DT], dk[DT], dtt[KTA];
 #pragma unroll
   for (int t = 0; t < DT; ++t) { dv[t] = zero16(); dk[t] = zero16(); }
@@ -1411,23 +1414,52 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
     // qb+1 are DMA'd in while the second half runs.
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
+      // Elementwise backward (bwd_elem's algebra) on register pairs: flags as float factors, so all but
+      // exp2, the P > 0 test, the clamp and the flag selects runs as packed fp32 (v_pk_*). A key past M
+      // computes lane-local garbage (its dK / dV / dT row is never stored); a query past N must add 0.
       float dsv[8], gv[8], awv[8];
 #pragma unroll
-      for (int rr = 0; rr < 8; ++rr) {
-        const int r = 8 * half + rr;
-        const int ii = i0 + crow(r, h);
-        const bool inside = (ii < p.N) && jv;
-        const f32x4 st = lds_f4(lds, SH::KS + 16 * crow(r, h));
-        const bool a = DENSE ? inside : ((wA >> crow(r, h)) & 1u);
-        const bool keep = (wR >> crow(r, h)) & 1u;
-        const int64_t me = ((int64_t)bh * p.N + imin(ii, p.N - 1)) * p.M + jc;
-        const float dgr = (DG && p.dgraph) ? ldz(p.dgraph, me, INT64_MAX, inside) : 0.f;
-        const float dam = (DG && p.dattn) ? ldz(p.dattn, me, INT64_MAX, inside) : 0.f;
-        const Elem e = bwd_elem(sacc[r], kbias, dpacc[r], a, keep, inside, st[0], st[1], st[2], st[3], p.scale, dscale,
-                                csp, dgr, dam);
-        dsv[rr] = e.ds;
-        gv[rr] = e.g;
-        awv[rr] = e.attw;
+      for (int rr = 0; rr < 8; rr += 2) {
+        f2 af, rmf, inf, lse2, invD2, big2, gam2;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int r = 8 * half + rr + u;
+          const bool in = i0 + crow(r, h) < p.N;
+          const f32x4 st = lds_f4(lds, SH::KS + 16 * crow(r, h));
+          af[u] = (DENSE ? in : ((wA >> crow(r, h)) & 1u)) ? 1.f : 0.f;
+          rmf[u] = ((wR >> crow(r, h)) & 1u) ? dscale : 0.f;
+          inf[u] = in ? 1.f : 0.f;
+          lse2[u] = st[0]; invD2[u] = st[1]; big2[u] = st[2]; gam2[u] = st[3];
+        }
+        const int r0 = 8 * half + rr;
+        const f2 s2 = {sacc[r0], sacc[r0 + 1]}, dpp2 = {dpacc[r0], dpacc[r0 + 1]};
+        const f2 x2 = __builtin_elementwise_fma(s2, (f2)c1, __builtin_elementwise_fma(lse2, (f2)(-LOG2E), (f2)kbias));
+        const f2 P2 = {__builtin_amdgcn_exp2f(x2[0]), __builtin_amdgcn_exp2f(x2[1])};
+        f2 dattn2 = dpp2 * rmf;
+        f2 dgr2 = {0.f, 0.f};
+        if constexpr (DG) {
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const int ii = i0 + crow(r0 + u, h);
+            const bool inside = (ii < p.N) && jv;
+            const int64_t me = ((int64_t)bh * p.N + imin(ii, p.N - 1)) * p.M + jc;
+            dgr2[u] = p.dgraph ? ldz(p.dgraph, me, INT64_MAX, inside) : 0.f;
+            dattn2[u] += p.dattn ? ldz(p.dattn, me, INT64_MAX, inside) : 0.f;
+          }
+        }
+        const f2 gsel = gam2 * big2, rho = gam2 - gsel;  // big in {0, 1}: gamma goes to dM or to rho
+        const f2 mpos = {P2[0] > 0.f ? af[0] : 0.f, P2[1] > 0.f ? af[1] : 0.f};  // sign(M) of F.normalize
+        const f2 dM2 = __builtin_elementwise_fma(mpos, -gsel, dattn2) * invD2;
+        const f2 ds2 = P2 * (dM2 * af - rho) * (p.scale * inf);
+        const f2 dA2 = __builtin_elementwise_fma(dM2, P2, dgr2 + csp);
+        const f2 ain = af * inf;
+        const f2 aw2 = P2 * invD2 * rmf * ain;  // dropout(attn) weight for dV
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          dsv[rr + u] = ds2[u];
+          gv[rr + u] = __builtin_amdgcn_fmed3f(dA2[u], -1.f, 1.f) * ain[u];  // STE.py:19 hardtanh(A * grad)
+          awv[rr + u] = aw2[u];
+        }
       }
       // dV^T += dX^T attw ; dK^T += Q^T ds ; dT^T += Qh^T G  (queries beyond N carry zeros)
       if constexpr (BF) {
