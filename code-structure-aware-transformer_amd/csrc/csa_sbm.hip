@@ -1198,6 +1198,8 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
   const float lse = st[0], invD = st[1], big = st[2];
   const float dscale = DROP ? 1.f / (1.f - p.attn_p) : 1.f;
   const float csp = (!DENSE && p.dsp) ? p.dsp[hd] / ((float)p.B * (float)p.N * (float)p.M) : 0.f;
+  const float c1 = p.scale * LOG2E, c0 = -lse * LOG2E;  // per-row constants of the elementwise below
+  const float rho = (big != 0.f) ? 0.f : gamma, gsel = (big != 0.f) ? gamma : 0.f;
   f32x16 dq[DT], dqh[KTA];
 #pragma unroll
   for (int t = 0; t < DT; ++t) dq[t] = zero16();
@@ -1264,7 +1266,11 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
       if constexpr (!DENSE) wAn = p.Abits[wrow + j0 + 32];
       if constexpr (DROP) wRn = p.Rbits[wrow + j0 + 32];
     }
+    // Elementwise backward (bwd_elem's algebra, oracle/closed_form.py) with the row's constants folded:
+    // P = exp2(s c1 + kb + c0), kb = 0 / -inf (P = 0 on masked and padded keys, so ds vanishes there without
+    // a test). A query row past N computes lane-local garbage: its dQ / dQh rows are never stored.
     float dsv[16], gv[16];
+    const int nvk = p.M - j0 - 4 * h;  // key crow(r,h) = j0 + crow(r,0) + 4h is < M iff crow(r,0) < nvk
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int jj = crow(r, h), j = j0 + jj;
@@ -1275,16 +1281,21 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
       const uint32_t a_w = DENSE ? 0xffffffffu : (uint32_t)__shfl((int)wA, jj, 64);
       const uint32_t r_w = DROP ? (uint32_t)__shfl((int)wR, jj, 64) : 0xffffffffu;
 #endif
-      const bool a = (a_w >> c) & 1u;
-      const bool keep = (r_w >> c) & 1u;
-      const bool inside = iv && (j < p.M);
-      const int64_t me = ((int64_t)bh * p.N + ic) * p.M + imin(j, p.M - 1);
-      const float dgr = (DG && p.dgraph) ? ldz(p.dgraph, me, INT64_MAX, inside) : 0.f;
-      const float dam = (DG && p.dattn) ? ldz(p.dattn, me, INT64_MAX, inside) : 0.f;
-      const Elem e = bwd_elem(sacc[r], bz[r >> 2][r & 3], dpacc[r], DENSE ? inside : a, keep, inside, lse, invD, big,
-                              gamma, p.scale, dscale, csp, dgr, dam);
-      dsv[r] = e.ds;
-      gv[r] = e.g;
+      const bool in = crow(r, 0) < nvk;
+      const bool a = DENSE ? in : ((a_w >> c) & 1u);
+      float dattn = ((r_w >> c) & 1u) ? dpacc[r] * dscale : 0.f;
+      float dgr = 0.f;
+      if constexpr (DG) {
+        const bool inside = iv && (j < p.M);
+        const int64_t me = ((int64_t)bh * p.N + ic) * p.M + imin(j, p.M - 1);
+        dgr = p.dgraph ? ldz(p.dgraph, me, INT64_MAX, inside) : 0.f;
+        dattn += p.dattn ? ldz(p.dattn, me, INT64_MAX, inside) : 0.f;
+      }
+      const float P = __builtin_amdgcn_exp2f(fmaf(sacc[r], c1, bz[r >> 2][r & 3] + c0));
+      const float dM = (dattn - ((a && P > 0.f) ? gsel : 0.f)) * invD;  // sign(M) of F.normalize
+      dsv[r] = P * ((a ? dM : 0.f) - rho) * p.scale;
+      const float dA = fmaf(dM, P, csp + dgr);
+      gv[r] = (a && in) ? __builtin_amdgcn_fmed3f(dA, -1.f, 1.f) : 0.f;  // STE.py:19 hardtanh(A * grad)
     }
     // dQ^T += K^T ds^T ; dQh^T += T^T G^T  (keys beyond M carry ds = G = 0)
     if constexpr (BF) {
