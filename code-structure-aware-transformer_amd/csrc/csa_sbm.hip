@@ -22,6 +22,7 @@
 #include "../../include/csa_hip.h"
 
 #include <algorithm>
+#include <mutex>
 #include <stdint.h>
 #include <math.h>
 #include <stdarg.h>
@@ -302,6 +303,7 @@ struct KArgs {
   float *dQ, *dK, *dV, *dQh, *dT, *slab;
   int64_t dx_sb, dx_sh, dx_sn, dq_sb, dq_sh, dq_sn, dk_sb, dk_sh, dk_sn, dv_sb, dv_sh, dv_sn;
   int G; int64_t slab_floats;
+  int gamma_pre;  // stats[.][3] (gamma) written by k_attn_gamma: k_attn_bwd_q leaves it alone
 };
 
 // One 16-bit uniform per element: Philox word e/2, low half for even e.
@@ -1091,6 +1093,29 @@ __global__ __launch_bounds__(64) void k_attn_gx(const KArgs p) {
   }
 }
 
+// gamma[b,h,i] = rowsum(dX * X) (+ gx) into stats[.][3], for k_attn_bwd_kv when it runs beside
+// k_attn_bwd_q on a second stream (launch_attn_bwd_v). Two lanes per row, each one half of the row in
+// k_attn_bwd_q's order (sequential fma over its 32 elements, then the two halves added), so both kernels
+// see the same gamma bit for bit. HBM-bound (2 x 256 B per row), it overlaps the MFMA-bound bwd_q.
+template <int D>
+__global__ __launch_bounds__(256) void k_attn_gamma(const KArgs p) {
+  constexpr int NS = D / 2;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x, row = t >> 1;
+  const int h = (int)(t & 1);
+  const bool rv = row < (int64_t)p.B * p.H * p.N;
+  const int64_t rc = rv ? row : 0;
+  const int i = (int)(rc % p.N), bh = (int)(rc / p.N), b = bh / p.H, hd = bh % p.H;
+  float dx[NS], xr[NS];
+  load_run<NS>(dx, p.dX + b * p.dx_sb + hd * p.dx_sh + (int64_t)i * p.dx_sn + h * NS, rv);
+  load_run<NS>(xr, p.X + b * p.x_sb + hd * p.x_sh + (int64_t)i * p.x_sn + h * NS, rv);
+  float gp = 0.f;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) gp = fmaf(dx[s], xr[s], gp);
+  float gamma = gp + __shfl_xor(gp, 1, 64);
+  if (p.dattn) gamma += p.gx[rc];
+  if (rv && h == 0) p.stats[rc * 4 + 3] = gamma;
+}
+
 // ------------------------------------------------------------------------------------
 // Backward elementwise core for one (query i, key j) element (see oracle/closed_form.py)
 // ------------------------------------------------------------------------------------
@@ -1194,7 +1219,7 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
   // attn-map gradient, sum_j dattn_ij attn_ij (k_attn_gx)
   const float gamma = xhalf_sum(gp) + ((DG && p.dattn) ? p.gx[(int64_t)bh * p.N + ic] : 0.f);
   f32x4 st = *reinterpret_cast<const f32x4*>(p.stats + ((int64_t)bh * p.N + ic) * 4);
-  if (iv && h == 0) p.stats[((int64_t)bh * p.N + i) * 4 + 3] = gamma;
+  if (iv && h == 0 && !p.gamma_pre) p.stats[((int64_t)bh * p.N + i) * 4 + 3] = gamma;
   const float lse = st[0], invD = st[1], big = st[2];
   const float dscale = DROP ? 1.f / (1.f - p.attn_p) : 1.f;
   const float csp = (!DENSE && p.dsp) ? p.dsp[hd] / ((float)p.B * (float)p.N * (float)p.M) : 0.f;
@@ -2683,9 +2708,68 @@ csa_status launch_fwd(const csa_sbm_fwd_args* a, const Layout& L, hipStream_t st
   return check_launch("csa_sbm_fwd");
 }
 
+// bwd_q and bwd_kv side by side: bwd_kv (after k_attn_gamma) on a library-owned second stream forked from
+// and joined back into the caller's stream with events (capture-safe). It pays when bwd_q's grid leaves a
+// partial last round of workgroups on the chip (java dims, B=64: 2.5 rounds, -4% per layer step), and
+// loses when the grid is whole rounds (python dims, B=256: exactly 5 rounds, +3%: the gamma pass is not
+// hidden). CSA_BWD_CONCUR=0 / 1 forces it off / on.
+bool bwd_concurrent(int64_t wgs, int waves_per_simd) {
+  const char* e = getenv("CSA_BWD_CONCUR");  // read per call: tests compare both schedules in one process
+  if (e && e[0]) return e[0] != '0';
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    return false;
+  const double r = (double)wgs / (4.0 * cus * waves_per_simd), full = ceil(r);
+  return (full - r) / full >= 0.1;
+}
+struct SideStream { hipStream_t s = nullptr; hipEvent_t fork = nullptr, join = nullptr; };
+const SideStream* side_stream() {
+  constexpr int MAXDEV = 64;
+  static SideStream ss[MAXDEV];
+  static std::once_flag once[MAXDEV];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAXDEV) return nullptr;
+  std::call_once(once[dev], [dev] {
+    SideStream t;
+    if (hipStreamCreateWithFlags(&t.s, hipStreamNonBlocking) == hipSuccess &&
+        hipEventCreateWithFlags(&t.fork, hipEventDisableTiming) == hipSuccess &&
+        hipEventCreateWithFlags(&t.join, hipEventDisableTiming) == hipSuccess)
+      ss[dev] = t;
+  });
+  return ss[dev].s ? &ss[dev] : nullptr;
+}
+
 template <int D, int KPH, bool DENSE, bool DROP, bool DG, bool BF>
-void launch_attn_bwd_v(const KArgs& p, int BH, const Layout& L, const csa_prof* pf, hipStream_t st) {
+void launch_attn_bwd_v(const KArgs& p0, int BH, const Layout& L, const csa_prof* pf, hipStream_t st) {
   using SH = AttnBwdShape<D, KPH>;
+  const SideStream* side =
+      bwd_concurrent((int64_t)L.NQB * BH, (D <= 64 && KPH <= 16) ? 2 : 1) ? side_stream() : nullptr;
+  KArgs p = p0;
+  if (side) {  // fork: gamma + bwd_kv on the side stream, bwd_q here, join before the projection backward
+    p.gamma_pre = 1;
+    (void)hipEventRecord(side->fork, st);
+    (void)hipStreamWaitEvent(side->s, side->fork, 0);
+    {
+      Stage sg(pf, CSA_STAGE_ATTN_BWD_KV, side->s);
+      const int64_t threads = 2LL * BH * p.N;
+      hipLaunchKernelGGL(k_attn_gamma<D>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, side->s, p);
+      hipLaunchKernelGGL((k_attn_bwd_kv<D, KPH, DENSE, DROP, DG, BF>), dim3(xcd_grid((int)L.NKB, BH)), dim3(64),
+                         SH::KV_BYTES, side->s, p);
+    }
+    {
+      Stage sg(pf, CSA_STAGE_ATTN_BWD_Q, st);
+      const size_t lds_bytes = SH::q_bytes((int)L.Mpad);
+      if (lds_bytes > 64 * 1024)
+        (void)hipFuncSetAttribute((const void*)k_attn_bwd_q<D, KPH, DENSE, DROP, DG, BF>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+      hipLaunchKernelGGL((k_attn_bwd_q<D, KPH, DENSE, DROP, DG, BF>), dim3(xcd_grid((int)L.NQB, BH)), dim3(64),
+                         lds_bytes, st, p);
+    }
+    (void)hipEventRecord(side->join, side->s);
+    (void)hipStreamWaitEvent(st, side->join, 0);
+    return;
+  }
   {
     Stage sg(pf, CSA_STAGE_ATTN_BWD_Q, st);
     const size_t lds_bytes = SH::q_bytes((int)L.Mpad);

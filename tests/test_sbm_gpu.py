@@ -260,6 +260,34 @@ def test_sbm_full_size_rows_match_oracle_and_deterministic():
 
 
 @pytest.mark.skipif(not has_gpu(), reason="needs GPU")
+@pytest.mark.parametrize("shape", [(64, 8, 150, 64, 10), (8, 8, 150, 96, 10)])
+def test_concurrent_backward_schedule_bit_identical(shape, monkeypatch):
+    """bwd_q beside (k_attn_gamma + bwd_kv) on the side stream vs the in-order schedule
+    (CSA_BWD_CONCUR=1 / 0): gamma is recomputed in bwd_q's summation order, so every output and
+    gradient is bitwise identical -- train mode with dropout, padded keys, and an upstream dattn."""
+    B, H, N, d, k = shape
+    Q, K, V, mask, _, dX, dsp, params = _rand_case(B, H, N, d, k, seed=41 + d)
+    cw = params["layer.weight"].cuda()
+    pw = [params[f"proj.{i}.weight"].cuda() for i in (0, 3, 6)]
+    pb = [params[f"proj.{i}.bias"].cuda() for i in (0, 3, 6)]
+    q, kk, v, mk = Q.cuda(), K.cuda(), V.cuda(), mask.cuda()
+    gen = torch.Generator().manual_seed(3)
+    dattn = torch.randn(B, H, N, N, generator=gen).cuda()
+    seed, offset = 0x5EED, 9
+    X, sp, state = torch.ops.csa.sbm_fwd(q, kk, v, mk, cw, pw, pb, None, k, seed, offset, 0.2, 0.1, False)
+    outs = []
+    for mode in ("0", "1"):
+        monkeypatch.setenv("CSA_BWD_CONCUR", mode)
+        g = torch.ops.csa.sbm_bwd(q, kk, v, mk, cw, pw, pb, k, 0.2, 0.1, seed, offset, False, state, X,
+                                  dX.cuda(), dsp.cuda(), None, dattn=dattn)
+        torch.cuda.synchronize()
+        outs.append([t.cpu() for t in g if isinstance(t, torch.Tensor)])
+    assert len(outs[0]) == len(outs[1]) > 0
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.skipif(not has_gpu(), reason="needs GPU")
 def test_train_mode_dropout_statistics_and_determinism():
     """Train mode (in-kernel Philox sampling + dropout): same seed -> identical; keep-rate ~0.8;
     sampled-edge rate matches E[clamp(expA)]."""
