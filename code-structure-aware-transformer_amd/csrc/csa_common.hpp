@@ -23,6 +23,9 @@
 #include <stdint.h>
 
 #include <utility>
+#include <math.h>
+#include <mutex>
+#include <stdlib.h>
 
 namespace csa {
 
@@ -339,6 +342,39 @@ __device__ __forceinline__ BhBlock xcd_block(int nb, int BH) {
   return r;
 }
 inline unsigned xcd_grid(int nb, int BH) { return (unsigned)(8 * ((BH + 7) / 8) * nb); }
+
+// The two halves of an attention backward side by side (SBM: bwd_q | gamma pass + bwd_kv; CSE: bwd_qf |
+// row-statistics pass + bwd_kf): the key half on a library-owned second stream, forked from and joined
+// back into the caller's stream with events (capture-safe). It pays when the query half's grid leaves a
+// partial last round of workgroups on the chip (SBM java dims, B=64: 2.5 rounds, -4% per layer step),
+// and loses when the grid is whole rounds (SBM python dims, B=256: exactly 5 rounds, +3%: the
+// statistics pass is not hidden). CSA_BWD_CONCUR=0 / 1 forces it off / on.
+inline bool bwd_concurrent(int64_t wgs, int waves_per_simd) {
+  const char* e = getenv("CSA_BWD_CONCUR");  // read per call: tests compare both schedules in one process
+  if (e && e[0]) return e[0] != '0';
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    return false;
+  const double r = (double)wgs / (4.0 * cus * waves_per_simd), full = ceil(r);
+  return (full - r) / full >= 0.1;
+}
+struct SideStream { hipStream_t s = nullptr; hipEvent_t fork = nullptr, join = nullptr; };
+inline const SideStream* side_stream() {
+  constexpr int MAXDEV = 64;
+  static SideStream ss[MAXDEV];
+  static std::once_flag once[MAXDEV];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAXDEV) return nullptr;
+  std::call_once(once[dev], [dev] {
+    SideStream t;
+    if (hipStreamCreateWithFlags(&t.s, hipStreamNonBlocking) == hipSuccess &&
+        hipEventCreateWithFlags(&t.fork, hipEventDisableTiming) == hipSuccess &&
+        hipEventCreateWithFlags(&t.join, hipEventDisableTiming) == hipSuccess)
+      ss[dev] = t;
+  });
+  return ss[dev].s ? &ss[dev] : nullptr;
+}
 
 // Per-thread last-error text shared by every translation unit (csa_last_error_str).
 void set_error(const char* fmt, ...) __attribute__((format(printf, 1, 2)));

@@ -182,6 +182,7 @@ struct RelArgs {
   int bf16;         // CSA_DTYPE_BF16: bf16 MFMA for c2c, PV and their gradients
   float *dk, *dv, *gc2p, *gp2ct, *qstat;
   const float *lq, *lk;
+  int qstat_pre;  // qstat written by k_rel_qstat (concurrent backward): k_rel_bwd_qf leaves it alone
 };
 
 __device__ __forceinline__ int64_t plane_off(const RelArgs& p, int b, int hd, int64_t sb, int64_t sh) {
@@ -907,13 +908,38 @@ __global__ __launch_bounds__(64, 1) void k_rel_bwd_qf(const RelArgs p) {
 #endif
   if (iv) {
     store_rows_f<DT>(p.dq + b * p.dq_sb + hd * p.dq_sh + (int64_t)i * p.dq_sn, dq);
-    if (h == 0) {
+    if (h == 0 && !p.qstat_pre) {
       f32x4 st;
       st[0] = rmax; st[1] = rinv; st[2] = delta; st[3] = 0.f;
       *reinterpret_cast<f32x4*>(p.qstat + ((int64_t)bh * p.N + i) * 4) = st;
     }
   }
   bins_store_t(p.gc2p + ((int64_t)hd * p.B + b) * p.Lp * p.ldx, p.ldx, i, bins, p.LB, p.KB2, p.Lp, iv);
+}
+
+// Per-query (row max, 1/row sum, delta = rowsum(dO * O), 0) into qstat for k_rel_bwd_kf when it runs
+// beside k_rel_bwd_qf on a second stream (csa_rel_attn_bwd). Two lanes per row, each one half of the
+// row in k_rel_bwd_qf's order (sequential fma over 32 elements, then the halves added): the same delta
+// bit for bit. HBM-bound (2 x 256 B per row).
+__global__ __launch_bounds__(256) void k_rel_qstat(const RelArgs p) {
+  constexpr int NS = 32;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x, row = t >> 1;
+  const int h = (int)(t & 1);
+  const bool rv = row < (int64_t)p.B * p.H * p.N;
+  const int64_t rc = rv ? row : 0;
+  const int i = (int)(rc % p.N), bh = (int)(rc / p.N), b = bh / p.H, hd = bh % p.H;
+  float dO[NS], o[NS];
+  load_run<NS>(dO, p.dout + b * p.do_sb + hd * p.do_sh + (int64_t)i * p.do_sn + h * NS, rv);
+  load_run<NS>(o, p.out + b * p.o_sb + hd * p.o_sh + (int64_t)i * p.o_sn + h * NS, rv);
+  float dp = 0.f;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) dp = fmaf(dO[s], o[s], dp);
+  const float delta = dp + __shfl_xor(dp, 1, 64);
+  if (rv && h == 0) {
+    f32x4 st;
+    st[0] = p.stats[rc * 2]; st[1] = p.stats[rc * 2 + 1]; st[2] = delta; st[3] = 0.f;
+    *reinterpret_cast<f32x4*>(p.qstat + rc * 4) = st;
+  }
 }
 
 // Backward, key side: one wave per (b,h, 32 keys), S orientation (queries = accumulator rows, keys =
@@ -1409,7 +1435,23 @@ csa_status csa_rel_attn_bwd(const csa_rel_attn_bwd_args* b, void* stream) {
     const size_t lq_bytes = 2 * 32 * 64 * 4 + 4096 + bins_lds_bytes(p);
     const size_t lk_bytes = 2 * 32 * 64 * 4 + 512 + 4096 + bins_lds_bytes(p);
     const dim3 gq(xcd_grid(p.NQB, B * H)), gk(xcd_grid(p.NKB, B * H));
-    if (p.bf16) {
+    const SideStream* side = bwd_concurrent((int64_t)p.NQB * B * H, 1) ? side_stream() : nullptr;
+    if (side) {  // fork: row statistics + bwd_kf on the side stream, bwd_qf here, join before the lgrad
+      p.qstat_pre = 1;
+      (void)hipEventRecord(side->fork, st);
+      (void)hipStreamWaitEvent(side->s, side->fork, 0);
+      const int64_t threads = 2LL * B * H * N;
+      hipLaunchKernelGGL(k_rel_qstat, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, side->s, p);
+      if (p.bf16) {
+        hipLaunchKernelGGL((k_rel_bwd_kf<64, true>), gk, dim3(64), lk_bytes, side->s, p);
+        hipLaunchKernelGGL((k_rel_bwd_qf<64, true>), gq, dim3(64), lq_bytes, st, p);
+      } else {
+        hipLaunchKernelGGL((k_rel_bwd_kf<64, false>), gk, dim3(64), lk_bytes, side->s, p);
+        hipLaunchKernelGGL((k_rel_bwd_qf<64, false>), gq, dim3(64), lq_bytes, st, p);
+      }
+      (void)hipEventRecord(side->join, side->s);
+      (void)hipStreamWaitEvent(st, side->join, 0);
+    } else if (p.bf16) {
       hipLaunchKernelGGL((k_rel_bwd_qf<64, true>), gq, dim3(64), lq_bytes, st, p);
       hipLaunchKernelGGL((k_rel_bwd_kf<64, true>), gk, dim3(64), lk_bytes, st, p);
     } else {

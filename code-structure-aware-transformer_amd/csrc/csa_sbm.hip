@@ -22,7 +22,6 @@
 #include "../../include/csa_hip.h"
 
 #include <algorithm>
-#include <mutex>
 #include <stdint.h>
 #include <math.h>
 #include <stdarg.h>
@@ -2706,38 +2705,6 @@ csa_status launch_fwd(const csa_sbm_fwd_args* a, const Layout& L, hipStream_t st
     launch_attn_fwd_any<D, 0, true>(p, BH, L, false, a->attn_dropout > 0.f, st);
   }
   return check_launch("csa_sbm_fwd");
-}
-
-// bwd_q and bwd_kv side by side: bwd_kv (after k_attn_gamma) on a library-owned second stream forked from
-// and joined back into the caller's stream with events (capture-safe). It pays when bwd_q's grid leaves a
-// partial last round of workgroups on the chip (java dims, B=64: 2.5 rounds, -4% per layer step), and
-// loses when the grid is whole rounds (python dims, B=256: exactly 5 rounds, +3%: the gamma pass is not
-// hidden). CSA_BWD_CONCUR=0 / 1 forces it off / on.
-bool bwd_concurrent(int64_t wgs, int waves_per_simd) {
-  const char* e = getenv("CSA_BWD_CONCUR");  // read per call: tests compare both schedules in one process
-  if (e && e[0]) return e[0] != '0';
-  int dev = 0, cus = 0;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-    return false;
-  const double r = (double)wgs / (4.0 * cus * waves_per_simd), full = ceil(r);
-  return (full - r) / full >= 0.1;
-}
-struct SideStream { hipStream_t s = nullptr; hipEvent_t fork = nullptr, join = nullptr; };
-const SideStream* side_stream() {
-  constexpr int MAXDEV = 64;
-  static SideStream ss[MAXDEV];
-  static std::once_flag once[MAXDEV];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAXDEV) return nullptr;
-  std::call_once(once[dev], [dev] {
-    SideStream t;
-    if (hipStreamCreateWithFlags(&t.s, hipStreamNonBlocking) == hipSuccess &&
-        hipEventCreateWithFlags(&t.fork, hipEventDisableTiming) == hipSuccess &&
-        hipEventCreateWithFlags(&t.join, hipEventDisableTiming) == hipSuccess)
-      ss[dev] = t;
-  });
-  return ss[dev].s ? &ss[dev] : nullptr;
 }
 
 template <int D, int KPH, bool DENSE, bool DROP, bool DG, bool BF>

@@ -94,9 +94,10 @@ def _run_rel(q, k, v, lq, lk, rel, mask, dO):
 
 
 @pytest.mark.skipif(not has_gpu(), reason="needs GPU")
-def test_rel_attn_full_size_rows_match_oracle_and_deterministic():
+def test_rel_attn_full_size_rows_match_oracle_and_deterministic(monkeypatch):
     """The java train step's CSE shape (B=64 per GPU, H=8, N=L=150, d_k=64) in the compact layout:
-    two runs are bitwise identical; out/dq/dk/dv of sampled batch rows match the fp64 oracle run on
+    two runs are bitwise identical (the first with the backward halves in order, the second with
+    bwd_kf beside bwd_qf on the side stream: CSA_BWD_CONCUR=0 / 1); out/dq/dk/dv of sampled batch rows match the fp64 oracle run on
     those rows alone (each row depends only on its AST); dlq/dlk (sums over the whole batch) match
     the fp64 oracle over all 64 rows."""
     from csa_amd.data import synthetic_batch
@@ -108,7 +109,9 @@ def test_rel_attn_full_size_rows_match_oracle_and_deterministic():
     lq, lk = (torch.randn(1, H, L, dk, generator=g) for _ in range(2))
     rel = torch.from_numpy(np.stack([sb["L"], sb["T"]], 1).astype(np.uint8))
     mask = torch.from_numpy(np.stack([sb["L_mask"], sb["T_mask"]], 1).astype(np.uint8))
+    monkeypatch.setenv("CSA_BWD_CONCUR", "0")
     r1 = _run_rel(q, k, v, lq, lk, rel, mask, dO)
+    monkeypatch.setenv("CSA_BWD_CONCUR", "1")
     r2 = _run_rel(q, k, v, lq, lk, rel, mask, dO)
     for a, b in zip(r1, r2):
         assert torch.equal(a, b)
