@@ -359,19 +359,23 @@ inline bool bwd_concurrent(int64_t wgs, int waves_per_simd) {
   const double r = (double)wgs / (4.0 * cus * waves_per_simd), full = ceil(r);
   return (full - r) / full >= 0.1;
 }
-struct SideStream { hipStream_t s = nullptr; hipEvent_t fork = nullptr, join = nullptr; };
-inline const SideStream* side_stream() {
+// mu: held from the fork record to the join wait, so host threads sharing the device's events
+// cannot interleave their records.
+struct SideStream { hipStream_t s = nullptr; hipEvent_t fork = nullptr, join = nullptr; std::mutex mu; };
+inline SideStream* side_stream() {
   constexpr int MAXDEV = 64;
   static SideStream ss[MAXDEV];
   static std::once_flag once[MAXDEV];
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAXDEV) return nullptr;
   std::call_once(once[dev], [dev] {
-    SideStream t;
-    if (hipStreamCreateWithFlags(&t.s, hipStreamNonBlocking) == hipSuccess &&
-        hipEventCreateWithFlags(&t.fork, hipEventDisableTiming) == hipSuccess &&
-        hipEventCreateWithFlags(&t.join, hipEventDisableTiming) == hipSuccess)
-      ss[dev] = t;
+    hipStream_t s = nullptr;
+    hipEvent_t f = nullptr, j = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess &&
+        hipEventCreateWithFlags(&f, hipEventDisableTiming) == hipSuccess &&
+        hipEventCreateWithFlags(&j, hipEventDisableTiming) == hipSuccess) {
+      ss[dev].fork = f; ss[dev].join = j; ss[dev].s = s;
+    }
   });
   return ss[dev].s ? &ss[dev] : nullptr;
 }

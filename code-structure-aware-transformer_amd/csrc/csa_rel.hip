@@ -1435,9 +1435,10 @@ csa_status csa_rel_attn_bwd(const csa_rel_attn_bwd_args* b, void* stream) {
     const size_t lq_bytes = 2 * 32 * 64 * 4 + 4096 + bins_lds_bytes(p);
     const size_t lk_bytes = 2 * 32 * 64 * 4 + 512 + 4096 + bins_lds_bytes(p);
     const dim3 gq(xcd_grid(p.NQB, B * H)), gk(xcd_grid(p.NKB, B * H));
-    const SideStream* side = bwd_concurrent((int64_t)p.NQB * B * H, 1) ? side_stream() : nullptr;
+    SideStream* side = bwd_concurrent((int64_t)p.NQB * B * H, 1) ? side_stream() : nullptr;
     if (side) {  // fork: row statistics + bwd_kf on the side stream, bwd_qf here, join before the lgrad
       p.qstat_pre = 1;
+      std::lock_guard<std::mutex> lock(side->mu);
       (void)hipEventRecord(side->fork, st);
       (void)hipStreamWaitEvent(side->s, side->fork, 0);
       const int64_t threads = 2LL * B * H * N;

@@ -2710,11 +2710,12 @@ csa_status launch_fwd(const csa_sbm_fwd_args* a, const Layout& L, hipStream_t st
 template <int D, int KPH, bool DENSE, bool DROP, bool DG, bool BF>
 void launch_attn_bwd_v(const KArgs& p0, int BH, const Layout& L, const csa_prof* pf, hipStream_t st) {
   using SH = AttnBwdShape<D, KPH>;
-  const SideStream* side =
+  SideStream* side =
       bwd_concurrent((int64_t)L.NQB * BH, (D <= 64 && KPH <= 16) ? 2 : 1) ? side_stream() : nullptr;
   KArgs p = p0;
   if (side) {  // fork: gamma + bwd_kv on the side stream, bwd_q here, join before the projection backward
     p.gamma_pre = 1;
+    std::lock_guard<std::mutex> lock(side->mu);
     (void)hipEventRecord(side->fork, st);
     (void)hipStreamWaitEvent(side->s, side->fork, 0);
     {
