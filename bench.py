@@ -367,6 +367,7 @@ def main():
     mod.train(not args.eval)
     model = mod
     if world > 1 and not args.dense:  # FullAttention has no parameters: no gradient exchange exists
+        os.environ.setdefault("CSA_BWD_CONCUR", "0")  # as csa_amd.train.wrap_ddp: no side stream beside RCCL
         model = torch.nn.parallel.DistributedDataParallel(mod, device_ids=[local])
     Q, K, V = (torch.randn(B, H, N, d, device=dev).requires_grad_(True) for _ in range(3))
     mask = torch.zeros(B, N, device=dev)

@@ -156,6 +156,12 @@ def init_distributed():
 
 def wrap_ddp(model, device):
     if dist.is_initialized() and dist.get_world_size() > 1:
+        # DDP's all-reduces overlap the backward on RCCL's stream. With 4 hardware queues per process
+        # (GPU_MAX_HW_QUEUES) the library's side stream may share a queue with it and then wait behind
+        # an in-flight all-reduce, so multi-rank training keeps each attention backward on one stream
+        # (an explicit CSA_BWD_CONCUR still wins).
+        if device.type == "cuda":
+            os.environ.setdefault("CSA_BWD_CONCUR", "0")
         return torch.nn.parallel.DistributedDataParallel(
             model, device_ids=[device.index] if device.type == "cuda" else None,
             gradient_as_bucket_view=True, bucket_cap_mb=64)
