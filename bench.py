@@ -430,12 +430,13 @@ def main():
     if args.dense:
         flops = {"attn_fwd": H * 4 * N * N * d, "attn_bwd_q": H * 4 * N * N * d, "attn_bwd_kv": H * 4 * N * N * d}
     timed = {s: v for s, v in stage_ms.items() if s in flops}
-    # side-stream backward (B=64 shapes): the bwd_kv window opens at the fork, before bwd_q starts, so
-    # neither window is one kernel's launch and neither can be the roofline kernel
-    pb0 = profs[0][1]
+    # side-stream backward (B=64 shapes): the bwd_kv window opens at the fork, before bwd_q ends (in
+    # order it opens after bwd_q's stop), so neither window is one kernel's launch and neither can be
+    # the roofline kernel
+    pb0 = profs[-1][1]
     sq, skv = STAGES["attn_bwd_q"], STAGES["attn_bwd_kv"]
-    overlapped = bool(pb0.start[sq] and pb0.start[skv]) and \
-        ev.elapsed_ms(ctypes.c_void_p(pb0.start[sq]), ctypes.c_void_p(pb0.start[skv])) < 0
+    overlapped = bool(pb0.stop[sq] and pb0.start[skv]) and \
+        ev.elapsed_ms(ctypes.c_void_p(pb0.stop[sq]), ctypes.c_void_p(pb0.start[skv])) < 0
     cand = {s: v for s, v in timed.items() if not (overlapped and s in ("attn_bwd_q", "attn_bwd_kv"))}
     dom = max(cand, key=cand.get) if cand else None
     kernel_of = dict(KERNEL_OF_STAGE)
