@@ -80,11 +80,54 @@ class HipEvents:
             self.hip.hipEventDestroy(e)
 
 
-def cpu_baseline(seconds, B=16, H=8, N=150, d=64, k=10):
-    """Oracle (torch-CPU restatement of sbm_attn.py:32-66 + STE.py) fwd+bwd, train mode, timed on host cores."""
+def host_cpu_info():
+    """What the CPU legs run on: the CPU model, the machine's logical CPUs (os.cpu_count()), the CPUs this
+    process may run on (sched_getaffinity) and the cgroup CPU quota (cpu.max), when readable."""
+    info = {"cpu": None, "machine_logical_cpus": os.cpu_count(), "affinity_cpus": None, "cgroup_cpu_quota": None}
+    try:
+        with open("/proc/cpuinfo") as fh:
+            info["cpu"] = next(ln.split(":", 1)[1].strip() for ln in fh if ln.startswith("model name"))
+    except (OSError, StopIteration):
+        pass
+    try:
+        info["affinity_cpus"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()[:2]
+            if q != "max":
+                info["cgroup_cpu_quota"] = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return info
+
+
+def pick_threads(step, info):
+    """Thread count for a CPU leg: os.cpu_count() as SURVEY 8(d) asks, unless the process is held to fewer
+    CPUs (affinity, cgroup quota, or the OMP_NUM_THREADS share the GPU box exports: 16) -- then both counts
+    are tried on one step and the faster is used (oversubscribing a share only slows the baseline down)."""
+    cands = {info["machine_logical_cpus"] or 1}
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)  # the box exports its CPU share here (16)
+    held = min(x for x in (info["affinity_cpus"], info["cgroup_cpu_quota"], omp, info["machine_logical_cpus"]) if x)
+    cands.add(max(1, int(held)))
+    if len(cands) == 1:
+        return cands.pop(), {}
+    trial = {}
+    for t in sorted(cands):
+        torch.set_num_threads(t)
+        t0 = time.perf_counter()
+        step()
+        trial[t] = round(time.perf_counter() - t0, 3)
+    best = min(trial, key=trial.get)
+    return best, {"thread_trial_s_per_step": trial}
+
+
+def cpu_baseline(seconds, B=256, H=8, N=150, d=64, k=10):
+    """Oracle (torch-CPU restatement of sbm_attn.py:32-66 + STE.py) fwd+bwd, train mode, timed on host cores,
+    at the headline batch (B=256) unless a smaller B is passed."""
     from oracle import sbm_ref
-    threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
-    torch.set_num_threads(threads)
+    info = host_cpu_info()
     g = torch.Generator().manual_seed(0)
     Q, K, V = (torch.randn(B, H, N, d, generator=g).requires_grad_(True) for _ in range(3))
     params = {"layer.weight": torch.nn.init.orthogonal_(torch.empty(H * k, d)).requires_grad_(True)}
@@ -102,7 +145,9 @@ def cpu_baseline(seconds, B=16, H=8, N=150, d=64, k=10):
         X, sp, graph, attn = sbm_ref.sbm_attention(Q, K, V, mask, params, u, k, attn_keep=keep, proj_keep=pk)
         torch.autograd.backward([X, sp], [dX, dsp])
 
-    step()
+    step()  # warm-up (allocator, thread pool)
+    threads, trial = pick_threads(step, info)
+    torch.set_num_threads(threads)
     n, t0 = 0, time.perf_counter()
     while True:
         step()
@@ -110,11 +155,12 @@ def cpu_baseline(seconds, B=16, H=8, N=150, d=64, k=10):
         el = time.perf_counter() - t0
         if el >= seconds and n >= 2:
             break
-    return {"value": round(n * B / el, 2), "unit": "ASTs/s", "cores": threads, "kind": "port",
-            "sample": f"{n} oracle fwd+bwd steps of B={B} (H={H},N={N},d={d},k={k}, train mode) in {el:.1f}s"}
+    return {"value": round(n * B / el, 2), "unit": "ASTs/s", "cores": threads, "kind": "port", **info, **trial,
+            "sample": f"{n} oracle fwd+bwd steps of B={B} (H={H},N={N},d={d},k={k}, train mode) in {el:.1f}s "
+                      f"on {threads} threads"}
 
 
-def cpu_config1(reps=2, B=32, N=150):
+def cpu_config1(reps=5, B=32, N=150):
     """BASELINE config 1: the csa_trans_time_memory.py:100-150 protocol on the host cores, restated on
     the oracle CSATrans (oracle/csatrans_ref.py, pinned to the reference's own CSATrans output):
     config/python.py dims, B synthetic 150-node ASTs, model.train() (dropouts and STE sampling from
@@ -124,9 +170,7 @@ def cpu_config1(reps=2, B=32, N=150):
     from csa_amd.data import synthetic_batch
     from csa_amd.model import CONFIGS
     from oracle import csatrans_ref
-    import platform
-    threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
-    torch.set_num_threads(threads)
+    info = host_cpu_info()
     torch.manual_seed(0)
     cfg = csatrans_ref.config(**CONFIGS["python"])
     params = {k: v.requires_grad_(True) for k, v in csatrans_ref.init_params(cfg, seed=0).items()}
@@ -155,6 +199,9 @@ def cpu_config1(reps=2, B=32, N=150):
         out, sp = model.forward(*args)
         (csatrans_ref.label_smoothing(out, tgt) + 1e-2 * sp).backward()
 
+    fwd()  # warm-up
+    threads, trial = pick_threads(fwd, info)
+    torch.set_num_threads(threads)
     res = {}
     for name, fn in (("fwd_no_grad", fwd), ("fwd_bwd_out_mean", fwd_bwd_mean), ("loss_sparsity_fwd_bwd", train_loss)):
         fn()
@@ -162,14 +209,9 @@ def cpu_config1(reps=2, B=32, N=150):
         for _ in range(reps):
             fn()
         res[name] = round(B * reps / (time.perf_counter() - t0), 2)
-    cpu = platform.processor() or platform.machine()
-    try:
-        with open("/proc/cpuinfo") as fh:
-            cpu = next(ln.split(":", 1)[1].strip() for ln in fh if ln.startswith("model name"))
-    except (OSError, StopIteration):
-        pass
-    return {"unit": "samples/s", "cores": threads, "cpu": cpu, "kind": "port", **res,
-            "sample": f"oracle CSATrans config/python.py, B={B}, N={N}, train mode, 1 warm-up + {reps} timed passes each"}
+    return {"unit": "samples/s", "cores": threads, "kind": "port", **info, **trial, **res,
+            "sample": f"oracle CSATrans config/python.py, B={B}, N={N}, train mode, 1 warm-up + {reps} timed passes "
+                      f"each (the script runs 20 test-loader sweeps per leg)"}
 
 
 def gpu_config1(dev, reps=10, B=32, N=150):
@@ -195,27 +237,33 @@ def gpu_config1(dev, reps=10, B=32, N=150):
         out, sp = model(x)[:2]
         (label_smoothing_loss(out, y) + 1e-2 * sp).backward()
 
-    res = {}
+    res, mem = {}, {}
     for name, fn in (("fwd_no_grad", fwd), ("fwd_bwd_out_mean", fwd_bwd_mean), ("loss_sparsity_fwd_bwd", train_loss)):
         for _ in range(3):
             fn()
         torch.cuda.synchronize()
+        # csa_trans_time_memory.py:88-93,117,141-146: allocated_bytes.all.peak per timing pass
+        torch.cuda.reset_peak_memory_stats(dev)
         t0 = time.perf_counter()
         for _ in range(reps):
             fn()
         torch.cuda.synchronize()
         res[name] = round(B * reps / (time.perf_counter() - t0), 1)
-    return {"unit": "samples/s", "config": f"config/python.py CSATrans, B={B}, N={N}, train mode", **res}
+        mem[name] = round(torch.cuda.max_memory_allocated(dev) / 2 ** 20, 1)
+    return {"unit": "samples/s", "config": f"config/python.py CSATrans, B={B}, N={N}, train mode", **res,
+            "peak_allocated_MiB": mem,
+            "peak_note": "torch.cuda.max_memory_allocated over each leg's timed passes (parameters and grads included)"}
 
 
-def train_step_bench(world, rank, dev, steps, warmup, config="java", per_gpu_batch=64, nbatches=3):
-    """script/train.py:_update (config/java.py dims) under DDP/RCCL; returns samples/s over all ranks."""
+def train_step_bench(world, rank, dev, steps, warmup, config="java", per_gpu_batch=64, nbatches=3, force_ddp=False):
+    """script/train.py:_update (config/java.py dims) under DDP/RCCL; returns samples/s over all ranks.
+    force_ddp: wrap in DDP even at world size 1 (needs an initialised process group)."""
     from csa_amd.data import synthetic_batch
     from csa_amd.model import CONFIGS, CSATrans, batch_to_device, label_smoothing_loss
     from csa_amd.train import AdamW, make_train_step, wrap_ddp
     torch.manual_seed(2021 + rank)  # set_seed(seed + rank), script/train.py:158
     model = CSATrans(**CONFIGS[config]).to(dev)
-    ddp = wrap_ddp(model, dev)
+    ddp = wrap_ddp(model, dev, force=force_ddp)
     opt = AdamW(model.parameters(), lr=1e-4, correct_bias=False)
     scaler = torch.amp.GradScaler("cuda")
     step = make_train_step(ddp, opt, label_smoothing_loss, sw=1e-2, scaler=scaler)
@@ -231,7 +279,9 @@ def train_step_bench(world, rank, dev, steps, warmup, config="java", per_gpu_bat
             "global_batch": per_gpu_batch * world, "steps": steps, "warmup": warmup,
             "ms_per_step": round(el * 1000 / steps, 3), "samples_per_s": round(world * per_gpu_batch * steps / el, 1),
             "params": nparam, "mean_loss": round(mean_loss, 4), "n_ranks": world,
-            "exchange": "DDP gradient all-reduce over RCCL (64 MB buckets)" if world > 1 else "none (1 GPU)"}
+            "exchange": ("DDP gradient all-reduce over RCCL (64 MB buckets)" if world > 1 else
+                         "DDP over a world-size-1 RCCL group (reducer + bucket copies, no peer)" if force_ddp else
+                         "none (1 GPU, unwrapped)")}
 
 
 def launch_ranks(nproc):
@@ -367,7 +417,7 @@ def main():
     mod.train(not args.eval)
     model = mod
     if world > 1 and not args.dense:  # FullAttention has no parameters: no gradient exchange exists
-        os.environ.setdefault("CSA_BWD_CONCUR", "0")  # as csa_amd.train.wrap_ddp: no side stream beside RCCL
+        mod.bwd_schedule = "in_order"  # as csa_amd.train.wrap_ddp: no side stream beside RCCL
         model = torch.nn.parallel.DistributedDataParallel(mod, device_ids=[local])
     Q, K, V = (torch.randn(B, H, N, d, device=dev).requires_grad_(True) for _ in range(3))
     mask = torch.zeros(B, N, device=dev)
@@ -505,9 +555,20 @@ def main():
     if not args.no_train:
         out["train"] = train_step_bench(world, rank, dev, args.train_steps, args.train_warmup)
         if world == 1:
+            # the same step wrapped in DDP over a world-size-1 RCCL group: the reducer's own cost on record
+            import socket
+            with socket.socket() as s_:
+                s_.bind(("127.0.0.1", 0))
+                port = s_.getsockname()[1]
+            dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=dev)
+            try:
+                out["train_ddp_world1"] = train_step_bench(1, rank, dev, args.train_steps, args.train_warmup,
+                                                           force_ddp=True)
+            finally:
+                dist.destroy_process_group()
             out["config1_gpu"] = gpu_config1(dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, B=16 if N <= 150 else 1, N=N, k=k)
+        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, B=B if N <= 150 else 1, N=N, k=k)
         if not args.no_cpu_config1:
             out["cpu_config1"] = cpu_config1()
     if rank == 0:

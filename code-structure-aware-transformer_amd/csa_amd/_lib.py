@@ -11,8 +11,10 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CSA_HIP_LIB", os.path.join(_HERE, "lib", "libcsa_hip.so"))
 
-CSA_ABI_VERSION = 4
+CSA_ABI_VERSION = 5
 CSA_FLAG_DENSE = 1
+CSA_SCHED_AUTO, CSA_SCHED_IN_ORDER, CSA_SCHED_CONCURRENT = 0, 1, 2
+SCHEDULES = {"auto": CSA_SCHED_AUTO, "in_order": CSA_SCHED_IN_ORDER, "concurrent": CSA_SCHED_CONCURRENT}
 CSA_DTYPE_F32, CSA_DTYPE_BF16 = 0, 1
 STATUS = {0: "CSA_OK", 1: "CSA_INVALID_ARG", 2: "CSA_UNSUPPORTED_SHAPE", 3: "CSA_LAUNCH_FAILED"}
 
@@ -59,6 +61,7 @@ class SbmBwdArgs(ctypes.Structure):
         ("dx_sb", i64), ("dx_sh", i64), ("dx_sn", i64), ("dq_sb", i64), ("dq_sh", i64), ("dq_sn", i64),
         ("dk_sb", i64), ("dk_sh", i64), ("dk_sn", i64), ("dv_sb", i64), ("dv_sh", i64), ("dv_sn", i64),
         ("dattn", vp),  # ABI v4
+        ("schedule", u32), ("side_stream", vp), ("side_fork", vp), ("side_join", vp),  # ABI v5
     ]
 
 
@@ -87,6 +90,7 @@ class RelAttnBwdArgs(ctypes.Structure):
         ("workspace", vp),
         ("do_sb", i64), ("do_sh", i64), ("do_sn", i64), ("dq_sb", i64), ("dq_sh", i64), ("dq_sn", i64),
         ("dk_sb", i64), ("dk_sh", i64), ("dk_sn", i64), ("dv_sb", i64), ("dv_sh", i64), ("dv_sn", i64),
+        ("schedule", u32), ("side_stream", vp), ("side_fork", vp), ("side_join", vp),  # ABI v5
     ]
 
 
@@ -138,6 +142,10 @@ def lib():
     L.csa_sbm_maps.argtypes = [ctypes.POINTER(SbmFwdArgs), vp, vp, vp]
     L.csa_sbm_bwd.restype = ctypes.c_int
     L.csa_sbm_bwd.argtypes = [ctypes.POINTER(SbmBwdArgs), vp]
+    L.csa_dense_attn_fwd.restype = ctypes.c_int
+    L.csa_dense_attn_fwd.argtypes = [ctypes.POINTER(SbmFwdArgs), vp]
+    L.csa_dense_attn_bwd.restype = ctypes.c_int
+    L.csa_dense_attn_bwd.argtypes = [ctypes.POINTER(SbmBwdArgs), vp]
     L.csa_ste_sample.restype = ctypes.c_int
     L.csa_ste_sample.argtypes = [vp, vp, vp, i64, f32, f32, vp]
     L.csa_ste_backward.restype = ctypes.c_int
@@ -195,7 +203,8 @@ def check(status, what):
 
 EXPORTED_SYMBOLS = (
     "csa_abi_version", "csa_source_hash", "csa_status_str", "csa_last_error_str", "csa_sbm_supported", "csa_sbm_state_bytes",
-    "csa_sbm_bwd_workspace_bytes", "csa_sbm_fwd", "csa_sbm_maps", "csa_sbm_bwd", "csa_ste_sample",
+    "csa_sbm_bwd_workspace_bytes", "csa_sbm_fwd", "csa_sbm_maps", "csa_sbm_bwd", "csa_dense_attn_fwd",
+    "csa_dense_attn_bwd", "csa_ste_sample",
     "csa_ste_backward", "csa_rel_attn_state_bytes", "csa_rel_attn_bwd_workspace_bytes", "csa_rel_attn_fwd", "csa_rel_attn_bwd",
     "csa_adamw_step", "csa_gen_logsoftmax_fwd", "csa_gen_logsoftmax_bwd",
     "csa_bias_grad_workspace_bytes", "csa_bias_grad", "csa_ast_relations",

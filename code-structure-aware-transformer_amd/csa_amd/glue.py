@@ -99,17 +99,30 @@ class _LinearPackedFn(torch.autograd.Function):
         gy2 = gy.reshape(-1, gy.shape[-1])
         dx = gy @ W if ctx.needs_input_grad[0] else None
         dw = gy2.t() @ x.reshape(-1, x.shape[-1])
-        g = gy2 if gy2.is_contiguous() and gy2.dtype == torch.float32 else gy2.float().contiguous()
-        db = bias_grad(g).to(gy.dtype)
+        if gy2.is_cuda:
+            g = gy2 if gy2.is_contiguous() and gy2.dtype == torch.float32 else gy2.float().contiguous()
+            db = bias_grad(g).to(gy.dtype)
+        else:  # host tensors (the gloo DDP tests): the same column sums on the CPU
+            db = gy2.sum(0)
         return (dx,) + tuple(dw[i * n:(i + 1) * n] for i in range(3)) + tuple(db[i * n:(i + 1) * n] for i in range(3))
+
+
+def pack_linears_(linears):
+    """Pack the weights and the biases of same-shape nn.Linear layers back to back (pack_adjacent_).
+    Modules that own such a triple call this at construction and after every device / dtype move
+    (_apply), so the packing exists before DDP builds its buckets or an optimizer sees the parameters."""
+    ws, bs = [l.weight for l in linears], [l.bias for l in linears]
+    if any(b is None for b in bs):
+        return False
+    return pack_adjacent_(ws) and pack_adjacent_(bs)
 
 
 def linear3(x, linears):
     """The three nn.Linear layers `linears` applied to the same x as one GEMM, outputs concatenated on
-    the last dim: (..., 3 out). Their parameters are packed back to back on first use (and again after
-    a device move), so no per-forward weight concatenation happens."""
+    the last dim: (..., 3 out). Their parameters are packed back to back (pack_linears_: eagerly by the
+    owning module, or here on first use), so no per-forward weight concatenation happens."""
     ws, bs = [l.weight for l in linears], [l.bias for l in linears]
-    if (x.is_cuda and x.dtype == torch.float32 and all(b is not None for b in bs)
+    if (x.dtype == torch.float32 and x.device == ws[0].device and all(b is not None for b in bs)
             and pack_adjacent_(ws) and pack_adjacent_(bs)):
         if _batch_major(x):
             return _LinearPackedFn.apply(x.transpose(0, 1), *ws, *bs).transpose(0, 1)

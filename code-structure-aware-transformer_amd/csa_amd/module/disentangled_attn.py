@@ -1,7 +1,9 @@
 """Drop-in DisentangledAttn (module/disentangled_attn.py:11-65): same constructor, forward signature,
 return tuple and state_dict keys; the relation attention runs in torch.ops.csa.rel_attn_*.
 ``module.attn_precision = "bf16"`` runs its c2c / PV contractions and their gradients on bf16 MFMA
-(d_k = 64; default "fp32", the reference's precision)."""
+(d_k = 64; default "fp32", the reference's precision); ``module.bwd_schedule`` as in
+csa_amd.module.sbm_attn. linear_layers[0..2] (the self-attention q / k / v) stay packed back to back
+from construction on and after every device move (one QKV GEMM)."""
 import copy
 
 import torch
@@ -9,7 +11,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import rel_ops
-from ..glue import Linear, linear3, split_heads3
+from ..glue import Linear, linear3, pack_linears_, split_heads3
 
 __all__ = ["DisentangledAttn", "transpose_for_scores", "_get_clones"]
 
@@ -37,6 +39,13 @@ class DisentangledAttn(nn.Module):
         self.l_linear = _get_clones(Linear(d_model, self.d_k * 4), 2)
         self.t_linear = _get_clones(Linear(d_model, self.d_k * 4), 2)
         self.attn_precision = "fp32"
+        self.bwd_schedule = "auto"
+        pack_linears_(self.linear_layers[:3])
+
+    def _apply(self, fn, *args, **kwargs):
+        out = super()._apply(fn, *args, **kwargs)
+        pack_linears_(self.linear_layers[:3])
+        return out
 
     def forward(self, query, key, value, rel_emb, rel, mask):
         if query is key and key is value:  # self-attention (CSE_layer, csa_trans.py:231-233): one QKV GEMM
@@ -51,10 +60,8 @@ class DisentangledAttn(nn.Module):
         tq, tk = [transpose_for_scores(lin(x), 4) for lin, x in zip(self.t_linear, (t, t))]
         lq = torch.cat([lq, tq], dim=1)  # 1, 8, L, d
         lk = torch.cat([lk, tk], dim=1)
-        if self.attn_precision == "bf16":
-            output = rel_ops.rel_attn(query, key, value, lq, lk, rel, mask, bf16=True)
-        else:
-            output = self.rel_attn(query, key, value, lq, lk, rel, mask)
+        output = rel_ops.rel_attn(query, key, value, lq, lk, rel, mask, bf16=self.attn_precision == "bf16",
+                                  schedule=self.bwd_schedule)
         output = output.permute(0, 2, 1, 3).contiguous()
         output = output.view(*(output.size()[:-2] + (-1,)))
         output = self.linear_layers[-1](output)

@@ -13,13 +13,19 @@ Extensions (all default to the reference behaviour):
   * ``config["attn_precision"]`` / ``module.attn_precision`` (default "fp32", the reference's
     forced precision, sbm_attn.py:120-126): "bf16" runs QK^T, PV and their gradients on bf16 MFMA
     (fp32 accumulation; the cluster projection, expA and the sampled graph stay fp32).
+  * ``module.bwd_schedule`` (default "auto"): "in_order" keeps the attention backward's two halves on
+    the current stream, "concurrent" puts the key half on a side stream beside the query half, "auto"
+    decides from the grid shape (csa_amd.train.wrap_ddp sets "in_order" beside RCCL). Bitwise-identical
+    results either way.
+  * ``Attention`` keeps W_q / W_k / W_v packed back to back (one QKV GEMM) from construction on and after
+    every ``.to()`` / ``.cuda()``: the packing exists before DDP or an optimizer sees the parameters.
 """
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
-from ..glue import Linear, linear3, split_heads3
+from ..glue import Linear, linear3, pack_linears_, split_heads3
 
 __all__ = ["SBMAttention", "FullAttention", "Attention"]
 
@@ -45,6 +51,7 @@ class SBMAttention(nn.Module):
         )
         self.return_maps = config.get("return_maps", True)
         self.attn_precision = config.get("attn_precision", "fp32")
+        self.bwd_schedule = "auto"
         self.uniforms = None
 
     def forward(self, Q, K, V, mask):
@@ -59,7 +66,7 @@ class SBMAttention(nn.Module):
             [self.proj[0].weight, self.proj[0].bias, self.proj[3].weight, self.proj[3].bias,
              self.proj[6].weight, self.proj[6].bias],
             k, uniforms=u, attn_p=attn_p, proj_p=proj_p, want_maps=self.return_maps,
-            bf16=self.attn_precision == "bf16")
+            bf16=self.attn_precision == "bf16", schedule=self.bwd_schedule)
         return X, sparsity, graph, attn
 
 
@@ -72,11 +79,12 @@ class FullAttention(nn.Module):
         self.dropout = nn.Dropout(0.2)
         self.return_maps = config.get("return_maps", True)
         self.attn_precision = config.get("attn_precision", "fp32")
+        self.bwd_schedule = "auto"
 
     def forward(self, Q, K, V, mask):
         attn_p = self.drop_attn.p if self.training else 0.0
         X, _, _, attn = ops.dense_attention(Q, K, V, mask, attn_p=attn_p, want_maps=self.return_maps,
-                                            bf16=self.attn_precision == "bf16")
+                                            bf16=self.attn_precision == "bf16", schedule=self.bwd_schedule)
         return X, None, mask, attn  # sbm_attn.py:84-87
 
 
@@ -96,6 +104,12 @@ class Attention(nn.Module):
         else:
             self.attn = SBMAttention(config, idx)
         self.ff = Linear(self.num_head * self.head_dim, self.dim)
+        pack_linears_((self.W_q, self.W_k, self.W_v))
+
+    def _apply(self, fn, *args, **kwargs):
+        out = super()._apply(fn, *args, **kwargs)
+        pack_linears_((self.W_q, self.W_k, self.W_v))  # a device / dtype move gives each parameter its own storage
+        return out
 
     def forward(self, inputs):
         X, mask, deliver = inputs

@@ -12,12 +12,13 @@ There is no CPU path: every op raises on a non-CUDA tensor or when the library i
 """
 import ctypes
 import math
+import os
 from typing import List, Optional, Tuple
 
 import torch
 
 from . import _lib
-from ._lib import CSA_DTYPE_BF16, CSA_DTYPE_F32, CSA_FLAG_DENSE, SbmBwdArgs, SbmFwdArgs, check, lib
+from ._lib import CSA_DTYPE_BF16, CSA_DTYPE_F32, CSA_FLAG_DENSE, SCHEDULES, SbmBwdArgs, SbmFwdArgs, check, lib
 
 __all__ = ["sbm_attention", "dense_attention", "ste_sample", "ste_backward", "rel_attn", "SBMAttentionFunction"]
 
@@ -47,11 +48,58 @@ def _require_gpu(*ts):
 
 def _bhnd(t: torch.Tensor) -> torch.Tensor:
     """(B,H,N,d) fp32 view usable by the kernels: last dim contiguous, 16-B aligned, strides % 4 == 0.
-    Non-contiguous split_heads views (sbm_attn.py:137-140) pass through without a copy."""
+    Non-contiguous split_heads views (sbm_attn.py:137-140) pass through without a copy. A zero leading
+    stride (a broadcast, e.g. the gradient of X.sum((0, 1, 2))) is materialised: the ABI reads an all-zero
+    stride triple as "contiguous", and the kernels' row arithmetic assumes distinct rows."""
     if t.dtype != torch.float32:
         t = t.float()
-    ok = (t.stride(3) == 1 and t.data_ptr() % 16 == 0 and all(s % 4 == 0 for s in t.stride()[:3]))
+    ok = (t.stride(3) == 1 and t.data_ptr() % 16 == 0 and all(s % 4 == 0 and s > 0 for s in t.stride()[:3]))
     return t if ok else t.contiguous()
+
+
+# ---------------------------------------------------------------------------------------
+# Backward schedule + the caller-owned side lane (ABI v5: the library owns no streams or events)
+# ---------------------------------------------------------------------------------------
+_SIDE = {}  # device index -> (torch.cuda.Stream, fork hipEvent_t, join hipEvent_t)
+# debugging override of every module's bwd_schedule: CSA_BWD_CONCUR=0 -> in_order, 1 -> concurrent
+_SCHED_OVERRIDE = {"0": "in_order", "1": "concurrent"}.get(os.environ.get("CSA_BWD_CONCUR", ""))
+
+
+def _hip_event(device):
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    hip.hipEventCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
+    e = ctypes.c_void_p()
+    with torch.cuda.device(device):
+        if hip.hipEventCreateWithFlags(ctypes.byref(e), 0x2) != 0:  # hipEventDisableTiming
+            raise RuntimeError("hipEventCreateWithFlags failed")
+    return e.value
+
+
+def side_lane(device):
+    """(side stream, fork event, join event) raw handles of `device`, created once per device and owned
+    here (Python), handed to every backward that may run its two halves side by side."""
+    idx = torch.device(device).index
+    idx = torch.cuda.current_device() if idx is None else idx
+    ent = _SIDE.get(idx)
+    if ent is None:
+        s = torch.cuda.Stream(device=idx)
+        ent = _SIDE[idx] = (s, _hip_event(idx), _hip_event(idx))
+    return ent[0].cuda_stream, ent[1], ent[2]
+
+
+def schedule_code(schedule: str) -> int:
+    """"auto" | "in_order" | "concurrent" -> CSA_SCHED_* (the CSA_BWD_CONCUR override wins)."""
+    s = _SCHED_OVERRIDE or schedule
+    if s not in SCHEDULES:
+        raise ValueError(f"bwd schedule must be one of {sorted(SCHEDULES)}, got {schedule!r}")
+    return SCHEDULES[s]
+
+
+def set_side_lane(args, device, schedule: int):
+    """Fill the ABI v5 schedule / side-lane fields of a bwd args struct."""
+    args.schedule = schedule
+    if schedule != SCHEDULES["in_order"]:
+        args.side_stream, args.side_fork, args.side_join = side_lane(device)
 
 
 def packed_qkv(Q, K, V) -> bool:
@@ -195,7 +243,7 @@ def sbm_bwd_op(Q: torch.Tensor, K: torch.Tensor, V: torch.Tensor, mask: Optional
                k: int, attn_p: float, proj_p: float, seed: int, offset: int, dense: bool, state: torch.Tensor,
                X: torch.Tensor, dX: torch.Tensor, dsparsity: Optional[torch.Tensor],
                dgraph: Optional[torch.Tensor], bf16: bool = False, packed: bool = False,
-               dattn: Optional[torch.Tensor] = None) -> List[torch.Tensor]:
+               dattn: Optional[torch.Tensor] = None, schedule: int = 0) -> List[torch.Tensor]:
     """Backward of csa::sbm_fwd. Returns [dQ, dK, dV] (+ [dcluster_w, dW0, db0, dW1, db1, dW2, db2] if not dense).
     dgraph / dattn: upstream gradients of the returned graph / attn maps (sbm_attn.py:66), or None.
     packed: [dQ, dK, dV] is replaced by ONE packed (B, N, 3, H, d) tensor (the gradient of a fused QKV
@@ -248,13 +296,14 @@ def sbm_bwd_op(Q: torch.Tensor, K: torch.Tensor, V: torch.Tensor, mask: Optional
             outs += [dw, db]
     if _PROF["bwd"] is not None:
         b.prof = ctypes.pointer(_PROF["bwd"])
+    set_side_lane(b, Q.device, schedule)
     check(L.csa_sbm_bwd(ctypes.byref(b), _stream(Q.device)), "csa_sbm_bwd")
     return outs
 
 
 @sbm_bwd_op.register_fake
 def _(Q, K, V, mask, cluster_w, proj_w, proj_b, k, attn_p, proj_p, seed, offset, dense, state, X, dX, dsparsity,
-      dgraph, bf16=False, packed=False, dattn=None):
+      dgraph, bf16=False, packed=False, dattn=None, schedule=0):
     B, H, N, d = Q.shape
     outs = [Q.new_empty(B, N, 3, H, d)] if packed else [torch.empty_like(Q), torch.empty_like(K), torch.empty_like(V)]
     if not dense:
@@ -309,7 +358,7 @@ class SBMAttentionFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, Q, K, V, mask, cluster_w, w0, b0, w1, b1, w2, b2, uniforms, k, attn_p, proj_p, dense,
-                want_maps, bf16=False):
+                want_maps, bf16=False, schedule=0):
         seed = _draw_seed()
         pw = [] if dense else [w0, w1, w2]
         pb = [] if dense else [b0, b1, b2]
@@ -319,7 +368,7 @@ class SBMAttentionFunction(torch.autograd.Function):
         if want_maps:
             graph, attn = torch.ops.csa.sbm_maps(Q, K, V, mask, state, k, dense)
         ctx.save_for_backward(Q, K, V, mask, cluster_w, w0, b0, w1, b1, w2, b2, state, X)
-        ctx.cfg = (k, attn_p, proj_p, seed, dense, bf16)
+        ctx.cfg = (k, attn_p, proj_p, seed, dense, bf16, schedule)
         ctx.packed = packed_qkv(Q, K, V)
         ctx.set_materialize_grads(False)
         return X, (sp if not dense else None), graph, attn
@@ -327,40 +376,43 @@ class SBMAttentionFunction(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dX, dsp, dgraph, dattn):
         Q, K, V, mask, cluster_w, w0, b0, w1, b1, w2, b2, state, X = ctx.saved_tensors
-        k, attn_p, proj_p, seed, dense, bf16 = ctx.cfg
+        k, attn_p, proj_p, seed, dense, bf16, schedule = ctx.cfg
         if dX is None:
             dX = torch.zeros_like(X)
         pw = [] if dense else [w0, w1, w2]
         pb = [] if dense else [b0, b1, b2]
         g = torch.ops.csa.sbm_bwd(Q, K, V, mask, None if dense else cluster_w, pw, pb, k, attn_p, proj_p, seed, 0,
-                                  dense, state, X, dX, dsp, None if dense else dgraph, bf16, ctx.packed, dattn)
+                                  dense, state, X, dX, dsp, None if dense else dgraph, bf16, ctx.packed, dattn,
+                                  schedule)
         if ctx.packed:  # the three head-major views of the packed gradient (split_heads3's backward takes it whole)
             dQ, dK, dV = (g[0][:, :, i].transpose(1, 2) for i in range(3))
             g = [None, None] + list(g)
         else:
             dQ, dK, dV = g[:3]
         if dense:
-            return (dQ, dK, dV) + (None,) * 15
+            return (dQ, dK, dV) + (None,) * 16
         dC, dw0, db0, dw1, db1, dw2, db2 = g[3:]
-        return dQ, dK, dV, None, dC, dw0, db0, dw1, db1, dw2, db2, None, None, None, None, None, None, None
+        return dQ, dK, dV, None, dC, dw0, db0, dw1, db1, dw2, db2, None, None, None, None, None, None, None, None
 
 
 def sbm_attention(Q, K, V, mask, cluster_w, proj, k, uniforms=None, attn_p=0.0, proj_p=0.0, want_maps=True,
-                  bf16=False):
+                  bf16=False, schedule="auto"):
     """Fused SBMAttention.forward (module/sbm_attn.py:32-66) -> (X, sparsity, graph, attn).
 
     proj: [w0, b0, w1, b1, w2, b2] (proj.0/.3/.6). uniforms: optional (B,H,N,M) host-supplied draws
     (bit-exact parity mode); otherwise in-kernel Philox. graph/attn are None when want_maps=False.
-    bf16: bf16-MFMA attention contractions (the maps, if requested, are still computed in fp32)."""
+    bf16: bf16-MFMA attention contractions (the maps, if requested, are still computed in fp32).
+    schedule: the backward's "auto" | "in_order" | "concurrent" (CSA_SCHED_*; bitwise-identical results)."""
     w0, b0, w1, b1, w2, b2 = proj
     return SBMAttentionFunction.apply(Q, K, V, mask, cluster_w, w0, b0, w1, b1, w2, b2, uniforms, int(k),
-                                      float(attn_p), float(proj_p), False, bool(want_maps), bool(bf16))
+                                      float(attn_p), float(proj_p), False, bool(want_maps), bool(bf16),
+                                      schedule_code(schedule))
 
 
-def dense_attention(Q, K, V, mask, attn_p=0.0, want_maps=True, bf16=False):
+def dense_attention(Q, K, V, mask, attn_p=0.0, want_maps=True, bf16=False, schedule="auto"):
     """Fused FullAttention.forward (module/sbm_attn.py:77-87) -> (X, None, graph(unused), attn)."""
     return SBMAttentionFunction.apply(Q, K, V, mask, None, None, None, None, None, None, None, None, 0,
-                                      float(attn_p), 0.0, True, bool(want_maps), bool(bf16))
+                                      float(attn_p), 0.0, True, bool(want_maps), bool(bf16), schedule_code(schedule))
 
 
 class _STEFunction(torch.autograd.Function):

@@ -6,7 +6,7 @@ from typing import List
 import torch
 
 from ._lib import CSA_DTYPE_BF16, CSA_DTYPE_F32, RelAttnArgs, RelAttnBwdArgs, check, lib
-from .ops import _bhnd, _require_gpu, _stream, head_major_out, packed_grads, packed_qkv
+from .ops import _bhnd, _require_gpu, _stream, head_major_out, packed_grads, packed_qkv, schedule_code, set_side_lane
 
 
 def _planes(rel: torch.Tensor, mask: torch.Tensor, H: int):
@@ -74,7 +74,7 @@ def _(q, k, v, lq, lk, rel, mask, group, bf16=False):
 def rel_attn_bwd_op(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, lq: torch.Tensor, lk: torch.Tensor,
                     rel: torch.Tensor, mask: torch.Tensor, group: int, out: torch.Tensor, lse: torch.Tensor,
                     state: torch.Tensor, dout: torch.Tensor, bf16: bool = False,
-                    packed: bool = False) -> List[torch.Tensor]:
+                    packed: bool = False, schedule: int = 0) -> List[torch.Tensor]:
     """Returns [dq, dk, dv, dlq (H,L,d), dlk (H,L,d)]; packed (d_k = 64): [dq, dk, dv] is ONE packed
     (B, N, 3, H, d) tensor, the gradient of the fused QKV projection (ops.packed_qkv)."""
     q, k, v = _bhnd(q), _bhnd(k), _bhnd(v)
@@ -98,12 +98,13 @@ def rel_attn_bwd_op(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, lq: torch
         b.dk_sb, b.dk_sh, b.dk_sn = dk.stride()[:3]
         b.dv_sb, b.dv_sh, b.dv_sn = dv.stride()[:3]
     b.dlq, b.dlk, b.workspace = dlq.data_ptr(), dlk.data_ptr(), ws.data_ptr()
+    set_side_lane(b, q.device, schedule)
     check(lib().csa_rel_attn_bwd(ctypes.byref(b), _stream(q.device)), "csa_rel_attn_bwd")
     return [P, dlq, dlk] if packed else [dq, dk, dv, dlq, dlk]
 
 
 @rel_attn_bwd_op.register_fake
-def _(q, k, v, lq, lk, rel, mask, group, out, lse, state, dout, bf16=False, packed=False):
+def _(q, k, v, lq, lk, rel, mask, group, out, lse, state, dout, bf16=False, packed=False, schedule=0):
     B, H, N, d = q.shape
     if packed:
         return [q.new_empty(B, N, 3, H, d), torch.empty_like(lq), torch.empty_like(lk)]
@@ -112,10 +113,10 @@ def _(q, k, v, lq, lk, rel, mask, group, out, lse, state, dout, bf16=False, pack
 
 class RelAttnFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, q, k, v, lq, lk, rel, mask, group, bf16=False):
+    def forward(ctx, q, k, v, lq, lk, rel, mask, group, bf16=False, schedule=0):
         out, lse, state = torch.ops.csa.rel_attn_fwd(q, k, v, lq, lk, rel, mask, group, bf16)
         ctx.save_for_backward(q, k, v, lq, lk, rel, mask, out, lse, state)
-        ctx.group, ctx.bf16 = group, bf16
+        ctx.group, ctx.bf16, ctx.schedule = group, bf16, schedule
         ctx.packed = q.shape[-1] == 64 and packed_qkv(q, k, v)
         return out
 
@@ -123,22 +124,23 @@ class RelAttnFunction(torch.autograd.Function):
     def backward(ctx, dout):
         q, k, v, lq, lk, rel, mask, out, lse, state = ctx.saved_tensors
         g = torch.ops.csa.rel_attn_bwd(q, k, v, lq, lk, rel, mask, ctx.group, out, lse, state, dout, ctx.bf16,
-                                       ctx.packed)
+                                       ctx.packed, ctx.schedule)
         if ctx.packed:  # head-major views of the packed gradient (split_heads3's backward takes it whole)
             dq, dk, dv = (g[0][:, :, i].transpose(1, 2) for i in range(3))
             dlq, dlk = g[1], g[2]
         else:
             dq, dk, dv, dlq, dlk = g
-        return dq, dk, dv, dlq, dlk, None, None, None, None
+        return dq, dk, dv, dlq, dlk, None, None, None, None, None
 
 
-def rel_attn(q, k, v, lq, lk, rel, mask, bf16=False):
+def rel_attn(q, k, v, lq, lk, rel, mask, bf16=False, schedule="auto"):
     """DisentangledAttn.rel_attn (module/disentangled_attn.py:44-65) on the GPU.
 
     q,k,v (B,H,N,d) (strided views fine); lq,lk (1,H,L,d) or (H,L,d); rel/mask (B,H,N,N) (reference
-    int64/bool layout) or (B,2,N,N) uint8 planes shared by head halves (compact CSE layout)."""
+    int64/bool layout) or (B,2,N,N) uint8 planes shared by head halves (compact CSE layout).
+    schedule: the backward's "auto" | "in_order" | "concurrent" (CSA_SCHED_*; bitwise-identical results)."""
     H = q.shape[1]
     rel, mask, group = _planes(rel, mask, H)
     if lq.dim() == 4:
         lq, lk = lq[0], lk[0]
-    return RelAttnFunction.apply(q, k, v, lq, lk, rel, mask, group, bool(bf16))
+    return RelAttnFunction.apply(q, k, v, lq, lk, rel, mask, group, bool(bf16), schedule_code(schedule))

@@ -154,25 +154,44 @@ def init_distributed():
     return rank, world, local, device
 
 
-def wrap_ddp(model, device):
-    if dist.is_initialized() and dist.get_world_size() > 1:
-        # DDP's all-reduces overlap the backward on RCCL's stream. With 4 hardware queues per process
-        # (GPU_MAX_HW_QUEUES) the library's side stream may share a queue with it and then wait behind
-        # an in-flight all-reduce, so multi-rank training keeps each attention backward on one stream
-        # (an explicit CSA_BWD_CONCUR still wins).
-        if device.type == "cuda":
-            os.environ.setdefault("CSA_BWD_CONCUR", "0")
+def set_bwd_schedule(model, schedule):
+    """Set the attention backward schedule ("auto" | "in_order" | "concurrent") of every SBM / dense / CSE
+    attention module inside `model` (csa_amd.module.*: bwd_schedule)."""
+    n = 0
+    for m in model.modules():
+        if hasattr(m, "bwd_schedule"):
+            m.bwd_schedule = schedule
+            n += 1
+    return n
+
+
+def wrap_ddp(model, device, force=False, bucket_cap_mb=64):
+    """DistributedDataParallel over the initialised process group (idist.auto_model, script/train.py:83),
+    gradient_as_bucket_view, 64 MB buckets. Without a process group of more than one rank the model is
+    returned unwrapped, unless `force` (DDP over a world-size-1 group: the reducer's own cost, tests).
+
+    The modules' packed parameters (Attention W_q/W_k/W_v, the CSE q/k/v linears) are packed at
+    construction and after every device move, so DDP's buckets and hooks see the final storages.
+    DDP's all-reduces overlap the backward on RCCL's stream; with 4 hardware queues per process
+    (GPU_MAX_HW_QUEUES) an attention backward's side stream could share a queue with it and wait behind
+    an in-flight all-reduce, so multi-rank GPU training keeps each attention backward on one stream
+    (bwd_schedule "in_order", per module: no process-global switch)."""
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    if world > 1 or (force and dist.is_initialized()):
+        if device.type == "cuda" and world > 1:
+            set_bwd_schedule(model, "in_order")
         return torch.nn.parallel.DistributedDataParallel(
             model, device_ids=[device.index] if device.type == "cuda" else None,
-            gradient_as_bucket_view=True, bucket_cap_mb=64)
+            gradient_as_bucket_view=True, bucket_cap_mb=bucket_cap_mb)
     return model
 
 
-def make_train_step(model, optimizer, loss_fn, sw=1e-2, scaler=None, sync_loss=False):
-    """Returns step(x, y) implementing script/train.py:_update (lines 103-116)."""
+def make_train_step(model, optimizer, loss_fn, sw=1e-2, scaler=None, sync_loss=False, train_mode=True):
+    """Returns step(x, y) implementing script/train.py:_update (lines 103-116). train_mode=False runs the
+    same step in eval mode (dropouts off; the parity tests against the eval-mode reference fixtures)."""
 
     def step(x, y):
-        model.train()
+        model.train(train_mode)
         optimizer.zero_grad(set_to_none=True)
         y_pred, sparsity, src_pe, graphs, attns = model(x)
         loss = loss_fn(y_pred, y)

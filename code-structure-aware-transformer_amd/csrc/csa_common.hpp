@@ -24,7 +24,6 @@
 
 #include <utility>
 #include <math.h>
-#include <mutex>
 #include <stdlib.h>
 
 namespace csa {
@@ -343,42 +342,63 @@ __device__ __forceinline__ BhBlock xcd_block(int nb, int BH) {
 }
 inline unsigned xcd_grid(int nb, int BH) { return (unsigned)(8 * ((BH + 7) / 8) * nb); }
 
+// ---------------------------------------------------------------------------------------
+// Host-side launch plumbing. Every entry point runs on the device of the stream it is given, not
+// on the calling thread's current device (DeviceGuard), and keeps no library-owned streams or events.
+// ---------------------------------------------------------------------------------------
+inline int stream_device(hipStream_t st) {
+  int dev = -1;
+  if (hipStreamGetDevice(st, &dev) != hipSuccess || dev < 0) {
+    (void)hipGetLastError();
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  }
+  return dev;
+}
+// Makes the stream's device current for the scope (restores the caller's on exit).
+struct DeviceGuard {
+  int dev = 0, prev = -1;
+  explicit DeviceGuard(hipStream_t st) : dev(stream_device(st)) {
+    int cur = -1;
+    if (hipGetDevice(&cur) == hipSuccess && cur != dev && hipSetDevice(dev) == hipSuccess) prev = cur;
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel instantiation, current device): the
+// attribute is idempotent, and this table of (kernel, device bits) is the library's only cached state.
+void set_dyn_lds(const void* kernel, int bytes);
+
 // The two halves of an attention backward side by side (SBM: bwd_q | gamma pass + bwd_kv; CSE: bwd_qf |
-// row-statistics pass + bwd_kf): the key half on a library-owned second stream, forked from and joined
-// back into the caller's stream with events (capture-safe). It pays when the query half's grid leaves a
-// partial last round of workgroups on the chip (SBM java dims, B=64: 2.5 rounds, -4% per layer step),
-// and loses when the grid is whole rounds (SBM python dims, B=256: exactly 5 rounds, +3%: the
-// statistics pass is not hidden). CSA_BWD_CONCUR=0 / 1 forces it off / on.
-inline bool bwd_concurrent(int64_t wgs, int waves_per_simd) {
-  const char* e = getenv("CSA_BWD_CONCUR");  // read per call: tests compare both schedules in one process
-  if (e && e[0]) return e[0] != '0';
-  int dev = 0, cus = 0;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+// row-statistics pass + bwd_kf): the key half on the CALLER's side stream (csa_*_bwd_args.side_stream),
+// forked from and joined back into the caller's stream with the caller's two events (capture-safe).
+// CSA_SCHED_AUTO picks it when the query half's grid leaves a partial last round of workgroups on the
+// chip (SBM java dims, B=64: 2.5 rounds, -4% per layer step) and not when the grid is whole rounds (SBM
+// python dims, B=256: exactly 5 rounds, +3%: the statistics pass is not hidden).
+inline bool bwd_concurrent(uint32_t sched, const void* side, int dev, int64_t wgs, int waves_per_simd) {
+  if (!side || sched == 1u /* CSA_SCHED_IN_ORDER */) return false;
+  if (sched == 2u /* CSA_SCHED_CONCURRENT */) return true;
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) {
+    (void)hipGetLastError();
     return false;
+  }
   const double r = (double)wgs / (4.0 * cus * waves_per_simd), full = ceil(r);
   return (full - r) / full >= 0.1;
 }
-// mu: held from the fork record to the join wait, so host threads sharing the device's events
-// cannot interleave their records.
-struct SideStream { hipStream_t s = nullptr; hipEvent_t fork = nullptr, join = nullptr; std::mutex mu; };
-inline SideStream* side_stream() {
-  constexpr int MAXDEV = 64;
-  static SideStream ss[MAXDEV];
-  static std::once_flag once[MAXDEV];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAXDEV) return nullptr;
-  std::call_once(once[dev], [dev] {
-    hipStream_t s = nullptr;
-    hipEvent_t f = nullptr, j = nullptr;
-    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess &&
-        hipEventCreateWithFlags(&f, hipEventDisableTiming) == hipSuccess &&
-        hipEventCreateWithFlags(&j, hipEventDisableTiming) == hipSuccess) {
-      ss[dev].fork = f; ss[dev].join = j; ss[dev].s = s;
-    }
-  });
-  return ss[dev].s ? &ss[dev] : nullptr;
-}
+// Caller-owned fork/join lane. fork(): record on the caller's stream, make the side stream wait;
+// join(): the reverse. Each returns false on a HIP error (the caller then reports CSA_LAUNCH_FAILED;
+// a failed fork launches nothing on the side stream).
+struct SideLane {
+  hipStream_t s; hipEvent_t fork_ev, join_ev;
+  bool fork(hipStream_t st) const {
+    return hipEventRecord(fork_ev, st) == hipSuccess && hipStreamWaitEvent(s, fork_ev, 0) == hipSuccess;
+  }
+  bool join(hipStream_t st) const {
+    return hipEventRecord(join_ev, s) == hipSuccess && hipStreamWaitEvent(st, join_ev, 0) == hipSuccess;
+  }
+};
 
 // Per-thread last-error text shared by every translation unit (csa_last_error_str).
 void set_error(const char* fmt, ...) __attribute__((format(printf, 1, 2)));

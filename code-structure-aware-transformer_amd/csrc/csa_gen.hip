@@ -350,6 +350,7 @@ csa_status csa_gen_logsoftmax_fwd(const float* logits, float* logp, int64_t rows
   if (rows == 0) return CSA_OK;
   if (!logits || !logp) return gfail(CSA_INVALID_ARG, "csa_gen_logsoftmax_fwd: null pointer");
   const hipStream_t st = (hipStream_t)stream;
+  const DeviceGuard guard(st);
   const dim3 grid((unsigned)rows);
   switch (reg_groups(V)) {
     case 1: hipLaunchKernelGGL(k_gen_fwd_r<1>, grid, dim3(RT), 0, st, logits, logp, a); break;
@@ -375,6 +376,7 @@ csa_status csa_gen_logsoftmax_bwd(const float* dlogp, const float* logp, float* 
   if (rows == 0) return CSA_OK;
   if (!dlogp || !logp || !dlogits) return gfail(CSA_INVALID_ARG, "csa_gen_logsoftmax_bwd: null pointer");
   const hipStream_t st = (hipStream_t)stream;
+  const DeviceGuard guard(st);
   const dim3 grid((unsigned)rows);
   switch (reg_groups(V)) {
     case 1: hipLaunchKernelGGL(k_gen_bwd_r<1>, grid, dim3(RT), 0, st, dlogp, logp, dlogits, a); break;

@@ -248,6 +248,7 @@ csa_status csa_bias_grad(const float* dy, float* db, int64_t rows, int64_t cols,
     return CSA_INVALID_ARG;
   }
   const hipStream_t st = (hipStream_t)stream;
+  const csa::DeviceGuard guard(st);
   if (rows == 0) {
     if (!accumulate && hipMemsetAsync(db, 0, sizeof(float) * cols, st) != hipSuccess) {
       csa::set_error("csa_bias_grad: memset failed");
@@ -290,6 +291,7 @@ csa_status csa_layernorm_fwd(const float* x, const float* gamma, const float* be
     return CSA_INVALID_ARG;
   }
   const hipStream_t st = (hipStream_t)stream;
+  const csa::DeviceGuard guard(st);
   const dim3 grid((unsigned)((rows + 3) / 4));
   switch (cpl) {
     case 1: hipLaunchKernelGGL(k_ln_fwd<1>, grid, dim3(256), 0, st, x, gamma, beta, y, stats, rows, (int)cols, eps); break;
@@ -318,6 +320,7 @@ csa_status csa_layernorm_bwd(const float* dy, const float* x, const float* stats
     return CSA_INVALID_ARG;
   }
   const hipStream_t st = (hipStream_t)stream;
+  const csa::DeviceGuard guard(st);
   if (rows == 0) {
     if (hipMemsetAsync(dgamma, 0, sizeof(float) * cols, st) != hipSuccess ||
         hipMemsetAsync(dbeta, 0, sizeof(float) * cols, st) != hipSuccess) {
@@ -432,6 +435,7 @@ static csa_status res_launch(bool bwd, const float* x, const float* o, float* y,
   const int64_t groups = (n + 7) >> 3;
   const unsigned blocks = (unsigned)std::min<int64_t>((groups + 255) / 256, 256 * 16);
   const hipStream_t st = (hipStream_t)stream;
+  const csa::DeviceGuard guard(st);
   if (bwd) hipLaunchKernelGGL(k_res_drop<true>, dim3(blocks), dim3(256), 0, st, nullptr, o, y, a);
   else hipLaunchKernelGGL(k_res_drop<false>, dim3(blocks), dim3(256), 0, st, x, o, y, a);
   hipError_t e = hipGetLastError();
@@ -540,6 +544,7 @@ static csa_status ffn_launch(bool bwd, const float* h, const float* dy, float* o
   const int64_t groups = (n + 7) >> 3;
   const unsigned blocks = (unsigned)std::min<int64_t>((groups + 255) / 256, 256 * 16);
   const hipStream_t st = (hipStream_t)stream;
+  const csa::DeviceGuard guard(st);
   if (bwd) hipLaunchKernelGGL(k_gelu_drop<true>, dim3(blocks), dim3(256), 0, st, h, dy, out, a);
   else hipLaunchKernelGGL(k_gelu_drop<false>, dim3(blocks), dim3(256), 0, st, h, nullptr, out, a);
   hipError_t e = hipGetLastError();

@@ -98,6 +98,7 @@ extern "C" csa_status csa_adamw_step(const csa_adamw_args* a, void* stream) {
   AdamElem c;
   c.b1 = a->beta1; c.b2 = a->beta2; c.om_b1 = a->one_minus_beta1; c.om_b2 = a->one_minus_beta2;
   c.eps = a->eps; c.neg_step = -a->step_size; c.neg_decay = -a->decay;
+  const csa::DeviceGuard guard((hipStream_t)stream);
   hipLaunchKernelGGL(k_adamw, dim3((unsigned)a->nchunks), dim3(256), 0, (hipStream_t)stream, a->tensors,
                      a->chunk_tensor, a->chunk_start, c, a->grad_scale, a->found_inf);
   hipError_t e = hipGetLastError();

@@ -1163,6 +1163,12 @@ csa_status rfail(csa_status s, const char* m) {
   return s;
 }
 
+csa_status rfail_hip(const char* what) {
+  const hipError_t e = hipGetLastError();
+  csa::set_error("%s: %s", what, hipGetErrorString(e));
+  return CSA_LAUNCH_FAILED;
+}
+
 csa_status rcheck(const char* what) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
@@ -1371,6 +1377,7 @@ csa_status csa_rel_attn_fwd(const csa_rel_attn_args* a, void* stream) {
   if (s != CSA_OK) return s;
   const RelLayout R = rel_layout(a->B, a->H, a->N, a->L, a->d);
   hipStream_t st = (hipStream_t)stream;
+  const DeviceGuard guard(st);
   RelArgs p = make_rel(a, R);
   const dim3 grid(xcd_grid(p.NQB, (int)(a->B * a->H)));
   if (R.fused) {
@@ -1398,8 +1405,10 @@ csa_status csa_rel_attn_bwd(const csa_rel_attn_bwd_args* b, void* stream) {
   if (s != CSA_OK) return s;
   if (!b->dout || !b->dq || !b->dk || !b->dv || !b->dlq || !b->dlk || !b->workspace)
     return rfail(CSA_INVALID_ARG, "null gradient pointer / workspace");
+  if (b->schedule > CSA_SCHED_CONCURRENT) return rfail(CSA_INVALID_ARG, "schedule must be a CSA_SCHED_* value");
   const RelLayout R = rel_layout(a->B, a->H, a->N, a->L, a->d);
   hipStream_t st = (hipStream_t)stream;
+  const DeviceGuard guard(st);
   void* ws = b->workspace;
   RelArgs p = make_rel(a, R);
   p.dout = b->dout; p.dq = b->dq;
@@ -1435,12 +1444,13 @@ csa_status csa_rel_attn_bwd(const csa_rel_attn_bwd_args* b, void* stream) {
     const size_t lq_bytes = 2 * 32 * 64 * 4 + 4096 + bins_lds_bytes(p);
     const size_t lk_bytes = 2 * 32 * 64 * 4 + 512 + 4096 + bins_lds_bytes(p);
     const dim3 gq(xcd_grid(p.NQB, B * H)), gk(xcd_grid(p.NKB, B * H));
-    SideStream* side = bwd_concurrent((int64_t)p.NQB * B * H, 1) ? side_stream() : nullptr;
+    const bool concur = b->side_stream && b->side_fork && b->side_join &&
+                        bwd_concurrent(b->schedule, b->side_stream, stream_device(st), (int64_t)p.NQB * B * H, 1);
+    const SideLane lane{(hipStream_t)b->side_stream, (hipEvent_t)b->side_fork, (hipEvent_t)b->side_join};
+    const SideLane* side = concur ? &lane : nullptr;
     if (side) {  // fork: row statistics + bwd_kf on the side stream, bwd_qf here, join before the lgrad
+      if (!side->fork(st)) return rfail_hip("csa_rel_attn_bwd: side-stream fork");
       p.qstat_pre = 1;
-      std::lock_guard<std::mutex> lock(side->mu);
-      (void)hipEventRecord(side->fork, st);
-      (void)hipStreamWaitEvent(side->s, side->fork, 0);
       const int64_t threads = 2LL * B * H * N;
       hipLaunchKernelGGL(k_rel_qstat, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, side->s, p);
       if (p.bf16) {
@@ -1450,8 +1460,7 @@ csa_status csa_rel_attn_bwd(const csa_rel_attn_bwd_args* b, void* stream) {
         hipLaunchKernelGGL((k_rel_bwd_kf<64, false>), gk, dim3(64), lk_bytes, side->s, p);
         hipLaunchKernelGGL((k_rel_bwd_qf<64, false>), gq, dim3(64), lq_bytes, st, p);
       }
-      (void)hipEventRecord(side->join, side->s);
-      (void)hipStreamWaitEvent(st, side->join, 0);
+      if (!side->join(st)) return rfail_hip("csa_rel_attn_bwd: side-stream join");
     } else if (p.bf16) {
       hipLaunchKernelGGL((k_rel_bwd_qf<64, true>), gq, dim3(64), lq_bytes, st, p);
       hipLaunchKernelGGL((k_rel_bwd_kf<64, true>), gk, dim3(64), lk_bytes, st, p);
@@ -1483,7 +1492,7 @@ csa_status csa_rel_attn_bwd(const csa_rel_attn_bwd_args* b, void* stream) {
   // gather backward
   const unsigned nrow = (unsigned)(((int64_t)B * H * N + 63) / 64);
   const size_t lds = sizeof(float) * 64 * Lp;
-  (void)hipFuncSetAttribute((const void*)k_rel_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  set_dyn_lds((const void*)k_rel_scatter, (int)lds);
   hipLaunchKernelGGL(k_rel_scatter, dim3(nrow), dim3(64), lds, st, p, gc2p, 0);
   hipLaunchKernelGGL(k_rel_scatter, dim3(nrow), dim3(64), lds, st, p, gp2ct, 1);
   // dq += G_c2p LK_h ; dk += G_p2cT LQ_h    (C(m=x, n=dd) = sum_r G(x,r) LK(r,dd))

@@ -22,6 +22,7 @@
 #include "../../include/csa_hip.h"
 
 #include <algorithm>
+#include <mutex>
 #include <stdint.h>
 #include <math.h>
 #include <stdarg.h>
@@ -40,6 +41,32 @@ void set_error(const char* fmt, ...) {
   va_end(ap);
 }
 const char* get_error() { return g_err; }
+
+void set_dyn_lds(const void* kernel, int bytes) {
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+  struct Ent { const void* k; int bytes; uint64_t devs; };
+  static std::mutex mu;
+  static Ent tab[256];
+  static int n = 0;
+  const uint64_t bit = (dev >= 0 && dev < 64) ? (1ull << dev) : 0ull;
+  // held across the HIP call: concurrent first calls for one kernel must not record a smaller size
+  std::lock_guard<std::mutex> lock(mu);
+  Ent* e = nullptr;
+  for (int i = 0; i < n; ++i)
+    if (tab[i].k == kernel) e = &tab[i];
+  if (e && bit && (e->devs & bit) && e->bytes >= bytes) return;
+  const int target = e && e->bytes > bytes ? e->bytes : bytes;  // never lower an attribute already set
+  if (hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, target) != hipSuccess) {
+    (void)hipGetLastError();  // the launch reports it
+    return;
+  }
+  if (!e && n < 256) e = &(tab[n++] = Ent{kernel, target, 0});
+  if (!e) return;
+  if (target > e->bytes) e->devs = 0;  // a larger size re-arms every device
+  e->bytes = target;
+  e->devs |= bit;
+}
 }  // namespace csa
 
 namespace {
@@ -2517,6 +2544,13 @@ csa_status fail(csa_status s, const char* msg) {
   return s;
 }
 
+// a HIP runtime call (not a launch) failed: report the thread's last HIP error
+csa_status fail_hip(const char* what) {
+  const hipError_t e = hipGetLastError();
+  csa::set_error("%s: %s", what, hipGetErrorString(e));
+  return CSA_LAUNCH_FAILED;
+}
+
 csa_status check_launch(const char* what) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
@@ -2524,12 +2558,6 @@ csa_status check_launch(const char* what) {
     return CSA_LAUNCH_FAILED;
   }
   return CSA_OK;
-}
-
-// LDS-resident weight fragments for the projection forward (CSA_PROJ_FWD_L=0 selects the L2 variant: A/B)
-bool proj_fwd_lds() {
-  static const bool on = [] { const char* e = getenv("CSA_PROJ_FWD_L"); return !(e && e[0] == '0'); }();
-  return on;
 }
 
 bool supported(int64_t d, int64_t k, uint32_t flags) {
@@ -2616,14 +2644,10 @@ void launch_attn_fwd(const KArgs& p, int BH, const Layout& L, bool has_u, bool d
   const size_t lds_bytes = AttnFwdLds<D, KPH>::bytes((int)L.Mpad);
   const dim3 grid(xcd_grid((int)L.NQB, BH));
   if (lds_bytes > 64 * 1024) {
-    (void)hipFuncSetAttribute((const void*)k_attn_fwd<D, KPH, DENSE, false, false, BF>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
-    (void)hipFuncSetAttribute((const void*)k_attn_fwd<D, KPH, DENSE, false, true, BF>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
-    (void)hipFuncSetAttribute((const void*)k_attn_fwd<D, KPH, DENSE, !DENSE, false, BF>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
-    (void)hipFuncSetAttribute((const void*)k_attn_fwd<D, KPH, DENSE, !DENSE, true, BF>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+    set_dyn_lds((const void*)k_attn_fwd<D, KPH, DENSE, false, false, BF>, (int)lds_bytes);
+    set_dyn_lds((const void*)k_attn_fwd<D, KPH, DENSE, false, true, BF>, (int)lds_bytes);
+    set_dyn_lds((const void*)k_attn_fwd<D, KPH, DENSE, !DENSE, false, BF>, (int)lds_bytes);
+    set_dyn_lds((const void*)k_attn_fwd<D, KPH, DENSE, !DENSE, true, BF>, (int)lds_bytes);
   }
   if (!DENSE && has_u) {
     if (drop) hipLaunchKernelGGL((k_attn_fwd<D, KPH, DENSE, !DENSE, true, BF>), grid, dim3(64), lds_bytes, st, p);
@@ -2683,11 +2707,10 @@ csa_status launch_fwd(const csa_sbm_fwd_args* a, const Layout& L, hipStream_t st
       bool done = false;
       if constexpr (KT == 1) {  // k <= 32: weight fragments in LDS
         using PL = ProjFwdLds<D, KT>;
-        if (proj_fwd_lds()) {
+        {
           const int64_t items = a->B * (L.NQB + L.NKB), slots = (D == 64 && PL::NW == 4 ? 2 : 1) * 256LL;
           const int G = (int)std::max<int64_t>(1, std::min<int64_t>(slots / a->H, (items + PL::NW - 1) / PL::NW));
-          (void)hipFuncSetAttribute((const void*)k_proj_fwd_l<D, KT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)PL::BYTES);
+          set_dyn_lds((const void*)k_proj_fwd_l<D, KT>, (int)PL::BYTES);
           hipLaunchKernelGGL((k_proj_fwd_l<D, KT>), dim3(G, a->H), dim3(64 * PL::NW), PL::BYTES, st, p);
           done = true;
         }
@@ -2707,17 +2730,18 @@ csa_status launch_fwd(const csa_sbm_fwd_args* a, const Layout& L, hipStream_t st
   return check_launch("csa_sbm_fwd");
 }
 
+// Returns false when a fork/join event operation failed (nothing is launched on the side stream when
+// the fork fails; a failed join leaves the caller's stream unordered behind the side stream).
 template <int D, int KPH, bool DENSE, bool DROP, bool DG, bool BF>
-void launch_attn_bwd_v(const KArgs& p0, int BH, const Layout& L, const csa_prof* pf, hipStream_t st) {
+bool launch_attn_bwd_v(const KArgs& p0, int BH, const Layout& L, const csa_prof* pf, const SideLane* side,
+                       hipStream_t st) {
   using SH = AttnBwdShape<D, KPH>;
-  SideStream* side =
-      bwd_concurrent((int64_t)L.NQB * BH, (D <= 64 && KPH <= 16) ? 2 : 1) ? side_stream() : nullptr;
   KArgs p = p0;
+  const size_t q_lds = SH::q_bytes((int)L.Mpad);
+  if (q_lds > 64 * 1024) set_dyn_lds((const void*)k_attn_bwd_q<D, KPH, DENSE, DROP, DG, BF>, (int)q_lds);
   if (side) {  // fork: gamma + bwd_kv on the side stream, bwd_q here, join before the projection backward
+    if (!side->fork(st)) return false;
     p.gamma_pre = 1;
-    std::lock_guard<std::mutex> lock(side->mu);
-    (void)hipEventRecord(side->fork, st);
-    (void)hipStreamWaitEvent(side->s, side->fork, 0);
     {
       Stage sg(pf, CSA_STAGE_ATTN_BWD_KV, side->s);
       const int64_t threads = 2LL * BH * p.N;
@@ -2727,51 +2751,56 @@ void launch_attn_bwd_v(const KArgs& p0, int BH, const Layout& L, const csa_prof*
     }
     {
       Stage sg(pf, CSA_STAGE_ATTN_BWD_Q, st);
-      const size_t lds_bytes = SH::q_bytes((int)L.Mpad);
-      if (lds_bytes > 64 * 1024)
-        (void)hipFuncSetAttribute((const void*)k_attn_bwd_q<D, KPH, DENSE, DROP, DG, BF>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
       hipLaunchKernelGGL((k_attn_bwd_q<D, KPH, DENSE, DROP, DG, BF>), dim3(xcd_grid((int)L.NQB, BH)), dim3(64),
-                         lds_bytes, st, p);
+                         q_lds, st, p);
     }
-    (void)hipEventRecord(side->join, side->s);
-    (void)hipStreamWaitEvent(st, side->join, 0);
-    return;
+    return side->join(st);
   }
   {
     Stage sg(pf, CSA_STAGE_ATTN_BWD_Q, st);
-    const size_t lds_bytes = SH::q_bytes((int)L.Mpad);
-    if (lds_bytes > 64 * 1024)
-      (void)hipFuncSetAttribute((const void*)k_attn_bwd_q<D, KPH, DENSE, DROP, DG, BF>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
     hipLaunchKernelGGL((k_attn_bwd_q<D, KPH, DENSE, DROP, DG, BF>), dim3(xcd_grid((int)L.NQB, BH)), dim3(64),
-                       lds_bytes, st, p);
+                       q_lds, st, p);
   }
   Stage sg(pf, CSA_STAGE_ATTN_BWD_KV, st);
   hipLaunchKernelGGL((k_attn_bwd_kv<D, KPH, DENSE, DROP, DG, BF>), dim3(xcd_grid((int)L.NKB, BH)), dim3(64),
                      SH::KV_BYTES, st, p);
+  return true;
 }
 
 template <int D, int KPH, bool DENSE, bool BF>
-void launch_attn_bwd_b(const KArgs& p, int BH, const Layout& L, bool drop, const csa_prof* pf, hipStream_t st) {
+bool launch_attn_bwd_b(const KArgs& p, int BH, const Layout& L, bool drop, const csa_prof* pf, const SideLane* side,
+                       hipStream_t st) {
   const bool dg = p.dgraph != nullptr || p.dattn != nullptr;
   if (p.dattn)  // sum_j dattn_ij attn_ij per query row, read by k_attn_bwd_q's gamma
     hipLaunchKernelGGL((k_attn_gx<D, DENSE>), dim3(xcd_grid((int)L.NQB, BH)), dim3(64), 0, st, p);
   if (drop) {
-    if (dg) launch_attn_bwd_v<D, KPH, DENSE, true, true, BF>(p, BH, L, pf, st);
-    else launch_attn_bwd_v<D, KPH, DENSE, true, false, BF>(p, BH, L, pf, st);
-  } else {
-    if (dg) launch_attn_bwd_v<D, KPH, DENSE, false, true, BF>(p, BH, L, pf, st);
-    else launch_attn_bwd_v<D, KPH, DENSE, false, false, BF>(p, BH, L, pf, st);
+    if (dg) return launch_attn_bwd_v<D, KPH, DENSE, true, true, BF>(p, BH, L, pf, side, st);
+    return launch_attn_bwd_v<D, KPH, DENSE, true, false, BF>(p, BH, L, pf, side, st);
   }
+  if (dg) return launch_attn_bwd_v<D, KPH, DENSE, false, true, BF>(p, BH, L, pf, side, st);
+  return launch_attn_bwd_v<D, KPH, DENSE, false, false, BF>(p, BH, L, pf, side, st);
 }
 
+// side: the caller's fork/join lane when the schedule puts the key half beside the query half, else null
 template <int D, int KPH, bool DENSE>
-void launch_attn_bwd(const KArgs& p, int BH, const Layout& L, bool drop, const csa_prof* pf, hipStream_t st) {
+bool launch_attn_bwd(const KArgs& p, int BH, const Layout& L, bool drop, const csa_prof* pf, const SideLane* side,
+                     hipStream_t st) {
   if constexpr (KPH <= 8) {
-    if (p.bf16) return launch_attn_bwd_b<D, KPH, DENSE, true>(p, BH, L, drop, pf, st);
+    if (p.bf16) return launch_attn_bwd_b<D, KPH, DENSE, true>(p, BH, L, drop, pf, side, st);
   }
-  launch_attn_bwd_b<D, KPH, DENSE, false>(p, BH, L, drop, pf, st);
+  return launch_attn_bwd_b<D, KPH, DENSE, false>(p, BH, L, drop, pf, side, st);
+}
+
+// The caller's side lane if csa_sbm_bwd_args.schedule (and, for CSA_SCHED_AUTO, the grid shape) asks for
+// the concurrent backward, else null.
+template <int D, int KPH>
+const SideLane* pick_side(const csa_sbm_bwd_args* b, const Layout& L, SideLane& lane, hipStream_t st) {
+  if (!b->side_stream || !b->side_fork || !b->side_join) return nullptr;
+  const int64_t wgs = L.NQB * L.B * L.H;
+  if (!bwd_concurrent(b->schedule, b->side_stream, stream_device(st), wgs, (D <= 64 && KPH <= 16) ? 2 : 1))
+    return nullptr;
+  lane = SideLane{(hipStream_t)b->side_stream, (hipEvent_t)b->side_fork, (hipEvent_t)b->side_join};
+  return &lane;
 }
 
 template <int D, int KPH, int KT>
@@ -2799,8 +2828,11 @@ csa_status launch_bwd(const csa_sbm_bwd_args* b, const Layout& L, hipStream_t st
   const int BH = (int)(a->B * a->H);
   (void)dense;
   const csa_prof* pf = b->prof;
+  SideLane lane;
+  const SideLane* side = pick_side<D, KPH>(b, L, lane, st);
   if constexpr (KT > 0) {
-    launch_attn_bwd<D, KPH, false>(p, BH, L, a->attn_dropout > 0.f, pf, st);
+    if (!launch_attn_bwd<D, KPH, false>(p, BH, L, a->attn_dropout > 0.f, pf, side, st))
+      return fail_hip("csa_sbm_bwd: side-stream fork/join");
     using Sh = ProjBwdShape<D, KT>;
     if (!Sh::REGACC && hipMemsetAsync(p.slab, 0, sizeof(float) * a->H * L.G * L.slab_floats, st) != hipSuccess)
       return check_launch("memset slabs");
@@ -2808,12 +2840,10 @@ csa_status launch_bwd(const csa_sbm_bwd_args* b, const Layout& L, hipStream_t st
       Stage sg(pf, CSA_STAGE_PROJ_BWD, st);
       if constexpr ((D == 64 || D == 96) && KPH == 8) {  // k <= 16
         using Ss = ProjBwdSmallShape<D>;
-        (void)hipFuncSetAttribute((const void*)k_proj_bwd_s<D>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)Ss::LDS_BYTES);
+        set_dyn_lds((const void*)k_proj_bwd_s<D>, (int)Ss::LDS_BYTES);
         hipLaunchKernelGGL((k_proj_bwd_s<D>), dim3(L.G, a->H), dim3(256), Ss::LDS_BYTES, st, p);
       } else {
-        (void)hipFuncSetAttribute((const void*)k_proj_bwd<D, KT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)Sh::LDS_BYTES);
+        set_dyn_lds((const void*)k_proj_bwd<D, KT>, (int)Sh::LDS_BYTES);
         hipLaunchKernelGGL((k_proj_bwd<D, KT>), dim3(L.G, a->H), dim3(256), Sh::LDS_BYTES, st, p);
       }
     }
@@ -2828,7 +2858,8 @@ csa_status launch_bwd(const csa_sbm_bwd_args* b, const Layout& L, hipStream_t st
     hipLaunchKernelGGL(k_cluster_grad, dim3((unsigned)a->k, (unsigned)a->H), dim3(128), 0, st, p.S, (const float*)dS_ws,
                        (const float*)dC_ws, a->cluster_w, b->dcluster_w, (int)a->k, D, KP32);
   } else {
-    launch_attn_bwd<D, 0, true>(p, BH, L, a->attn_dropout > 0.f, pf, st);
+    if (!launch_attn_bwd<D, 0, true>(p, BH, L, a->attn_dropout > 0.f, pf, side, st))
+      return fail_hip("csa_sbm_bwd: side-stream fork/join");
   }
   return check_launch("csa_sbm_bwd");
 }
@@ -2866,6 +2897,7 @@ csa_status csa_sbm_fwd(const csa_sbm_fwd_args* a, void* stream) {
   if (s != CSA_OK) return s;
   const Layout L = make_layout(a->B, a->H, a->N, a->M, a->d, a->k, a->flags & CSA_FLAG_DENSE);
   hipStream_t st = (hipStream_t)stream;
+  const DeviceGuard guard(st);
   const bool dense = a->flags & CSA_FLAG_DENSE;
   if (a->d == 64) {
     if (dense) return launch_fwd<64, 0, 1>(a, L, st);
@@ -2888,6 +2920,7 @@ csa_status csa_sbm_maps(const csa_sbm_fwd_args* a, float* graph, float* attn, vo
   const Layout L = make_layout(a->B, a->H, a->N, a->M, a->d, a->k, dense);
   KArgs p = make_kargs(a, L);
   hipStream_t st = (hipStream_t)stream;
+  const DeviceGuard guard(st);
   const dim3 grid(xcd_grid((int)L.NQB, (int)(a->B * a->H)));
   if (a->d == 64) {
     if (dense) hipLaunchKernelGGL((k_maps<64, true>), grid, dim3(64), 0, st, p, graph, attn);
@@ -2918,8 +2951,10 @@ csa_status csa_sbm_bwd(const csa_sbm_bwd_args* b, void* stream) {
   if (!dense && (!b->dcluster_w || !b->dproj_w[0] || !b->dproj_w[1] || !b->dproj_w[2] || !b->dproj_b[0] ||
                  !b->dproj_b[1] || !b->dproj_b[2]))
     return fail(CSA_INVALID_ARG, "null parameter-gradient output");
+  if (b->schedule > CSA_SCHED_CONCURRENT) return fail(CSA_INVALID_ARG, "schedule must be a CSA_SCHED_* value");
   const Layout L = make_layout(a->B, a->H, a->N, a->M, a->d, a->k, dense);
   hipStream_t st = (hipStream_t)stream;
+  const DeviceGuard guard(st);
   if (a->d == 64) {
     if (dense) return launch_bwd<64, 0, 0>(b, L, st);
     switch (L.kp) {
@@ -2937,6 +2972,7 @@ csa_status csa_ste_sample(const float* pr, const float* u, float* A, int64_t n, 
   if (!pr || !u || !A || n < 0) return fail(CSA_INVALID_ARG, "null pointer or negative n");
   if (n == 0) return CSA_OK;
   const unsigned grid = (unsigned)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
+  const DeviceGuard guard((hipStream_t)stream);
   hipLaunchKernelGGL(k_ste_sample, dim3(grid), dim3(256), 0, (hipStream_t)stream, pr, u, A, n, lo, hi);
   return check_launch("csa_ste_sample");
 }
@@ -2945,8 +2981,29 @@ csa_status csa_ste_backward(const float* A, const float* g, float* out, int64_t 
   if (!A || !g || !out || n < 0) return fail(CSA_INVALID_ARG, "null pointer or negative n");
   if (n == 0) return CSA_OK;
   const unsigned grid = (unsigned)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
+  const DeviceGuard guard((hipStream_t)stream);
   hipLaunchKernelGGL(k_ste_backward, dim3(grid), dim3(256), 0, (hipStream_t)stream, A, g, out, n);
   return check_launch("csa_ste_backward");
+}
+
+// FullAttention (module/sbm_attn.py:77-87): csa_sbm_fwd / csa_sbm_bwd with CSA_FLAG_DENSE set (k, cluster_w,
+// proj_*, uniforms and sparsity are ignored)
+csa_status csa_dense_attn_fwd(const csa_sbm_fwd_args* a, void* stream) {
+  if (!a) return fail(CSA_INVALID_ARG, "null args");
+  csa_sbm_fwd_args d = *a;
+  d.flags |= CSA_FLAG_DENSE;
+  d.k = 0;
+  return csa_sbm_fwd(&d, stream);
+}
+
+csa_status csa_dense_attn_bwd(const csa_sbm_bwd_args* b, void* stream) {
+  if (!b || !b->fwd) return fail(CSA_INVALID_ARG, "null args");
+  csa_sbm_fwd_args d = *b->fwd;
+  d.flags |= CSA_FLAG_DENSE;
+  d.k = 0;
+  csa_sbm_bwd_args e = *b;
+  e.fwd = &d;
+  return csa_sbm_bwd(&e, stream);
 }
 
 }  // extern "C"

@@ -7,6 +7,7 @@
  *                      module/sbm_attn.py:77-87   FullAttention.forward   (flags & CSA_FLAG_DENSE)
  *   csa_sbm_maps       module/sbm_attn.py:62,57   the returned `attn` / `graph` maps (optional)
  *   csa_sbm_bwd        autograd of the above incl. STE.py:17-19 (hardtanh straight-through)
+ *   csa_dense_attn_fwd/_bwd  module/sbm_attn.py:69-87 FullAttention (csa_sbm_* with CSA_FLAG_DENSE)
  *   csa_ste_sample     module/STE.py:10-15        standalone sampler (bit-exact test surface)
  *   csa_rel_attn_fwd   module/disentangled_attn.py:44-65 DisentangledAttn.rel_attn
  *   csa_rel_attn_bwd   autograd of rel_attn (gather backward = deterministic scatter-add)
@@ -21,10 +22,14 @@
  *     (feature) dimension is always contiguous, so a (B,H,N,d) operand is described by its
  *     b/h/n strides (the non-contiguous split_heads view of sbm_attn.py:137-140 is accepted).
  *   - The caller allocates every output, the saved state and the workspace (sizes from the
- *     *_bytes() queries). The library never allocates, never synchronises the host, never
- *     throws, keeps no mutable globals, and enqueues everything on `stream` (stream-ordered,
- *     graph-capturable, re-entrant). Results are deterministic for fixed inputs (integer
- *     atomics only; float reductions use fixed-order partial slabs).
+ *     *_bytes() queries), and owns every stream and event: the library never allocates, never
+ *     creates a stream or event, never synchronises the host and never throws. It enqueues
+ *     everything on `stream` (stream-ordered, graph-capturable, re-entrant) on the device that
+ *     stream belongs to, whatever the calling thread's current device is. Its only state is a
+ *     per-thread last-error string and a cache of which kernels already had their (idempotent)
+ *     dynamic-LDS attribute raised on which device. Results are deterministic for fixed inputs
+ *     (integer atomics only; float reductions use fixed-order partial slabs), whatever the
+ *     backward schedule.
  *   - Errors: CSA_INVALID_ARG (null/inconsistent arguments), CSA_UNSUPPORTED_SHAPE (outside
  *     the compiled instantiations, see csa_sbm_supported), CSA_LAUNCH_FAILED (HIP error; text
  *     via csa_last_error_str on the calling thread).
@@ -38,7 +43,7 @@
 extern "C" {
 #endif
 
-#define CSA_ABI_VERSION 4
+#define CSA_ABI_VERSION 5
 
 typedef enum csa_status {
   CSA_OK = 0,
@@ -49,6 +54,15 @@ typedef enum csa_status {
 
 /* flags */
 #define CSA_FLAG_DENSE 1u /* FullAttention (graph == 1, no cluster projection, no sampling) */
+
+/* ABI v5: schedule of an attention backward's two halves (csa_sbm_bwd_args / csa_rel_attn_bwd_args
+ * .schedule). The key half may run on a caller-owned side stream beside the query half, forked from
+ * and joined back into `stream` with two caller-owned events (capture-safe); outputs are bitwise the
+ * same either way. AUTO uses the side stream when the query half's grid leaves a partial last round of
+ * workgroups on the device (side_stream must be set, else it runs in order). */
+#define CSA_SCHED_AUTO 0u
+#define CSA_SCHED_IN_ORDER 1u
+#define CSA_SCHED_CONCURRENT 2u /* needs side_stream / side_fork / side_join */
 
 /* operand precision of the N^2 attention contractions (dtype field of the args structs). Storage is
  * fp32 either way. CSA_DTYPE_F32 is the reference's precision (sbm_attn.py:120-126 forces fp32) and
@@ -116,6 +130,10 @@ typedef struct csa_sbm_bwd_args {
   /* ABI v4: (B,H,N,M) contiguous upstream gradient of the returned attn map (sbm_attn.py:62, the tensor the
    * reference returns), or NULL. Needs the workspace, also for DENSE. */
   const float* dattn;
+  /* ABI v5: CSA_SCHED_* and the caller's side lane: a hipStream_t of the same device as `stream` and two
+   * hipEvent_t (hipEventDisableTiming) used only between this call's fork and join. NULL = in order. */
+  uint32_t schedule;
+  void* side_stream; void* side_fork; void* side_join;
 } csa_sbm_bwd_args;
 
 int csa_abi_version(void);
@@ -133,6 +151,10 @@ csa_status csa_sbm_fwd(const csa_sbm_fwd_args* a, void* stream);
 /* Materialise attn (B,H,N,M) and/or graph (B,H,N,M) fp32 maps from a completed forward. */
 csa_status csa_sbm_maps(const csa_sbm_fwd_args* a, float* graph, float* attn, void* stream);
 csa_status csa_sbm_bwd(const csa_sbm_bwd_args* a, void* stream);
+/* FullAttention (module/sbm_attn.py:77-87): the two calls above with CSA_FLAG_DENSE forced (k, cluster_w,
+ * proj_*, uniforms and sparsity ignored). */
+csa_status csa_dense_attn_fwd(const csa_sbm_fwd_args* a, void* stream);
+csa_status csa_dense_attn_bwd(const csa_sbm_bwd_args* a, void* stream);
 
 /* STE.py:10-15 as A = (u < clamp(p, lo, hi)); n elements, contiguous. */
 csa_status csa_ste_sample(const float* p, const float* u, float* A, int64_t n, float lo, float hi, void* stream);
@@ -167,6 +189,9 @@ typedef struct csa_rel_attn_bwd_args {
   void* workspace;
   /* ABI v3: element strides (b, h, row); a zero triple = contiguous; non-contiguous needs d = 64 */
   int64_t do_sb, do_sh, do_sn, dq_sb, dq_sh, dq_sn, dk_sb, dk_sh, dk_sn, dv_sb, dv_sh, dv_sn;
+  /* ABI v5: schedule and side lane as in csa_sbm_bwd_args; only the d_k = 64 fused path uses them */
+  uint32_t schedule;
+  void* side_stream; void* side_fork; void* side_join;
 } csa_rel_attn_bwd_args;
 
 size_t csa_rel_attn_state_bytes(int64_t B, int64_t H, int64_t N, int64_t L, int64_t d);

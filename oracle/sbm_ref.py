@@ -131,11 +131,14 @@ def attention_layer(X, mask, params, u, num_head, head_dim, num_clusters, full_a
     Q = split_heads(F.linear(X, params["W_q.weight"], params["W_q.bias"]), num_head, head_dim)
     K = split_heads(F.linear(X, params["W_k.weight"], params["W_k.bias"]), num_head, head_dim)
     V = split_heads(F.linear(X, params["W_v.weight"], params["W_v.bias"]), num_head, head_dim)
+    # the reference forces fp32 here (sbm_attn.py:120-126); an fp64 X (the error-budget runs of
+    # tools/gen_golden.py) stays fp64
+    cd = torch.float64 if X.dtype == torch.float64 else torch.float32
     if full_att:
-        out, sparsity, graph, attn = full_attention(Q.float(), K.float(), V.float(), mask.float(), attn_p=attn_p)
+        out, sparsity, graph, attn = full_attention(Q.to(cd), K.to(cd), V.to(cd), mask.to(cd), attn_p=attn_p)
     else:
         sp = {k[len("attn."):]: v for k, v in params.items() if k.startswith("attn.")}
-        out, sparsity, graph, attn = sbm_attention(Q.float(), K.float(), V.float(), mask.float(), sp, u, num_clusters,
+        out, sparsity, graph, attn = sbm_attention(Q.to(cd), K.to(cd), V.to(cd), mask.to(cd), sp, u, num_clusters,
                                                    attn_p=attn_p, proj_p=proj_p)
     out = combine_heads(out, num_head, head_dim)
     return F.linear(out, params["ff.weight"], params["ff.bias"]), sparsity, graph, attn

@@ -11,6 +11,13 @@ for p in (ROOT, PKG):
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
+# torch.ops.csa.* are registered when csa_amd.ops / rel_ops / gen_ops are imported: import them once for
+# every test, so a test that calls torch.ops.csa.* directly passes alone as well as after the others.
+# (Importing does not load libcsa_hip.so or touch a GPU.)
+import csa_amd.ops  # noqa: E402,F401
+import csa_amd.rel_ops  # noqa: E402,F401
+import csa_amd.gen_ops  # noqa: E402,F401
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP kernels)")

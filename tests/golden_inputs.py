@@ -14,6 +14,10 @@ JAVA_OUT_COL_STRIDE = 16  # the fixture keeps out[:, :, ::16] (20000-wide log-pr
 JAVA_GRAD_KEYS = ("SBM.transformer_0.mha.attn.", "SBM.transformer_3.mha.attn.", "pegen.layers.0.self_attn.l_linear.0",
                   "pegen.layers.3.self_attn.t_linear.1", "pegen.L_q", "pegen.T_q", "SBM.out.bias",
                   "SBM.pe_expand.bias", "generator.linear.bias", "pegen.layers.2.self_attn.linear_layers.0.bias")
+PYTHON = dict(src_vocab_size=10000, tgt_vocab_size=20000, hidden_size=512, num_heads=8, num_layers=4, sbm_layers=4,
+              use_pegen="pegen", dim_feed_forward=2048, dropout=0.2, pe_dim=256, pegen_dim=512, sbm_enc_dim=512,
+              clusters=[10, 10, 10, 10], full_att=False)  # config/python.py via module/csa_trans.py:67-158
+PY_B, PY_N, PY_SEED = 2, 150, 83
 TIE_MARGIN = 5e-4  # STE uniforms closer than this to clamp(expA) are moved off the tie (see nudge_uniforms)
 
 
@@ -32,6 +36,17 @@ def fill_params_deterministic(model, seed):
 def java_uniforms(layer, B=JAVA_B, H=8, N=JAVA_N, seed=JAVA_SEED):
     """Host-supplied STE uniforms of SBM layer `layer` before tie nudging, (B,H,N,N) fp32."""
     return np.random.default_rng([seed, 1000 + layer]).random((B, H, N, N), dtype=np.float32)
+
+
+def python_uniforms(layer):
+    """java_uniforms for the config/python.py fixture (csatrans_python)."""
+    return java_uniforms(layer, B=PY_B, N=PY_N, seed=PY_SEED)
+
+
+def e64(z, key):
+    """The fixture's fp64-oracle value of `key` (float64): the reference's fp32 value plus the stored
+    difference z['e64:' + key] = fp64 - fp32 (tools/gen_golden.py:csatrans_dims_case)."""
+    return z[key].astype(np.float64) + z["e64:" + key].astype(np.float64)
 
 
 def apply_nudges(u, idx, val):

@@ -84,20 +84,20 @@ def test_rel_attn_production_head_size_matches_reference(golden, layout):
         np.testing.assert_allclose(x.grad.cpu().numpy(), z[n], rtol=RTOL, atol=ATOL, err_msg=n)
 
 
-def _run_rel(q, k, v, lq, lk, rel, mask, dO):
+def _run_rel(q, k, v, lq, lk, rel, mask, dO, schedule="auto"):
     from csa_amd import rel_ops
     t = [x.cuda().requires_grad_(True) for x in (q, k, v, lq, lk)]
-    o = rel_ops.rel_attn(*t, rel.cuda(), mask.cuda())
+    o = rel_ops.rel_attn(*t, rel.cuda(), mask.cuda(), schedule=schedule)
     (o * dO.cuda()).sum().backward()
     torch.cuda.synchronize()
     return [o.detach().cpu()] + [x.grad.cpu() for x in t]
 
 
 @pytest.mark.skipif(not has_gpu(), reason="needs GPU")
-def test_rel_attn_full_size_rows_match_oracle_and_deterministic(monkeypatch):
+def test_rel_attn_full_size_rows_match_oracle_and_deterministic():
     """The java train step's CSE shape (B=64 per GPU, H=8, N=L=150, d_k=64) in the compact layout:
     two runs are bitwise identical (the first with the backward halves in order, the second with
-    bwd_kf beside bwd_qf on the side stream: CSA_BWD_CONCUR=0 / 1); out/dq/dk/dv of sampled batch rows match the fp64 oracle run on
+    bwd_kf beside bwd_qf on the caller's side stream: schedule "in_order" / "concurrent"); out/dq/dk/dv of sampled batch rows match the fp64 oracle run on
     those rows alone (each row depends only on its AST); dlq/dlk (sums over the whole batch) match
     the fp64 oracle over all 64 rows."""
     from csa_amd.data import synthetic_batch
@@ -109,10 +109,8 @@ def test_rel_attn_full_size_rows_match_oracle_and_deterministic(monkeypatch):
     lq, lk = (torch.randn(1, H, L, dk, generator=g) for _ in range(2))
     rel = torch.from_numpy(np.stack([sb["L"], sb["T"]], 1).astype(np.uint8))
     mask = torch.from_numpy(np.stack([sb["L_mask"], sb["T_mask"]], 1).astype(np.uint8))
-    monkeypatch.setenv("CSA_BWD_CONCUR", "0")
-    r1 = _run_rel(q, k, v, lq, lk, rel, mask, dO)
-    monkeypatch.setenv("CSA_BWD_CONCUR", "1")
-    r2 = _run_rel(q, k, v, lq, lk, rel, mask, dO)
+    r1 = _run_rel(q, k, v, lq, lk, rel, mask, dO, schedule="in_order")
+    r2 = _run_rel(q, k, v, lq, lk, rel, mask, dO, schedule="concurrent")
     for a, b in zip(r1, r2):
         assert torch.equal(a, b)
     refrel, refmask = cse_ref.build_rel_mask(*(torch.from_numpy(sb[n]) for n in ("L", "T", "L_mask", "T_mask")))

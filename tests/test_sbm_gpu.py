@@ -4,6 +4,7 @@ import pytest
 import torch
 
 from conftest import has_gpu
+from csa_amd._lib import CSA_SCHED_CONCURRENT, CSA_SCHED_IN_ORDER
 from oracle import closed_form
 
 pytestmark = pytest.mark.gpu
@@ -234,8 +235,9 @@ def test_sbm_shapes_vs_oracle(shape):
 @pytest.mark.skipif(not has_gpu(), reason="needs GPU")
 def test_sbm_full_size_rows_match_oracle_and_deterministic():
     """BASELINE config 2 size (B=256, H=8, N=150, d=64, k=10): per-AST outputs/grads depend only on that
-    AST, so sampled batch rows are checked against the oracle run on those rows alone; and two runs
-    are bitwise identical (fixed-order reductions, integer atomics only)."""
+    AST, so sampled batch rows are checked against the oracle run on those rows alone; the batch-reduced
+    parameter gradients against the fp64 oracle over the whole batch; and two runs are bitwise identical
+    (fixed-order reductions, integer atomics only)."""
     B, H, N, d, k = 256, 8, 150, 64, 10
     Q, K, V, mask, u, dX, dsp, params = _rand_case(B, H, N, d, k, seed=7)
     r1 = _run_module(Q, K, V, mask, u, dX, dsp, params, k)
@@ -257,13 +259,28 @@ def test_sbm_full_size_rows_match_oracle_and_deterministic():
         np.testing.assert_allclose(dQ[sl].numpy(), rg2["Q"].numpy(), rtol=RTOL, atol=ATOL)
         np.testing.assert_allclose(dK[sl].numpy(), rg2["K"].numpy(), rtol=RTOL, atol=ATOL)
     np.testing.assert_allclose(sp.numpy(), graph.sum((0, 2, 3)).numpy() / (B * N * N), rtol=1e-6)
+    # the batch-reduced parameter gradients (dC, dW, db: sums over all 256 x 8 x 300 rows through the
+    # per-workgroup slabs and k_reduce_slabs) against the fp64 closed form summed over 16-row chunks (each
+    # chunk's sparsity gradient rescaled to the whole batch's 1 / (B N M))
+    C = 16
+    tot = None
+    for b0 in range(0, B, C):
+        sl = slice(b0, b0 + C)
+        _, rg = closed_form.sbm_fwd_bwd(Q[sl], K[sl], V[sl], mask[sl], params, u[sl], k, dX[sl], dsp * C / B,
+                                        graph_override=graph[sl])
+        part = {n: rg[n] for n in params}
+        tot = part if tot is None else {n: tot[n] + part[n] for n in params}
+    for n, ref in tot.items():
+        got = r1[6][n]
+        np.testing.assert_allclose(got.numpy(), ref.numpy(), rtol=RTOL, atol=ATOL * max(1.0, float(ref.abs().max())),
+                                   err_msg=n)
 
 
 @pytest.mark.skipif(not has_gpu(), reason="needs GPU")
 @pytest.mark.parametrize("shape", [(64, 8, 150, 64, 10), (8, 8, 150, 96, 10)])
-def test_concurrent_backward_schedule_bit_identical(shape, monkeypatch):
-    """bwd_q beside (k_attn_gamma + bwd_kv) on the side stream vs the in-order schedule
-    (CSA_BWD_CONCUR=1 / 0): gamma is recomputed in bwd_q's summation order, so every output and
+def test_concurrent_backward_schedule_bit_identical(shape):
+    """bwd_q beside (k_attn_gamma + bwd_kv) on the caller's side stream vs the in-order schedule
+    (CSA_SCHED_CONCURRENT / CSA_SCHED_IN_ORDER): gamma is recomputed in bwd_q's summation order, so every output and
     gradient is bitwise identical -- train mode with dropout, padded keys, and an upstream dattn."""
     B, H, N, d, k = shape
     Q, K, V, mask, _, dX, dsp, params = _rand_case(B, H, N, d, k, seed=41 + d)
@@ -276,10 +293,9 @@ def test_concurrent_backward_schedule_bit_identical(shape, monkeypatch):
     seed, offset = 0x5EED, 9
     X, sp, state = torch.ops.csa.sbm_fwd(q, kk, v, mk, cw, pw, pb, None, k, seed, offset, 0.2, 0.1, False)
     outs = []
-    for mode in ("0", "1"):
-        monkeypatch.setenv("CSA_BWD_CONCUR", mode)
+    for mode in (CSA_SCHED_IN_ORDER, CSA_SCHED_CONCURRENT):
         g = torch.ops.csa.sbm_bwd(q, kk, v, mk, cw, pw, pb, k, 0.2, 0.1, seed, offset, False, state, X,
-                                  dX.cuda(), dsp.cuda(), None, dattn=dattn)
+                                  dX.cuda(), dsp.cuda(), None, dattn=dattn, schedule=mode)
         torch.cuda.synchronize()
         outs.append([t.cpu() for t in g if isinstance(t, torch.Tensor)])
     assert len(outs[0]) == len(outs[1]) > 0
@@ -347,3 +363,46 @@ def test_train_mode_matches_oracle_with_regenerated_masks(shape):
              "proj.6.weight", "proj.6.bias"]
     for name, t in zip(names, g):
         np.testing.assert_allclose(t.cpu().numpy(), rg[name].numpy(), rtol=RTOL, atol=ATOL, err_msg=name)
+
+
+@pytest.mark.skipif(not has_gpu(), reason="needs GPU")
+def test_broadcast_upstream_gradient_is_materialised():
+    """X.sum((0, 1, 2)) hands the backward a (B,H,N,d) gradient with strides (0, 0, 0, 1). The ABI reads an
+    all-zero stride triple as "contiguous", so the op must materialise it: the gradients must equal those of
+    an explicit contiguous ones() upstream gradient, bit for bit (SBM and CSE)."""
+    from csa_amd import rel_ops
+    from csa_amd.module.sbm_attn import SBMAttention
+    B, H, N, d, k = 2, 8, 37, 64, 10
+    Q, K, V, mask, u, _, _, params = _rand_case(B, H, N, d, k, seed=5)
+    m = SBMAttention({"attention_dropout": 0.2, "head_dim": d, "num_head": H, "num_clusters": [k]}, 0)
+    m.load_state_dict(params, strict=False)
+    m = m.cuda().eval()
+    outs = []
+    for broadcast in (True, False):
+        q, kk, v = (t.cuda().requires_grad_(True) for t in (Q, K, V))
+        m.uniforms = u.cuda()
+        X, sp, _, _ = m(q, kk, v, mask.cuda())
+        if broadcast:
+            X.sum((0, 1, 2)).sum().backward()
+        else:
+            X.backward(torch.ones(X.shape, device="cuda"))
+        outs.append([q.grad.cpu(), kk.grad.cpu(), v.grad.cpu()] + [p.grad.cpu() for p in m.parameters()])
+        m.zero_grad(set_to_none=True)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    g = torch.Generator().manual_seed(3)
+    q, kk, v = (torch.randn(B, H, N, 64, generator=g) for _ in range(3))
+    lq, lk = (torch.randn(1, H, 150, 64, generator=g) for _ in range(2))
+    rel = torch.randint(0, 150, (B, 2, N, N), generator=g).to(torch.uint8)
+    msk = (torch.rand(B, 2, N, N, generator=g) < 0.1).to(torch.uint8)
+    outs = []
+    for broadcast in (True, False):
+        t = [x.cuda().requires_grad_(True) for x in (q, kk, v, lq, lk)]
+        o = rel_ops.rel_attn(*t, rel.cuda(), msk.cuda())
+        if broadcast:
+            o.sum((0, 1, 2)).sum().backward()
+        else:
+            o.backward(torch.ones(o.shape, device="cuda"))
+        outs.append([x.grad.cpu() for x in t])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)

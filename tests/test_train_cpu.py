@@ -48,16 +48,41 @@ def test_synthetic_relations_follow_reference_encoding():
 
 
 class Tiny(torch.nn.Module):
-    """Stand-in with the CSATrans output signature (out, sparsity, pe, graphs, attns)."""
+    """Stand-in with the CSATrans output signature (out, sparsity, pe, graphs, attns) around a packed QKV
+    triple, as csa_amd.module.sbm_attn.Attention has: glue.Linear q / k / v packed back to back at
+    construction (pack_linears_), one GEMM over the packed memory (glue.linear3 -> _LinearPackedFn)."""
 
-    def __init__(self):
+    def __init__(self, packed=True):
         super().__init__()
+        from csa_amd.glue import Linear, pack_linears_
+        self.packed = packed
+        self.q, self.k, self.v = Linear(6, 6), Linear(6, 6), Linear(6, 6)
         self.lin = torch.nn.Linear(6, 5)
         self.gate = torch.nn.Linear(6, 1)
+        if packed:
+            pack_linears_((self.q, self.k, self.v))
+
+    def _apply(self, fn, *args, **kwargs):
+        from csa_amd.glue import pack_linears_
+        out = super()._apply(fn, *args, **kwargs)
+        if self.packed:
+            pack_linears_((self.q, self.k, self.v))
+        return out
 
     def forward(self, x):
-        out = torch.log(torch.softmax(self.lin(x), -1))
+        if self.packed:
+            from csa_amd.glue import linear3
+            q, k, v = linear3(x, (self.q, self.k, self.v)).split(6, -1)
+        else:  # the plain per-layer reference
+            q, k, v = (torch.nn.functional.linear(x, l.weight, l.bias) for l in (self.q, self.k, self.v))
+        h = q * torch.sigmoid(k) + v
+        out = torch.log(torch.softmax(self.lin(h), -1))
         return out, torch.sigmoid(self.gate(x)).mean(), None, [], []
+
+
+def _packed_storage(model):
+    ws = [model.q.weight, model.k.weight, model.v.weight]
+    return len({w.untyped_storage().data_ptr() for w in ws}) == 1
 
 
 def _worker(rank, world, port, q):
@@ -68,13 +93,16 @@ def _worker(rank, world, port, q):
     r, w, _, dev = init_distributed()
     torch.manual_seed(0)
     model = Tiny()
+    assert _packed_storage(model)
     ddp = wrap_ddp(model, dev)
+    assert isinstance(ddp, torch.nn.parallel.DistributedDataParallel)
     opt = AdamW(model.parameters(), lr=1e-3, correct_bias=False)
     g = torch.Generator().manual_seed(100 + rank)  # per-rank shard (set_seed(seed + rank))
     x = torch.randn(4, 3, 6, generator=g)
     y = torch.randint(1, 5, (4, 3), generator=g)
     step = make_train_step(ddp, opt, label_smoothing_loss, sw=1e-2)
     step(x, y)
+    assert _packed_storage(model)  # DDP and the optimizer kept the packed storages
     q.put((rank, [p.grad.numpy().copy() for p in model.parameters()],
            [p.detach().numpy().copy() for p in model.parameters()]))
     dist.barrier()
@@ -90,7 +118,9 @@ def _free_port():
 
 
 def test_ddp_two_ranks_average_gradients():
-    """2-rank gloo DDP step == mean of the per-rank single-process gradients (DDP semantics)."""
+    """2-rank gloo DDP step == mean of the per-rank single-process gradients (DDP semantics), through the
+    packed QKV path (parameters packed before DDP is built, one GEMM forward, three gradient views of one
+    GEMM backward landing in gradient_as_bucket_view buckets) against plain unpacked per-rank GEMMs."""
     from csa_amd.model import label_smoothing_loss
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -106,7 +136,7 @@ def test_ddp_two_ranks_average_gradients():
     ref = []
     for rank in range(2):
         torch.manual_seed(0)
-        m = Tiny()
+        m = Tiny(packed=False)  # same initial values, plain per-layer GEMMs
         g = torch.Generator().manual_seed(100 + rank)
         x = torch.randn(4, 3, 6, generator=g)
         y = torch.randint(1, 5, (4, 3), generator=g)

@@ -7,8 +7,9 @@ re-verifies that this is bit-identical to the real CPU draw), runs forward + bac
 seeded inputs, and writes small ``.npz`` fixtures to tests/golden/. The reference never
 travels to the GPU box; only these fixtures do.
 
-Run:  PYTHONDONTWRITEBYTECODE=1 python tools/gen_golden.py [large]
-      (`large` = only the production-shape fixtures: rel_attn_n150_dk64, greedy_tiny, csatrans_java)
+Run:  PYTHONDONTWRITEBYTECODE=1 python tools/gen_golden.py [large | dims | mapgrad | ast]
+      (`large` = only the production-shape fixtures: rel_attn_n150_dk64, greedy_tiny, csatrans_java;
+       `dims` = csatrans_java + csatrans_python with their fp64 error budgets)
 """
 import importlib.util
 import math
@@ -23,6 +24,7 @@ REF = "/root/reference"
 OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tests", "golden")
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "code-structure-aware-transformer_amd"))
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tests"))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))  # oracle/ (fp64 error budget)
 from csa_amd.data import synthetic_batch  # noqa: E402
 import golden_inputs as gi  # noqa: E402
 
@@ -411,29 +413,50 @@ def _java_batch(B, N, seed):
     return synthetic_batch(B, max_size=N, seed=seed, min_nodes=100, max_nodes=N)
 
 
-def csatrans_java_case(name):
-    """CSATrans at config/java.py dims (sbm_enc_dim 768 -> SBM d=96, pe 128, pegen 512 -> CSE d_k=64,
-    N=150, 4 CSE + 4 SBM layers), eval mode, loss + sw*sparsity backward. Weights and STE uniforms are
+def _oracle_fp64(model, dims, sb, us, B, N):
+    """The pinned oracle CSATrans (oracle/csatrans_ref.py) in fp64 on the reference model's weights, batch and
+    (nudged) STE uniforms: the error-budget baseline. Returns (log-probs, sparsity, loss, {name: grad})."""
+    from oracle import csatrans_ref
+    cfg = csatrans_ref.config(**dims)
+    params = {k: p.detach().double().clone().requires_grad_(True) for k, p in model.named_parameters()
+              if k in csatrans_ref.param_shapes(cfg)}
+    om = csatrans_ref.Model(cfg, params, training=False)
+    f = lambda k, dt: torch.from_numpy(np.asarray(sb[k])).to(dt)
+    out, sp = om.forward(f("src_seq", torch.int64), f("tgt_seq", torch.int64), f("L", torch.int64), f("T", torch.int64),
+                         f("L_mask", torch.bool), f("T_mask", torch.bool), u_list=[torch.from_numpy(u) for u in us])
+    loss = csatrans_ref.label_smoothing(out, f("target", torch.int64))
+    (loss + 1e-2 * sp).backward()
+    return out.detach(), sp.detach(), loss.detach(), {k: p.grad for k, p in params.items()}
+
+
+def csatrans_dims_case(name, dims, B, N, seed, uniforms, grad_keys):
+    """CSATrans at production dims (config/java.py: sbm_enc_dim 768 -> SBM d=96, pe 128; config/python.py:
+    sbm_enc_dim 512 -> SBM d=64, pe 256; both pegen 512 -> CSE d_k=64, N=150, 4 CSE + 4 SBM layers), eval
+    mode, loss + sw*sparsity backward, then one reference AdamW step. Weights and STE uniforms are
     regenerated from PCG64 (tests/golden_inputs.py); the uniforms are moved off fp32 ties with the
-    probability the reference's sampler actually sees, and only those moves are stored."""
+    probability the reference's sampler actually sees, and only those moves are stored.
+
+    Error budget: the same model, batch and uniforms through the oracle CSATrans in fp64; the fixture keeps
+    fp64 - fp32(reference) as 'e64:<key>' for the log-prob columns, the loss and every stored gradient, so
+    the GPU test can compare its own error against the reference's fp32 error on the same inputs."""
     refmod, Data = load_full_reference_package()
     s = importlib.util.spec_from_file_location("ref_label_smooth", f"{REF}/utils/label_smooth.py")
     ls = importlib.util.module_from_spec(s)
     s.loader.exec_module(ls)
-    torch.manual_seed(gi.JAVA_SEED)
-    model = refmod.CSATrans(**gi.JAVA).eval()
-    gi.fill_params_deterministic(model, gi.JAVA_SEED)
-    B, N = gi.JAVA_B, gi.JAVA_N
-    sb = _java_batch(B, N, gi.JAVA_SEED)
+    torch.manual_seed(seed)
+    model = refmod.CSATrans(**dims).eval()
+    gi.fill_params_deterministic(model, seed)
+    sb = _java_batch(B, N, seed)
     f = lambda a: torch.from_numpy(np.asarray(a))
     data = Data(src_seq=f(sb["src_seq"]), tgt_seq=f(sb["tgt_seq"]), L=f(sb["L"]).float(), T=f(sb["T"]).float(),
                 L_mask=f(sb["L_mask"]), T_mask=f(sb["T_mask"]))
-    nudges = []
+    nudges, used = [], []
 
     def bern(p):
         layer = len(nudges)
-        u, idx, val = gi.nudge_uniforms(gi.java_uniforms(layer), p.detach().numpy())
+        u, idx, val = gi.nudge_uniforms(uniforms(layer), p.detach().numpy())
         nudges.append((idx, val))
+        used.append(u)
         return (torch.from_numpy(u) < p).to(p.dtype)
 
     torch.bernoulli = bern
@@ -441,30 +464,55 @@ def csatrans_java_case(name):
         out, sparsity, src_pe, graphs, attns = model(data)
     finally:
         torch.bernoulli = _real_bernoulli
-    assert len(nudges) == 4
+    assert len(nudges) == dims["sbm_layers"]
     loss = ls.LabelSmoothing(padding_idx=0, smoothing=0.0)(out, f(sb["target"]))
     (loss + 1e-2 * sparsity).backward()
-    res = {"out_cols": np32(out[:, :, ::gi.JAVA_OUT_COL_STRIDE]), "sparsity": np.array([sparsity.item()], np.float32),
+    col = gi.JAVA_OUT_COL_STRIDE
+    res = {"out_cols": np32(out[:, :, ::col]), "sparsity": np.array([sparsity.item()], np.float32),
            "loss": np.array([loss.item()], np.float32), "out_rowmax": np32(out.max(-1).values),
            "out_argmax": out.argmax(-1).numpy().astype(np.int32)}
     for i, (idx, val) in enumerate(nudges):
         res[f"nudge_idx{i}"], res[f"nudge_val{i}"] = idx, val
     res["state_keys"] = np.array(sorted(model.state_dict().keys()))
     for k, p in model.named_parameters():
-        if any(k.startswith(t) for t in gi.JAVA_GRAD_KEYS):
+        if any(k.startswith(t) for t in grad_keys):
             res["g:" + k] = np32(p.grad)
+    # fp64 oracle on the same inputs (the graph is the same: every draw is >= TIE_MARGIN from its p)
+    o64, sp64, loss64, g64 = _oracle_fp64(model, dims, sb, used, B, N)
+    assert sp64.item() == pytest_approx(sparsity.item()), (sp64.item(), sparsity.item())
+    res["e64:out_cols"] = (o64[:, :, ::col].numpy() - res["out_cols"].astype(np.float64)).astype(np.float32)
+    res["e64:loss"] = np.array([loss64.item() - float(res["loss"][0])], np.float32)
+    for k in [k for k in res if k.startswith("g:")]:
+        res["e64:" + k] = (g64[k[2:]].numpy() - res[k].astype(np.float64)).astype(np.float32)
     # one optimizer step of the train step (script/train.py:80,110: the reference AdamW, lr 1e-4 from
-    # config/java.py:49, correct_bias=False; the GradScaler's power-of-two scale cancels exactly)
+    # config/java.py:49 and config/python.py, correct_bias=False; the GradScaler's power-of-two scale cancels)
     so = importlib.util.spec_from_file_location("ref_optimizer", f"{REF}/script/optimizer.py")
     om = importlib.util.module_from_spec(so)
     so.loader.exec_module(om)
     om.AdamW(model.parameters(), lr=1e-4, correct_bias=False).step()
     for k, p in model.named_parameters():
-        if any(k.startswith(t) for t in gi.JAVA_GRAD_KEYS):
+        if any(k.startswith(t) for t in grad_keys):
             res["p1:" + k] = np32(p)
     np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **res)
+    rel = lambda k: float(np.abs(res["e64:" + k]).max() / max(np.abs(res[k]).max(), 1e-30))
     print(f"{name}: loss={loss.item():.5f} sparsity={sparsity.item():.5f} nudged={[len(n[0]) for n in nudges]}"
-          f" grads={sum(k.startswith('g:') for k in res)}")
+          f" grads={sum(k.startswith('g:') for k in res)} ref-fp32 vs fp64: out {rel('out_cols'):.2e},"
+          f" worst grad {max(rel(k) for k in res if k.startswith('g:')):.2e}")
+
+
+def pytest_approx(x, rel=1e-6):
+    class _A:
+        def __eq__(self, y):
+            return abs(y - x) <= rel * max(abs(x), 1e-30)
+    return _A()
+
+
+def csatrans_java_case(name):
+    csatrans_dims_case(name, gi.JAVA, gi.JAVA_B, gi.JAVA_N, gi.JAVA_SEED, gi.java_uniforms, gi.JAVA_GRAD_KEYS)
+
+
+def csatrans_python_case(name):
+    csatrans_dims_case(name, gi.PYTHON, gi.PY_B, gi.PY_N, gi.PY_SEED, gi.python_uniforms, gi.JAVA_GRAD_KEYS)
 
 
 def greedy_tiny_case(name, seed, max_tgt_len=7):
@@ -557,6 +605,10 @@ def main():
         sbm_case("sbm_n33_d96_mapgrad", B=1, H=2, N=33, d=96, k=10, pad_counts=[1], seed=18, map_grads=True)
         full_case("full_n37_mapgrad", B=2, H=2, N=37, d=64, pad_counts=[0, 5], seed=23, map_grads=True)
         return
+    if sys.argv[1:] == ["dims"]:  # round 3: production-dims CSATrans with the fp64 error budget
+        csatrans_java_case("csatrans_java")
+        csatrans_python_case("csatrans_python")
+        return
     if sys.argv[1:] == ["large"]:  # only the round-2 production-shape fixtures
         rel_attn_large_case("rel_attn_n150_dk64", B=1, N=150, dk=64, L=150, seed=44)
         greedy_tiny_case("greedy_tiny", seed=72)
@@ -591,6 +643,7 @@ def main():
         rel_attn_large_case("rel_attn_n150_dk64", B=1, N=150, dk=64, L=150, seed=44)
         greedy_tiny_case("greedy_tiny", seed=72)
         csatrans_java_case("csatrans_java")
+        csatrans_python_case("csatrans_python")
 
 
 if __name__ == "__main__":
