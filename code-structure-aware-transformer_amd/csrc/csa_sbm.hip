@@ -181,10 +181,38 @@ __device__ __forceinline__ f32x4 frag4_lds(const float* __restrict__ f, int it, 
   return *reinterpret_cast<const f32x4*>(f + ((it * (nsteps >> 2) + s4) * 64 + lane_id()) * 4);
 }
 
-template <int NTO, int S4N, int LA = 1, bool FL = false, typename BF>
-__device__ __forceinline__ void frag_chain(const float* __restrict__ frag, int nsteps, f32x16 (&out)[NTO], BF bval) {
+// BF16: the same chain on v_mfma_f32_32x32x16_bf16 (CSA_DTYPE_BF16's projection contractions): one
+// instruction takes two consecutive K-groups (8 K-steps, csa_common.hpp pack8), both operands rounded to
+// bf16 (RNE) as they are packed; accumulation stays fp32. S4N must be even.
+template <int NTO, int S4N, int LA = 1, bool FL = false, bool BF16 = false, typename BV>
+__device__ __forceinline__ void frag_chain(const float* __restrict__ frag, int nsteps, f32x16 (&out)[NTO], BV bval) {
   static_assert(LA == 1 || LA == 2, "lookahead of one or two K-groups");
   auto ld = [&](int t, int s4) { return FL ? frag4_lds(frag, t, nsteps, s4) : frag4(frag, t, nsteps, s4); };
+  if constexpr (BF16) {
+    static_assert(S4N % 2 == 0, "bf16 chains take K-groups in pairs");
+    constexpr int S8N = S4N / 2;
+    f32x4 wq[2][NTO][2];
+#pragma unroll
+    for (int t = 0; t < NTO; ++t) { wq[0][t][0] = ld(t, 0); wq[0][t][1] = ld(t, 1); }
+#pragma unroll
+    for (int s8 = 0; s8 < S8N; ++s8) {
+      if (s8 + 1 < S8N) {
+#pragma unroll
+        for (int t = 0; t < NTO; ++t) {
+          wq[(s8 + 1) & 1][t][0] = ld(t, 2 * s8 + 2);
+          wq[(s8 + 1) & 1][t][1] = ld(t, 2 * s8 + 3);
+        }
+      }
+      float bv[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) bv[e] = bval(8 * s8 + e);
+      const bf16x8 b8 = pack8(bv);
+#pragma unroll
+      for (int t = 0; t < NTO; ++t) out[t] = mfma_bf(pack8(wq[s8 & 1][t][0], wq[s8 & 1][t][1]), b8, out[t]);
+      fence_sched();
+    }
+    return;
+  }
   f32x4 wq[LA + 1][NTO];
 #pragma unroll
   for (int a = 0; a < LA; ++a)
@@ -393,7 +421,7 @@ __device__ __forceinline__ void add_bias(const float (&ba)[D / 32], f32x16 (&a)[
 struct FwdFrags { const float* W[3]; const float* C; const float* S; const float* b[3]; };
 
 // h1 = relu(drop(W0 x + b0)) from lin-perm input rows
-template <int D, bool FL>
+template <int D, bool FL, bool BF = false>
 __device__ __forceinline__ void mlp_layer0(const KArgs& p, const float* W0, const float* b0, const float (&x)[D / 2],
                                            f32x16 (&h1)[D / 32], int row, int bh, int isK) {
   constexpr int DT = D / 32, NS = D / 2;
@@ -401,13 +429,13 @@ __device__ __forceinline__ void mlp_layer0(const KArgs& p, const float* W0, cons
   bias_operand<D>(b0, ba);
 #pragma unroll
   for (int ot = 0; ot < DT; ++ot) h1[ot] = zero16();
-  frag_chain<DT, NS / 4, FL ? FL_LA : MLP_LA, FL>(W0, NS, h1, [&](int s) { return x[s]; });
+  frag_chain<DT, NS / 4, FL ? FL_LA : MLP_LA, FL, BF>(W0, NS, h1, [&](int s) { return x[s]; });
   add_bias<D>(ba, h1);
   mlp_act<D>(p, h1, 0, row, bh, isK);
 }
 
 // out = W_l in + b_l  (acc-perm input), l = 1, 2
-template <int D, bool FL>
+template <int D, bool FL, bool BF = false>
 __device__ __forceinline__ void mlp_layer(const float* Wl, const float* bl, const f32x16 (&in)[D / 32],
                                           f32x16 (&out)[D / 32]) {
   constexpr int DT = D / 32, NS = D / 2;
@@ -415,27 +443,28 @@ __device__ __forceinline__ void mlp_layer(const float* Wl, const float* bl, cons
   bias_operand<D>(bl, ba);
 #pragma unroll
   for (int ot = 0; ot < DT; ++ot) out[ot] = zero16();
-  frag_chain<DT, NS / 4, FL ? FL_LA : MLP_LA, FL>(Wl, NS, out, [&](int s) { return in[s / 16][s % 16]; });
+  frag_chain<DT, NS / 4, FL ? FL_LA : MLP_LA, FL, BF>(Wl, NS, out, [&](int s) { return in[s / 16][s % 16]; });
   add_bias<D>(ba, out);
 }
 
-template <int D, bool FL>
+// BF: CSA_DTYPE_BF16 (the three d x d layers on bf16 MFMA; biases, dropout and ReLU in fp32)
+template <int D, bool FL, bool BF = false>
 __device__ __forceinline__ void mlp_fwd(const KArgs& p, const FwdFrags& F, const float (&x)[D / 2], f32x16 (&h1)[D / 32],
                                         f32x16 (&h2)[D / 32], f32x16 (&po)[D / 32], int row, int bh, int isK) {
-  mlp_layer0<D, FL>(p, F.W[0], F.b[0], x, h1, row, bh, isK);
-  mlp_layer<D, FL>(F.W[1], F.b[1], h1, h2);
+  mlp_layer0<D, FL, BF>(p, F.W[0], F.b[0], x, h1, row, bh, isK);
+  mlp_layer<D, FL, BF>(F.W[1], F.b[1], h1, h2);
   mlp_act<D>(p, h2, 1, row, bh, isK);
-  mlp_layer<D, FL>(F.W[2], F.b[2], h2, po);
+  mlp_layer<D, FL, BF>(F.W[2], F.b[2], h2, po);
 }
 
 // hat^T = sigmoid(C_h p^T), rows (clusters) >= k zeroed. Cf: the head's cluster fragments.
-template <int D, int KT, bool FL>
+template <int D, int KT, bool FL, bool BF = false>
 __device__ __forceinline__ void cluster_hat(const KArgs& p, const float* Cf, const f32x16 (&po)[D / 32], f32x16 (&hat)[KT]) {
   constexpr int NS = D / 2;
   const int h = lane_id() >> 5;
 #pragma unroll
   for (int kt = 0; kt < KT; ++kt) hat[kt] = zero16();
-  frag_chain<KT, NS / 4, 1, FL>(Cf, NS, hat, [&](int s) { return po[s / 16][s % 16]; });
+  frag_chain<KT, NS / 4, 1, FL, BF>(Cf, NS, hat, [&](int s) { return po[s / 16][s % 16]; });
 #pragma unroll
   for (int kt = 0; kt < KT; ++kt) {
 #pragma unroll
@@ -545,7 +574,7 @@ __device__ __forceinline__ void load_item_x(const KArgs& p, int b, int hd, int r
 // F2 body: item r of (b, hd) from its x rows. `next` runs once every product is done and x is dead,
 // before the stores (the persistent kernel issues the next item's x loads there: a later vmcnt wait
 // for them then does not also wait for this item's stores, which drain under the next item).
-template <int D, int KT, bool FL, typename NEXT>
+template <int D, int KT, bool FL, typename NEXT, bool BF = false>
 __device__ __forceinline__ void proj_fwd_item(const KArgs& p, const FwdFrags& F, int b, int hd, int r, float (&x)[D / 2],
                                               float* scr, NEXT next) {
   const int lane = lane_id(), c = lane & 31, h = lane >> 5;
@@ -558,8 +587,8 @@ __device__ __forceinline__ void proj_fwd_item(const KArgs& p, const FwdFrags& F,
   f32x16 h1[D / 32], h2[D / 32], po[D / 32], hat[KT], t[KT];
 #pragma unroll
   for (int i = 0; i < D / 2; ++i) x[i] = rv ? x[i] : 0.f;
-  mlp_fwd<D, FL>(p, F, x, h1, h2, po, row, bh, isK);
-  cluster_hat<D, KT, FL>(p, F.C, po, hat);
+  mlp_fwd<D, FL, BF>(p, F, x, h1, h2, po, row, bh, isK);
+  cluster_hat<D, KT, FL, BF>(p, F.C, po, hat);
   if (isK) small_mm<KT, FL>(F.S, hat, t);
   next();
 #ifndef CSA_EXP_NO_ACT
@@ -623,12 +652,9 @@ struct ProjFwdLds {
   static_assert((3 * WB + CB + SB) % 1024 == 0, "whole 1 KiB DMA pieces");
 };
 
-template <int D, int KT>
-#ifdef CSA_EXP_PF6
+// BF: CSA_DTYPE_BF16 (MLP and cluster projection on bf16 MFMA; T = Kh S^T stays fp32)
+template <int D, int KT, bool BF = false>
 __global__ __launch_bounds__((64 * ProjFwdLds<D, KT>::NW)) void k_proj_fwd_l(const KArgs p) {
-#else
-__global__ __launch_bounds__((64 * ProjFwdLds<D, KT>::NW)) void k_proj_fwd_l(const KArgs p) {
-#endif
   using LY = ProjFwdLds<D, KT>;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -656,9 +682,10 @@ __global__ __launch_bounds__((64 * ProjFwdLds<D, KT>::NW)) void k_proj_fwd_l(con
   float* scr = lds + LY::FBYTES / 4 + 1024 * w;
   for (int it = i_lo + w; it < i_hi; it += LY::NW) {
     const int nx = it + LY::NW;
-    proj_fwd_item<D, KT, true>(p, F, it / per_b, hd, it % per_b, x, scr, [&] {
+    auto nextf = [&] {
       if (nx < i_hi) load_item_x<D>(p, nx / per_b, hd, nx % per_b, x);
-    });
+    };
+    proj_fwd_item<D, KT, true, decltype(nextf), BF>(p, F, it / per_b, hd, it % per_b, x, scr, nextf);
   }
 }
 
@@ -1648,13 +1675,28 @@ __device__ __forceinline__ void read_act(f32x16 (&a)[NT], const float* __restric
 
 // acc += sum over the 128 staged rows of DS[32ot + i][row] * IN[32it + j][row]
 // K-step s of half h takes rows 64h + s: region 2h + s/32, chunk (s%32)/4.
-template <int REG>
+// BF: on bf16 MFMA, K-groups s4 = 2 s8, 2 s8 + 1 (8 consecutive staged rows) per instruction
+template <int REG, bool BF = false>
 __device__ __forceinline__ f32x16 outer_tile(const float* __restrict__ ds, const float* __restrict__ in, int ot, int it,
                                              f32x16 acc, int lane) {
   asm volatile("" : "+v"(lane));
   const int c = lane & 31, h = lane >> 5, sw = (c >> 1) & 7;
   const float* a = ds + 2 * h * REG + (32 * ot + c) * 32;
   const float* b = in + 2 * h * REG + (32 * it + c) * 32;
+  if constexpr (BF) {
+#pragma unroll
+    for (int s8 = 0; s8 < 8; ++s8) {
+      f32x4 av[2], bv[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int s4 = 2 * s8 + u, off = (s4 >> 3) * REG + 4 * ((s4 & 7) ^ sw);
+        av[u] = *reinterpret_cast<const f32x4*>(a + off);
+        bv[u] = *reinterpret_cast<const f32x4*>(b + off);
+      }
+      acc = mfma_bf(pack8(av[0], av[1]), pack8(bv[0], bv[1]), acc);
+    }
+    return acc;
+  }
 #pragma unroll
   for (int s4 = 0; s4 < 16; ++s4) {
     const int off = (s4 >> 3) * REG + 4 * ((s4 & 7) ^ sw);
@@ -1752,12 +1794,13 @@ __device__ __forceinline__ void mm_acc(const float* __restrict__ frag, const f32
 
 // mm_acc over fragments held in LDS (FL) or global memory; NSTEP = the K-steps of the stored layout
 // (8 for the compacted k <= 16 cluster fragments: only K-groups 0 and 1 of each tile are copied).
-template <int NTO, int NTI, int S4MAX, int NSTEP, bool FL>
+template <int NTO, int NTI, int S4MAX, int NSTEP, bool FL, bool BF = false>
 __device__ __forceinline__ void mm_acc_f(const float* __restrict__ frag, const f32x16 (&in)[NTI], f32x16 (&out)[NTO]) {
 #pragma unroll
   for (int t = 0; t < NTO; ++t) out[t] = zero16();
   // L2 fragments two K-groups ahead (measured 2% faster k_proj_bwd_s<64> than one), LDS fragments one
-  frag_chain<NTO, S4MAX, S4MAX < 4 ? 1 : (FL ? FL_LA : 2), FL>(frag, NSTEP, out, [&](int s) { return in[s / 16][s % 16]; });
+  frag_chain<NTO, S4MAX, S4MAX < 4 ? 1 : (FL ? FL_LA : 2), FL, BF>(frag, NSTEP, out,
+                                                                  [&](int s) { return in[s / 16][s % 16]; });
 }
 
 template <int D, int KT>
@@ -2012,7 +2055,7 @@ __device__ __forceinline__ void quarter_load(const float* __restrict__ a, const 
 // combined in a fixed order at the end. The operand reads of the next position are issued before the
 // current position's MFMAs (unconditionally: every read is in bounds), so only the MFMA blocks sit
 // under the wave-uniform activity branches.
-template <int REG>
+template <int REG, bool BF = false>
 __device__ __forceinline__ void outer_stage96(const float* __restrict__ ds, const float* __restrict__ in,
                                               f32x16 (&acc)[3], int w, int lane) {
   asm volatile("" : "+v"(lane));
@@ -2032,20 +2075,26 @@ __device__ __forceinline__ void outer_stage96(const float* __restrict__ ds, cons
     const int j = P >> 2, q = P & 3;
     if (P + 1 < 12) quarter_load<REG>(a[(P + 1) >> 2], b[(P + 1) >> 2], (P + 1) & 3, sw, av[(P + 1) & 1], bv[(P + 1) & 1]);
     if (j == 1 || (j == 0 ? q >= w : q <= w)) {
+      if constexpr (BF) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; i += 2)
+          acc[j] = mfma_bf(pack8(av[P & 1][i], av[P & 1][i + 1]), pack8(bv[P & 1][i], bv[P & 1][i + 1]), acc[j]);
+      } else {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) acc[j] = mfma(av[P & 1][i][e], bv[P & 1][i][e], acc[j]);
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[j] = mfma(av[P & 1][i][e], bv[P & 1][i][e], acc[j]);
+      }
     }
     fence_sched();
   }
 }
 
-template <int D>
+template <int D, bool BF = false>
 __device__ __forceinline__ void outer_stage_s(const float* __restrict__ ds, const float* __restrict__ in,
                                               f32x16 (&acc)[ProjBwdSmallShape<D>::NSL], int w, int lane) {
-  if constexpr (D == 64) acc[0] = outer_tile<ProjBwdSmallShape<D>::REG>(ds, in, w >> 1, w & 1, acc[0], lane);
-  else outer_stage96<ProjBwdSmallShape<D>::REG>(ds, in, acc, w, lane);
+  if constexpr (D == 64) acc[0] = outer_tile<ProjBwdSmallShape<D>::REG, BF>(ds, in, w >> 1, w & 1, acc[0], lane);
+  else outer_stage96<ProjBwdSmallShape<D>::REG, BF>(ds, in, acc, w, lane);
 }
 
 // bias-gradient partial of this wave: sums of its own staged rows, feature lane (and lane + 64 for d = 96).
@@ -2069,7 +2118,9 @@ __device__ __forceinline__ void own_rowsum(const float* __restrict__ dsw, float 
   }
 }
 
-template <int D>
+// BF: CSA_DTYPE_BF16 (the C^T dZ chain, the three W^T chains and the three d x d weight-gradient outer products on
+// bf16 MFMA; the S^T dT chain, dS, dC, the bias sums and every elementwise step stay fp32)
+template <int D, bool BF = false>
 __global__ __launch_bounds__(256, ProjBwdSmallShape<D>::LCS ? 1 : 2) void k_proj_bwd_s(const KArgs p) {
   static_assert(D == 64 || D == 96, "d x d stages split over 4 waves for d = 64 and 96");
   using Sh = ProjBwdSmallShape<D>;
@@ -2213,7 +2264,7 @@ __global__ __launch_bounds__(256, ProjBwdSmallShape<D>::LCS ? 1 : 2) void k_proj
     }
     // ---- dp^T = C^T dZ^T (clusters < 16)
     f32x16 dcur[DT];
-    mm_acc_f<DT, 1, 2, LCS ? 8 : 16, LCS>(LCS ? CFs : CfT, dz, dcur);
+    mm_acc_f<DT, 1, 2, LCS ? 8 : 16, LCS, BF>(LCS ? CFs : CfT, dz, dcur);
     wait_vm_all();  // po (LW: and the W2 fragments)
     // ---- dC_h += dZ^T po, private 16x16x4: A = dZ[row 4s + g4][cluster c16], B = po[row 4s + g4][16t + c16]
 #pragma unroll
@@ -2229,13 +2280,13 @@ __global__ __launch_bounds__(256, ProjBwdSmallShape<D>::LCS ? 1 : 2) void k_proj
     if constexpr (LW) __syncthreads();  // B0: every wave's quarter of the W2 fragments landed
     dma_block16<D * 128>(INl, ar, 32 * D * 4);  // h2
     f32x16 dh[DT];
-    mm_acc_f<DT, DT, 4 * DT, 16 * DT, LW>(LW ? WFs : p.WfT[2], dcur, dh);
+    mm_acc_f<DT, DT, 4 * DT, 16 * DT, LW, BF>(LW ? WFs : p.WfT[2], dcur, dh);
     wait_vm_all();
     PHASE(7);
     __syncthreads();  // B1: dp, h2 of every wave staged
     PHASE(2);
     if constexpr (LW) load_wf(1);  // every wave is past its W2 chain
-    outer_stage_s<D>(DS, IN, acc[0], w, ln);
+    outer_stage_s<D, BF>(DS, IN, acc[0], w, ln);
     own_rowsum<D>(DSw, dbp[2], ln);
     {
       f32x16 hv[DT];
@@ -2259,13 +2310,13 @@ __global__ __launch_bounds__(256, ProjBwdSmallShape<D>::LCS ? 1 : 2) void k_proj
 #pragma unroll
       for (int j = 0; j < NS / 4; ++j) x4[j] = *reinterpret_cast<const f32x4*>(X + h * NS + 4 * j);
     }
-    mm_acc_f<DT, DT, 4 * DT, 16 * DT, LW>(LW ? WFs : p.WfT[1], dcur, dh);
+    mm_acc_f<DT, DT, 4 * DT, 16 * DT, LW, BF>(LW ? WFs : p.WfT[1], dcur, dh);
     wait_vm_all();
     PHASE(4);
     __syncthreads();  // B3
     PHASE(2);
     if constexpr (LW) load_wf(0);  // every wave is past its W1 chain
-    outer_stage_s<D>(DS, IN, acc[1], w, ln);
+    outer_stage_s<D, BF>(DS, IN, acc[1], w, ln);
     own_rowsum<D>(DSw, dbp[1], ln);
     {
       f32x16 hv[DT];
@@ -2312,12 +2363,12 @@ __global__ __launch_bounds__(256, ProjBwdSmallShape<D>::LCS ? 1 : 2) void k_proj
     __syncthreads();  // B5
     PHASE(2);
     if constexpr (LW && !HIN_DS) prefetch_next();  // (after the W0 wait above)
-    outer_stage_s<D>(DS, IN, acc[2], w, ln);
+    outer_stage_s<D, BF>(DS, IN, acc[2], w, ln);
     own_rowsum<D>(DSw, dbp[0], ln);
     if constexpr (LW) load_old();  // LW: the dQ / dK rows load under the dx chain (fewer live registers)
     PHASE(3);
     f32x16 dxm[DT];
-    mm_acc_f<DT, DT, 4 * DT, 16 * DT, LW>(LW ? WFs : p.WfT[0], dcur, dxm);  // second-path dx = W0^T dh1
+    mm_acc_f<DT, DT, 4 * DT, 16 * DT, LW, BF>(LW ? WFs : p.WfT[0], dcur, dxm);  // second-path dx = W0^T dh1
     if (rv) {  // dQ / dK += MLP backward
 #pragma unroll
       for (int t = 0; t < DT; ++t)
@@ -2710,8 +2761,13 @@ csa_status launch_fwd(const csa_sbm_fwd_args* a, const Layout& L, hipStream_t st
         {
           const int64_t items = a->B * (L.NQB + L.NKB), slots = (D == 64 && PL::NW == 4 ? 2 : 1) * 256LL;
           const int G = (int)std::max<int64_t>(1, std::min<int64_t>(slots / a->H, (items + PL::NW - 1) / PL::NW));
-          set_dyn_lds((const void*)k_proj_fwd_l<D, KT>, (int)PL::BYTES);
-          hipLaunchKernelGGL((k_proj_fwd_l<D, KT>), dim3(G, a->H), dim3(64 * PL::NW), PL::BYTES, st, p);
+          if (p.bf16) {  // CSA_DTYPE_BF16: MLP + cluster projection on bf16 MFMA
+            set_dyn_lds((const void*)k_proj_fwd_l<D, KT, true>, (int)PL::BYTES);
+            hipLaunchKernelGGL((k_proj_fwd_l<D, KT, true>), dim3(G, a->H), dim3(64 * PL::NW), PL::BYTES, st, p);
+          } else {
+            set_dyn_lds((const void*)k_proj_fwd_l<D, KT>, (int)PL::BYTES);
+            hipLaunchKernelGGL((k_proj_fwd_l<D, KT>), dim3(G, a->H), dim3(64 * PL::NW), PL::BYTES, st, p);
+          }
           done = true;
         }
       }
@@ -2840,8 +2896,13 @@ csa_status launch_bwd(const csa_sbm_bwd_args* b, const Layout& L, hipStream_t st
       Stage sg(pf, CSA_STAGE_PROJ_BWD, st);
       if constexpr ((D == 64 || D == 96) && KPH == 8) {  // k <= 16
         using Ss = ProjBwdSmallShape<D>;
-        set_dyn_lds((const void*)k_proj_bwd_s<D>, (int)Ss::LDS_BYTES);
-        hipLaunchKernelGGL((k_proj_bwd_s<D>), dim3(L.G, a->H), dim3(256), Ss::LDS_BYTES, st, p);
+        if (p.bf16) {  // CSA_DTYPE_BF16: projection contractions on bf16 MFMA
+          set_dyn_lds((const void*)k_proj_bwd_s<D, true>, (int)Ss::LDS_BYTES);
+          hipLaunchKernelGGL((k_proj_bwd_s<D, true>), dim3(L.G, a->H), dim3(256), Ss::LDS_BYTES, st, p);
+        } else {
+          set_dyn_lds((const void*)k_proj_bwd_s<D>, (int)Ss::LDS_BYTES);
+          hipLaunchKernelGGL((k_proj_bwd_s<D>), dim3(L.G, a->H), dim3(256), Ss::LDS_BYTES, st, p);
+        }
       } else {
         set_dyn_lds((const void*)k_proj_bwd<D, KT>, (int)Sh::LDS_BYTES);
         hipLaunchKernelGGL((k_proj_bwd<D, KT>), dim3(L.G, a->H), dim3(256), Sh::LDS_BYTES, st, p);
