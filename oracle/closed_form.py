@@ -31,47 +31,64 @@ import torch
 EPS = 1e-12
 
 
-def _mlp_fwd(x, W, keep):
-    """Returns (out, [inputs of each Linear], [relu masks])."""
+def _ident(t):
+    return t
+
+
+def _bf16_round(t):
+    """Round to bf16 (RNE) and back: the operand rounding of a bf16-MFMA contraction (v_cvt_pk_bf16_f32)."""
+    return t.to(torch.bfloat16).to(t.dtype)
+
+
+def _mlp_fwd(x, W, keep, R=_ident):
+    """Returns (out, [inputs of each Linear], [relu masks]). R rounds the operands of each x W^T product
+    (bf16 emulation); the bias is added exactly, as the kernels do."""
     W0, b0, W1, b1, W2, b2 = W
-    z0 = x @ W0.T + b0
+    z0 = R(x) @ R(W0).T + b0
     if keep is not None and keep[0] is not None:
         z0 = z0 * keep[0]
     h1 = torch.relu(z0)
-    z1 = h1 @ W1.T + b1
+    z1 = R(h1) @ R(W1).T + b1
     if keep is not None and keep[1] is not None:
         z1 = z1 * keep[1]
     h2 = torch.relu(z1)
-    out = h2 @ W2.T + b2
+    out = R(h2) @ R(W2).T + b2
     return out, (x, h1, h2), (z0 > 0, z1 > 0)
 
 
-def _mlp_bwd(dout, W, acts, masks, keep):
+def _mlp_bwd(dout, W, acts, masks, keep, R=_ident):
     W0, b0, W1, b1, W2, b2 = W
     x, h1, h2 = acts
     m0, m1 = masks
     g = {}
-    g["proj.6.weight"] = torch.einsum("...o,...i->oi", dout, h2)
+    g["proj.6.weight"] = torch.einsum("...o,...i->oi", R(dout), R(h2))
     g["proj.6.bias"] = dout.reshape(-1, dout.shape[-1]).sum(0)
-    dh2 = dout @ W2
+    dh2 = R(dout) @ R(W2)
     dz1 = dh2 * m1
     if keep is not None and keep[1] is not None:
         dz1 = dz1 * keep[1]
-    g["proj.3.weight"] = torch.einsum("...o,...i->oi", dz1, h1)
+    g["proj.3.weight"] = torch.einsum("...o,...i->oi", R(dz1), R(h1))
     g["proj.3.bias"] = dz1.reshape(-1, dz1.shape[-1]).sum(0)
-    dh1 = dz1 @ W1
+    dh1 = R(dz1) @ R(W1)
     dz0 = dh1 * m0
     if keep is not None and keep[0] is not None:
         dz0 = dz0 * keep[0]
-    g["proj.0.weight"] = torch.einsum("...o,...i->oi", dz0, x)
+    g["proj.0.weight"] = torch.einsum("...o,...i->oi", R(dz0), R(x))
     g["proj.0.bias"] = dz0.reshape(-1, dz0.shape[-1]).sum(0)
-    dx = dz0 @ W0
+    dx = R(dz0) @ R(W0)
     return dx, g
 
 
 def sbm_fwd_bwd(Q, K, V, mask, params, u, num_clusters, dX, dsparsity, attn_keep=None, proj_keep=None,
-                graph_override=None):
-    """fp64 closed-form forward + backward. Returns (outputs dict, grads dict)."""
+                graph_override=None, bf16=False):
+    """fp64 closed-form forward + backward. Returns (outputs dict, grads dict).
+
+    bf16=True: an ideal CSA_DTYPE_BF16 implementation -- the operands of every contraction the bf16 mode
+    runs on bf16 MFMA are rounded to bf16 (QK^T, dX V^T, PV with the unnormalised weights e A r, dV, dQ,
+    dK, the three MLP layers and .C^T forward, C^T dZ, the W^T chains and the dW outer products backward),
+    everything else (accumulation, biases, softmax, sampling, expA, T, dQh, dT, dS, dC) exact. The error of
+    this emulation against the fp32 reference is what a bf16-operand implementation cannot avoid."""
+    R = _bf16_round if bf16 else _ident
     f = lambda t: None if t is None else t.detach().double()
     Q, K, V, mask, u, dX, dsparsity = map(f, (Q, K, V, mask, u, dX, dsparsity))
     attn_keep = f(attn_keep)
@@ -84,17 +101,17 @@ def sbm_fwd_bwd(Q, K, V, mask, params, u, num_clusters, dX, dsparsity, attn_keep
     C = f(params["layer.weight"]).reshape(H, k, d)
     D2 = C @ C.transpose(-1, -2)
     S = torch.softmax(D2.reshape(H, k * k), -1).reshape(H, k, k)
-    Qp, qacts, qmasks = _mlp_fwd(Q, W, (pk.get("q0"), pk.get("q1")))
-    Kp, kacts, kmasks = _mlp_fwd(K, W, (pk.get("k0"), pk.get("k1")))
-    Qh = torch.sigmoid(Qp @ C.transpose(-1, -2).unsqueeze(0))
-    Kh = torch.sigmoid(Kp @ C.transpose(-1, -2).unsqueeze(0))
+    Qp, qacts, qmasks = _mlp_fwd(Q, W, (pk.get("q0"), pk.get("q1")), R)
+    Kp, kacts, kmasks = _mlp_fwd(K, W, (pk.get("k0"), pk.get("k1")), R)
+    Qh = torch.sigmoid(R(Qp) @ R(C).transpose(-1, -2).unsqueeze(0))
+    Kh = torch.sigmoid(R(Kp) @ R(C).transpose(-1, -2).unsqueeze(0))
     T = Kh @ S.transpose(-1, -2).unsqueeze(0)  # T_j = S Kh_j
     expA = Qh @ T.transpose(-1, -2)
     if graph_override is not None:
         A = f(graph_override)
     else:
         A = (u < expA.clamp(0.01, 0.99)).double()
-    s = (Q @ K.transpose(-1, -2)) / math.sqrt(d)
+    s = (R(Q) @ R(K).transpose(-1, -2)) / math.sqrt(d)
     s = s.masked_fill(mask[:, None, None, :] == 1, float("-inf"))
     mrow = s.max(-1, keepdim=True).values
     e = torch.exp(s - mrow)
@@ -105,14 +122,17 @@ def sbm_fwd_bwd(Q, K, V, mask, params, u, num_clusters, dX, dsparsity, attn_keep
     Dn = n.clamp_min(EPS)
     attn = Mm / Dn
     r = attn_keep if attn_keep is not None else torch.ones_like(attn)
-    X = (attn * r) @ V
+    if bf16:  # the kernel rounds the unnormalised weights e A r (r: the dropout multiplier) and scales after
+        X = (R(e * A * r) @ R(V)) / (Z * Dn)
+    else:
+        X = (attn * r) @ V
     sparsity = A.sum((0, 2, 3)) / (B * N * M)
     out = dict(X=X, sparsity=sparsity, graph=A, attn=attn, expA=expA, Qhat=Qh, Khat=Kh, T=T, S=S,
                rowmax=mrow[..., 0], Z=Z[..., 0], n=n[..., 0])
 
     g = {}
-    g["V"] = (attn * r).transpose(-1, -2) @ dX
-    dattn = (dX @ V.transpose(-1, -2)) * r
+    g["V"] = R(attn * r).transpose(-1, -2) @ R(dX)
+    dattn = (R(dX) @ R(V).transpose(-1, -2)) * r
     gamma = (dX * X).sum(-1, keepdim=True)
     big = (n >= EPS).double()
     dM = (dattn - big * (Mm > 0).double() * gamma) / Dn
@@ -120,8 +140,8 @@ def sbm_fwd_bwd(Q, K, V, mask, params, u, num_clusters, dX, dsparsity, attn_keep
     rho = (1 - big) * gamma
     ds = P * (dP - rho) / math.sqrt(d)
     ds = torch.nan_to_num(ds)  # pad keys: P == 0
-    dQ = ds @ K
-    dK = ds.transpose(-1, -2) @ Q
+    dQ = R(ds) @ R(K)
+    dK = R(ds).transpose(-1, -2) @ R(Q)
     dA = dM * P + (dsparsity / (B * N * M)).view(1, H, 1, 1)
     G = (A * dA).clamp(-1, 1)
     dQh = G @ T
@@ -130,13 +150,13 @@ def sbm_fwd_bwd(Q, K, V, mask, params, u, num_clusters, dX, dsparsity, attn_keep
     dS = torch.einsum("bhja,bhjc->hac", dT, Kh)
     dZq = dQh * Qh * (1 - Qh)
     dZk = dKh * Kh * (1 - Kh)
-    dQp = dZq @ C.unsqueeze(0)
-    dKp = dZk @ C.unsqueeze(0)
+    dQp = R(dZq) @ R(C).unsqueeze(0)
+    dKp = R(dZk) @ R(C).unsqueeze(0)
     dC = torch.einsum("bhnk,bhnd->hkd", dZq, Qp) + torch.einsum("bhnk,bhnd->hkd", dZk, Kp)
     dD = S * (dS - (S * dS).sum((-1, -2), keepdim=True))
     dC = dC + (dD + dD.transpose(-1, -2)) @ C
-    dQm, gq = _mlp_bwd(dQp, W, qacts, qmasks, (pk.get("q0"), pk.get("q1")))
-    dKm, gk = _mlp_bwd(dKp, W, kacts, kmasks, (pk.get("k0"), pk.get("k1")))
+    dQm, gq = _mlp_bwd(dQp, W, qacts, qmasks, (pk.get("q0"), pk.get("q1")), R)
+    dKm, gk = _mlp_bwd(dKp, W, kacts, kmasks, (pk.get("k0"), pk.get("k1")), R)
     g["Q"] = dQ + dQm
     g["K"] = dK + dKm
     g["layer.weight"] = dC.reshape(H * k, d)
