@@ -551,7 +551,8 @@ def main():
         mod.attn_precision = "fp32"
         out["bf16_mode"] = {"value": round(world * B * args.steps / el_bf, 1), "unit": "ASTs/s",
                             "ms_per_step": round(el_bf * 1000.0 / args.steps, 4),
-                            "note": "QK^T/PV/dP/dQ/dK/dV on bf16 MFMA; projection MLP, expA, sampling fp32"}
+                            "note": "QK^T/PV/dP/dQ/dK/dV, the projection MLP and sigmoid(.C^T) (fwd+bwd) on bf16 MFMA; "
+                                    "T = Kh S^T, expA, sampling and all elementwise fp32"}
     if not args.no_train:
         out["train"] = train_step_bench(world, rank, dev, args.train_steps, args.train_warmup)
         if world == 1:

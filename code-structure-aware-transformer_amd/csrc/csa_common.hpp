@@ -38,6 +38,12 @@ __device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 acc) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
 }
 
+// v_mfma_f32_16x16x4_f32 (exact fp32, 32 cycles/SIMD, the same rate per FLOP): lane l = (x16 = l & 15,
+// g = l >> 4) holds A[x16][k = g] / B[k = g][x16]; C/D register i holds D[4 g + i][x16].
+__device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 acc) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+}
+
 // bf16 mode (CSA_DTYPE_BF16): the N^2 contractions run on v_mfma_f32_32x32x16_bf16 (16x the f32 MFMA
 // rate, fp32 accumulation). One instruction takes 8 consecutive K-steps of the f32 chains above from
 // each lane (lane half h, element j <-> K-step 8 s + j), so a chain keeps its K permutation and both

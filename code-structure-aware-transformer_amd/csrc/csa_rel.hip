@@ -183,6 +183,7 @@ struct RelArgs {
   float *dk, *dv, *gc2p, *gp2ct, *qstat;
   const float *lq, *lk;
   int qstat_pre;  // qstat written by k_rel_qstat (concurrent backward): k_rel_bwd_qf leaves it alone
+  int LB16, Q4;   // 16-row bins (k_rel_bwd_qh / kh): row stride and the per-lane-group K range
 };
 
 __device__ __forceinline__ int64_t plane_off(const RelArgs& p, int b, int hd, int64_t sb, int64_t sh) {
@@ -917,14 +918,15 @@ __global__ __launch_bounds__(64, 1) void k_rel_bwd_qf(const RelArgs p) {
   bins_store_t(p.gc2p + ((int64_t)hd * p.B + b) * p.Lp * p.ldx, p.ldx, i, bins, p.LB, p.KB2, p.Lp, iv);
 }
 
-// Per-query (row max, 1/row sum, delta = rowsum(dO * O), 0) into qstat for k_rel_bwd_kf when it runs
-// beside k_rel_bwd_qf on a second stream (csa_rel_attn_bwd). Two lanes per row, each one half of the
-// row in k_rel_bwd_qf's order (sequential fma over 32 elements, then the halves added): the same delta
-// bit for bit. HBM-bound (2 x 256 B per row).
+// Per-query (row max, 1/row sum, delta = rowsum(dO * O), 0) into qstat for the key-side kernel when it runs
+// beside the query-side one on a second stream (csa_rel_attn_bwd). PARTS lanes per row, each a run of
+// 64 / PARTS elements in the query-side kernel's order (sequential fma, then the parts added pairwise:
+// PARTS = 2 for k_rel_bwd_qf, 4 for k_rel_bwd_qh): the same delta bit for bit. HBM-bound (2 x 256 B per row).
+template <int PARTS>
 __global__ __launch_bounds__(256) void k_rel_qstat(const RelArgs p) {
-  constexpr int NS = 32;
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x, row = t >> 1;
-  const int h = (int)(t & 1);
+  constexpr int NS = 64 / PARTS;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x, row = t / PARTS;
+  const int h = (int)(t % PARTS);
   const bool rv = row < (int64_t)p.B * p.H * p.N;
   const int64_t rc = rv ? row : 0;
   const int i = (int)(rc % p.N), bh = (int)(rc / p.N), b = bh / p.H, hd = bh % p.H;
@@ -934,7 +936,8 @@ __global__ __launch_bounds__(256) void k_rel_qstat(const RelArgs p) {
   float dp = 0.f;
 #pragma unroll
   for (int s = 0; s < NS; ++s) dp = fmaf(dO[s], o[s], dp);
-  const float delta = dp + __shfl_xor(dp, 1, 64);
+  float delta = dp + __shfl_xor(dp, 1, 64);
+  if constexpr (PARTS == 4) delta = delta + __shfl_xor(delta, 2, 64);
   if (rv && h == 0) {
     f32x4 st;
     st[0] = p.stats[rc * 2]; st[1] = p.stats[rc * 2 + 1]; st[2] = delta; st[3] = 0.f;
@@ -1080,6 +1083,355 @@ __global__ __launch_bounds__(64, 1) void k_rel_bwd_kf(const RelArgs p) {
     store_rows_f<DT>(p.dv + b * p.dv_sb + hd * p.dv_sh + (int64_t)j * p.dv_sn, dv);
   }
   bins_store_t(p.gp2ct + ((int64_t)hd * p.B + b) * p.Lp * p.ldx, p.ldx, j, bins, p.LB, p.KB2, p.Lp, jv);
+}
+
+// ------------------------------------------------------------------------------------
+// fp32 backward with 16-row waves (k_rel_bwd_qh / k_rel_bwd_kh). The 32-row kernels above hold 40 KB of
+// LDS per wave (K/V images 16 KB, bias tile 4 KB, bins 20 KB): one wave per SIMD, latency-bound. Here a
+// workgroup of two waves covers the same 32-row block: the two waves share the tile images and the bias
+// tile (each DMAs half of them), and each owns 16 rows and a 16-row bins table (~10 KB), so the workgroup
+// needs ~40 KB for two waves and a CU holds four: two waves per SIMD. The contractions run on the exact
+// fp32 v_mfma_f32_16x16x4_f32 (same FLOP rate as 32x32x2). Lane l = (x16 = l & 15, g = l >> 4):
+//   query side: S^T / dP^T tiles D[key 16 st + 4 g + i][query x16] (st = 0, 1: the two 16-key halves of
+//               a 32-key tile), dq^T[d][query] += K^T[d][key] g^T[key][query] (acc K-permutation);
+//   key side:   S / dP tiles D[query 16 st + 4 g + i][key x16], dv^T / dk^T[d][key] += X^T[d][query] (.).
+// A lane's 8 elements (st, i) of one tile sit at prepared-plane / bias-tile positions
+// pbase(g) + 8 st + i with pbase(g) = 16 (g & 1) + 4 (g >> 1) (= tile_pos(16 st + 4 g + i)): two 8-B code
+// loads and two 16-B bias reads per tile.
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ int pbase16(int g) { return 16 * (g & 1) + 4 * (g >> 1); }
+
+struct Codes8 { uint32_t w[4]; };
+// the lane's 8 codes (e = 4 st + i) of one tile from ITS OWN prepared row
+__device__ __forceinline__ Codes8 load_codes8(const uint16_t* __restrict__ row, int tile) {
+  const uint16_t* q = row + 32 * tile + pbase16(lane_id() >> 4);
+  const uint2 a = *reinterpret_cast<const uint2*>(q), b = *reinterpret_cast<const uint2*>(q + 8);
+  return Codes8{{a.x, a.y, b.x, b.y}};
+}
+__device__ __forceinline__ uint32_t code8(const Codes8& k, int e) { return (k.w[e >> 1] >> (16 * (e & 1))) & 0xffffu; }
+
+// byte offset of element (row, col) of a SW_BOTH / SW_ROW 32 x 64 image
+__device__ __forceinline__ int img_elem(int row, int col, const int sw) { return 256 * row + 16 * ((col >> 2) ^ swz(sw, row)) + 4 * (col & 3); }
+
+// 16-row bins (16 rows x LB floats, LB / 2 odd: the 16 rows of a b64 read hit distinct bank pairs) += g at
+// column rel; the four lane groups share the rows, so they add in four exec-masked passes, lanes of a pass
+// own distinct rows and a row's additions happen in a fixed order -> deterministic.
+__device__ __forceinline__ void bins_scatter16(float* bins, int LB, const float (&gv)[8], const uint32_t (&col)[8]) {
+  const int x16 = lane_id() & 15, g = lane_id() >> 4;
+  float* row = bins + x16 * LB;
+#pragma unroll
+  for (int pass = 0; pass < 4; ++pass) {
+    if (g == pass) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (gv[e] != 0.f) atomicAdd(row + col[e], gv[e]);
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this pass's adds land before the next pass's
+  }
+}
+
+// acc[t] (rows d = 16 t + 4 g + i, lanes = the bins' rows) += sum_r Lmat[r][d] bins[row][r] (dq_rel = G_c2p LK
+// or dk_rel = G_p2cT LQ). K-step s of lane group g is r = g Q4 + s (Q4 even, 4 Q4 >= L; rows >= L read 0); the
+// Lmat operand comes from L2 with a ring of RING groups of two K-steps in flight.
+__device__ __forceinline__ void bins_times16(f32x4 (&acc)[4], const float* bins, int LB, int Q4,
+                                             const float* __restrict__ Lmat, int L) {
+  constexpr int D = 64, RING = 8;
+  const int x16 = lane_id() & 15, g = lane_id() >> 4;
+  const float* brow = bins + x16 * LB + g * Q4;
+  auto lmat = [&](int s2, float (&v)[2][4]) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int r = g * Q4 + 2 * s2 + e;
+      const float* lr = Lmat + (int64_t)(r < L ? r : 0) * D;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const float lv = lr[16 * t + x16];
+        v[e][t] = r < L ? lv : 0.f;
+      }
+    }
+  };
+  auto group = [&](int s2, const float (&v)[2][4]) {
+    const float2 bv = *reinterpret_cast<const float2*>(brow + 2 * s2);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      acc[t] = mfma16(v[0][t], bv.x, acc[t]);
+      acc[t] = mfma16(v[1][t], bv.y, acc[t]);
+    }
+  };
+  const int ng = Q4 / 2, ngf = ng / RING * RING;
+  float lv[RING][2][4];
+#pragma unroll
+  for (int u = 0; u < RING - 1; ++u) lmat(u, lv[u]);
+  for (int g0 = 0; g0 < ngf; g0 += RING) {
+#pragma unroll
+    for (int u = 0; u < RING; ++u) {
+      lmat(g0 + u + RING - 1, lv[(u + RING - 1) % RING]);  // past the end: a clamped, never-used row
+      group(g0 + u, lv[u]);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < RING - 1; ++u)
+    if (ngf + u < ng) group(ngf + u, lv[u]);
+}
+
+// bins row of this lane (row x16, the group's columns [g Q4, g Q4 + Q4) clipped to Lp) -> column `row` of the
+// transposed (Lp, ldx) table (16 lanes of a group store 16 consecutive floats per bin)
+__device__ __forceinline__ void bins_store16(float* __restrict__ outT, int64_t ldx, int row, const float* bins, int LB,
+                                             int Q4, int Lp, bool valid) {
+  if (!valid) return;
+  const int x16 = lane_id() & 15, g = lane_id() >> 4;
+  const float* brow = bins + x16 * LB;
+  const int r1 = imin(g * Q4 + Q4, Lp);
+  for (int r = g * Q4; r < r1; ++r) outT[(int64_t)r * ldx + row] = brow[r];
+}
+
+// LDS of the 16-row kernels: images | (key side: 512 B of query stats) | 4 KB bias tile | 2 x 16-row bins
+__host__ __device__ constexpr int rel16_bins_off(bool key_side) { return 2 * 32 * 64 * 4 + (key_side ? 512 : 0) + 4096; }
+
+// Query side, 16-row waves: workgroup = (b,h, 32-query block), wave w = queries 16 w .. 16 w + 15.
+// Same algebra and outputs as k_rel_bwd_qf.
+__global__ __launch_bounds__(128, 2) void k_rel_bwd_qh(const RelArgs p) {
+  constexpr int D = 64, IMG = 32 * D * 4;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const uint32_t Kl = lds_offset(lds), Vl = Kl + IMG, Rl = Kl + 2 * IMG;
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int lane = lane_id(), x16 = lane & 15, g = lane >> 4;
+  float* bins = lds + rel16_bins_off(false) / 4 + w * 16 * p.LB16;
+  const BhBlock xb = xcd_block(p.NQB, p.B * p.H);
+  if (!xb.valid) return;  // whole workgroup
+  const int qb = xb.blk, bh = xb.bh, b = bh / p.H, hd = bh % p.H;
+  const int xr = 16 * w + x16, i = qb * 32 + xr;
+  const bool iv = i < p.N;
+  const int ic = imin(i, p.N - 1);
+  const int kld = (int)p.k_sn * 4, vld = (int)p.v_sn * 4;
+  const __amdgpu_buffer_rsrc_t kr = make_rsrc(p.k + b * p.k_sb + hd * p.k_sh, (p.N - 1) * kld + D * 4);
+  const __amdgpu_buffer_rsrc_t vr = make_rsrc(p.v + b * p.v_sb + hd * p.v_sh, (p.N - 1) * vld + D * 4);
+  const __amdgpu_buffer_rsrc_t rbr = make_rsrc(p.RB + ((int64_t)bh * p.NQB + qb) * p.NKB * 1024, p.NKB * 4096);
+  // rows past N are never fetched: the images hold zeros there (zeroed before any DMA can land)
+  for (int e = (int)threadIdx.x; e < 2 * IMG / 16; e += 128) reinterpret_cast<f32x4*>(lds)[e] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int e = lane; e < 16 * p.LB16; e += 64) bins[e] = 0.f;
+  __syncthreads();
+  const DmaPat kpat = dma_pat(SW_BOTH, kld), vpat = dma_pat(SW_ROW, vld);
+  const uint16_t* rmrow = prep_row(p, p.RM, b, hd, ic);
+  Codes8 cm = load_codes8(rmrow, 0);
+  float q[16], dO[16];
+  load_run<16>(q, p.q + b * p.q_sb + hd * p.q_sh + (int64_t)ic * p.q_sn + 16 * g, iv);
+  load_run<16>(dO, p.dout + b * p.do_sb + hd * p.do_sh + (int64_t)ic * p.do_sn + 16 * g, iv);
+  // wave w fetches rows 16 w .. 16 w + 15 of each image and half of the bias tile
+  dma64(Kl, kr, kpat, kld, 0, 4 * w, 4 * w + 4);
+  dma64(Vl, vr, vpat, vld, 0, 4 * w, 4 * w + 4);
+  dma_block16<2048>(Rl + 2048 * w, rbr, 2048 * w);
+  float dp = 0.f;
+  {
+    float o[16];
+    load_run<16>(o, p.out + b * p.o_sb + hd * p.o_sh + (int64_t)ic * p.o_sn + 16 * g, iv);
+#pragma unroll
+    for (int s = 0; s < 16; ++s) dp = fmaf(dO[s], o[s], dp);
+  }
+  const float dp2 = dp + __shfl_xor(dp, 16, 64);
+  const float delta = dp2 + __shfl_xor(dp2, 32, 64);  // (q0 + q1) + (q2 + q3): k_rel_qstat<4>'s order
+  const float rmax = p.stats[((int64_t)bh * p.N + ic) * 2];
+  const float rinv = p.stats[((int64_t)bh * p.N + ic) * 2 + 1];
+  f32x4 dq[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) dq[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int kt = 0; kt < p.NKB; ++kt) {
+    const int j0 = kt * 32;
+    wait_vm_all();
+    __syncthreads();  // both waves' pieces of tile kt landed
+    float gl[8];
+    uint32_t col[8];
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const f32x4 v = lds_f4(lds, 2 * IMG + 4 * rb_off(xr, pbase16(g) + 8 * st));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) gl[4 * st + e] = v[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) col[e] = code8(cm, e) & 0xffu;  // rel[x][y]: the c2p gather's column
+    f32x4 sacc[2], dpacc[2];
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      sacc[st] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dpacc[st] = sacc[st];
+      const int kk = 16 * st + x16;
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const f32x4 kv = lds_f4(lds, img_elem(kk, 16 * g + 4 * s4, SW_BOTH));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sacc[st] = mfma16(kv[e], q[4 * s4 + e], sacc[st]);
+      }
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const f32x4 vv = lds_f4(lds, IMG + img_elem(kk, 16 * g + 4 * s4, SW_ROW));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dpacc[st] = mfma16(vv[e], dO[4 * s4 + e], dpacc[st]);
+      }
+    }
+    float kT[4][8];  // A operands of dq: K[key 16 st + 4 g + i][d = 16 t + x16]
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) kT[t][e] = lds_f1(lds, img_elem(16 * (e >> 2) + 4 * g + (e & 3), 16 * t + x16, SW_BOTH));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();  // both waves read tile kt out: refill
+    if (kt + 1 < p.NKB) {
+      dma64(Kl, kr, kpat, kld, j0 + 32, 4 * w, 4 * w + 4);
+      dma64(Vl, vr, vpat, vld, j0 + 32, 4 * w, 4 * w + 4);
+      dma_block16<2048>(Rl + 2048 * w, rbr, (kt + 1) * 4096 + 2048 * w);
+      cm = load_codes8(rmrow, kt + 1);
+    }
+    float gv[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float sa = sacc[e >> 2][e & 3], dpa = dpacc[e >> 2][e & 3];
+      const bool inside = iv && (j0 + 16 * (e >> 2) + 4 * g + (e & 3) < p.N);
+      const bool msk = gl[e] == NEG_INF;
+      const float s = msk ? -1e9f : (sa + gl[e]) * p.inv_scale;
+      const float P = inside ? __expf(s - rmax) * rinv : 0.f;
+      gv[e] = (inside && !msk) ? P * (dpa - delta) * p.inv_scale : 0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) dq[t] = mfma16(kT[t][e], gv[e], dq[t]);
+    bins_scatter16(bins, p.LB16, gv, col);
+  }
+  bins_times16(dq, bins, p.LB16, p.Q4, p.lk + (int64_t)hd * p.L * D, p.L);
+  if (iv) {
+    float* dst = p.dq + b * p.dq_sb + hd * p.dq_sh + (int64_t)i * p.dq_sn + 4 * g;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) *reinterpret_cast<f32x4*>(dst + 16 * t) = dq[t];
+    if (g == 0 && !p.qstat_pre) {
+      f32x4 st;
+      st[0] = rmax; st[1] = rinv; st[2] = delta; st[3] = 0.f;
+      *reinterpret_cast<f32x4*>(p.qstat + ((int64_t)bh * p.N + i) * 4) = st;
+    }
+  }
+  bins_store16(p.gc2p + ((int64_t)hd * p.B + b) * p.Lp * p.ldx, p.ldx, i, bins, p.LB16, p.Q4, p.Lp, iv);
+}
+
+// Key side, 16-row waves: workgroup = (b,h, 32-key block), wave w = keys 16 w .. 16 w + 15. Same algebra and
+// outputs as k_rel_bwd_kf.
+__global__ __launch_bounds__(128, 2) void k_rel_bwd_kh(const RelArgs p) {
+  constexpr int D = 64, IMG = 32 * D * 4;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const uint32_t L0 = lds_offset(lds), Ql = L0, Xl = L0 + IMG, Sl = L0 + 2 * IMG, Rl = L0 + 2 * IMG + 512;
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int lane = lane_id(), x16 = lane & 15, g = lane >> 4;
+  float* bins = lds + rel16_bins_off(true) / 4 + w * 16 * p.LB16;
+  const BhBlock xb = xcd_block(p.NKB, p.B * p.H);
+  if (!xb.valid) return;
+  const int kbi = xb.blk, bh = xb.bh, b = bh / p.H, hd = bh % p.H;
+  const int yr = 16 * w + x16, j = kbi * 32 + yr;
+  const bool jv = j < p.N;
+  const int jc = imin(j, p.N - 1);
+  const int qld = (int)p.q_sn * 4, xld = (int)p.do_sn * 4;
+  const __amdgpu_buffer_rsrc_t qr_ = make_rsrc(p.q + b * p.q_sb + hd * p.q_sh, (p.N - 1) * qld + D * 4);
+  const __amdgpu_buffer_rsrc_t xr_ = make_rsrc(p.dout + b * p.do_sb + hd * p.do_sh, (p.N - 1) * xld + D * 4);
+  const __amdgpu_buffer_rsrc_t sr_ = make_rsrc(p.qstat + (int64_t)bh * p.N * 4, p.N * 16);
+  const __amdgpu_buffer_rsrc_t rbr = make_rsrc(p.RB + (int64_t)bh * p.NQB * p.NKB * 1024, p.NQB * p.NKB * 4096);
+  for (int e = (int)threadIdx.x; e < (2 * IMG + 512) / 16; e += 128)
+    reinterpret_cast<f32x4*>(lds)[e] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int e = lane; e < 16 * p.LB16; e += 64) bins[e] = 0.f;
+  __syncthreads();
+  const DmaPat qpat = dma_pat(SW_BOTH, qld), xpat = dma_pat(SW_BOTH, xld);
+  const uint16_t* rmrow = prep_row(p, p.RM, b, hd, jc);
+  Codes8 cm = load_codes8(rmrow, 0);
+  float kr[16], vr[16];
+  load_run<16>(kr, p.k + b * p.k_sb + hd * p.k_sh + (int64_t)jc * p.k_sn + 16 * g, jv);
+  load_run<16>(vr, p.v + b * p.v_sb + hd * p.v_sh + (int64_t)jc * p.v_sn + 16 * g, jv);
+  dma64(Ql, qr_, qpat, qld, 0, 4 * w, 4 * w + 4);
+  dma64(Xl, xr_, xpat, xld, 0, 4 * w, 4 * w + 4);
+  dma_tile_contig<4>(Sl, sr_, 0, w, w + 1);
+  dma_block16<2048>(Rl + 2048 * w, rbr, kbi * 4096 + 2048 * w);
+  const int ypos = tile_pos(yr);
+  f32x4 dv[4], dk[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) { dv[t] = f32x4{0.f, 0.f, 0.f, 0.f}; dk[t] = dv[t]; }
+  for (int qb = 0; qb < p.NQB; ++qb) {
+    const int i0 = qb * 32;
+    wait_vm_all();
+    __syncthreads();
+    float gl[8], rm[8], ri[8], dl[8];
+    uint32_t col[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int x = 16 * (e >> 2) + 4 * g + (e & 3);  // query of element e in the tile
+      gl[e] = lds_f1(lds, 2 * IMG + 512 + 4 * rb_off(x, ypos));
+      const f32x4 st = lds_f4(lds, 2 * IMG + 16 * x);
+      rm[e] = st[0]; ri[e] = st[1]; dl[e] = st[2];
+      col[e] = code8(cm, e) & 0xffu;  // rel[y][x]: the p2c gather's column
+    }
+    f32x4 sacc[2], dpacc[2];
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      sacc[st] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dpacc[st] = sacc[st];
+      const int xx = 16 * st + x16;
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const f32x4 qv = lds_f4(lds, img_elem(xx, 16 * g + 4 * s4, SW_BOTH));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sacc[st] = mfma16(qv[e], kr[4 * s4 + e], sacc[st]);
+      }
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const f32x4 xv = lds_f4(lds, IMG + img_elem(xx, 16 * g + 4 * s4, SW_BOTH));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dpacc[st] = mfma16(xv[e], vr[4 * s4 + e], dpacc[st]);
+      }
+    }
+    // elementwise first: the bias / statistics registers die before the column operands are read
+    float Pv[8], gv[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float sa = sacc[e >> 2][e & 3], dpa = dpacc[e >> 2][e & 3];
+      const bool inside = (i0 + 16 * (e >> 2) + 4 * g + (e & 3) < p.N) && jv;
+      const bool msk = gl[e] == NEG_INF;
+      const float s = msk ? -1e9f : (sa + gl[e]) * p.inv_scale;
+      const float P = inside ? __expf(s - rm[e]) * ri[e] : 0.f;
+      Pv[e] = P;
+      gv[e] = (inside && !msk) ? P * (dpa - dl[e]) * p.inv_scale : 0.f;
+    }
+    float xc[4][8], qc[4][8];  // A operands of dv / dk: X[query 16 st + 4 g + i][d = 16 t + x16]
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int off = img_elem(16 * (e >> 2) + 4 * g + (e & 3), 16 * t + x16, SW_BOTH);
+        xc[t][e] = lds_f1(lds, IMG + off);
+        qc[t][e] = lds_f1(lds, off);
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (qb + 1 < p.NQB) {
+      dma64(Ql, qr_, qpat, qld, i0 + 32, 4 * w, 4 * w + 4);
+      dma64(Xl, xr_, xpat, xld, i0 + 32, 4 * w, 4 * w + 4);
+      dma_tile_contig<4>(Sl, sr_, i0 + 32, w, w + 1);
+      dma_block16<2048>(Rl + 2048 * w, rbr, ((qb + 1) * p.NKB + kbi) * 4096 + 2048 * w);
+      cm = load_codes8(rmrow, qb + 1);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        dv[t] = mfma16(xc[t][e], Pv[e], dv[t]);
+        dk[t] = mfma16(qc[t][e], gv[e], dk[t]);
+      }
+    bins_scatter16(bins, p.LB16, gv, col);
+  }
+  bins_times16(dk, bins, p.LB16, p.Q4, p.lq + (int64_t)hd * p.L * D, p.L);
+  if (jv) {
+    float* dkp = p.dk + b * p.dk_sb + hd * p.dk_sh + (int64_t)j * p.dk_sn + 4 * g;
+    float* dvp = p.dv + b * p.dv_sb + hd * p.dv_sh + (int64_t)j * p.dv_sn + 4 * g;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      *reinterpret_cast<f32x4*>(dkp + 16 * t) = dk[t];
+      *reinterpret_cast<f32x4*>(dvp + 16 * t) = dv[t];
+    }
+  }
+  bins_store16(p.gp2ct + ((int64_t)hd * p.B + b) * p.Lp * p.ldx, p.ldx, j, bins, p.LB16, p.Q4, p.Lp, jv);
 }
 
 // Relation-embedding gradients of the fused path, split over the batch (deterministic):
@@ -1293,11 +1645,24 @@ RelArgs make_rel(const csa_rel_attn_args* a, const RelLayout& R) {
     p.ldx = R.ldx;
     p.KB2 = (int)(((a->L + 7) / 8) * 4);  // bins K loop: 2 KB2 >= L, KB2 a multiple of 4
     p.LB = 2 * p.KB2 + (((2 * p.KB2 / 4) % 2 == 0) ? 4 : 0);  // LB / 4 odd (conflict-free b128 rows)
+    p.Q4 = (int)(((a->L + 7) / 8) * 2);  // 16-row bins: 4 Q4 >= L, Q4 even (b64 reads)
+    p.LB16 = 4 * p.Q4 + 2;               // LB16 / 2 odd (conflict-free b64 rows)
   }
   return p;
 }
 
 size_t bins_lds_bytes(const RelArgs& p) { return sizeof(float) * 32 * (size_t)p.LB; }
+size_t bins16_lds_bytes(const RelArgs& p) { return sizeof(float) * 2 * 16 * (size_t)p.LB16; }
+
+// fp32 backward on the 16-row kernels (two waves per SIMD); bf16 mode keeps the 32-row kernels.
+// CSA_EXP_REL32: experiment build that keeps the 32-row fp32 kernels (DESIGN.md §3 CSE A/B).
+inline bool rel_use16(const RelArgs& p) {
+#ifdef CSA_EXP_REL32
+  return false;
+#else
+  return !p.bf16;
+#endif
+}
 
 // relation logits: C2P[b,h] = Q LK_h^T (N x L), P2CT[b,h] = K LQ_h^T (N x L)
 void rel_logits(const csa_rel_attn_args* a, const RelLayout& R, hipStream_t st) {
@@ -1441,32 +1806,47 @@ csa_status csa_rel_attn_bwd(const csa_rel_attn_bwd_args* b, void* stream) {
   if (R.fused) {
     p.dk = b->dk; p.dv = b->dv; p.gc2p = gc2p; p.gp2ct = gp2ct;
     p.qstat = (float*)((char*)ws + R.qstat);
-    const size_t lq_bytes = 2 * 32 * 64 * 4 + 4096 + bins_lds_bytes(p);
-    const size_t lk_bytes = 2 * 32 * 64 * 4 + 512 + 4096 + bins_lds_bytes(p);
-    const dim3 gq(xcd_grid(p.NQB, B * H)), gk(xcd_grid(p.NKB, B * H));
+    const bool w16 = rel_use16(p);
+    const size_t lq_bytes = w16 ? rel16_bins_off(false) + bins16_lds_bytes(p) : 2 * 32 * 64 * 4 + 4096 + bins_lds_bytes(p);
+    const size_t lk_bytes = w16 ? rel16_bins_off(true) + bins16_lds_bytes(p) : 2 * 32 * 64 * 4 + 512 + 4096 + bins_lds_bytes(p);
+    const dim3 gq(xcd_grid(p.NQB, B * H)), gk(xcd_grid(p.NKB, B * H)), blk(w16 ? 128 : 64);
     const bool concur = b->side_stream && b->side_fork && b->side_join &&
                         bwd_concurrent(b->schedule, b->side_stream, stream_device(st), (int64_t)p.NQB * B * H, 1);
     const SideLane lane{(hipStream_t)b->side_stream, (hipEvent_t)b->side_fork, (hipEvent_t)b->side_join};
     const SideLane* side = concur ? &lane : nullptr;
-    if (side) {  // fork: row statistics + bwd_kf on the side stream, bwd_qf here, join before the lgrad
+    auto launch_q = [&](hipStream_t s_) {
+      if (w16) {
+        set_dyn_lds((const void*)k_rel_bwd_qh, (int)lq_bytes);
+        hipLaunchKernelGGL(k_rel_bwd_qh, gq, blk, lq_bytes, s_, p);
+      } else if (p.bf16) {
+        hipLaunchKernelGGL((k_rel_bwd_qf<64, true>), gq, blk, lq_bytes, s_, p);
+      } else {
+        hipLaunchKernelGGL((k_rel_bwd_qf<64, false>), gq, blk, lq_bytes, s_, p);
+      }
+    };
+    auto launch_k = [&](hipStream_t s_) {
+      if (w16) {
+        set_dyn_lds((const void*)k_rel_bwd_kh, (int)lk_bytes);
+        hipLaunchKernelGGL(k_rel_bwd_kh, gk, blk, lk_bytes, s_, p);
+      } else if (p.bf16) {
+        hipLaunchKernelGGL((k_rel_bwd_kf<64, true>), gk, blk, lk_bytes, s_, p);
+      } else {
+        hipLaunchKernelGGL((k_rel_bwd_kf<64, false>), gk, blk, lk_bytes, s_, p);
+      }
+    };
+    if (side) {  // fork: row statistics + key side on the side stream, query side here, join before the lgrad
       if (!side->fork(st)) return rfail_hip("csa_rel_attn_bwd: side-stream fork");
       p.qstat_pre = 1;
-      const int64_t threads = 2LL * B * H * N;
-      hipLaunchKernelGGL(k_rel_qstat, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, side->s, p);
-      if (p.bf16) {
-        hipLaunchKernelGGL((k_rel_bwd_kf<64, true>), gk, dim3(64), lk_bytes, side->s, p);
-        hipLaunchKernelGGL((k_rel_bwd_qf<64, true>), gq, dim3(64), lq_bytes, st, p);
-      } else {
-        hipLaunchKernelGGL((k_rel_bwd_kf<64, false>), gk, dim3(64), lk_bytes, side->s, p);
-        hipLaunchKernelGGL((k_rel_bwd_qf<64, false>), gq, dim3(64), lq_bytes, st, p);
-      }
+      const int parts = w16 ? 4 : 2;
+      const int64_t threads = (int64_t)parts * B * H * N;
+      if (w16) hipLaunchKernelGGL(k_rel_qstat<4>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, side->s, p);
+      else hipLaunchKernelGGL(k_rel_qstat<2>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, side->s, p);
+      launch_k(side->s);
+      launch_q(st);
       if (!side->join(st)) return rfail_hip("csa_rel_attn_bwd: side-stream join");
-    } else if (p.bf16) {
-      hipLaunchKernelGGL((k_rel_bwd_qf<64, true>), gq, dim3(64), lq_bytes, st, p);
-      hipLaunchKernelGGL((k_rel_bwd_kf<64, true>), gk, dim3(64), lk_bytes, st, p);
     } else {
-      hipLaunchKernelGGL((k_rel_bwd_qf<64, false>), gq, dim3(64), lq_bytes, st, p);
-      hipLaunchKernelGGL((k_rel_bwd_kf<64, false>), gk, dim3(64), lk_bytes, st, p);
+      launch_q(st);
+      launch_k(st);
     }
     rel_param_grads(a, b, R, gc2p, gp2ct, st);
     return rcheck("csa_rel_attn_bwd");

@@ -597,6 +597,9 @@ __device__ __forceinline__ void proj_fwd_item(const KArgs& p, const FwdFrags& F,
     float* blk = p.Act + ((int64_t)bh * (p.NQB + p.NKB) + r) * ABLK;
     store_act_lds<D / 32>(blk, h1, scr);
     store_act_lds<D / 32>(blk + 32 * D, h2, scr);
+#ifdef CSA_EXP_RECOMP_PO  // experiment: k_proj_bwd_s<64> recomputes po from h2
+    if (!(D == 64 && KT == 1 && p.kp <= 16))
+#endif
     store_act_lds<D / 32>(blk + 64 * D, po, scr);
     bool hat16 = false;
     if constexpr (KT == 1) {
@@ -805,6 +808,9 @@ __device__ __forceinline__ void key_bias_store(float* bias, const KArgs& p, int 
 // uniforms u16 / 65536 (STE.py:13 draws u < p with p = clamp(expA, .01, .99)).
 template <int D, int KPH, bool DENSE, bool HAS_U, bool DROP, bool BF>
 __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd(const KArgs p) {
+#ifdef CSA_EXP_PRIO  // experiment: half of the waves (by dispatch slot parity) at priority 1
+  if ((blockIdx.x >> 3) & 1) __builtin_amdgcn_s_setprio(1);
+#endif
   using LY = AttnFwdLds<D, KPH>;
   constexpr int DT = D / 32, NS = D / 2, DP = LY::DP, KP = LY::KP;
   constexpr bool SWZ = LY::SWZ;
@@ -1221,6 +1227,9 @@ struct AttnBwdShape {
 // DG: an upstream gradient of the graph and / or attn output is present (p.dgraph, p.dattn)
 template <int D, int KPH, bool DENSE, bool DROP, bool DG, bool BF>
 __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd_q(const KArgs p) {
+#ifdef CSA_EXP_PRIO  // experiment: half of the waves (by dispatch slot parity) at priority 1
+  if ((blockIdx.x >> 3) & 1) __builtin_amdgcn_s_setprio(1);
+#endif
   using SH = AttnBwdShape<D, KPH>;
   constexpr int DT = D / 32, NS = D / 2, DP = SH::DP, KP = SH::KP, KPN = SH::KPN, KTA = SH::KTA;
   constexpr bool SWZ = SH::SWZ;
@@ -1406,6 +1415,9 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
 // ------------------------------------------------------------------------------------
 template <int D, int KPH, bool DENSE, bool DROP, bool DG, bool BF>
 __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd_kv(const KArgs p) {
+#ifdef CSA_EXP_PRIO  // experiment: half of the waves (by dispatch slot parity) at priority 1
+  if ((blockIdx.x >> 3) & 1) __builtin_amdgcn_s_setprio(1);
+#endif
   using SH = AttnBwdShape<D, KPH>;
   constexpr int DT = D / 32, NS = D / 2, DP = SH::DP, KP = SH::KP, KPN = SH::KPN, KTA = SH::KTA;
   constexpr bool SWZ = SH::SWZ;
@@ -1994,10 +2006,6 @@ __global__ __launch_bounds__(256, (D <= 64 && KT <= 1 ? 2 : 1)) void k_proj_bwd(
   }
 }
 
-__device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 acc) {
-  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
-}
-
 // ------------------------------------------------------------------------------------
 // B3s: projection backward for k <= 16 clusters and d = 64 or 96 (config/python.py and config/java.py).
 // Same math and slab layout as k_proj_bwd. Differences:
@@ -2221,7 +2229,11 @@ __global__ __launch_bounds__(256, ProjBwdSmallShape<D>::LCS ? 1 : 2) void k_proj
     if constexpr (LW) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D * D / 1024) : "memory");
     else wait_vm_all();
     PHASE(0);
+#ifdef CSA_EXP_RECOMP_PO
+    dma_block16<D * 128>(INl, ar, (D == 64 ? 32 : 64) * D * 4);  // experiment: h2 (po is recomputed from it)
+#else
     dma_block16<D * 128>(INl, ar, 64 * D * 4);  // po -> own IN region (free since B6), lands under dS / dZ / dp
+#endif
     f32x16 gin[1];
     float dTt[8];
 #pragma unroll
@@ -2266,6 +2278,15 @@ __global__ __launch_bounds__(256, ProjBwdSmallShape<D>::LCS ? 1 : 2) void k_proj
     f32x16 dcur[DT];
     mm_acc_f<DT, 1, 2, LCS ? 8 : 16, LCS, BF>(LCS ? CFs : CfT, dz, dcur);
     wait_vm_all();  // po (LW: and the W2 fragments)
+#ifdef CSA_EXP_RECOMP_PO
+    if constexpr (D == 64) {  // po = W2 h2 + b2: the forward's own chain (L2 fragments), bit-identical
+      f32x16 h2v[DT], pov[DT];
+      read_act<DT>(h2v, INw, ln);
+      mlp_layer<D, false, BF>(p.Wf[2], p.pb[2], h2v, pov);
+      stage_ds<DT>(INw, pov, D, ln);  // same wave: its LDS reads above complete before these writes
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+#endif
     // ---- dC_h += dZ^T po, private 16x16x4: A = dZ[row 4s + g4][cluster c16], B = po[row 4s + g4][16t + c16]
 #pragma unroll
     for (int s = 0; s < 8; ++s) {

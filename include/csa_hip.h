@@ -67,9 +67,10 @@ typedef enum csa_status {
 /* operand precision of the N^2 attention contractions (dtype field of the args structs). Storage is
  * fp32 either way. CSA_DTYPE_F32 is the reference's precision (sbm_attn.py:120-126 forces fp32) and
  * the parity mode (rtol 1e-4 / atol 1e-5). CSA_DTYPE_BF16 rounds the operands of QK^T, dX V^T, PV, dQ,
- * dK, dV (SBM) and of the CSE's c2c, PV and their gradients to bf16 for v_mfma_f32_32x32x16_bf16
- * (fp32 accumulation; north_star tolerance 2e-2). The cluster projection, expA (so the sampled graph)
- * and every softmax / normalisation stay fp32. */
+ * dK, dV, of the projection MLP (three d x d layers, forward and backward chains and weight-gradient
+ * products) and of sigmoid(. C^T) and its backward (SBM), and of the CSE's c2c, PV and their gradients
+ * to bf16 for v_mfma_f32_32x32x16_bf16 (fp32 accumulation; north_star tolerance 2e-2). T = Kh S^T, expA,
+ * the sampling threshold and every softmax / normalisation / elementwise step stay fp32. */
 #define CSA_DTYPE_F32 0
 #define CSA_DTYPE_BF16 1
 
