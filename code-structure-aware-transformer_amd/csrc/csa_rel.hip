@@ -1115,7 +1115,8 @@ __device__ __forceinline__ int img_elem(int row, int col, const int sw) { return
 
 // 16-row bins (16 rows x LB floats, LB / 2 odd: the 16 rows of a b64 read hit distinct bank pairs) += g at
 // column rel; the four lane groups share the rows, so they add in four exec-masked passes, lanes of a pass
-// own distinct rows and a row's additions happen in a fixed order -> deterministic.
+// own distinct rows and a row's additions happen in a fixed order -> deterministic. An element whose g is
+// zero in every lane of the pass (masked relations: most of the matrix) skips its add.
 __device__ __forceinline__ void bins_scatter16(float* bins, int LB, const float (&gv)[8], const uint32_t (&col)[8]) {
   const int x16 = lane_id() & 15, g = lane_id() >> 4;
   float* row = bins + x16 * LB;
@@ -1126,7 +1127,11 @@ __device__ __forceinline__ void bins_scatter16(float* bins, int LB, const float 
       for (int e = 0; e < 8; ++e)
         if (gv[e] != 0.f) atomicAdd(row + col[e], gv[e]);
     }
+#ifdef CSA_EXP_NOPASSWAIT
+    asm volatile("" ::: "memory");  // keeps the passes apart (the compiler would merge them into one)
+#else
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this pass's adds land before the next pass's
+#endif
   }
 }
 
@@ -1235,10 +1240,18 @@ __global__ __launch_bounds__(128, 2) void k_rel_bwd_qh(const RelArgs p) {
   f32x4 dq[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) dq[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // CSA_EXP_DEFER (experiment): the bins scatter of tile kt at the top of iteration kt + 1, after the wait for
+  // tile kt + 1's DMA (the compiler orders every LDS access behind the LDS-DMAs in flight, so the scatter
+  // right after the refill waits for it); measured slower (DESIGN.md §3 CSE A/B)
+  float gsv[8];
+  uint32_t csv[8];
   for (int kt = 0; kt < p.NKB; ++kt) {
     const int j0 = kt * 32;
     wait_vm_all();
     __syncthreads();  // both waves' pieces of tile kt landed
+#ifdef CSA_EXP_DEFER
+    if (kt > 0) bins_scatter16(bins, p.LB16, gsv, csv);
+#endif
     float gl[8];
     uint32_t col[8];
 #pragma unroll
@@ -1249,24 +1262,33 @@ __global__ __launch_bounds__(128, 2) void k_rel_bwd_qh(const RelArgs p) {
     }
 #pragma unroll
     for (int e = 0; e < 8; ++e) col[e] = code8(cm, e) & 0xffu;  // rel[x][y]: the c2p gather's column
+    // the four chains (S^T, dP^T of both key halves) interleaved: a 16x16x4 result feeds its own chain
+    // after 40 cycles, its issue slot is 32, so one chain alone would run at 80% of the pipe rate
     f32x4 sacc[2], dpacc[2];
 #pragma unroll
-    for (int st = 0; st < 2; ++st) {
-      sacc[st] = f32x4{0.f, 0.f, 0.f, 0.f};
-      dpacc[st] = sacc[st];
-      const int kk = 16 * st + x16;
+    for (int st = 0; st < 2; ++st) { sacc[st] = f32x4{0.f, 0.f, 0.f, 0.f}; dpacc[st] = sacc[st]; }
+    f32x4 kv[2][2], vv[2][2];  // operand groups, one K-group of reads ahead of the MFMAs
+    auto rd = [&](int s4, f32x4 (&kd)[2], f32x4 (&vd)[2]) {
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) {
-        const f32x4 kv = lds_f4(lds, img_elem(kk, 16 * g + 4 * s4, SW_BOTH));
-#pragma unroll
-        for (int e = 0; e < 4; ++e) sacc[st] = mfma16(kv[e], q[4 * s4 + e], sacc[st]);
+      for (int st = 0; st < 2; ++st) {
+        kd[st] = lds_f4(lds, img_elem(16 * st + x16, 16 * g + 4 * s4, SW_BOTH));
+        vd[st] = lds_f4(lds, IMG + img_elem(16 * st + x16, 16 * g + 4 * s4, SW_ROW));
       }
+    };
+    rd(0, kv[0], vv[0]);
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) {
-        const f32x4 vv = lds_f4(lds, IMG + img_elem(kk, 16 * g + 4 * s4, SW_ROW));
+    for (int s4 = 0; s4 < 4; ++s4) {
+      if (s4 + 1 < 4) rd(s4 + 1, kv[(s4 + 1) & 1], vv[(s4 + 1) & 1]);
+#ifndef CSA_EXP_NOSB
+      __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead of this group's MFMAs
+#endif
 #pragma unroll
-        for (int e = 0; e < 4; ++e) dpacc[st] = mfma16(vv[e], dO[4 * s4 + e], dpacc[st]);
-      }
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          sacc[st] = mfma16(kv[s4 & 1][st][e], q[4 * s4 + e], sacc[st]);
+          dpacc[st] = mfma16(vv[s4 & 1][st][e], dO[4 * s4 + e], dpacc[st]);
+        }
     }
     float kT[4][8];  // A operands of dq: K[key 16 st + 4 g + i][d = 16 t + x16]
 #pragma unroll
@@ -1295,8 +1317,15 @@ __global__ __launch_bounds__(128, 2) void k_rel_bwd_qh(const RelArgs p) {
     for (int e = 0; e < 8; ++e)
 #pragma unroll
       for (int t = 0; t < 4; ++t) dq[t] = mfma16(kT[t][e], gv[e], dq[t]);
+#ifndef CSA_EXP_DEFER
     bins_scatter16(bins, p.LB16, gv, col);
   }
+#else
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { gsv[e] = gv[e]; csv[e] = col[e]; }
+  }
+  bins_scatter16(bins, p.LB16, gsv, csv);
+#endif
   bins_times16(dq, bins, p.LB16, p.Q4, p.lk + (int64_t)hd * p.L * D, p.L);
   if (iv) {
     float* dst = p.dq + b * p.dq_sb + hd * p.dq_sh + (int64_t)i * p.dq_sn + 4 * g;
@@ -1349,10 +1378,15 @@ __global__ __launch_bounds__(128, 2) void k_rel_bwd_kh(const RelArgs p) {
   f32x4 dv[4], dk[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) { dv[t] = f32x4{0.f, 0.f, 0.f, 0.f}; dk[t] = dv[t]; }
+  float gsv[8];  // deferred bins scatter (see k_rel_bwd_qh)
+  uint32_t csv[8];
   for (int qb = 0; qb < p.NQB; ++qb) {
     const int i0 = qb * 32;
     wait_vm_all();
     __syncthreads();
+#ifdef CSA_EXP_DEFER
+    if (qb > 0) bins_scatter16(bins, p.LB16, gsv, csv);
+#endif
     float gl[8], rm[8], ri[8], dl[8];
     uint32_t col[8];
 #pragma unroll
@@ -1363,24 +1397,31 @@ __global__ __launch_bounds__(128, 2) void k_rel_bwd_kh(const RelArgs p) {
       rm[e] = st[0]; ri[e] = st[1]; dl[e] = st[2];
       col[e] = code8(cm, e) & 0xffu;  // rel[y][x]: the p2c gather's column
     }
-    f32x4 sacc[2], dpacc[2];
+    f32x4 sacc[2], dpacc[2];  // four interleaved chains (see k_rel_bwd_qh)
 #pragma unroll
-    for (int st = 0; st < 2; ++st) {
-      sacc[st] = f32x4{0.f, 0.f, 0.f, 0.f};
-      dpacc[st] = sacc[st];
-      const int xx = 16 * st + x16;
+    for (int st = 0; st < 2; ++st) { sacc[st] = f32x4{0.f, 0.f, 0.f, 0.f}; dpacc[st] = sacc[st]; }
+    f32x4 qv[2][2], xv[2][2];
+    auto rd = [&](int s4, f32x4 (&qd)[2], f32x4 (&xd)[2]) {
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) {
-        const f32x4 qv = lds_f4(lds, img_elem(xx, 16 * g + 4 * s4, SW_BOTH));
-#pragma unroll
-        for (int e = 0; e < 4; ++e) sacc[st] = mfma16(qv[e], kr[4 * s4 + e], sacc[st]);
+      for (int st = 0; st < 2; ++st) {
+        qd[st] = lds_f4(lds, img_elem(16 * st + x16, 16 * g + 4 * s4, SW_BOTH));
+        xd[st] = lds_f4(lds, IMG + img_elem(16 * st + x16, 16 * g + 4 * s4, SW_BOTH));
       }
+    };
+    rd(0, qv[0], xv[0]);
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) {
-        const f32x4 xv = lds_f4(lds, IMG + img_elem(xx, 16 * g + 4 * s4, SW_BOTH));
+    for (int s4 = 0; s4 < 4; ++s4) {
+      if (s4 + 1 < 4) rd(s4 + 1, qv[(s4 + 1) & 1], xv[(s4 + 1) & 1]);
+#ifndef CSA_EXP_NOSB
+      __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
-        for (int e = 0; e < 4; ++e) dpacc[st] = mfma16(xv[e], vr[4 * s4 + e], dpacc[st]);
-      }
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          sacc[st] = mfma16(qv[s4 & 1][st][e], kr[4 * s4 + e], sacc[st]);
+          dpacc[st] = mfma16(xv[s4 & 1][st][e], vr[4 * s4 + e], dpacc[st]);
+        }
     }
     // elementwise first: the bias / statistics registers die before the column operands are read
     float Pv[8], gv[8];
@@ -1419,8 +1460,15 @@ __global__ __launch_bounds__(128, 2) void k_rel_bwd_kh(const RelArgs p) {
         dv[t] = mfma16(xc[t][e], Pv[e], dv[t]);
         dk[t] = mfma16(qc[t][e], gv[e], dk[t]);
       }
+#ifndef CSA_EXP_DEFER
     bins_scatter16(bins, p.LB16, gv, col);
   }
+#else
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { gsv[e] = gv[e]; csv[e] = col[e]; }
+  }
+  bins_scatter16(bins, p.LB16, gsv, csv);
+#endif
   bins_times16(dk, bins, p.LB16, p.Q4, p.lq + (int64_t)hd * p.L * D, p.L);
   if (jv) {
     float* dkp = p.dk + b * p.dk_sb + hd * p.dk_sh + (int64_t)j * p.dk_sn + 4 * g;
