@@ -103,13 +103,25 @@ def host_cpu_info():
     return info
 
 
+def progress(msg):
+    """One stderr line per bench leg, so a long default run is never silent for minutes."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def pick_threads(step, info):
     """Thread count for a CPU leg: os.cpu_count() as SURVEY 8(d) asks, unless the process is held to fewer
-    CPUs (affinity, cgroup quota, or the OMP_NUM_THREADS share the GPU box exports: 16) -- then both counts
-    are tried on one step and the faster is used (oversubscribing a share only slows the baseline down)."""
-    cands = {info["machine_logical_cpus"] or 1}
-    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)  # the box exports its CPU share here (16)
-    held = min(x for x in (info["affinity_cpus"], info["cgroup_cpu_quota"], omp, info["machine_logical_cpus"]) if x)
+    CPUs by a cgroup CPU quota (the GPU box: os.cpu_count() = 256, quota 16): then the quota. Oversubscribing
+    a quota only slows the baseline down -- measured on the box, one reduced-batch trial step took 0.06 s on
+    16 threads and 18.8 s on 256 (SBM oracle), 0.24 s vs 104 s (CSATrans oracle): profiles/r03_bench_v1.json.
+    Held by affinity or OMP_NUM_THREADS only (no quota): both counts are tried on one small trial step
+    (`step`) and the faster is used."""
+    machine = info["machine_logical_cpus"] or 1
+    quota = info["cgroup_cpu_quota"]
+    if quota and quota < machine:
+        return max(1, int(quota)), {"thread_choice": f"cgroup CPU quota {quota:g} of {machine} logical CPUs"}
+    cands = {machine}
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    held = min(x for x in (info["affinity_cpus"], omp, machine) if x)
     cands.add(max(1, int(held)))
     if len(cands) == 1:
         return cands.pop(), {}
@@ -138,15 +150,16 @@ def cpu_baseline(seconds, B=256, H=8, N=150, d=64, k=10):
     dX = torch.randn(B, H, N, d, generator=g)
     dsp = torch.full((H,), 3.125e-4)
 
-    def step():
-        u = torch.rand(B, H, N, N)  # == torch.bernoulli's draws
-        keep = (torch.rand(B, H, N, N) >= 0.2).float() / 0.8
-        pk = {n: (torch.rand(B, H, N, d) >= 0.2).float() / 0.8 for n in ("q0", "q1", "k0", "k1")}
-        X, sp, graph, attn = sbm_ref.sbm_attention(Q, K, V, mask, params, u, k, attn_keep=keep, proj_keep=pk)
-        torch.autograd.backward([X, sp], [dX, dsp])
+    def step(nb=B):
+        u = torch.rand(nb, H, N, N)  # == torch.bernoulli's draws
+        keep = (torch.rand(nb, H, N, N) >= 0.2).float() / 0.8
+        pk = {n: (torch.rand(nb, H, N, d) >= 0.2).float() / 0.8 for n in ("q0", "q1", "k0", "k1")}
+        X, sp, graph, attn = sbm_ref.sbm_attention(Q[:nb], K[:nb], V[:nb], mask[:nb], params, u, k, attn_keep=keep,
+                                                   proj_keep=pk)
+        torch.autograd.backward([X, sp], [dX[:nb], dsp])
 
-    step()  # warm-up (allocator, thread pool)
-    threads, trial = pick_threads(step, info)
+    step(min(B, 4))  # warm-up (allocator, thread pool)
+    threads, trial = pick_threads(lambda: step(min(B, 8)), info)
     torch.set_num_threads(threads)
     n, t0 = 0, time.perf_counter()
     while True:
@@ -199,8 +212,12 @@ def cpu_config1(reps=5, B=32, N=150):
         out, sp = model.forward(*args)
         (csatrans_ref.label_smoothing(out, tgt) + 1e-2 * sp).backward()
 
-    fwd()  # warm-up
-    threads, trial = pick_threads(fwd, info)
+    def fwd_small():  # thread-count trial on 4 of the batch's ASTs
+        with torch.no_grad():
+            model.forward(*(a[:4] for a in args))
+
+    fwd_small()  # warm-up
+    threads, trial = pick_threads(fwd_small, info)
     torch.set_num_threads(threads)
     res = {}
     for name, fn in (("fwd_no_grad", fwd), ("fwd_bwd_out_mean", fwd_bwd_mean), ("loss_sparsity_fwd_bwd", train_loss)):
@@ -435,6 +452,7 @@ def main():
         else:
             torch.autograd.backward([X, sp], [dX, dsp])
 
+    progress(f"SBM layer B={B} N={N} d={d} k={k}: warm-up")
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -544,6 +562,7 @@ def main():
     }
     if args.precision == "fp32" and not args.no_bf16_leg and not args.dense and N <= 150:
         # the same layer with CSA_DTYPE_BF16 (north_star's bf16 variant): side measurement, same step
+        progress("bf16-mode leg")
         mod.attn_precision = "bf16"
         for _ in range(args.warmup):
             step()
@@ -554,6 +573,7 @@ def main():
                             "note": "QK^T/PV/dP/dQ/dK/dV, the projection MLP and sigmoid(.C^T) (fwd+bwd) on bf16 MFMA; "
                                     "T = Kh S^T, expA, sampling and all elementwise fp32"}
     if not args.no_train:
+        progress("train-step leg (config/java.py, 64 ASTs per GPU)")
         out["train"] = train_step_bench(world, rank, dev, args.train_steps, args.train_warmup)
         if world == 1:
             # the same step wrapped in DDP over a world-size-1 RCCL group: the reducer's own cost on record
@@ -567,10 +587,13 @@ def main():
                                                            force_ddp=True)
             finally:
                 dist.destroy_process_group()
+            progress("config-1 protocol on the GPU")
             out["config1_gpu"] = gpu_config1(dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        progress("CPU baseline (oracle SBM layer on host cores)")
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, B=B if N <= 150 else 1, N=N, k=k)
         if not args.no_cpu_config1:
+            progress("config-1 protocol on host cores (oracle CSATrans)")
             out["cpu_config1"] = cpu_config1()
     if rank == 0:
         print(json.dumps(out), flush=True)
