@@ -97,7 +97,8 @@ def _run_rel(q, k, v, lq, lk, rel, mask, dO, schedule="auto"):
 def test_rel_attn_full_size_rows_match_oracle_and_deterministic():
     """The java train step's CSE shape (B=64 per GPU, H=8, N=L=150, d_k=64) in the compact layout:
     two runs are bitwise identical (the first with the backward halves in order, the second with
-    bwd_kf beside bwd_qf on the caller's side stream: schedule "in_order" / "concurrent"); out/dq/dk/dv of sampled batch rows match the fp64 oracle run on
+    the key-side kernel beside the query-side one on the caller's side stream: schedule "in_order" /
+    "concurrent"); out/dq/dk/dv of sampled batch rows match the fp64 oracle run on
     those rows alone (each row depends only on its AST); dlq/dlk (sums over the whole batch) match
     the fp64 oracle over all 64 rows."""
     from csa_amd.data import synthetic_batch
