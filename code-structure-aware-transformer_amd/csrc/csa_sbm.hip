@@ -574,6 +574,9 @@ __device__ __forceinline__ void load_item_x(const KArgs& p, int b, int hd, int r
 // F2 body: item r of (b, hd) from its x rows. `next` runs once every product is done and x is dead,
 // before the stores (the persistent kernel issues the next item's x loads there: a later vmcnt wait
 // for them then does not also wait for this item's stores, which drain under the next item).
+#ifdef CSA_PHASES_FWD
+__device__ unsigned long long g_phf[16][8];
+#endif
 template <int D, int KT, bool FL, typename NEXT, bool BF = false>
 __device__ __forceinline__ void proj_fwd_item(const KArgs& p, const FwdFrags& F, int b, int hd, int r, float (&x)[D / 2],
                                               float* scr, NEXT next) {
@@ -587,10 +590,29 @@ __device__ __forceinline__ void proj_fwd_item(const KArgs& p, const FwdFrags& F,
   f32x16 h1[D / 32], h2[D / 32], po[D / 32], hat[KT], t[KT];
 #pragma unroll
   for (int i = 0; i < D / 2; ++i) x[i] = rv ? x[i] : 0.f;
+#ifdef CSA_PHASES_FWD  // dev instrumentation: issue-to-issue cycles by phase (s_memtime), see k_proj_fwd_l
+  unsigned long long* ph = g_phf[threadIdx.x >> 6];
+  unsigned long long tq = __builtin_amdgcn_s_memtime();
+#define PHF(i) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if ((blockIdx.x | blockIdx.y) == 0) ph[i] += t_ - tq; tq = t_; }
+  mlp_layer0<D, FL, BF>(p, F.W[0], F.b[0], x, h1, row, bh, isK);
+  PHF(0)
+  mlp_layer<D, FL, BF>(F.W[1], F.b[1], h1, h2);
+  PHF(1)
+  mlp_act<D>(p, h2, 1, row, bh, isK);
+  PHF(2)
+  mlp_layer<D, FL, BF>(F.W[2], F.b[2], h2, po);
+  PHF(3)
+  cluster_hat<D, KT, FL, BF>(p, F.C, po, hat);
+  PHF(4)
+  if (isK) small_mm<KT, FL>(F.S, hat, t);
+  next();
+  PHF(5)
+#else
   mlp_fwd<D, FL, BF>(p, F, x, h1, h2, po, row, bh, isK);
   cluster_hat<D, KT, FL, BF>(p, F.C, po, hat);
   if (isK) small_mm<KT, FL>(F.S, hat, t);
   next();
+#endif
 #ifndef CSA_EXP_NO_ACT
   {  // save the activations for k_proj_bwd (item r of this (b,h): Q blocks, then K blocks)
     constexpr int ABLK = (3 * D + 32 * KT) * 32;
@@ -617,6 +639,10 @@ __device__ __forceinline__ void proj_fwd_item(const KArgs& p, const FwdFrags& F,
     store_rows<KT>(p.Kh + ((int64_t)bh * p.M + row) * p.kp, p.kp, p.kp, hat, rv);
     store_rows<KT>(p.T + ((int64_t)bh * p.M + row) * p.kp, p.kp, p.kp, t, rv);
   }
+#ifdef CSA_PHASES_FWD
+  PHF(6)
+#undef PHF
+#endif
   (void)lane; (void)h;
 }
 
@@ -690,6 +716,13 @@ __global__ __launch_bounds__((64 * ProjFwdLds<D, KT>::NW)) void k_proj_fwd_l(con
     };
     proj_fwd_item<D, KT, true, decltype(nextf), BF>(p, F, it / per_b, hd, it % per_b, x, scr, nextf);
   }
+#ifdef CSA_PHASES_FWD
+  if (blockIdx.x == 0 && blockIdx.y == 0 && lane_id() == 0) {
+    const unsigned long long* q = g_phf[w];
+    printf("PHF d=%d w=%d layer0+act %llu layer1 %llu act1 %llu layer2 %llu hat %llu T+next %llu stores %llu\n", D, w,
+           q[0], q[1], q[2], q[3], q[4], q[5], q[6]);
+  }
+#endif
 }
 
 // ------------------------------------------------------------------------------------
