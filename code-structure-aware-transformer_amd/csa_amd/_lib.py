@@ -122,7 +122,9 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise CsaError(f"libcsa_hip.so not found at {LIB_PATH}: run `python __graft_entry__.py build` "
                        "(there is no CPU fallback for the hot path)")
-    L = ctypes.CDLL(LIB_PATH)
+    # RTLD_GLOBAL: the C++ op shim (libcsa_torch.so, csa_amd.ops) resolves its csa_* symbols against THIS
+    # library at its own load time, so both always use one instance (also for a CSA_HIP_LIB variant build)
+    L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
     L.csa_abi_version.restype = ctypes.c_int
     L.csa_source_hash.restype = ctypes.c_char_p
     L.csa_status_str.restype = ctypes.c_char_p

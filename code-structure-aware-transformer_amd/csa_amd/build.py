@@ -12,6 +12,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(os.path.dirname(HERE), "csrc")
 OUT = os.path.join(HERE, "lib", "libcsa_hip.so")
 SOURCES = ["csa_sbm.hip", "csa_rel.hip", "csa_optim.hip", "csa_gen.hip", "csa_glue.hip", "csa_host.cpp"]
+# the C++ TORCH_LIBRARY shim (torch.ops.csa.* of the hot path): host code against the torch headers; its
+# csa_* symbols resolve at load time to the libcsa_hip.so that csa_amd._lib loaded (RTLD_GLOBAL) first
+SHIM = "csa_torch.cpp"
+SHIM_OUT = os.path.join(HERE, "lib", "libcsa_torch.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-shared", "-fPIC", "-Wall", "-Wno-unused-result",
          "-Wno-unused-function"]
@@ -23,7 +27,7 @@ HEADER = os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "csa_hi
 def _deps():
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
     hdrs = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hpp", ".h")))
-    return srcs, srcs + hdrs + [HEADER]
+    return srcs, srcs + [os.path.join(CSRC, SHIM)] + hdrs + [HEADER]
 
 
 def source_hash():
@@ -44,10 +48,21 @@ def built_hash():
         return None
 
 
+def shim_cmd():
+    """hipcc line of libcsa_torch.so (host C++; torch's headers and HIP runtime; no kernels)."""
+    import torch
+    tdir = os.path.dirname(torch.__file__)
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    return [HIPCC, "-O2", "-std=c++17", "-fPIC", "-shared", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DUSE_ROCM",
+            "-I" + os.path.join(tdir, "include"), "-I" + os.path.join(tdir, "include", "torch", "csrc", "api", "include"),
+            os.path.join(CSRC, SHIM), "-L" + os.path.join(tdir, "lib"), "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu",
+            "-ltorch_hip", "-o", SHIM_OUT + ".tmp"]
+
+
 def build(force=False, verbose=True):
     srcs, deps = _deps()
     digest = source_hash()
-    if not force and os.path.exists(OUT) and built_hash() == digest:
+    if not force and os.path.exists(OUT) and os.path.exists(SHIM_OUT) and built_hash() == digest:
         return OUT
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
     objs = []
@@ -59,11 +74,13 @@ def build(force=False, verbose=True):
         cmd = [c for c in cmd if c != "-shared"]
         procs.append((subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT), cmd))
         objs.append(o)
+    procs.append((subprocess.Popen(shim_cmd(), stdout=subprocess.PIPE, stderr=subprocess.STDOUT), shim_cmd()))
     for p, cmd in procs:
         out, _ = p.communicate()
         if p.returncode != 0:
             sys.stderr.write(out.decode())
             raise RuntimeError("hipcc failed: " + " ".join(cmd))
+    os.replace(SHIM_OUT + ".tmp", SHIM_OUT)
     cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", OUT + ".tmp"] + objs
     subprocess.check_call(cmd)
     os.replace(OUT + ".tmp", OUT)

@@ -78,3 +78,14 @@ def test_adamw_step_validates_without_gpu():
     a = _lib.AdamwArgs(nchunks=3, ntensors=1, beta1=0.9, beta2=0.999)  # null tables
     assert L.csa_adamw_step(ctypes.byref(a), None) == 1
     assert b"null tensor table" in L.csa_last_error_str()
+
+
+def test_torch_shim_registers_gpu_implementations():
+    """The C++ TORCH_LIBRARY_IMPL shim (csrc/csa_torch.cpp, libcsa_torch.so) is loaded by csa_amd.ops and
+    registers a CUDA (HIP) kernel for every hot-path op schema; there is no CPU kernel (no fallback)."""
+    import torch
+    import csa_amd.ops as ops
+    assert ops._SHIM is not None and os.path.exists(ops.SHIM_PATH)
+    for name in ops._SCHEMAS:
+        assert torch._C._dispatch_has_kernel_for_dispatch_key("csa::" + name, "CUDA"), name
+        assert not torch._C._dispatch_has_kernel_for_dispatch_key("csa::" + name, "CPU"), name
