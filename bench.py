@@ -400,6 +400,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cpu-config1", action="store_true", help="skip the config-1 CPU CSATrans protocol")
     ap.add_argument("--no-train", action="store_true", help="skip the full train-step measurement")
+    ap.add_argument("--default-gemms", action="store_true",
+                    help="train legs on hipBLASLt's default GEMM heuristic instead of the tuned table")
     ap.add_argument("--train-steps", type=int, default=50)
     ap.add_argument("--train-warmup", type=int, default=20)
     ap.add_argument("--device", choices=("cuda", "cpu"), default="cuda",
@@ -574,7 +576,11 @@ def main():
                                     "T = Kh S^T, expA, sampling and all elementwise fp32"}
     if not args.no_train:
         progress("train-step leg (config/java.py, 64 ASTs per GPU)")
+        from csa_amd.train import GEMM_TABLE, use_tuned_gemms
+        ntuned = use_tuned_gemms(not args.default_gemms)
         out["train"] = train_step_bench(world, rank, dev, args.train_steps, args.train_warmup)
+        out["train"]["gemms"] = (f"TunableOp table {os.path.basename(GEMM_TABLE)} ({ntuned} shapes)" if ntuned
+                                 else "hipBLASLt default heuristic")
         if world == 1:
             # the same step wrapped in DDP over a world-size-1 RCCL group: the reducer's own cost on record
             import socket
@@ -589,6 +595,13 @@ def main():
                 dist.destroy_process_group()
             progress("config-1 protocol on the GPU")
             out["config1_gpu"] = gpu_config1(dev)
+            if ntuned:
+                # the unwrapped step once more on hipBLASLt's default GEMM choice: what the table buys
+                progress("train-step leg on default GEMMs")
+                use_tuned_gemms(False)
+                out["train_default_gemms"] = {k: v for k, v in train_step_bench(
+                    world, rank, dev, args.train_steps, args.train_warmup).items()
+                    if k in ("ms_per_step", "samples_per_s", "mean_loss")}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         progress("CPU baseline (oracle SBM layer on host cores)")
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, B=B if N <= 150 else 1, N=N, k=k)

@@ -154,6 +154,40 @@ def init_distributed():
     return rank, world, local, device
 
 
+GEMM_TABLE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_tuned_gfx950.csv")
+
+
+def use_tuned_gemms(on=True, path=GEMM_TABLE, tune=False):
+    """Select the stock fp32 GEMMs of the model (encoder/decoder Linears, the fused QKV projection, the
+    generator) from a per-shape table instead of hipBLASLt's default heuristic: PyTorch TunableOp with
+    the committed table `gemm_tuned_gfx950.csv` (tools/tune_gemms.py measured every GEMM shape of the
+    config/java.py train step at 64 ASTs per GPU and of the config/python.py protocol at B=32 on an
+    MI355X, picking the fastest hipBLASLt or rocBLAS solution per shape). Same fp32 arithmetic, only
+    the kernel (tile shape, summation order) differs; shapes not in the table keep the default.
+    The table is validated against the running PyTorch / HIP / hipBLASLt / rocBLAS versions and the
+    gfx arch (its Validator rows); on a mismatch nothing is loaded. Process-global (torch.cuda.tunable),
+    so every rank of a DDP job calls it for itself. Returns the number of table entries in effect.
+    tune=True searches shapes missing from the table (tools/tune_gemms.py)."""
+    import torch.cuda.tunable as tunable
+    if not on:
+        tunable.enable(False)
+        return 0
+    tunable.enable(True)
+    tunable.tuning_enable(tune)
+    tunable.set_max_tuning_duration(15)
+    tunable.set_filename(path, insert_device_ordinal=False)
+    if os.path.exists(path) and not tunable.read_file(path):
+        tunable.enable(False)
+        return 0
+    if not tune:
+        # results are written back to the current filename at exit: point it at a per-process scratch
+        # file, so concurrent ranks never rewrite the shared table
+        import tempfile
+        tunable.set_filename(os.path.join(tempfile.gettempdir(), f"csa_tunableop_{os.getpid()}.csv"),
+                             insert_device_ordinal=False)
+    return len(tunable.get_results())
+
+
 def set_bwd_schedule(model, schedule):
     """Set the attention backward schedule ("auto" | "in_order" | "concurrent") of every SBM / dense / CSE
     attention module inside `model` (csa_amd.module.*: bwd_schedule)."""

@@ -89,3 +89,19 @@ def test_torch_shim_registers_gpu_implementations():
     for name in ops._SCHEMAS:
         assert torch._C._dispatch_has_kernel_for_dispatch_key("csa::" + name, "CUDA"), name
         assert not torch._C._dispatch_has_kernel_for_dispatch_key("csa::" + name, "CPU"), name
+
+
+def test_tuned_gemm_table_is_well_formed():
+    """csa_amd/gemm_tuned_gfx950.csv (tools/tune_gemms.py, loaded by csa_amd.train.use_tuned_gemms): TunableOp's
+    CSV with validator rows for gfx950 and one fp32 GEMM solution per shape of the java train step."""
+    import csv
+
+    from csa_amd.train import GEMM_TABLE
+    rows = list(csv.reader(open(GEMM_TABLE)))
+    val = {r[1]: r[2] for r in rows if r[0] == "Validator"}
+    assert val["GCN_ARCH_NAME"].startswith("gfx950") and "PT_VERSION" in val
+    ent = [r for r in rows if r[0] != "Validator"]
+    assert len(ent) >= 30 and all(r[0].startswith("Gemm") and "float" in r[0] for r in ent)
+    assert len({(r[0], r[1]) for r in ent}) == len(ent)
+    # the 9600-row (64 ASTs x 150 nodes) encoder shapes of the train step are covered
+    assert any("_9600_" in r[1] for r in ent)

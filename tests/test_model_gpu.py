@@ -270,3 +270,59 @@ def test_greedy_generator_matches_reference(golden):
     h.remove()
     np.testing.assert_allclose(torch.stack(steps).numpy(), z["step_logp"], rtol=1e-4, atol=1e-4)
     np.testing.assert_array_equal(ys.cpu().numpy(), z["ys"])
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not has_gpu(), reason="needs GPU")
+def test_tuned_gemm_table_keeps_the_train_step():
+    """csa_amd.train.use_tuned_gemms (TunableOp table csa_amd/gemm_tuned_gfx950.csv, the stock fp32 GEMMs
+    of the java train step at 64 ASTs): the table loads on this box (its validators match), and one eval-mode
+    fwd+bwd of the config/java.py CSATrans at the tuned shapes gives the same loss and gradients as
+    hipBLASLt's default kernels up to fp32 summation order (same seed, so the same Philox uniforms; an
+    fp32-order difference can flip an STE edge whose uniform sits within ~1e-7 of expA, hence a norm-wise
+    bound per tensor)."""
+    import golden_inputs as gi
+    from csa_amd.data import synthetic_batch
+    from csa_amd.model import CSATrans, batch_to_device, label_smoothing_loss
+    from csa_amd.train import use_tuned_gemms
+    dev = torch.device("cuda")
+    m = CSATrans(**gi.JAVA)
+    gi.fill_params_deterministic(m, 5)
+    m = m.to(dev).eval()
+    x, y = batch_to_device(synthetic_batch(64, 150, seed=3), dev)
+
+    def run():
+        m.zero_grad(set_to_none=True)
+        torch.manual_seed(11)
+        out, sp = m(x)[:2]
+        loss = label_smoothing_loss(out, y) + 1e-2 * sp
+        loss.backward()
+        return float(loss), {k: p.grad.detach().clone() for k, p in m.named_parameters() if p.grad is not None}
+
+    try:
+        assert use_tuned_gemms() >= 30
+        l_t, g_t = run()
+        use_tuned_gemms(False)
+        l_d, g_d = run()
+    finally:
+        use_tuned_gemms(False)
+    assert abs(l_t - l_d) <= 1e-5 * abs(l_d)
+    assert g_t.keys() == g_d.keys() and len(g_d) > 50
+    rel, noise, bad = [], [], []
+    for k in g_d:
+        d = float((g_t[k] - g_d[k]).norm())
+        n = float(g_d[k].norm())
+        wk = k[:-len(".bias")] + ".weight" if k.endswith(".bias") else None
+        wn = float(g_d[wk].norm()) if wk in g_d else 0.0
+        if n < 1e-3 * wn:
+            # a bias whose exact gradient is 0 (it feeds a shift-invariant softmax): rounding noise either
+            # way, so it must only stay noise next to its layer's weight gradient
+            noise.append(k)
+            if d > 1e-3 * wn:
+                bad.append((k, d / wn))
+        else:
+            rel.append((d / max(n, 1e-30), k))
+            if d > 2e-3 * n:
+                bad.append((k, d / n))
+    print("worst per-tensor gradient difference (tuned vs default GEMMs):", max(rel), f"({len(noise)} noise-level biases)")
+    assert not bad, bad

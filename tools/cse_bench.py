@@ -27,6 +27,9 @@ for t in (q, k, v, lq, lk):
 
 
 def step():
+    # fresh gradients each step, as in the train step (zero_grad(set_to_none=True)): no .grad accumulation adds
+    for t in (q, k, v, lq, lk):
+        t.grad = None
     o = rel_ops.rel_attn(q, k, v, lq, lk, rel, mask)
     o.backward(dO)
 
