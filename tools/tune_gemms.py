@@ -3,7 +3,7 @@ csa_amd.train.use_tuned_gemms loads. Runs the config/java.py train step (64 ASTs
 config/python.py protocol legs (B=32) with PyTorch TunableOp searching every stock fp32 GEMM shape
 they issue; the table is written to OUT when the process exits (TunableOp's own writer).
 
-usage: python tools/tune_gemms.py OUT.csv"""
+usage: python tools/tune_gemms.py OUT.csv [ms of timing per candidate solution, default 15]"""
 import os
 import sys
 
@@ -20,6 +20,8 @@ if __name__ == "__main__":
     if os.path.exists(out):
         os.remove(out)
     use_tuned_gemms(path=out, tune=True)
+    if len(sys.argv) > 2:
+        torch.cuda.tunable.set_max_tuning_duration(int(sys.argv[2]))
     dev = torch.device("cuda:0")
     print("java train step", bench.train_step_bench(1, 0, dev, 3, 1), flush=True)
     print("python protocol", bench.gpu_config1(dev, reps=2), flush=True)
