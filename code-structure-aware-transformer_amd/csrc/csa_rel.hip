@@ -163,6 +163,28 @@ __global__ __launch_bounds__(256) void k_sum_splits(const float* __restrict__ pa
   }
 }
 
+// The two partial sets of k_rel_lgrad (dlk: blockIdx.y = 0, dlq: 1) in one launch: out[e] = sum_{s < RS}
+// part[s * n + e] in split order (bit-identical to k_sum_splits), eight independent loads in flight per step
+__global__ __launch_bounds__(256) void k_sum_splits2(const float* __restrict__ part0, const float* __restrict__ part1,
+                                                     float* __restrict__ out0, float* __restrict__ out1, int64_t n,
+                                                     int RS) {
+  const float* part = blockIdx.y ? part1 : part0;
+  float* out = blockIdx.y ? out1 : out0;
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= n) return;
+  float v = 0.f;
+  int s = 0;
+  for (; s + 8 <= RS; s += 8) {
+    float t[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t[u] = part[(int64_t)(s + u) * n + e];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v += t[u];
+  }
+  for (; s < RS; ++s) v += part[(int64_t)s * n + e];
+  out[e] = v;
+}
+
 struct RelArgs {
   int B, H, N, L, Lp, NQB, NKB, group;
   int ldg;  // row stride of the G^T / P^T images (N rounded up to 4: 16-B aligned rows)
@@ -1488,7 +1510,7 @@ __global__ __launch_bounds__(128, 2) void k_rel_bwd_kh(const RelArgs p) {
 // (H, B, Lp, NP), x = n (written by bins_store_t; columns n >= N are never written and masked here).
 // One wave per (32-row l tile, head, split) computes both 32-column halves of dd: A = G rows (dwordx4 runs
 // of x in the acc K-permutation), B = the chunk's 32 X rows by LDS-DMA into a double-buffered SW_COL image
-// (column reads conflict-free); chunk c + 1 lands while chunk c's 32 MFMAs run. k_sum_splits adds the
+// (column reads conflict-free); chunk c + 1 lands while chunk c's 32 MFMAs run. k_sum_splits2 adds the
 // splits in order.
 struct LgradArgs {
   const float* G[2];   // G_c2p, G_p2cT tables (H, Lp, ldx)
@@ -1746,9 +1768,8 @@ void rel_param_grads(const csa_rel_attn_args* a, const csa_rel_attn_bwd_args* b,
     g.ldx = R.ldx; g.Lp = (int)Lp; g.L = L; g.NP = (int)R.NP; g.B = B; g.N = N; g.H = H; g.nsplit = R.RS;
     hipLaunchKernelGGL(k_rel_lgrad, dim3((unsigned)H, (unsigned)(2 * R.RS)), dim3(64 * (unsigned)((L + 31) / 32)),
                        2 * 32 * 64 * 4, st, g);
-    for (int which = 0; which < 2; ++which)
-      hipLaunchKernelGGL(k_sum_splits, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, g.part[which],
-                         which == 0 ? b->dlk : b->dlq, n, R.RS, n);
+    hipLaunchKernelGGL(k_sum_splits2, dim3((unsigned)((n + 255) / 256), 2), dim3(256), 0, st, g.part[0], g.part[1],
+                       b->dlk, b->dlq, n, R.RS);
     return;
   }
   for (int which = 0; which < 2; ++which) {
