@@ -35,6 +35,10 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "SBM-attn fwd+bwd ASTs/sec (L=150) + train samples/sec @1/2/4/8 GPU"
 PEAK_F32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32-input MFMA dense peak
 PEAK_HBM_GBS = 8000.0
+# ideal fused bytes per AST (fwd+bwd; Q,K,V,dX in, X, graph, dQ,dK,dV out) with fp32
+# operands (the bf16 mode's own I/O: it takes and returns fp32 tensors) and with bf16 operands
+IDEAL_BYTES_PER_AST_F32IO = 3.739e6
+IDEAL_BYTES_PER_AST_BF16IO = 2.050e6
 
 
 def stage_flops_per_ast(H, N, M, D, k):
@@ -574,6 +578,15 @@ def main():
                             "ms_per_step": round(el_bf * 1000.0 / args.steps, 4),
                             "note": "QK^T/PV/dP/dQ/dK/dV, the projection MLP and sigmoid(.C^T) (fwd+bwd) on bf16 MFMA; "
                                     "T = Kh S^T, expA, sampling and all elementwise fp32"}
+        vb = out["bf16_mode"]["value"] / world  # per GPU
+        out["bf16_mode"]["roofline"] = {
+            "bound": "hbm", "unit": "GB/s", "peak": PEAK_HBM_GBS,
+            "achieved": round(vb * IDEAL_BYTES_PER_AST_F32IO / 1e9, 1),
+            "frac": round(vb * IDEAL_BYTES_PER_AST_F32IO / 1e9 / PEAK_HBM_GBS, 4),
+            "ideal_bytes_per_ast": IDEAL_BYTES_PER_AST_F32IO,
+            "frac_at_bf16_io": round(vb * IDEAL_BYTES_PER_AST_BF16IO / 1e9 / PEAK_HBM_GBS, 4),
+            "note": "ideal fused bytes per AST x ASTs/s against 8 TB/s (SURVEY 8(d) config 2); frac with the "
+                    "fp32 I/O the mode takes and returns, frac_at_bf16_io with 2.05 MB/AST bf16 I/O"}
     if not args.no_train:
         progress("train-step leg (config/java.py, 64 ASTs per GPU)")
         from csa_amd.train import GEMM_TABLE, use_tuned_gemms

@@ -549,6 +549,63 @@ __device__ __forceinline__ void store_act_lds(float* __restrict__ blk, const f32
   }
 }
 
+// CSA_DTYPE_BF16 (d = 64 / 96, k <= 16): h1 | h2 | po are saved as bf16 in the first half of their slices,
+// rounded as pack8 rounds them for the bf16 MFMAs (RNE), so the backward's bf16 outer products see the same
+// operands; the relu masks keep their signs. Halves the activation traffic of the bf16 mode.
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+template <int NT>
+__device__ __forceinline__ void store_act_lds_bf(float* __restrict__ blk, const f32x16 (&a)[NT], float* __restrict__ scr) {
+  const int lane = lane_id(), c = lane & 31, h = lane >> 5;
+  u32x2v* out = reinterpret_cast<u32x2v*>(blk);  // element e at 16-bit slot e
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) scr[act_off(crow(r, h), c)] = a[t][r];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(scr + 4 * (lane + 64 * k));
+      bf16x4 b;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) b[e] = (__bf16)v[e];
+      __builtin_nontemporal_store(__builtin_bit_cast(u32x2v, b), out + 256 * t + lane + 64 * k);
+    }
+  }
+}
+
+// The bf16 slice of store_act_lds_bf, DMA'd into the upper half of a wave's R-float LDS region, widened in
+// place to the fp32 slice over the whole region (element order, hence the act_off layout, unchanged).
+// Elements [0, R/2) first: their fp32 lands below the bf16 data. Then [R/2, R): every read of the phase
+// completes before its writes, which overlap only that phase's own (consumed) sources.
+template <int R>
+__device__ __forceinline__ void widen_act_bf(float* __restrict__ reg, int lane) {
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(reg + R / 2);
+  constexpr int NJ = R / 1024;  // 8-element reads per lane per phase
+#pragma unroll
+  for (int ph = 0; ph < 2; ++ph) {
+    u32x4v w[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) w[j] = *reinterpret_cast<const u32x4v*>(src + ph * (R / 4) + 4 * (lane + 64 * j));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      f32x4 lo, hi;
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        lo[2 * e] = __builtin_bit_cast(float, w[j][e] << 16);
+        lo[2 * e + 1] = __builtin_bit_cast(float, w[j][e] & 0xffff0000u);
+        hi[2 * e] = __builtin_bit_cast(float, w[j][2 + e] << 16);
+        hi[2 * e + 1] = __builtin_bit_cast(float, w[j][2 + e] & 0xffff0000u);
+      }
+      float* dst = reg + ph * (R / 2) + 8 * (lane + 64 * j);
+      *reinterpret_cast<f32x4*>(dst) = lo;
+      *reinterpret_cast<f32x4*>(dst + 4) = hi;
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
 // ------------------------------------------------------------------------------------
 // F2 body: one 32-row item (block rb of Q, or of K when isK) of batch element b, head hd.
 // ------------------------------------------------------------------------------------
@@ -617,12 +674,19 @@ __device__ __forceinline__ void proj_fwd_item(const KArgs& p, const FwdFrags& F,
   {  // save the activations for k_proj_bwd (item r of this (b,h): Q blocks, then K blocks)
     constexpr int ABLK = (3 * D + 32 * KT) * 32;
     float* blk = p.Act + ((int64_t)bh * (p.NQB + p.NKB) + r) * ABLK;
-    store_act_lds<D / 32>(blk, h1, scr);
-    store_act_lds<D / 32>(blk + 32 * D, h2, scr);
+    constexpr bool ABF = BF && (D == 64 || D == 96) && KT == 1;  // read back by k_proj_bwd_s<D, true>
+    if (ABF && p.kp <= 16) {
+      store_act_lds_bf<D / 32>(blk, h1, scr);
+      store_act_lds_bf<D / 32>(blk + 32 * D, h2, scr);
+      store_act_lds_bf<D / 32>(blk + 64 * D, po, scr);
+    } else {
+      store_act_lds<D / 32>(blk, h1, scr);
+      store_act_lds<D / 32>(blk + 32 * D, h2, scr);
 #ifdef CSA_EXP_RECOMP_PO  // experiment: k_proj_bwd_s<64> recomputes po from h2
-    if (!(D == 64 && KT == 1 && p.kp <= 16))
+      if (!(D == 64 && KT == 1 && p.kp <= 16))
 #endif
-    store_act_lds<D / 32>(blk + 64 * D, po, scr);
+      store_act_lds<D / 32>(blk + 64 * D, po, scr);
+    }
     bool hat16 = false;
     if constexpr (KT == 1) {
       if ((D == 64 || D == 96) && p.kp <= 16) {  // clusters >= 16 are zero, never read back (k_proj_bwd_s)
@@ -2265,7 +2329,8 @@ __global__ __launch_bounds__(256, ProjBwdSmallShape<D>::LCS ? 1 : 2) void k_proj
 #ifdef CSA_EXP_RECOMP_PO
     dma_block16<D * 128>(INl, ar, (D == 64 ? 32 : 64) * D * 4);  // experiment: h2 (po is recomputed from it)
 #else
-    dma_block16<D * 128>(INl, ar, 64 * D * 4);  // po -> own IN region (free since B6), lands under dS / dZ / dp
+    if constexpr (BF) dma_block16<D * 64>(INl + 2 * REG, ar, 64 * D * 4);  // bf16 po -> upper half (widened below)
+    else dma_block16<D * 128>(INl, ar, 64 * D * 4);  // po -> own IN region (free since B6), lands under dS / dZ / dp
 #endif
     f32x16 gin[1];
     float dTt[8];
@@ -2311,6 +2376,9 @@ __global__ __launch_bounds__(256, ProjBwdSmallShape<D>::LCS ? 1 : 2) void k_proj
     f32x16 dcur[DT];
     mm_acc_f<DT, 1, 2, LCS ? 8 : 16, LCS, BF>(LCS ? CFs : CfT, dz, dcur);
     wait_vm_all();  // po (LW: and the W2 fragments)
+#ifndef CSA_EXP_RECOMP_PO
+    if constexpr (BF) widen_act_bf<REG>(INw, ln);
+#endif
 #ifdef CSA_EXP_RECOMP_PO
     if constexpr (D == 64) {  // po = W2 h2 + b2: the forward's own chain (L2 fragments), bit-identical
       f32x16 h2v[DT], pov[DT];
@@ -2332,10 +2400,12 @@ __global__ __launch_bounds__(256, ProjBwdSmallShape<D>::LCS ? 1 : 2) void k_proj
     // ---- layer 2 (proj.6): stage dp, h2 -> IN; dh2_pre = W2^T dp under the DMA
     stage_ds<DT>(DSw, dcur, D, ln);
     if constexpr (LW) __syncthreads();  // B0: every wave's quarter of the W2 fragments landed
-    dma_block16<D * 128>(INl, ar, 32 * D * 4);  // h2
+    if constexpr (BF) dma_block16<D * 64>(INl + 2 * REG, ar, 32 * D * 4);  // bf16 h2 -> upper half
+    else dma_block16<D * 128>(INl, ar, 32 * D * 4);  // h2
     f32x16 dh[DT];
     mm_acc_f<DT, DT, 4 * DT, 16 * DT, LW, BF>(LW ? WFs : p.WfT[2], dcur, dh);
     wait_vm_all();
+    if constexpr (BF) widen_act_bf<REG>(INw, ln);
     PHASE(7);
     __syncthreads();  // B1: dp, h2 of every wave staged
     PHASE(2);
@@ -2356,7 +2426,8 @@ __global__ __launch_bounds__(256, ProjBwdSmallShape<D>::LCS ? 1 : 2) void k_proj
     PHASE(2);
     // ---- layer 1 (proj.3): stage dh2, h1 -> IN and x rows under dh1_pre = W1^T dh2
     stage_ds<DT>(DSw, dcur, D, ln);
-    dma_block16<D * 128>(INl, ar, 0);  // h1
+    if constexpr (BF) dma_block16<D * 64>(INl + 2 * REG, ar, 0);  // bf16 h1 -> upper half
+    else dma_block16<D * 128>(INl, ar, 0);  // h1
     f32x4 x4[NS / 4];  // raw (clamped-row) loads: the row mask is applied when x is staged, so the
     {                  // loads do not wait here
       const float* X = it.isK ? p.K + it.b * p.k_sb + hd * p.k_sh + (int64_t)rowc * p.k_sn
@@ -2366,6 +2437,7 @@ __global__ __launch_bounds__(256, ProjBwdSmallShape<D>::LCS ? 1 : 2) void k_proj
     }
     mm_acc_f<DT, DT, 4 * DT, 16 * DT, LW, BF>(LW ? WFs : p.WfT[1], dcur, dh);
     wait_vm_all();
+    if constexpr (BF) widen_act_bf<REG>(INw, ln);
     PHASE(4);
     __syncthreads();  // B3
     PHASE(2);

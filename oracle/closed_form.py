@@ -85,9 +85,10 @@ def sbm_fwd_bwd(Q, K, V, mask, params, u, num_clusters, dX, dsparsity, attn_keep
 
     bf16=True: an ideal CSA_DTYPE_BF16 implementation -- the operands of every contraction the bf16 mode
     runs on bf16 MFMA are rounded to bf16 (QK^T, dX V^T, PV with the unnormalised weights e A r, dV, dQ,
-    dK, the three MLP layers and .C^T forward, C^T dZ, the W^T chains and the dW outer products backward),
-    everything else (accumulation, biases, softmax, sampling, expA, T, dQh, dT, dS, dC) exact. The error of
-    this emulation against the fp32 reference is what a bf16-operand implementation cannot avoid."""
+    dK, the three MLP layers and .C^T forward, C^T dZ, the W^T chains and the dW outer products backward;
+    dC reads the projection output p as the bf16 mode saves it, rounded to bf16), everything else
+    (accumulation, biases, softmax, sampling, expA, T, dQh, dT, dS, dZ) exact. The error of this emulation
+    against the fp32 reference is what a bf16-operand implementation cannot avoid."""
     R = _bf16_round if bf16 else _ident
     f = lambda t: None if t is None else t.detach().double()
     Q, K, V, mask, u, dX, dsparsity = map(f, (Q, K, V, mask, u, dX, dsparsity))
@@ -152,7 +153,7 @@ def sbm_fwd_bwd(Q, K, V, mask, params, u, num_clusters, dX, dsparsity, attn_keep
     dZk = dKh * Kh * (1 - Kh)
     dQp = R(dZq) @ R(C).unsqueeze(0)
     dKp = R(dZk) @ R(C).unsqueeze(0)
-    dC = torch.einsum("bhnk,bhnd->hkd", dZq, Qp) + torch.einsum("bhnk,bhnd->hkd", dZk, Kp)
+    dC = torch.einsum("bhnk,bhnd->hkd", dZq, R(Qp)) + torch.einsum("bhnk,bhnd->hkd", dZk, R(Kp))
     dD = S * (dS - (S * dS).sum((-1, -2), keepdim=True))
     dC = dC + (dD + dD.transpose(-1, -2)) @ C
     dQm, gq = _mlp_bwd(dQp, W, qacts, qmasks, (pk.get("q0"), pk.get("q1")), R)
