@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-3 capture: default bench line (CPU baselines, train leg), rocprofv3 kernel stats of the SBM layer
+# Round-3 capture (bf16-mode stats and traffic included): default bench line (CPU baselines, train leg), rocprofv3 kernel stats of the SBM layer
 # bench / CSE layer / java train step, and the PMC traffic + MFMA passes of the SBM layer bench.
 set -o pipefail
 export TMPDIR=/tmp
@@ -16,6 +16,12 @@ timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc2
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc3" -o run -- python bench.py $B > "$OUT/pmc3.log" 2>&1 || exit $?
 python tools/pmc_traffic.py "$OUT/pmc2/run_counter_collection.csv" "$OUT/pmc3/run_counter_collection.csv" > "$OUT/pmc_traffic.json" || exit $?
 python tools/pmc_summary.py "$OUT"/pmc*/run_counter_collection.csv > "$OUT/pmc_summary.txt"
+# bf16 mode: kernel stats and HBM traffic of the same layer step
+BB="--precision bf16 --steps 5 --warmup 2 --no-cpu-baseline --no-train --no-cpu-config1"
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/sbm_bf16" -o run -- python bench.py $BB > "$OUT/sbm_bf16.log" 2>&1 || exit $?
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmcb2" -o run -- python bench.py $BB > "$OUT/pmcb2.log" 2>&1 || exit $?
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmcb3" -o run -- python bench.py $BB > "$OUT/pmcb3.log" 2>&1 || exit $?
+python tools/pmc_traffic.py "$OUT/pmcb2/run_counter_collection.csv" "$OUT/pmcb3/run_counter_collection.csv" > "$OUT/pmc_traffic_bf16.json" || exit $?
 rm -f "$OUT"/*/run_kernel_trace.csv "$OUT"/pmc*/run_counter_collection.csv.bak
 # the headline command under rocprofv3 in one process (live events vs rocprof average of the same launches)
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/pair" -o run -- python bench.py --no-cpu-baseline --no-train > "$OUT/bench_pair.json" 2> "$OUT/pair.log" || exit $?
