@@ -70,7 +70,9 @@ typedef enum csa_status {
  * dK, dV, of the projection MLP (three d x d layers, forward and backward chains and weight-gradient
  * products) and of sigmoid(. C^T) and its backward (SBM), and of the CSE's c2c, PV and their gradients
  * to bf16 for v_mfma_f32_32x32x16_bf16 (fp32 accumulation; north_star tolerance 2e-2). T = Kh S^T, expA,
- * the sampling threshold and every softmax / normalisation / elementwise step stay fp32. */
+ * the sampling threshold and every softmax / normalisation / elementwise step stay fp32. Inside the saved
+ * state (opaque, csa_sbm_state_bytes unchanged) bf16 mode keeps the projection MLP's activations as bf16,
+ * rounded as its MFMAs round them; the backward of the same call pair reads them back. */
 #define CSA_DTYPE_F32 0
 #define CSA_DTYPE_BF16 1
 
