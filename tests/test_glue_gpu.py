@@ -223,6 +223,8 @@ def test_gelu_dropout_matches_oracle(shape, batch_major, p):
     np.testing.assert_allclose(to_mem(h.grad.cpu()).numpy(), hr.grad.numpy(), rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.skipif(__import__("os").environ.get("CSA_BIAS_GRAD_FUSED") != "1",
+                    reason="csa_bias_grad_fused is opt-in (CSA_BIAS_GRAD_FUSED=1) until measured on the box")
 def test_bias_grad_one_launch_counters_and_accumulate():
     """csa_bias_grad_fused (one launch, last-arriving row slice sums the partials): the arrival counters are left
     zero by every call, so back-to-back calls of any shape on one counter buffer stay exact and bit-identical
