@@ -164,10 +164,6 @@ def lib():
     L.csa_bias_grad_workspace_bytes.argtypes = [i64, i64]
     L.csa_bias_grad.restype = ctypes.c_int
     L.csa_bias_grad.argtypes = [vp, vp, i64, i64, ctypes.c_int, vp, vp]
-    L.csa_bias_grad_counters.restype = ctypes.c_size_t
-    L.csa_bias_grad_counters.argtypes = [i64]
-    L.csa_bias_grad_fused.restype = ctypes.c_int
-    L.csa_bias_grad_fused.argtypes = [vp, vp, i64, i64, ctypes.c_int, vp, vp, vp]
     L.csa_layernorm_supported.restype = ctypes.c_int
     L.csa_layernorm_supported.argtypes = [i64]
     L.csa_layernorm_bwd_workspace_bytes.restype = ctypes.c_size_t
@@ -213,7 +209,7 @@ EXPORTED_SYMBOLS = (
     "csa_dense_attn_bwd", "csa_ste_sample",
     "csa_ste_backward", "csa_rel_attn_state_bytes", "csa_rel_attn_bwd_workspace_bytes", "csa_rel_attn_fwd", "csa_rel_attn_bwd",
     "csa_adamw_step", "csa_gen_logsoftmax_fwd", "csa_gen_logsoftmax_bwd",
-    "csa_bias_grad_workspace_bytes", "csa_bias_grad", "csa_bias_grad_counters", "csa_bias_grad_fused", "csa_ast_relations",
+    "csa_bias_grad_workspace_bytes", "csa_bias_grad", "csa_ast_relations",
     "csa_layernorm_supported", "csa_layernorm_bwd_workspace_bytes", "csa_layernorm_fwd", "csa_layernorm_bwd",
     "csa_residual_dropout_fwd", "csa_residual_dropout_bwd", "csa_gelu_dropout_fwd", "csa_gelu_dropout_bwd",
     "csa_collate_relations",

@@ -2,7 +2,6 @@
 csa_bias_grad (csrc/csa_glue.hip) instead of torch's generic strided reduction. Forward and the
 two GEMMs of the backward stay on hipBLASLt. Same parameters and state_dict keys as nn.Linear."""
 import ctypes
-import os
 
 import torch
 import torch.nn as nn
@@ -11,35 +10,15 @@ import torch.nn.functional as F
 from ._lib import check, lib
 
 
-_COUNTERS = {}  # (device index, stream) -> zeroed uint32 arrival counters of csa_bias_grad_fused (left zero by each call)
-_TWO_PASS = os.environ.get("CSA_BIAS_GRAD_FUSED") != "1"  # A/B switch (pending validation): csa_bias_grad_fused
-
-
-def _bias_grad_counters(dev, stream, n):
-    key = (dev.index, stream)
-    t = _COUNTERS.get(key)
-    if t is None or t.numel() < n:
-        t = torch.zeros(max(n, 64), dtype=torch.int32, device=dev)  # stream-ordered on `stream` (caller's)
-        _COUNTERS[key] = t
-    return t
-
-
 def bias_grad(gy2: torch.Tensor) -> torch.Tensor:
-    """(rows, cols) contiguous fp32 on the GPU -> (cols,) column sums (deterministic order), one launch
-    (csa_bias_grad_fused: the last row slice of each column block adds the partials)."""
+    """(rows, cols) contiguous fp32 on the GPU -> (cols,) column sums (deterministic order)."""
     rows, cols = gy2.shape
     db = torch.empty(cols, device=gy2.device, dtype=torch.float32)
     L = lib()
     ws = torch.empty(max(1, L.csa_bias_grad_workspace_bytes(rows, cols)), dtype=torch.uint8, device=gy2.device)
-    s = torch.cuda.current_stream(gy2.device).cuda_stream
-    if _TWO_PASS:
-        check(L.csa_bias_grad(ctypes.c_void_p(gy2.data_ptr()), ctypes.c_void_p(db.data_ptr()), rows, cols, 0,
-                              ctypes.c_void_p(ws.data_ptr()), ctypes.c_void_p(s)), "csa_bias_grad")
-        return db
-    cnt = _bias_grad_counters(gy2.device, s, L.csa_bias_grad_counters(cols))
-    check(L.csa_bias_grad_fused(ctypes.c_void_p(gy2.data_ptr()), ctypes.c_void_p(db.data_ptr()), rows, cols, 0,
-                            ctypes.c_void_p(ws.data_ptr()), ctypes.c_void_p(cnt.data_ptr()), ctypes.c_void_p(s)),
-          "csa_bias_grad_fused")
+    stream = ctypes.c_void_p(torch.cuda.current_stream(gy2.device).cuda_stream)
+    check(L.csa_bias_grad(ctypes.c_void_p(gy2.data_ptr()), ctypes.c_void_p(db.data_ptr()), rows, cols, 0,
+                          ctypes.c_void_p(ws.data_ptr()), stream), "csa_bias_grad")
     return db
 
 

@@ -54,65 +54,6 @@ __global__ __launch_bounds__(256) void k_bias_grad_part(const float* __restrict_
   }
 }
 
-// One launch (csa_bias_grad_fused): k_bias_grad_part's slab sums, then the last workgroup of each 64-column
-// block to arrive (a per-block arrival counter in the caller's zeroed counter buffer) adds the block's RS
-// partials in slice order and resets the counter. Deterministic: the summation order depends only on
-// (rows, cols), whichever workgroup finishes last. Saves the second launch of the two-pass form (a
-// latency-bound 4-5 us at the java step's 79 Linear bias gradients per step).
-__global__ __launch_bounds__(256) void k_bias_grad_fused(const float* __restrict__ dy, float* __restrict__ part,
-                                                     float* __restrict__ db, unsigned* __restrict__ cnt, int64_t rows,
-                                                     int64_t cols, int64_t rows_per_slice, int accumulate) {
-  __shared__ float red[BG_RL][BG_COLS + 4];
-  __shared__ unsigned last;
-  const int cq = threadIdx.x & 15, rl = threadIdx.x >> 4;
-  const int64_t c0 = (int64_t)blockIdx.x * BG_COLS + 4 * cq;
-  const int64_t r_lo = (int64_t)blockIdx.y * rows_per_slice;
-  const int64_t r_hi = r_lo + rows_per_slice < rows ? r_lo + rows_per_slice : rows;
-  const bool vec = (cols % 4 == 0) && (((uintptr_t)dy) & 15) == 0;
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  if (vec && c0 + 4 <= cols) {
-#pragma unroll 4
-    for (int64_t r = r_lo + rl; r < r_hi; r += BG_RL) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(dy + r * cols + c0);
-      acc[0] += v[0]; acc[1] += v[1]; acc[2] += v[2]; acc[3] += v[3];
-    }
-  } else {
-    for (int64_t r = r_lo + rl; r < r_hi; r += BG_RL)
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (c0 + e < cols) acc[e] += dy[r * cols + c0 + e];
-  }
-#pragma unroll
-  for (int e = 0; e < 4; ++e) red[rl][4 * cq + e] = acc[e];
-  __syncthreads();
-  const int64_t c = (int64_t)blockIdx.x * BG_COLS + threadIdx.x;
-  if (threadIdx.x < BG_COLS) {
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < BG_RL; ++i) s += red[i][threadIdx.x];
-    if (c < cols) part[(int64_t)blockIdx.y * cols + c] = s;
-  }
-  __threadfence();  // release: this slab's partials are visible device-wide (every XCD) before the arrival
-  __syncthreads();
-  if (threadIdx.x == 0) last = atomicAdd(&cnt[blockIdx.x], 1u) == gridDim.y - 1 ? 1u : 0u;
-  __syncthreads();
-  if (!last) return;
-  __threadfence();  // acquire: the other slabs' partials
-  if (threadIdx.x < BG_COLS && c < cols) {
-    const int rs = (int)gridDim.y;
-    float t = 0.f;
-    for (int i0 = 0; i0 < rs; i0 += 8) {
-      float v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = i0 + u < rs ? part[(int64_t)(i0 + u) * cols + c] : 0.f;
-#pragma unroll
-      for (int u = 0; u < 8; ++u) t += v[u];
-    }
-    db[c] = accumulate ? db[c] + t : t;
-  }
-  if (threadIdx.x == 0) cnt[blockIdx.x] = 0u;  // zero again for the next call on this stream
-}
-
 // Partials -> column sums. One workgroup per 16 columns; its 16 row groups each sum the partials
 // i = rg, rg + 16, ... (8 loads in flight, added in index order), then one thread per column adds
 // the 16 row-group sums in order. The order depends only on (rs, cols): deterministic. (One thread
@@ -325,29 +266,6 @@ csa_status csa_bias_grad(const float* dy, float* db, int64_t rows, int64_t cols,
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     csa::set_error("csa_bias_grad: %s", hipGetErrorString(e));
-    return CSA_LAUNCH_FAILED;
-  }
-  return CSA_OK;
-}
-
-size_t csa_bias_grad_counters(int64_t cols) { return cols > 0 ? (size_t)((cols + BG_COLS - 1) / BG_COLS) : 0; }
-
-csa_status csa_bias_grad_fused(const float* dy, float* db, int64_t rows, int64_t cols, int accumulate, void* workspace,
-                           uint32_t* counters, void* stream) {
-  if (rows <= 0 || cols <= 0) return csa_bias_grad(dy, db, rows, cols, accumulate, workspace, stream);
-  if (!db || !dy || !workspace || !counters) {
-    csa::set_error("csa_bias_grad_fused: null pointer");
-    return CSA_INVALID_ARG;
-  }
-  const hipStream_t st = (hipStream_t)stream;
-  const csa::DeviceGuard guard(st);
-  const int rs = bg_slices(rows);
-  const int64_t per = (rows + rs - 1) / rs;
-  hipLaunchKernelGGL(k_bias_grad_fused, dim3((unsigned)((cols + BG_COLS - 1) / BG_COLS), (unsigned)rs), dim3(256), 0, st,
-                     dy, (float*)workspace, db, (unsigned*)counters, rows, cols, per, accumulate);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) {
-    csa::set_error("csa_bias_grad_fused: %s", hipGetErrorString(e));
     return CSA_LAUNCH_FAILED;
   }
   return CSA_OK;

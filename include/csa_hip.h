@@ -13,7 +13,7 @@
  *   csa_rel_attn_bwd   autograd of rel_attn (gather backward = deterministic scatter-add)
  *   csa_adamw_step     script/optimizer.py:49-106 AdamW.step (all parameters in one launch)
  *   csa_gen_logsoftmax_fwd/_bwd  module/components.py:95-102 Generator: log(softmax(dropout(logits)))
- *   csa_bias_grad(_1)  Linear bias gradient (column sums of dY) of the encoder/decoder glue
+ *   csa_bias_grad      Linear bias gradient (column sums of dY) of the encoder/decoder glue
  *   csa_layernorm_fwd/_bwd  nn.LayerNorm of the encoder glue (module/components.py SublayerConnection)
  *   csa_ast_relations  my_ast.py:198-273 + dataset/base_data_set.py:33-36 (host C++, no GPU)
  *
@@ -243,12 +243,6 @@ csa_status csa_gen_logsoftmax_bwd(const float* dlogp, const float* logp, float* 
 size_t csa_bias_grad_workspace_bytes(int64_t rows, int64_t cols);
 csa_status csa_bias_grad(const float* dy, float* db, int64_t rows, int64_t cols, int accumulate, void* workspace,
                          void* stream);
-/* The same sums in ONE launch: the last row slice to finish per 64-column block adds the partials (same
- * workspace). `counters`: csa_bias_grad_counters(cols) uint32 arrival counters owned by the caller, zero
- * before the first call and left zero by every call; calls sharing a counter buffer must be stream-ordered. */
-size_t csa_bias_grad_counters(int64_t cols);
-csa_status csa_bias_grad_fused(const float* dy, float* db, int64_t rows, int64_t cols, int accumulate, void* workspace,
-                           uint32_t* counters, void* stream);
 
 /* ---- LayerNorm over the last dim (nn.LayerNorm(cols), affine) of the encoder/decoder glue ----
  * x, y, dy, dx: (rows, cols) contiguous fp32, cols % 4 == 0 and cols <= 1024 (csa_layernorm_supported);
