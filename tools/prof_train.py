@@ -18,5 +18,8 @@ if __name__ == "__main__":
     from csa_amd.train import GEMM_TABLE, use_tuned_gemms
     if table != "default":
         print("tuned GEMM shapes:", use_tuned_gemms(path=table or GEMM_TABLE), flush=True)
+    if os.environ.get("CSA_SDP") == "math":  # A/B: the decoder's SDPA on the math backend
+        torch.backends.cuda.enable_flash_sdp(False)
+        torch.backends.cuda.enable_mem_efficient_sdp(False)
     r = bench.train_step_bench(1, 0, torch.device("cuda:0"), steps, 3)
     print(r)
