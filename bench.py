@@ -42,12 +42,14 @@ IDEAL_BYTES_PER_AST_BF16IO = 2.050e6
 
 
 def stage_flops_per_ast(H, N, M, D, k):
-    """Algorithmic FLOPs per AST (one batch element, all heads) per kernel stage."""
+    """Algorithmic FLOPs per AST (one batch element, all heads) per kernel stage. The attention
+    backward's algorithmic work (dP, dV, dK, dT | dQ, dQh) is split as its kernels do it: k_attn_bwd_kv computes
+    dP = dX V^T (plus the S it recomputes, not counted) and dV, dK, dT; k_attn_bwd_qg dQ and dQh."""
     return {
         "proj_fwd": H * ((N + M) * (6 * D * D + 2 * k * D) + M * 2 * k * k),
         "attn_fwd": H * (4 * N * M * D + 2 * N * M * k),
-        "attn_bwd_q": H * (4 * N * M * D + 2 * N * M * k),
-        "attn_bwd_kv": H * (4 * N * M * D + 2 * N * M * k),
+        "attn_bwd_q": H * (2 * N * M * D + 2 * N * M * k),
+        "attn_bwd_kv": H * (6 * N * M * D + 2 * N * M * k),
         "proj_bwd": H * ((N + M) * (12 * D * D + 4 * k * D) + M * 4 * k * k),
     }
 
@@ -502,7 +504,7 @@ def main():
     stage_ms = stage_times(profs, list(STAGES))
     flops = stage_flops_per_ast(H, N, N, d, 0 if args.dense else k)
     if args.dense:
-        flops = {"attn_fwd": H * 4 * N * N * d, "attn_bwd_q": H * 4 * N * N * d, "attn_bwd_kv": H * 4 * N * N * d}
+        flops = {"attn_fwd": H * 4 * N * N * d, "attn_bwd_q": H * 2 * N * N * d, "attn_bwd_kv": H * 6 * N * N * d}
     timed = {s: v for s, v in stage_ms.items() if s in flops}
     # side-stream backward (B=64 shapes): the bwd_kv window opens at the fork, before bwd_q ends (in
     # order it opens after bwd_q's stop), so neither window is one kernel's launch and neither can be

@@ -5,13 +5,14 @@ after torch so that it binds to the HIP runtime torch already loaded (same SONAM
 libamdhip64.so.7). There is deliberately no fallback: if the library is missing, every op
 raises.
 """
+import contextlib
 import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CSA_HIP_LIB", os.path.join(_HERE, "lib", "libcsa_hip.so"))
 
-CSA_ABI_VERSION = 5
+CSA_ABI_VERSION = 6
 CSA_FLAG_DENSE = 1
 CSA_SCHED_AUTO, CSA_SCHED_IN_ORDER, CSA_SCHED_CONCURRENT = 0, 1, 2
 SCHEDULES = {"auto": CSA_SCHED_AUTO, "in_order": CSA_SCHED_IN_ORDER, "concurrent": CSA_SCHED_CONCURRENT}
@@ -23,8 +24,18 @@ i64, u64, u32, f32, vp = ctypes.c_int64, ctypes.c_uint64, ctypes.c_uint32, ctype
 
 CSA_STAGE_COUNT = 8
 STAGES = {"prep": 0, "proj_fwd": 1, "attn_fwd": 2, "attn_bwd_q": 3, "attn_bwd_kv": 4, "proj_bwd": 5, "reduce": 6}
-KERNEL_OF_STAGE = {"proj_fwd": "k_proj_fwd", "attn_fwd": "k_attn_fwd", "attn_bwd_q": "k_attn_bwd_q",
+KERNEL_OF_STAGE = {"proj_fwd": "k_proj_fwd", "attn_fwd": "k_attn_fwd", "attn_bwd_q": "k_attn_bwd_qg",
                    "attn_bwd_kv": "k_attn_bwd_kv", "proj_bwd": "k_proj_bwd"}
+
+
+def on_device(device):
+    """Makes `device` the calling thread's current device for one library call. The library runs on the device
+    of the stream it is given, but PyTorch's default stream is the null handle, which HIP resolves to the
+    thread's current device: a tensor on cuda:1 called while cuda:0 is current would otherwise launch on 0."""
+    import torch
+    if device.type != "cuda" or device.index is None or device.index == torch.cuda.current_device():
+        return contextlib.nullcontext()
+    return torch.cuda.device(device)
 
 
 class CsaProf(ctypes.Structure):

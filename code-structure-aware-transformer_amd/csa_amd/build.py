@@ -59,33 +59,57 @@ def shim_cmd():
             "-ltorch_hip", "-o", SHIM_OUT + ".tmp"]
 
 
+def shim_stamp(digest):
+    """What libcsa_torch.so depends on: the sources, and the torch it is compiled and linked against (its
+    headers, libraries and C++ ABI flag), so a torch upgrade rebuilds the shim even when csrc/ is unchanged."""
+    import torch
+    return f"{digest} torch={torch.__version__} cxx11abi={int(torch._C._GLIBCXX_USE_CXX11_ABI)}"
+
+
+def _read(path):
+    try:
+        with open(path) as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
 def build(force=False, verbose=True):
     srcs, deps = _deps()
     digest = source_hash()
-    if not force and os.path.exists(OUT) and os.path.exists(SHIM_OUT) and built_hash() == digest:
+    stamp = shim_stamp(digest)
+    lib_ok = not force and os.path.exists(OUT) and built_hash() == digest
+    shim_ok = not force and os.path.exists(SHIM_OUT) and _read(SHIM_OUT + ".stamp") == stamp
+    if lib_ok and shim_ok:
         return OUT
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
     objs = []
     procs = []
-    for s in srcs:
-        o = os.path.join(os.path.dirname(OUT), os.path.basename(s) + ".o")
-        cmd = [HIPCC] + FLAGS[:-3] + ["-c", "-fPIC", "-Wall", "-Wno-unused-result", f'-DCSA_SOURCE_HASH="{digest}"',
-                                      "-o", o, s]
-        cmd = [c for c in cmd if c != "-shared"]
-        procs.append((subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT), cmd))
-        objs.append(o)
-    procs.append((subprocess.Popen(shim_cmd(), stdout=subprocess.PIPE, stderr=subprocess.STDOUT), shim_cmd()))
+    if not lib_ok:
+        for s in srcs:
+            o = os.path.join(os.path.dirname(OUT), os.path.basename(s) + ".o")
+            cmd = [HIPCC] + FLAGS[:-3] + ["-c", "-fPIC", "-Wall", "-Wno-unused-result",
+                                          f'-DCSA_SOURCE_HASH="{digest}"', "-o", o, s]
+            cmd = [c for c in cmd if c != "-shared"]
+            procs.append((subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT), cmd))
+            objs.append(o)
+    if not shim_ok:
+        procs.append((subprocess.Popen(shim_cmd(), stdout=subprocess.PIPE, stderr=subprocess.STDOUT), shim_cmd()))
     for p, cmd in procs:
         out, _ = p.communicate()
         if p.returncode != 0:
             sys.stderr.write(out.decode())
             raise RuntimeError("hipcc failed: " + " ".join(cmd))
-    os.replace(SHIM_OUT + ".tmp", SHIM_OUT)
-    cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", OUT + ".tmp"] + objs
-    subprocess.check_call(cmd)
-    os.replace(OUT + ".tmp", OUT)
-    with open(OUT + ".sha256", "w") as f:
-        f.write(digest + "\n")
+    if not shim_ok:
+        os.replace(SHIM_OUT + ".tmp", SHIM_OUT)
+        with open(SHIM_OUT + ".stamp", "w") as f:
+            f.write(stamp + "\n")
+    if not lib_ok:
+        cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", OUT + ".tmp"] + objs
+        subprocess.check_call(cmd)
+        os.replace(OUT + ".tmp", OUT)
+        with open(OUT + ".sha256", "w") as f:
+            f.write(digest + "\n")
     if verbose:
         print("built", OUT)
     return OUT

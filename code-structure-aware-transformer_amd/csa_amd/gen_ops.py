@@ -4,7 +4,7 @@ import ctypes
 
 import torch
 
-from ._lib import check, lib
+from ._lib import check, lib, on_device
 from .ops import _draw_seed, _require_gpu, _stream
 
 
@@ -21,8 +21,9 @@ class GenLogSoftmax(torch.autograd.Function):
         rows = z.numel() // V if V else 0
         out = torch.empty_like(z)
         seed = _draw_seed() if p > 0.0 else 0
-        check(lib().csa_gen_logsoftmax_fwd(ctypes.c_void_p(z.data_ptr()), ctypes.c_void_p(out.data_ptr()), rows, V,
-                                           p, seed, 0, _stream(z.device)), "csa_gen_logsoftmax_fwd")
+        with on_device(z.device):
+            check(lib().csa_gen_logsoftmax_fwd(ctypes.c_void_p(z.data_ptr()), ctypes.c_void_p(out.data_ptr()), rows, V,
+                                               p, seed, 0, _stream(z.device)), "csa_gen_logsoftmax_fwd")
         ctx.save_for_backward(out)
         ctx.cfg = (rows, V, p, seed)
         return out
@@ -33,9 +34,10 @@ class GenLogSoftmax(torch.autograd.Function):
         rows, V, p, seed = ctx.cfg
         g = g.contiguous()
         dz = torch.empty_like(logp)
-        check(lib().csa_gen_logsoftmax_bwd(ctypes.c_void_p(g.data_ptr()), ctypes.c_void_p(logp.data_ptr()),
-                                           ctypes.c_void_p(dz.data_ptr()), rows, V, p, seed, 0, _stream(g.device)),
-              "csa_gen_logsoftmax_bwd")
+        with on_device(g.device):
+            check(lib().csa_gen_logsoftmax_bwd(ctypes.c_void_p(g.data_ptr()), ctypes.c_void_p(logp.data_ptr()),
+                                               ctypes.c_void_p(dz.data_ptr()), rows, V, p, seed, 0, _stream(g.device)),
+                  "csa_gen_logsoftmax_bwd")
         return dz, None
 
 

@@ -7,7 +7,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ._lib import check, lib
+from ._lib import check, lib, on_device
 
 
 def bias_grad(gy2: torch.Tensor) -> torch.Tensor:
@@ -17,8 +17,9 @@ def bias_grad(gy2: torch.Tensor) -> torch.Tensor:
     L = lib()
     ws = torch.empty(max(1, L.csa_bias_grad_workspace_bytes(rows, cols)), dtype=torch.uint8, device=gy2.device)
     stream = ctypes.c_void_p(torch.cuda.current_stream(gy2.device).cuda_stream)
-    check(L.csa_bias_grad(ctypes.c_void_p(gy2.data_ptr()), ctypes.c_void_p(db.data_ptr()), rows, cols, 0,
-                          ctypes.c_void_p(ws.data_ptr()), stream), "csa_bias_grad")
+    with on_device(gy2.device):
+        check(L.csa_bias_grad(ctypes.c_void_p(gy2.data_ptr()), ctypes.c_void_p(db.data_ptr()), rows, cols, 0,
+                              ctypes.c_void_p(ws.data_ptr()), stream), "csa_bias_grad")
     return db
 
 
@@ -147,8 +148,9 @@ class _LayerNormFn(torch.autograd.Function):
         stats = torch.empty(x2.shape[0], 2, device=x.device, dtype=torch.float32)
         stream = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
         p = lambda t: ctypes.c_void_p(t.data_ptr())
-        check(L.csa_layernorm_fwd(p(x2), p(w), p(b), p(y), p(stats), x2.shape[0], cols, eps, stream),
-              "csa_layernorm_fwd")
+        with on_device(x.device):
+            check(L.csa_layernorm_fwd(p(x2), p(w), p(b), p(y), p(stats), x2.shape[0], cols, eps, stream),
+                  "csa_layernorm_fwd")
         ctx.save_for_backward(x2, w, stats)
         return y.view(x.shape)
 
@@ -165,8 +167,9 @@ class _LayerNormFn(torch.autograd.Function):
                          device=x2.device)
         stream = ctypes.c_void_p(torch.cuda.current_stream(x2.device).cuda_stream)
         p = lambda t: ctypes.c_void_p(t.data_ptr())
-        check(L.csa_layernorm_bwd(p(gy2), p(x2), p(stats), p(w), p(dx), p(dw), p(db), rows, cols, p(ws), stream),
-              "csa_layernorm_bwd")
+        with on_device(x2.device):
+            check(L.csa_layernorm_bwd(p(gy2), p(x2), p(stats), p(w), p(dx), p(dw), p(db), rows, cols, p(ws), stream),
+                  "csa_layernorm_bwd")
         return dx.view(gy.shape), dw, db, None
 
 
@@ -294,9 +297,10 @@ class _ResidualDropoutFn(torch.autograd.Function):
         y = torch.empty_like(xm)
         seed = _draw_seed()
         p_ = lambda t: ctypes.c_void_p(t.data_ptr())
-        check(lib().csa_residual_dropout_fwd(p_(xm), p_(om), p_(y), y.numel(), p, seed, 0,
-                                             ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)),
-              "csa_residual_dropout_fwd")
+        with on_device(x.device):
+            check(lib().csa_residual_dropout_fwd(p_(xm), p_(om), p_(y), y.numel(), p, seed, 0,
+                                                 ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)),
+                  "csa_residual_dropout_fwd")
         ctx.cfg = (bm, p, seed)
         return y.transpose(0, 1) if bm else y
 
@@ -306,9 +310,10 @@ class _ResidualDropoutFn(torch.autograd.Function):
         g = (gy.transpose(0, 1) if bm else gy).contiguous()  # same memory order as the forward
         d_o = torch.empty_like(g)
         p_ = lambda t: ctypes.c_void_p(t.data_ptr())
-        check(lib().csa_residual_dropout_bwd(p_(g), p_(d_o), g.numel(), p, seed, 0,
-                                             ctypes.c_void_p(torch.cuda.current_stream(g.device).cuda_stream)),
-              "csa_residual_dropout_bwd")
+        with on_device(g.device):
+            check(lib().csa_residual_dropout_bwd(p_(g), p_(d_o), g.numel(), p, seed, 0,
+                                                 ctypes.c_void_p(torch.cuda.current_stream(g.device).cuda_stream)),
+                  "csa_residual_dropout_bwd")
         return gy, (d_o.transpose(0, 1) if bm else d_o), None
 
 
@@ -337,9 +342,10 @@ class _GeluDropoutFn(torch.autograd.Function):
         y = torch.empty_like(hm)
         seed = _draw_seed() if p > 0.0 else 0
         p_ = lambda t: ctypes.c_void_p(t.data_ptr())
-        check(lib().csa_gelu_dropout_fwd(p_(hm), p_(y), y.numel(), p, seed, 0,
-                                         ctypes.c_void_p(torch.cuda.current_stream(h.device).cuda_stream)),
-              "csa_gelu_dropout_fwd")
+        with on_device(h.device):
+            check(lib().csa_gelu_dropout_fwd(p_(hm), p_(y), y.numel(), p, seed, 0,
+                                             ctypes.c_void_p(torch.cuda.current_stream(h.device).cuda_stream)),
+                  "csa_gelu_dropout_fwd")
         ctx.save_for_backward(hm)
         ctx.cfg = (bm, p, seed)
         return y.transpose(0, 1) if bm else y
@@ -351,9 +357,10 @@ class _GeluDropoutFn(torch.autograd.Function):
         g = (gy.transpose(0, 1) if bm else gy).contiguous()
         dh = torch.empty_like(hm)
         p_ = lambda t: ctypes.c_void_p(t.data_ptr())
-        check(lib().csa_gelu_dropout_bwd(p_(g), p_(hm), p_(dh), g.numel(), p, seed, 0,
-                                         ctypes.c_void_p(torch.cuda.current_stream(g.device).cuda_stream)),
-              "csa_gelu_dropout_bwd")
+        with on_device(g.device):
+            check(lib().csa_gelu_dropout_bwd(p_(g), p_(hm), p_(dh), g.numel(), p, seed, 0,
+                                             ctypes.c_void_p(torch.cuda.current_stream(g.device).cuda_stream)),
+                  "csa_gelu_dropout_bwd")
         return (dh.transpose(0, 1) if bm else dh), None
 
 

@@ -99,8 +99,9 @@ _SCHED_OVERRIDE = {"0": "in_order", "1": "concurrent"}.get(os.environ.get("CSA_B
 
 
 def schedule_code(schedule: str) -> int:
-    """"auto" | "in_order" | "concurrent" -> CSA_SCHED_* (the CSA_BWD_CONCUR override wins)."""
-    s = _SCHED_OVERRIDE or schedule
+    """"auto" | "in_order" | "concurrent" -> CSA_SCHED_* (CSA_BWD_CONCUR overrides "auto" only: an explicit
+    schedule passed by the caller wins)."""
+    s = (_SCHED_OVERRIDE or schedule) if schedule == "auto" else schedule
     if s not in SCHEDULES:
         raise ValueError(f"bwd schedule must be one of {sorted(SCHEDULES)}, got {schedule!r}")
     return SCHEDULES[s]

@@ -72,7 +72,7 @@ class AdamW(torch.optim.Optimizer):
         return ent["desc"], ent["owner"], ent["start"], len(ps), ent["nchunks"]
 
     def _fused_step(self, gi, group, ps, grads, m, v, step_size, grad_scale=None, found_inf=None):
-        from ._lib import AdamwArgs, check, lib
+        from ._lib import AdamwArgs, check, lib, on_device
         for t in ps + grads + m + v:
             if t.dtype != torch.float32 or not t.is_contiguous():
                 raise RuntimeError("csa_adamw_step: parameters, grads and state must be contiguous fp32")
@@ -85,7 +85,8 @@ class AdamW(torch.optim.Optimizer):
                       grad_scale=None if grad_scale is None else grad_scale.data_ptr(),
                       found_inf=None if found_inf is None else found_inf.data_ptr())
         stream = ctypes.c_void_p(torch.cuda.current_stream(ps[0].device).cuda_stream)
-        check(lib().csa_adamw_step(ctypes.byref(a), stream), "csa_adamw_step")
+        with on_device(ps[0].device):
+            check(lib().csa_adamw_step(ctypes.byref(a), stream), "csa_adamw_step")
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -180,12 +181,31 @@ def use_tuned_gemms(on=True, path=GEMM_TABLE, tune=False):
         tunable.enable(False)
         return 0
     if not tune:
-        # results are written back to the current filename at exit: point it at a per-process scratch
-        # file, so concurrent ranks never rewrite the shared table
+        # results may be written back to the current filename at exit (this torch has no switch to turn that
+        # off): point it at a per-process scratch file, so concurrent ranks never rewrite the shared table,
+        # remove it at exit and sweep the scratch files of processes that are gone
+        import atexit
+        import glob
         import tempfile
-        tunable.set_filename(os.path.join(tempfile.gettempdir(), f"csa_tunableop_{os.getpid()}.csv"),
-                             insert_device_ordinal=False)
+        for f in glob.glob(os.path.join(tempfile.gettempdir(), "csa_tunableop_*.csv")):
+            try:
+                pid = int(os.path.basename(f)[len("csa_tunableop_"):-len(".csv")])
+                os.kill(pid, 0)
+            except ProcessLookupError:
+                _remove_quiet(f)
+            except (ValueError, PermissionError):
+                pass
+        scratch = os.path.join(tempfile.gettempdir(), f"csa_tunableop_{os.getpid()}.csv")
+        tunable.set_filename(scratch, insert_device_ordinal=False)
+        atexit.register(_remove_quiet, scratch)
     return len(tunable.get_results())
+
+
+def _remove_quiet(path):
+    try:
+        os.remove(path)
+    except OSError:
+        pass
 
 
 def set_bwd_schedule(model, schedule):

@@ -44,6 +44,14 @@ __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 acc) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
 }
 
+// v_mfma_f32_16x16x1_4b_f32 (exact fp32, four independent 16x16 blocks, K = 1 each, 32 cycles/SIMD: the same
+// rate per FLOP). Block b takes its operands from lanes 16b .. 16b+15 (A[i = l & 15], B[j = l & 15]); C/D
+// register 4b + e of lane l holds block b's D[4 (l >> 4) + e][l & 15] (tools/mfma_probe.hip). Used where one
+// product dimension is a 16-wide cluster index: a 32x32 tile would be half padding.
+__device__ __forceinline__ f32x16 mfma4b(float a, float b, f32x16 acc) {
+  return __builtin_amdgcn_mfma_f32_16x16x1f32(a, b, acc, 0, 0, 0);
+}
+
 // bf16 mode (CSA_DTYPE_BF16): the N^2 contractions run on v_mfma_f32_32x32x16_bf16 (16x the f32 MFMA
 // rate, fp32 accumulation). One instruction takes 8 consecutive K-steps of the f32 chains above from
 // each lane (lane half h, element j <-> K-step 8 s + j), so a chain keeps its K permutation and both

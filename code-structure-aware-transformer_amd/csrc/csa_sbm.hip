@@ -9,8 +9,10 @@
 //        k_attn_fwd          expA tile, u < clamp(expA) sampling, online softmax
 //                            with graph-masked L1 renormalisation, dropout, PV    sbm_attn.py:55-64, STE.py:10-15
 //        k_sparsity_finish   integer edge counts -> head-wise sparsity            sbm_attn.py:64
-//   bwd: k_attn_bwd_q        dQ (attention path), dQh, gamma = rowsum(dX*X)
-//        k_attn_bwd_kv       dK (attention path), dV, dT
+//   bwd: k_attn_gamma        gamma = rowsum(dX*X) (the F.normalize term)
+//        k_attn_bwd_kv       S, dP, the elementwise backward once per element; dK (attention path),
+//                            dV, dT; ds and G tiles to the workspace
+//        k_attn_bwd_qg       dQ (attention path) = ds K, dQh = G T from those tiles
 //        k_proj_bwd          STE/sigmoid/cluster/MLP backward (+dQ, +dK second path),
 //                            per-workgroup fixed-order partial slabs for dW, db, dC, dS
 //        k_param_reduce      fixed-order slab reduction, softmax_{k^2} backward -> dC
@@ -83,8 +85,8 @@ struct Layout {
   int64_t B, H, N, M, D, k, kp, KT, NQB, NKB, Mpad;
   size_t S, Qh, Kh, T, stats, Abits, Rbits, cnt, Wf[3], WfT[3], Cf, CfT, Sf, SfT, Act, total;
   // bwd workspace
-  size_t w_dQh, w_dT, w_slab, w_dS, w_dC, w_gx, w_total;
-  int64_t G, slab_floats;
+  size_t w_dQh, w_dT, w_slab, w_dS, w_dC, w_gx, w_dsg, w_total;
+  int64_t G, slab_floats, w_dsg_plane;
 };
 
 inline size_t al(size_t x) { return (x + 255) & ~size_t(255); }
@@ -143,6 +145,10 @@ Layout make_layout(int64_t B, int64_t H, int64_t N, int64_t M, int64_t D, int64_
   L.w_dS = take(sizeof(float) * H * KP32 * KP32);
   L.w_dC = take(sizeof(float) * H * KP32 * D);
   L.w_gx = take(sizeof(float) * B * H * N);  // used only when an attn-map gradient is passed
+  // ds and G (STE gradient) tiles handed from k_attn_bwd_kv to k_attn_bwd_qg: (b,h, query block, key block)
+  // 32 x 32 fp32 tiles [key][query]; G only with clusters
+  L.w_dsg_plane = B * H * L.NQB * L.NKB * 1024;
+  L.w_dsg = take(sizeof(float) * L.w_dsg_plane * (dense ? 1 : 2));
   L.w_total = o;
   return L;
 }
@@ -355,9 +361,9 @@ struct KArgs {
   const float *dX, *dsp, *dgraph, *dattn;  // dgraph / dattn: upstream grads of the returned maps (or null)
   float* gx;                               // dattn: per query row sum_j dattn_ij attn_ij (k_attn_gx)
   float *dQ, *dK, *dV, *dQh, *dT, *slab;
+  float* dsg; int64_t gplane;  // ds | G tiles (Layout::w_dsg), G at dsg + gplane
   int64_t dx_sb, dx_sh, dx_sn, dq_sb, dq_sh, dq_sn, dk_sb, dk_sh, dk_sn, dv_sb, dv_sh, dv_sn;
   int G; int64_t slab_floats;
-  int gamma_pre;  // stats[.][3] (gamma) written by k_attn_gamma: k_attn_bwd_q leaves it alone
 };
 
 // One 16-bit uniform per element: Philox word e/2, low half for even e.
@@ -1197,7 +1203,7 @@ __global__ __launch_bounds__(64) void k_maps(const KArgs p, float* __restrict__ 
 
 // gx[b,h,i] = sum_j dattn[b,h,i,j] * attn[b,h,i,j] for an upstream gradient of the returned attn map
 // (sbm_attn.py:62 F.normalize backward needs sum_j G_ij attn_ij over the TOTAL gradient G of attn; the
-// dX V^T part is rowsum(dX * X), computed by k_attn_bwd_q). Recomputes attn like k_maps (S orientation:
+// dX V^T part is rowsum(dX * X), computed by k_attn_gamma). Recomputes attn like k_maps (S orientation:
 // keys on lanes, queries in registers), one wave per (b, h, 32 queries); lane sums, then one reduction.
 template <int D, bool DENSE>
 __global__ __launch_bounds__(64) void k_attn_gx(const KArgs p) {
@@ -1249,10 +1255,9 @@ __global__ __launch_bounds__(64) void k_attn_gx(const KArgs p) {
   }
 }
 
-// gamma[b,h,i] = rowsum(dX * X) (+ gx) into stats[.][3], for k_attn_bwd_kv when it runs beside
-// k_attn_bwd_q on a second stream (launch_attn_bwd_v). Two lanes per row, each one half of the row in
-// k_attn_bwd_q's order (sequential fma over its 32 elements, then the two halves added), so both kernels
-// see the same gamma bit for bit. HBM-bound (2 x 256 B per row), it overlaps the MFMA-bound bwd_q.
+// gamma[b,h,i] = rowsum(dX * X) (+ gx) into stats[.][3], read by k_attn_bwd_kv's elementwise backward (the
+// F.normalize term of sbm_attn.py:62). Two lanes per row, each one half of the row (sequential fma over its
+// d/2 elements, then the two halves added). HBM-bound: 2 x 4d B per row.
 template <int D>
 __global__ __launch_bounds__(256) void k_attn_gamma(const KArgs p) {
   constexpr int NS = D / 2;
@@ -1308,9 +1313,9 @@ struct AttnBwdShape {
   static constexpr int KT = KPH == 0 ? 0 : (KP <= 32 ? 1 : KP / 32), KTA = KT > 0 ? KT : 1;
   static constexpr int IMG = SWZ ? 32 * 64 * 4 : 32 * DP * 4;  // one 32 x D image
   static constexpr int NIMG = 32 * KPN * 4;                    // one 32 x KP narrow image
-  // bwd_q: K | V | T | key bias row (Mpad floats)
-  static constexpr int QK = 0, QV = IMG, QT = 2 * IMG, QB = 2 * IMG + NIMG;
-  static size_t q_bytes(int Mpad) { return (size_t)QB + 4 * (size_t)Mpad; }
+  // bwd_qg: K | T
+  static constexpr int GK = 0, GT = IMG;
+  static constexpr size_t G_BYTES = (size_t)IMG + NIMG;
   // bwd_kv: Q | dX | Qh | stats (32 rows x 4)
   static constexpr int KQ = 0, KX = IMG, KH = 2 * IMG, KS = 2 * IMG + NIMG;
   static constexpr size_t KV_BYTES = (size_t)KS + 32 * 16;
@@ -1318,72 +1323,75 @@ struct AttnBwdShape {
 
 // key bias row in LDS: 0 for a valid key, -inf for a padded one or one beyond M (sbm_attn.py:61)
 
+// kp = 16 (k <= 16): the dQh / dT products run on mfma4b with the cluster index on the 16 lanes of a block
+// instead of 32x32 tiles with 16 (of 32) padded cluster rows: half the MFMA cycles. Lane (c, h) feeds the
+// blocks b = 2h + (c >> 4) with the operand values it holds anyway (row crow(r, h), its own column c); blocks
+// b and b + 2 then hold the two lane halves' partial sums for columns 16 b .. 16 b + 15.
+// Rows 16 b + (l & 15) (b = 0, 1) of a 32-row block, clusters 4 (l >> 4) .. + 3: the two halves added, stored
+// as one f32x4 per lane and block (rows >= nrows are skipped).
+__device__ __forceinline__ void store_mb4(float* __restrict__ out, int nrows, int kp, const f32x16& d) {
+  const int l = lane_id(), rr = l & 15, cl = 4 * (l >> 4);
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const int row = 16 * b + rr;
+    f32x4 v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = d[4 * b + e] + d[8 + 4 * b + e];
+    if (row < nrows) *reinterpret_cast<f32x4*>(out + (int64_t)row * kp + cl) = v;
+  }
+}
+
 // ------------------------------------------------------------------------------------
-// B2: per (b,h, query block), S^T orientation: dQ (attention path), dQh, gamma
+// B2: per (b,h, query block), S^T orientation (keys = accumulator K-steps, queries = lanes):
+//   dQ (attention path) = ds K, dQh = G T
+// from the ds / G tiles k_attn_bwd_kv computed in S orientation (Layout::w_dsg, [key][query] per tile), so
+// neither S = QK^T nor dP = dX V^T is recomputed here and the elementwise backward runs once per element.
+// Lane (c, h) reads its query's 16 values of a tile (keys crow(r,h)) with coalesced dword loads; the K tile
+// (SW_COL image: column reads only) and T tile arrive by LDS-DMA. The kernel streams 8 KB of ds / G per
+// tile from HBM against 48 MFMAs, so it runs four waves per SIMD (d = 64, k <= 16: <= 128 VGPRs, 10 KB of
+// LDS per wave): the ds / G registers are refilled right behind the MFMAs that read them and the K / T
+// operands are read from LDS just before their MFMAs, and the other waves' MFMAs cover the load latency.
 // ------------------------------------------------------------------------------------
-// DG: an upstream gradient of the graph and / or attn output is present (p.dgraph, p.dattn)
-template <int D, int KPH, bool DENSE, bool DROP, bool DG, bool BF>
-__global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd_q(const KArgs p) {
-#ifdef CSA_EXP_PRIO  // experiment: half of the waves (by dispatch slot parity) at priority 1
-  if ((blockIdx.x >> 3) & 1) __builtin_amdgcn_s_setprio(1);
-#endif
+template <int D, int KPH, bool DENSE, bool BF>
+__global__ __launch_bounds__(64, (D <= 64 && KPH <= 8) ? 4 : 2) void k_attn_bwd_qg(const KArgs p) {
   using SH = AttnBwdShape<D, KPH>;
-  constexpr int DT = D / 32, NS = D / 2, DP = SH::DP, KP = SH::KP, KPN = SH::KPN, KTA = SH::KTA;
+  constexpr int DT = D / 32, DP = SH::DP, KP = SH::KP, KPN = SH::KPN, KTA = SH::KTA;
   constexpr bool SWZ = SH::SWZ;
+  constexpr bool MB4 = !DENSE && KP == 16;  // dQh on mfma4b (store_mb4)
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  const uint32_t L0 = lds_offset(lds), Kl = L0 + SH::QK, Vl = L0 + SH::QV, Tl = L0 + SH::QT;
+  const uint32_t L0 = lds_offset(lds), Kl = L0 + SH::GK, Tl = L0 + SH::GT;
   const int lane = lane_id(), c = lane & 31, h = lane >> 5;
   const BhBlock xb = xcd_block(p.NQB, p.B * p.H);
   if (!xb.valid) return;
   const int qb = xb.blk, bh = xb.bh, b = bh / p.H, hd = bh % p.H;
   const int i = qb * 32 + c;
   const bool iv = i < p.N;
-  const int ic = imin(i, p.N - 1);
-  const int kld = (int)p.k_sn * 4, vld = (int)p.v_sn * 4;
+  const int kld = (int)p.k_sn * 4;
   const __amdgpu_buffer_rsrc_t kr = make_rsrc(p.K + b * p.k_sb + hd * p.k_sh, SWZ ? (p.M - 1) * kld + D * 4 : 0x7fffffff);
-  const __amdgpu_buffer_rsrc_t vr = make_rsrc(p.V + b * p.v_sb + hd * p.v_sh, SWZ ? (p.M - 1) * vld + D * 4 : 0x7fffffff);
   const __amdgpu_buffer_rsrc_t tr = make_rsrc(DENSE ? p.K : p.T + (int64_t)bh * p.M * p.kp, p.M * p.kp * 4);
-  // rows past M are never fetched: zero the images once so they only ever hold finite data
-  if constexpr (SWZ) lds_zero<(2 * SH::IMG + SH::NIMG) / 4>(lds);
-  else if constexpr (!DENSE) lds_zero<SH::NIMG / 4>(lds + SH::QT / 4);
-  const DmaPat kpat = dma_pat(SW_BOTH, kld), vpat = dma_pat(SW_ROW, vld);
-#define CSA_ISSUE_BQ(row0)                          \
-  do {                                              \
-    if constexpr (SWZ) {                            \
-      dma64(Kl, kr, kpat, kld, (row0));             \
-      dma64(Vl, vr, vpat, vld, (row0));             \
-    } else {                                        \
-      dma_rows<D>(Kl, kr, kld, (row0), p.M);        \
-      dma_rows<D>(Vl, vr, vld, (row0), p.M);        \
-    }                                               \
-    if constexpr (!DENSE) dma_narrow(Tl, tr, (row0), KPN); \
+  // rows past M are never fetched: zero the images once so they only ever hold finite data (those keys carry
+  // ds = G = 0 in the tiles)
+  if constexpr (SWZ) lds_zero<(SH::IMG + SH::NIMG) / 4>(lds);
+  else if constexpr (!DENSE) lds_zero<SH::NIMG / 4>(lds + SH::GT / 4);
+  const DmaPat kpat = dma_pat(SW_COL, kld);
+#define CSA_ISSUE_BQ(row0)                                  \
+  do {                                                      \
+    if constexpr (SWZ) dma64(Kl, kr, kpat, kld, (row0));    \
+    else dma_rows<D>(Kl, kr, kld, (row0), p.M);             \
+    if constexpr (!DENSE) dma_narrow(Tl, tr, (row0), KPN);  \
   } while (0)
-  const KeyMask km = key_mask_load(p, b);
-  CSA_ISSUE_BQ(0);
-  key_bias_store(lds + SH::QB / 4, p, b, km);
-  const int64_t wrow = ((int64_t)bh * p.NQB + qb) * p.Mpad + c;
-  uint32_t wAn = DENSE ? 0xffffffffu : p.Abits[wrow];
-  uint32_t wRn = DROP ? p.Rbits[wrow] : 0xffffffffu;
-  float q[NS], dx[NS];
-  load_run<NS>(q, p.Q + b * p.q_sb + hd * p.q_sh + (int64_t)ic * p.q_sn + h * NS, iv);
-  load_run<NS>(dx, p.dX + b * p.dx_sb + hd * p.dx_sh + (int64_t)ic * p.dx_sn + h * NS, iv);
-  float gp = 0.f;
-  {
-    float xr[NS];
-    load_run<NS>(xr, p.X + b * p.x_sb + hd * p.x_sh + (int64_t)ic * p.x_sn + h * NS, iv);
+  // element (key crow(r,h), query c) of tile kt: tb + kt * 1024 + 32 crow(r,h)
+  const float* tb = p.dsg + ((int64_t)bh * p.NQB + qb) * p.NKB * 1024 + c;
+  float dsv[16], gv[16];
+  auto load_tile = [&](int kt) {
 #pragma unroll
-    for (int s = 0; s < NS; ++s) gp = fmaf(dx[s], xr[s], gp);
-  }
-  // gamma = sum_j G_ij attn_ij with G the total upstream gradient of attn: rowsum(dX * X) plus, with an
-  // attn-map gradient, sum_j dattn_ij attn_ij (k_attn_gx)
-  const float gamma = xhalf_sum(gp) + ((DG && p.dattn) ? p.gx[(int64_t)bh * p.N + ic] : 0.f);
-  f32x4 st = *reinterpret_cast<const f32x4*>(p.stats + ((int64_t)bh * p.N + ic) * 4);
-  if (iv && h == 0 && !p.gamma_pre) p.stats[((int64_t)bh * p.N + i) * 4 + 3] = gamma;
-  const float lse = st[0], invD = st[1], big = st[2];
-  const float dscale = DROP ? 1.f / (1.f - p.attn_p) : 1.f;
-  const float csp = (!DENSE && p.dsp) ? p.dsp[hd] / ((float)p.B * (float)p.N * (float)p.M) : 0.f;
-  const float c1 = p.scale * LOG2E, c0 = -lse * LOG2E;  // per-row constants of the elementwise below
-  const float rho = (big != 0.f) ? 0.f : gamma, gsel = (big != 0.f) ? gamma : 0.f;
+    for (int r = 0; r < 16; ++r) {
+      dsv[r] = tb[kt * 1024 + 32 * crow(r, h)];
+      if constexpr (!DENSE) gv[r] = tb[p.gplane + kt * 1024 + 32 * crow(r, h)];
+    }
+  };
+  CSA_ISSUE_BQ(0);
+  load_tile(0);
   f32x16 dq[DT], dqh[KTA];
 #pragma unroll
   for (int t = 0; t < DT; ++t) dq[t] = zero16();
@@ -1393,118 +1401,53 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
     int ln = threadIdx.x;  // opaque per iteration: keeps the per-row LDS addresses out of the prologue
     asm volatile("" : "+v"(ln));
     const int c = ln & 31, h = (ln >> 5) & 1;
-    const int j0 = kt * 32;
-    wait_vm_all();  // tile kt's K/V/T images and its bit words have landed
-    const uint32_t wA = wAn, wR = wRn;
-    f32x16 sacc = zero16(), dpacc = zero16();
-    const int kb = SWZ ? row_base64(c, h, SW_BOTH) : 4 * (c * DP + NS * h);
-    const int vb = SH::QV + (SWZ ? row_base64(c, h, SW_ROW) : 4 * (c * DP + NS * h));
-    if constexpr (BF) {
-#pragma unroll
-      for (int j2 = 0; j2 < NS / 8; ++j2) {
-        const f32x4 k0 = lds_f4(lds, SWZ ? (kb ^ (32 * j2)) : kb + 32 * j2);
-        const f32x4 k1 = lds_f4(lds, SWZ ? (kb ^ (32 * j2 + 16)) : kb + 32 * j2 + 16);
-        sacc = mfma_bf(pack8(k0, k1), pack8(&q[8 * j2]), sacc);
-        const f32x4 v0 = lds_f4(lds, SWZ ? (vb ^ (32 * j2)) : vb + 32 * j2);
-        const f32x4 v1 = lds_f4(lds, SWZ ? (vb ^ (32 * j2 + 16)) : vb + 32 * j2 + 16);
-        dpacc = mfma_bf(pack8(v0, v1), pack8(&dx[8 * j2]), dpacc);
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < NS / 4; ++j) {
-        const f32x4 kv = lds_f4(lds, SWZ ? (kb ^ (16 * j)) : kb + 16 * j);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) sacc = mfma(kv[e], q[4 * j + e], sacc);
-      }
-#pragma unroll
-      for (int j = 0; j < NS / 4; ++j) {
-        const f32x4 vv = lds_f4(lds, SWZ ? (vb ^ (16 * j)) : vb + 16 * j);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) dpacc = mfma(vv[e], dx[4 * j + e], dpacc);
-      }
-    }
-    // transposed operands of this tile's dQ / dQh products (lane d holds K[key crow(r,h)][d])
-    float kT[DT][16], tT[KTA][16];
+    const bool more = kt + 1 < p.NKB;
+    wait_vm_all();  // tile kt's K / T images and ds / G values have landed
+    // dQ^T += K^T ds^T (lane d holds K[key crow(r,h)][d], read from the SW_COL / padded image per K-step)
 #pragma unroll
     for (int t = 0; t < DT; ++t) {
-      const int tb = SWZ ? both_base64(t, c, h) : 4 * (32 * t + c) + 16 * DP * h;
+      const int cb = SH::GK + (SWZ ? col_base64(t, c, h) : 4 * (32 * t + c) + 16 * DP * h);
+      float kT[16];
 #pragma unroll
-      for (int r = 0; r < 16; ++r)
-        kT[t][r] = SWZ ? both_read(lds, tb, r, SH::QK) : lds_f1(lds, tb + 4 * DP * crow(r, 0));
+      for (int r = 0; r < 16; ++r) kT[r] = lds_f1(lds, cb + (SWZ ? 256 * crow(r, 0) : 4 * DP * crow(r, 0)));
+      if constexpr (BF) {
+        dq[t] = mfma_bf(pack8(&kT[0]), pack8(&dsv[0]), dq[t]);
+        dq[t] = mfma_bf(pack8(&kT[8]), pack8(&dsv[8]), dq[t]);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dq[t] = mfma(kT[r], dsv[r], dq[t]);
+      }
     }
-    if constexpr (!DENSE) {
+    // dQh^T += T^T G^T
+    if constexpr (MB4) {  // lane (c, h): T[key crow(r,h)][cluster c & 15]
+      float tT[16];
 #pragma unroll
-      for (int at = 0; at < KTA; ++at)
+      for (int r = 0; r < 16; ++r) tT[r] = lds_f1(lds, SH::GT + narrow_elem(crow(r, h), c & 15, KPN));
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dqh[0] = mfma4b(tT[r], gv[r], dqh[0]);
+    } else if constexpr (!DENSE) {
+#pragma unroll
+      for (int at = 0; at < KTA; ++at) {
+        float tT[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float v = lds_f1(lds, SH::QT + narrow_elem(crow(r, h), imin(32 * at + c, KP - 1), KPN));
-          tT[at][r] = (KP >= 32 || c < KP) ? v : 0.f;
+          const float v = lds_f1(lds, SH::GT + narrow_elem(crow(r, h), imin(32 * at + c, KP - 1), KPN));
+          tT[r] = (KP >= 32 || c < KP) ? v : 0.f;
         }
-    }
-    f32x4 bz[4];  // key bias of registers 4g..4g+3
 #pragma unroll
-    for (int g = 0; g < 4; ++g) bz[g] = lds_f4(lds, SH::QB + 4 * (j0 + 8 * g + 4 * h));
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (kt + 1 < p.NKB) {  // tile kt+1 streams in under the elementwise work and the products below
-      CSA_ISSUE_BQ(j0 + 32);
-      if constexpr (!DENSE) wAn = p.Abits[wrow + j0 + 32];
-      if constexpr (DROP) wRn = p.Rbits[wrow + j0 + 32];
-    }
-    // Elementwise backward (bwd_elem's algebra, oracle/closed_form.py) with the row's constants folded:
-    // P = exp2(s c1 + kb + c0), kb = 0 / -inf (P = 0 on masked and padded keys, so ds vanishes there without
-    // a test). A query row past N computes lane-local garbage: its dQ / dQh rows are never stored.
-    float dsv[16], gv[16];
-    const int nvk = p.M - j0 - 4 * h;  // key crow(r,h) = j0 + crow(r,0) + 4h is < M iff crow(r,0) < nvk
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int jj = crow(r, h), j = j0 + jj;
-#ifdef CSA_EXP_NO_SHFL
-      const uint32_t a_w = DENSE ? 0xffffffffu : wA ^ jj;
-      const uint32_t r_w = DROP ? wR ^ jj : 0xffffffffu;
-#else
-      const uint32_t a_w = DENSE ? 0xffffffffu : (uint32_t)__shfl((int)wA, jj, 64);
-      const uint32_t r_w = DROP ? (uint32_t)__shfl((int)wR, jj, 64) : 0xffffffffu;
-#endif
-      const bool in = crow(r, 0) < nvk;
-      const bool a = DENSE ? in : ((a_w >> c) & 1u);
-      float dattn = ((r_w >> c) & 1u) ? dpacc[r] * dscale : 0.f;
-      float dgr = 0.f;
-      if constexpr (DG) {
-        const bool inside = iv && (j < p.M);
-        const int64_t me = ((int64_t)bh * p.N + ic) * p.M + imin(j, p.M - 1);
-        dgr = p.dgraph ? ldz(p.dgraph, me, INT64_MAX, inside) : 0.f;
-        dattn += p.dattn ? ldz(p.dattn, me, INT64_MAX, inside) : 0.f;
+        for (int r = 0; r < 16; ++r) dqh[at] = mfma(tT[r], gv[r], dqh[at]);
       }
-      const float P = __builtin_amdgcn_exp2f(fmaf(sacc[r], c1, bz[r >> 2][r & 3] + c0));
-      const float dM = (dattn - ((a && P > 0.f) ? gsel : 0.f)) * invD;  // sign(M) of F.normalize
-      dsv[r] = P * ((a ? dM : 0.f) - rho) * p.scale;
-      const float dA = fmaf(dM, P, csp + dgr);
-      gv[r] = (a && in) ? __builtin_amdgcn_fmed3f(dA, -1.f, 1.f) : 0.f;  // STE.py:19 hardtanh(A * grad)
     }
-    // dQ^T += K^T ds^T ; dQh^T += T^T G^T  (keys beyond M carry ds = G = 0)
-    if constexpr (BF) {
-      const bf16x8 s0 = pack8(&dsv[0]), s1 = pack8(&dsv[8]);
-#pragma unroll
-      for (int t = 0; t < DT; ++t) {
-        dq[t] = mfma_bf(pack8(&kT[t][0]), s0, dq[t]);
-        dq[t] = mfma_bf(pack8(&kT[t][8]), s1, dq[t]);
-      }
-    } else {
-#pragma unroll
-      for (int t = 0; t < DT; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) dq[t] = mfma(kT[t][r], dsv[r], dq[t]);
-    }
-    if constexpr (!DENSE) {
-#pragma unroll
-      for (int at = 0; at < KTA; ++at)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) dqh[at] = mfma(tT[at][r], gv[r], dqh[at]);
+    if (more) {  // images read out and ds / G consumed by the MFMAs above: tile kt+1 streams in
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      CSA_ISSUE_BQ(kt * 32 + 32);
+      load_tile(kt + 1);
     }
   }
 #undef CSA_ISSUE_BQ
   store_rows<DT>(p.dQ + b * p.dq_sb + hd * p.dq_sh + (int64_t)i * p.dq_sn, D, D, dq, iv);
-  if constexpr (!DENSE) store_rows<KTA>(p.dQh + ((int64_t)bh * p.N + i) * p.kp, p.kp, p.kp, dqh, iv);
+  if constexpr (MB4) store_mb4(p.dQh + ((int64_t)bh * p.N + qb * 32) * p.kp, p.N - qb * 32, p.kp, dqh[0]);
+  else if constexpr (!DENSE) store_rows<KTA>(p.dQh + ((int64_t)bh * p.N + i) * p.kp, p.kp, p.kp, dqh, iv);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1518,6 +1461,11 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
   using SH = AttnBwdShape<D, KPH>;
   constexpr int DT = D / 32, NS = D / 2, DP = SH::DP, KP = SH::KP, KPN = SH::KPN, KTA = SH::KTA;
   constexpr bool SWZ = SH::SWZ;
+#ifdef CSA_EXP_NO_MB4
+  constexpr bool MB4 = false;
+#else
+  constexpr bool MB4 = !DENSE && KP == 16;  // dT on mfma4b (store_mb4)
+#endif
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const uint32_t L0 = lds_offset(lds), Ql = L0 + SH::KQ, Xl = L0 + SH::KX, Hl = L0 + SH::KH, Sl = L0 + SH::KS;
   const int lane = lane_id(), c = lane & 31, h = lane >> 5;
@@ -1551,6 +1499,9 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
   const float* mk = p.mask ? p.mask + b * p.mask_sb : nullptr;
   const float mval = mk ? mk[jc] : 0.f;
   const float kbias = (jv && mval == 0.f) ? 0.f : NEG_INF;  // this lane's key (sbm_attn.py:61)
+  const float jvf = jv ? 1.f : 0.f;  // G of a key past M is stored as 0 (its sampled bit may be set)
+  // this lane's row (key j) of the ds / G tiles handed to k_attn_bwd_qg, tile (qb, kbi) at + qb * NKB * 1024
+  float* dsw = p.dsg + ((int64_t)bh * p.NQB * p.NKB + kbi) * 1024 + c * 32 + 4 * h;
   float kr[NS], vr[NS];
   load_run<NS>(kr, p.K + b * p.k_sb + hd * p.k_sh + (int64_t)jc * p.k_sn + h * NS, jv);
   load_run<NS>(vr, p.V + b * p.v_sb + hd * p.v_sh + (int64_t)jc * p.v_sn + h * NS, jv);
@@ -1650,15 +1601,34 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
         const f2 dM2 = __builtin_elementwise_fma(mpos, -gsel, dattn2) * invD2;
         const f2 ds2 = P2 * (dM2 * af - rho) * (p.scale * inf);
         const f2 dA2 = __builtin_elementwise_fma(dM2, P2, dgr2 + csp);
-        const f2 ain = af * inf;
+        const f2 ain = af * inf * jvf;
         const f2 aw2 = P2 * invD2 * rmf * ain;  // dropout(attn) weight for dV
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
           dsv[rr + u] = ds2[u];
           gv[rr + u] = __builtin_amdgcn_fmed3f(dA2[u], -1.f, 1.f) * ain[u];  // STE.py:19 hardtanh(A * grad)
           awv[rr + u] = aw2[u];
+#ifdef CSA_EXP_NO_ELEM  // experiment: timing without the elementwise algebra (wrong results)
+          dsv[rr + u] = sacc[r0 + u] * dpacc[r0 + u];
+          gv[rr + u] = dpacc[r0 + u];
+          awv[rr + u] = sacc[r0 + u];
+#endif
         }
       }
+#ifndef CSA_EXP_NO_DSG_STORE  // experiment: timing without the ds / G stores (wrong results)
+      {  // queries 16 half + 4 h + (0..3) and + 8: two f32x4 per tile, for ds and for G
+        float* w = dsw + (int64_t)qb * p.NKB * 1024 + 16 * half;
+        // non-temporal: the tiles are read once, by the next kernel (same-box A/B: k_attn_bwd_qg 157 -> 134 us)
+#define CSA_ST4(ptr, val) __builtin_nontemporal_store((val), reinterpret_cast<f32x4*>(ptr))
+        CSA_ST4(w, (f32x4{dsv[0], dsv[1], dsv[2], dsv[3]}));
+        CSA_ST4(w + 8, (f32x4{dsv[4], dsv[5], dsv[6], dsv[7]}));
+        if constexpr (!DENSE) {
+          CSA_ST4(w + p.gplane, (f32x4{gv[0], gv[1], gv[2], gv[3]}));
+          CSA_ST4(w + p.gplane + 8, (f32x4{gv[4], gv[5], gv[6], gv[7]}));
+        }
+#undef CSA_ST4
+      }
+#endif
       // dV^T += dX^T attw ; dK^T += Q^T ds ; dT^T += Qh^T G  (queries beyond N carry zeros)
       if constexpr (BF) {
         const bf16x8 aw8 = pack8(awv), ds8 = pack8(dsv);
@@ -1680,7 +1650,11 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
 #pragma unroll
           for (int rr = 0; rr < 8; ++rr) dk[t] = mfma(colv(SH::KQ, t, 8 * half + rr), dsv[rr], dk[t]);
       }
-      if constexpr (!DENSE) {
+      if constexpr (MB4) {  // lane (c, h): Qh[query crow(r,h)][cluster c & 15]
+#pragma unroll
+        for (int rr = 0; rr < 8; ++rr)
+          dtt[0] = mfma4b(lds_f1(lds, SH::KH + narrow_elem(crow(8 * half + rr, h), c & 15, KPN)), gv[rr], dtt[0]);
+      } else if constexpr (!DENSE) {
 #pragma unroll
         for (int at = 0; at < KTA; ++at)
 #pragma unroll
@@ -1690,7 +1664,11 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
             dtt[at] = mfma((KP >= 32 || c < KP) ? v : 0.f, gv[rr], dtt[at]);
           }
       }
+#ifdef CSA_EXP_NO_LOOP_DMA  // experiment: timing without the in-loop refills (wrong results)
+      if (false) {
+#else
       if (more) {
+#endif
         if constexpr (SWZ) {  // rows 16 half .. 16 half + 15 of every image are free again
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           dma64(Xl, xr_, xpat, xld, i0 + 32, 4 * half, 4 * half + 4);
@@ -1709,7 +1687,8 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
   }
   store_rows<DT>(p.dK + b * p.dk_sb + hd * p.dk_sh + (int64_t)j * p.dk_sn, D, D, dk, jv);
   store_rows<DT>(p.dV + b * p.dv_sb + hd * p.dv_sh + (int64_t)j * p.dv_sn, D, D, dv, jv);
-  if constexpr (!DENSE) store_rows<KTA>(p.dT + ((int64_t)bh * p.M + j) * p.kp, p.kp, p.kp, dtt, jv);
+  if constexpr (MB4) store_mb4(p.dT + ((int64_t)bh * p.M + kbi * 32) * p.kp, p.M - kbi * 32, p.kp, dtt[0]);
+  else if constexpr (!DENSE) store_rows<KTA>(p.dT + ((int64_t)bh * p.M + j) * p.kp, p.kp, p.kp, dtt, jv);
 }
 
 // ------------------------------------------------------------------------------------
@@ -2912,77 +2891,40 @@ csa_status launch_fwd(const csa_sbm_fwd_args* a, const Layout& L, hipStream_t st
   return check_launch("csa_sbm_fwd");
 }
 
-// Returns false when a fork/join event operation failed (nothing is launched on the side stream when
-// the fork fails; a failed join leaves the caller's stream unordered behind the side stream).
+// gamma, then k_attn_bwd_kv (the elementwise backward; ds / G tiles out), then k_attn_bwd_qg, in stream order.
 template <int D, int KPH, bool DENSE, bool DROP, bool DG, bool BF>
-bool launch_attn_bwd_v(const KArgs& p0, int BH, const Layout& L, const csa_prof* pf, const SideLane* side,
-                       hipStream_t st) {
+void launch_attn_bwd_v(const KArgs& p, int BH, const Layout& L, const csa_prof* pf, hipStream_t st) {
   using SH = AttnBwdShape<D, KPH>;
-  KArgs p = p0;
-  const size_t q_lds = SH::q_bytes((int)L.Mpad);
-  if (q_lds > 64 * 1024) set_dyn_lds((const void*)k_attn_bwd_q<D, KPH, DENSE, DROP, DG, BF>, (int)q_lds);
-  if (side) {  // fork: gamma + bwd_kv on the side stream, bwd_q here, join before the projection backward
-    if (!side->fork(st)) return false;
-    p.gamma_pre = 1;
-    {
-      Stage sg(pf, CSA_STAGE_ATTN_BWD_KV, side->s);
-      const int64_t threads = 2LL * BH * p.N;
-      hipLaunchKernelGGL(k_attn_gamma<D>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, side->s, p);
-      hipLaunchKernelGGL((k_attn_bwd_kv<D, KPH, DENSE, DROP, DG, BF>), dim3(xcd_grid((int)L.NKB, BH)), dim3(64),
-                         SH::KV_BYTES, side->s, p);
-    }
-    {
-      Stage sg(pf, CSA_STAGE_ATTN_BWD_Q, st);
-      hipLaunchKernelGGL((k_attn_bwd_q<D, KPH, DENSE, DROP, DG, BF>), dim3(xcd_grid((int)L.NQB, BH)), dim3(64),
-                         q_lds, st, p);
-    }
-    return side->join(st);
-  }
   {
-    Stage sg(pf, CSA_STAGE_ATTN_BWD_Q, st);
-    hipLaunchKernelGGL((k_attn_bwd_q<D, KPH, DENSE, DROP, DG, BF>), dim3(xcd_grid((int)L.NQB, BH)), dim3(64),
-                       q_lds, st, p);
+    Stage sg(pf, CSA_STAGE_ATTN_BWD_KV, st);
+    const int64_t threads = 2LL * BH * p.N;
+    hipLaunchKernelGGL(k_attn_gamma<D>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, p);
+    hipLaunchKernelGGL((k_attn_bwd_kv<D, KPH, DENSE, DROP, DG, BF>), dim3(xcd_grid((int)L.NKB, BH)), dim3(64),
+                       SH::KV_BYTES, st, p);
   }
-  Stage sg(pf, CSA_STAGE_ATTN_BWD_KV, st);
-  hipLaunchKernelGGL((k_attn_bwd_kv<D, KPH, DENSE, DROP, DG, BF>), dim3(xcd_grid((int)L.NKB, BH)), dim3(64),
-                     SH::KV_BYTES, st, p);
-  return true;
+  Stage sg(pf, CSA_STAGE_ATTN_BWD_Q, st);
+  hipLaunchKernelGGL((k_attn_bwd_qg<D, KPH, DENSE, BF>), dim3(xcd_grid((int)L.NQB, BH)), dim3(64), SH::G_BYTES, st, p);
 }
 
 template <int D, int KPH, bool DENSE, bool BF>
-bool launch_attn_bwd_b(const KArgs& p, int BH, const Layout& L, bool drop, const csa_prof* pf, const SideLane* side,
-                       hipStream_t st) {
+void launch_attn_bwd_b(const KArgs& p, int BH, const Layout& L, bool drop, const csa_prof* pf, hipStream_t st) {
   const bool dg = p.dgraph != nullptr || p.dattn != nullptr;
-  if (p.dattn)  // sum_j dattn_ij attn_ij per query row, read by k_attn_bwd_q's gamma
+  if (p.dattn)  // sum_j dattn_ij attn_ij per query row, added to gamma by k_attn_gamma
     hipLaunchKernelGGL((k_attn_gx<D, DENSE>), dim3(xcd_grid((int)L.NQB, BH)), dim3(64), 0, st, p);
   if (drop) {
-    if (dg) return launch_attn_bwd_v<D, KPH, DENSE, true, true, BF>(p, BH, L, pf, side, st);
-    return launch_attn_bwd_v<D, KPH, DENSE, true, false, BF>(p, BH, L, pf, side, st);
+    if (dg) return launch_attn_bwd_v<D, KPH, DENSE, true, true, BF>(p, BH, L, pf, st);
+    return launch_attn_bwd_v<D, KPH, DENSE, true, false, BF>(p, BH, L, pf, st);
   }
-  if (dg) return launch_attn_bwd_v<D, KPH, DENSE, false, true, BF>(p, BH, L, pf, side, st);
-  return launch_attn_bwd_v<D, KPH, DENSE, false, false, BF>(p, BH, L, pf, side, st);
+  if (dg) return launch_attn_bwd_v<D, KPH, DENSE, false, true, BF>(p, BH, L, pf, st);
+  return launch_attn_bwd_v<D, KPH, DENSE, false, false, BF>(p, BH, L, pf, st);
 }
 
-// side: the caller's fork/join lane when the schedule puts the key half beside the query half, else null
 template <int D, int KPH, bool DENSE>
-bool launch_attn_bwd(const KArgs& p, int BH, const Layout& L, bool drop, const csa_prof* pf, const SideLane* side,
-                     hipStream_t st) {
+void launch_attn_bwd(const KArgs& p, int BH, const Layout& L, bool drop, const csa_prof* pf, hipStream_t st) {
   if constexpr (KPH <= 8) {
-    if (p.bf16) return launch_attn_bwd_b<D, KPH, DENSE, true>(p, BH, L, drop, pf, side, st);
+    if (p.bf16) return launch_attn_bwd_b<D, KPH, DENSE, true>(p, BH, L, drop, pf, st);
   }
-  return launch_attn_bwd_b<D, KPH, DENSE, false>(p, BH, L, drop, pf, side, st);
-}
-
-// The caller's side lane if csa_sbm_bwd_args.schedule (and, for CSA_SCHED_AUTO, the grid shape) asks for
-// the concurrent backward, else null.
-template <int D, int KPH>
-const SideLane* pick_side(const csa_sbm_bwd_args* b, const Layout& L, SideLane& lane, hipStream_t st) {
-  if (!b->side_stream || !b->side_fork || !b->side_join) return nullptr;
-  const int64_t wgs = L.NQB * L.B * L.H;
-  if (!bwd_concurrent(b->schedule, b->side_stream, stream_device(st), wgs, (D <= 64 && KPH <= 16) ? 2 : 1))
-    return nullptr;
-  lane = SideLane{(hipStream_t)b->side_stream, (hipEvent_t)b->side_fork, (hipEvent_t)b->side_join};
-  return &lane;
+  return launch_attn_bwd_b<D, KPH, DENSE, false>(p, BH, L, drop, pf, st);
 }
 
 template <int D, int KPH, int KT>
@@ -3007,14 +2949,12 @@ csa_status launch_bwd(const csa_sbm_bwd_args* b, const Layout& L, hipStream_t st
   p.dT = (float*)((char*)b->workspace + L.w_dT);
   p.slab = (float*)((char*)b->workspace + L.w_slab);
   p.G = (int)L.G; p.slab_floats = L.slab_floats;
+  p.dsg = (float*)((char*)b->workspace + L.w_dsg); p.gplane = L.w_dsg_plane;
   const int BH = (int)(a->B * a->H);
   (void)dense;
   const csa_prof* pf = b->prof;
-  SideLane lane;
-  const SideLane* side = pick_side<D, KPH>(b, L, lane, st);
   if constexpr (KT > 0) {
-    if (!launch_attn_bwd<D, KPH, false>(p, BH, L, a->attn_dropout > 0.f, pf, side, st))
-      return fail_hip("csa_sbm_bwd: side-stream fork/join");
+    launch_attn_bwd<D, KPH, false>(p, BH, L, a->attn_dropout > 0.f, pf, st);
     using Sh = ProjBwdShape<D, KT>;
     if (!Sh::REGACC && hipMemsetAsync(p.slab, 0, sizeof(float) * a->H * L.G * L.slab_floats, st) != hipSuccess)
       return check_launch("memset slabs");
@@ -3045,8 +2985,7 @@ csa_status launch_bwd(const csa_sbm_bwd_args* b, const Layout& L, hipStream_t st
     hipLaunchKernelGGL(k_cluster_grad, dim3((unsigned)a->k, (unsigned)a->H), dim3(128), 0, st, p.S, (const float*)dS_ws,
                        (const float*)dC_ws, a->cluster_w, b->dcluster_w, (int)a->k, D, KP32);
   } else {
-    if (!launch_attn_bwd<D, 0, true>(p, BH, L, a->attn_dropout > 0.f, pf, side, st))
-      return fail_hip("csa_sbm_bwd: side-stream fork/join");
+    launch_attn_bwd<D, 0, true>(p, BH, L, a->attn_dropout > 0.f, pf, st);
   }
   return check_launch("csa_sbm_bwd");
 }
@@ -3125,8 +3064,7 @@ csa_status csa_sbm_bwd(const csa_sbm_bwd_args* b, void* stream) {
   if (s != CSA_OK) return s;
   const csa_sbm_fwd_args* a = b->fwd;
   const bool dense = a->flags & CSA_FLAG_DENSE;
-  if (!b->dX || !b->dQ || !b->dK || !b->dV || ((!dense || b->dattn) && !b->workspace))
-    return fail(CSA_INVALID_ARG, "null dX/dQ/dK/dV/workspace (the workspace is required unless DENSE without dattn)");
+  if (!b->dX || !b->dQ || !b->dK || !b->dV || !b->workspace) return fail(CSA_INVALID_ARG, "null dX/dQ/dK/dV/workspace");
   {
     auto al16 = [](const void* ptr, int64_t sb, int64_t sh, int64_t sn) {
       return (((uintptr_t)ptr) % 16 == 0) && sb % 4 == 0 && sh % 4 == 0 && sn % 4 == 0;

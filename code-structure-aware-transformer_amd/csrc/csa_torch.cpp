@@ -10,10 +10,12 @@
 //   ste_sample / ste_backward       SampleGraphSparseGraph (module/STE.py:8-19)
 //   rel_attn_fwd / rel_attn_bwd     DisentangledAttn.rel_attn (module/disentangled_attn.py:44-65)
 #include <ATen/ATen.h>
+#include <ATen/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
 #include <torch/library.h>
 
+#include <memory>
 #include <mutex>
 #include <vector>
 
@@ -32,6 +34,9 @@ void check(csa_status s, const char* what) {
   TORCH_CHECK(s == CSA_OK, what, " failed: ", csa_status_str(s), ": ", csa_last_error_str());
 }
 
+// The current stream of t's device. PyTorch's default stream has a null handle, which the library resolves to
+// the calling thread's current device: every op therefore opens a device guard on its first tensor
+// (OptionalDeviceGuard below) before it reads the stream, as codegen'd ATen ops do.
 void* cur_stream(const Tensor& t) { return (void*)c10::hip::getCurrentHIPStream(t.device().index()).stream(); }
 
 void require_gpu(const Tensor& t, const char* name) {
@@ -57,13 +62,15 @@ Tensor head_major_out(int64_t B, int64_t H, int64_t N, int64_t d, const at::Tens
 }
 
 // caller-owned side lane of a device (ABI v5): one non-blocking stream and two timing-free events, created
-// on first use and kept for the process lifetime
-struct Lane { void* s; void* fork; void* join; };
+// on first use and kept for the process lifetime, plus the mutex a call holds from its fork to its join (two
+// host threads sharing a device's lane could otherwise interleave their event records)
+struct Lane { void* s; void* fork; void* join; std::mutex* mu; };
 Lane side_lane(int dev) {
   static std::mutex mu;
   static std::vector<Lane> lanes;
+  static std::vector<std::unique_ptr<std::mutex>> call_mu;
   std::lock_guard<std::mutex> lock(mu);
-  if ((int)lanes.size() <= dev) lanes.resize(dev + 1, Lane{nullptr, nullptr, nullptr});
+  if ((int)lanes.size() <= dev) lanes.resize(dev + 1, Lane{nullptr, nullptr, nullptr, nullptr});
   Lane& l = lanes[dev];
   if (!l.s) {
     int prev = -1;
@@ -75,17 +82,20 @@ Lane side_lane(int dev) {
                     hipEventCreateWithFlags(&j, hipEventDisableTiming) == hipSuccess;
     (void)hipSetDevice(prev);
     TORCH_CHECK(ok, "csa side lane: stream / event creation failed");
-    l = Lane{(void*)s, (void*)f, (void*)j};
+    call_mu.emplace_back(new std::mutex());
+    l = Lane{(void*)s, (void*)f, (void*)j, call_mu.back().get()};
   }
   return l;
 }
+// Hands the device's side lane to b unless the schedule is in order; the returned lock (empty when no lane
+// is handed over) must be held until the library call that uses the lane has returned.
 template <typename Args>
-void set_side_lane(Args& b, const Tensor& t, int64_t schedule) {
+std::unique_lock<std::mutex> set_side_lane(Args& b, const Tensor& t, int64_t schedule) {
   b.schedule = (uint32_t)schedule;
-  if (schedule != CSA_SCHED_IN_ORDER) {
-    const Lane l = side_lane(t.device().index());
-    b.side_stream = l.s; b.side_fork = l.fork; b.side_join = l.join;
-  }
+  if (schedule == CSA_SCHED_IN_ORDER) return {};
+  const Lane l = side_lane(t.device().index());
+  b.side_stream = l.s; b.side_fork = l.fork; b.side_join = l.join;
+  return std::unique_lock<std::mutex>(*l.mu);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -137,6 +147,7 @@ std::tuple<Tensor, Tensor, Tensor> sbm_fwd(const Tensor& Q, const Tensor& K, con
                                            at::TensorList proj_w, at::TensorList proj_b,
                                            const optional<Tensor>& uniforms, int64_t k, int64_t seed,
                                            int64_t offset, double attn_p, double proj_p, bool dense, bool bf16) {
+  const at::OptionalDeviceGuard guard(at::device_of(Q));
   const SbmIn in = sbm_prep(Q, K, V, mask, cluster_w, proj_w, proj_b, uniforms);
   const int64_t B = in.Q.size(0), H = in.Q.size(1), N = in.Q.size(2), d = in.Q.size(3), M = in.K.size(2);
   const uint32_t flags = dense ? CSA_FLAG_DENSE : 0u;
@@ -157,6 +168,7 @@ std::tuple<Tensor, Tensor, Tensor> sbm_fwd(const Tensor& Q, const Tensor& K, con
 // The (graph, attn) maps SBMAttention returns (sbm_attn.py:57,62), from a forward's state.
 std::tuple<Tensor, Tensor> sbm_maps(const Tensor& Q, const Tensor& K, const Tensor& V, const optional<Tensor>& mask,
                                     const Tensor& state, int64_t k, bool dense) {
+  const at::OptionalDeviceGuard guard(at::device_of(Q));
   const SbmIn in = sbm_prep(Q, K, V, mask, c10::nullopt, {}, {}, c10::nullopt);
   const int64_t B = in.Q.size(0), H = in.Q.size(1), N = in.Q.size(2), M = in.K.size(2);
   Tensor graph = at::empty({B, H, N, M}, in.Q.options().dtype(at::kFloat));
@@ -182,6 +194,7 @@ std::vector<Tensor> sbm_bwd(const Tensor& Q, const Tensor& K, const Tensor& V, c
                             const Tensor& state, const Tensor& X, const Tensor& dX_,
                             const optional<Tensor>& dsparsity, const optional<Tensor>& dgraph, bool bf16,
                             bool packed, const optional<Tensor>& dattn, int64_t schedule) {
+  const at::OptionalDeviceGuard guard(at::device_of(Q));
   const SbmIn in = sbm_prep(Q, K, V, mask, cluster_w, proj_w, proj_b, c10::nullopt);
   const int64_t B = in.Q.size(0), H = in.Q.size(1), N = in.Q.size(2), d = in.Q.size(3), M = in.K.size(2);
   const uint32_t flags = dense ? CSA_FLAG_DENSE : 0u;
@@ -212,10 +225,8 @@ std::vector<Tensor> sbm_bwd(const Tensor& Q, const Tensor& K, const Tensor& V, c
   b.dk_sb = dK.stride(0); b.dk_sh = dK.stride(1); b.dk_sn = dK.stride(2);
   b.dv_sb = dV.stride(0); b.dv_sh = dV.stride(1); b.dv_sn = dV.stride(2);
   Tensor ws, da, dsp, dg;
-  if (dattn || !dense) {
-    ws = at::empty({(int64_t)csa_sbm_bwd_workspace_bytes(B, H, N, M, d, k, flags)}, o.dtype(at::kByte));
-    b.workspace = ws.data_ptr();
-  }
+  ws = at::empty({(int64_t)csa_sbm_bwd_workspace_bytes(B, H, N, M, d, k, flags)}, o.dtype(at::kByte));
+  b.workspace = ws.data_ptr();
   if (dattn) { da = f32c(*dattn); b.dattn = fp(da); }
   if (!dense) {
     if (dsparsity) { dsp = f32c(*dsparsity); b.dsparsity = fp(dsp); }
@@ -230,13 +241,14 @@ std::vector<Tensor> sbm_bwd(const Tensor& Q, const Tensor& K, const Tensor& V, c
     }
   }
   b.prof = g_prof_bwd;
-  set_side_lane(b, in.Q, schedule);
+  b.schedule = (uint32_t)schedule;  // ABI v6: validated, no side lane (the SBM backward runs in order)
   check(csa_sbm_bwd(&b, cur_stream(in.Q)), "csa_sbm_bwd");
   return outs;
 }
 
 // STE.py:10-15: A = (u < clamp(p, lo, hi)) as fp32 {0,1}.
 Tensor ste_sample(const Tensor& p_, const Tensor& u_, double lo, double hi) {
+  const at::OptionalDeviceGuard guard(at::device_of(p_));
   require_gpu(p_, "p"); require_gpu(u_, "u");
   const Tensor p = f32c(p_), u = f32c(u_);
   TORCH_CHECK(p.numel() == u.numel(), "csa::ste_sample: p and u differ in size");
@@ -247,6 +259,7 @@ Tensor ste_sample(const Tensor& p_, const Tensor& u_, double lo, double hi) {
 
 // STE.py:17-19: hardtanh(A * grad).
 Tensor ste_backward(const Tensor& A_, const Tensor& g_) {
+  const at::OptionalDeviceGuard guard(at::device_of(g_));
   require_gpu(A_, "A"); require_gpu(g_, "g");
   const Tensor A = f32c(A_), g = f32c(g_);
   TORCH_CHECK(A.numel() == g.numel(), "csa::ste_backward: A and g differ in size");
@@ -280,6 +293,7 @@ csa_rel_attn_args rel_args(const Tensor& q, const Tensor& k, const Tensor& v, co
 // [out (B,H,N,d), row_stats (B,H,N,2), state (uint8)]; d_k = 64: out is a (B,H,N,d) view of (B,N,H,d) memory
 std::vector<Tensor> rel_attn_fwd(const Tensor& q_, const Tensor& k_, const Tensor& v_, const Tensor& lq_,
                                  const Tensor& lk_, const Tensor& rel, const Tensor& mask, int64_t group, bool bf16) {
+  const at::OptionalDeviceGuard guard(at::device_of(q_));
   require_gpu(q_, "q"); require_gpu(k_, "k"); require_gpu(v_, "v"); require_gpu(lq_, "lq"); require_gpu(lk_, "lk");
   require_gpu(rel, "rel"); require_gpu(mask, "mask");
   const Tensor q = bhnd(q_), k = bhnd(k_), v = bhnd(v_), lq = f32c(lq_), lk = f32c(lk_);
@@ -300,6 +314,7 @@ std::vector<Tensor> rel_attn_bwd(const Tensor& q_, const Tensor& k_, const Tenso
                                  const Tensor& lk_, const Tensor& rel, const Tensor& mask, int64_t group,
                                  const Tensor& out, const Tensor& lse, const Tensor& state, const Tensor& dout_,
                                  bool bf16, bool packed, int64_t schedule) {
+  const at::OptionalDeviceGuard guard(at::device_of(q_));
   const Tensor q = bhnd(q_), k = bhnd(k_), v = bhnd(v_), lq = f32c(lq_), lk = f32c(lk_);
   const int64_t B = q.size(0), H = q.size(1), N = q.size(2), d = q.size(3), L = lq.size(1);
   const Tensor dout = d == 64 ? bhnd(dout_) : f32c(dout_);
@@ -328,8 +343,10 @@ std::vector<Tensor> rel_attn_bwd(const Tensor& q_, const Tensor& k_, const Tenso
     b.dv_sb = dv.stride(0); b.dv_sh = dv.stride(1); b.dv_sn = dv.stride(2);
   }
   b.dlq = fpw(dlq); b.dlk = fpw(dlk); b.workspace = ws.data_ptr();
-  set_side_lane(b, q, schedule);
-  check(csa_rel_attn_bwd(&b, cur_stream(q)), "csa_rel_attn_bwd");
+  {
+    const std::unique_lock<std::mutex> lane_lock = set_side_lane(b, q, schedule);
+    check(csa_rel_attn_bwd(&b, cur_stream(q)), "csa_rel_attn_bwd");
+  }
   if (packed) return {P, dlq, dlk};
   return {dq, dk, dv, dlq, dlk};
 }

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define CSA_ABI_VERSION 5
+#define CSA_ABI_VERSION 6
 
 typedef enum csa_status {
   CSA_OK = 0,
@@ -55,11 +55,12 @@ typedef enum csa_status {
 /* flags */
 #define CSA_FLAG_DENSE 1u /* FullAttention (graph == 1, no cluster projection, no sampling) */
 
-/* ABI v5: schedule of an attention backward's two halves (csa_sbm_bwd_args / csa_rel_attn_bwd_args
- * .schedule). The key half may run on a caller-owned side stream beside the query half, forked from
- * and joined back into `stream` with two caller-owned events (capture-safe); outputs are bitwise the
- * same either way. AUTO uses the side stream when the query half's grid leaves a partial last round of
- * workgroups on the device (side_stream must be set, else it runs in order). */
+/* ABI v5: schedule of an attention backward's two halves (csa_rel_attn_bwd_args .schedule). The key half
+ * may run on a caller-owned side stream beside the query half, forked from and joined back into `stream`
+ * with two caller-owned events (capture-safe); outputs are bitwise the same either way. AUTO uses the side
+ * stream when the query half's grid leaves a partial last round of workgroups on the device (side_stream
+ * must be set, else it runs in order). ABI v6: the SBM backward's query half consumes the ds / G tiles
+ * its key half writes, so csa_sbm_bwd always runs in order (its schedule fields are accepted and unused). */
 #define CSA_SCHED_AUTO 0u
 #define CSA_SCHED_IN_ORDER 1u
 #define CSA_SCHED_CONCURRENT 2u /* needs side_stream / side_fork / side_join */
@@ -125,16 +126,16 @@ typedef struct csa_sbm_bwd_args {
   float* dQ; float* dK; float* dV; /* out (B,H,N|M,d), strides dq_* / dk_* / dv_* below */
   float* dcluster_w;           /* out (H*k, d); NULL if DENSE */
   float* dproj_w[3]; float* dproj_b[3]; /* out; NULL if DENSE */
-  void* workspace;             /* csa_sbm_bwd_workspace_bytes() */
+  void* workspace;             /* csa_sbm_bwd_workspace_bytes(); required (ABI v6: also for DENSE) */
   const csa_prof* prof;        /* optional stage timing (NULL = off) */
   /* ABI v3: element strides (b, h, row) of dX, dQ, dK, dV; a zero triple = contiguous. E.g. dQ/dK/dV
    * as the three head-major views of one packed (B,N,3,H,d) gradient of a fused QKV projection. */
   int64_t dx_sb, dx_sh, dx_sn, dq_sb, dq_sh, dq_sn, dk_sb, dk_sh, dk_sn, dv_sb, dv_sh, dv_sn;
   /* ABI v4: (B,H,N,M) contiguous upstream gradient of the returned attn map (sbm_attn.py:62, the tensor the
-   * reference returns), or NULL. Needs the workspace, also for DENSE. */
+   * reference returns), or NULL. */
   const float* dattn;
-  /* ABI v5: CSA_SCHED_* and the caller's side lane: a hipStream_t of the same device as `stream` and two
-   * hipEvent_t (hipEventDisableTiming) used only between this call's fork and join. NULL = in order. */
+  /* ABI v5: CSA_SCHED_* and a side lane (hipStream_t + two hipEvent_t). ABI v6: validated (schedule must be
+   * a CSA_SCHED_* value) and otherwise unused: the SBM backward is one stream-ordered chain. */
   uint32_t schedule;
   void* side_stream; void* side_fork; void* side_join;
 } csa_sbm_bwd_args;

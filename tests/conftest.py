@@ -13,7 +13,8 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 # torch.ops.csa.* are registered when csa_amd.ops / rel_ops / gen_ops are imported: import them once for
 # every test, so a test that calls torch.ops.csa.* directly passes alone as well as after the others.
-# (Importing does not load libcsa_hip.so or touch a GPU.)
+# (Importing loads libcsa_hip.so and the C++ op shim libcsa_torch.so when they are built, registering the
+# GPU implementations; it does not touch a GPU.)
 import csa_amd.ops  # noqa: E402,F401
 import csa_amd.rel_ops  # noqa: E402,F401
 import csa_amd.gen_ops  # noqa: E402,F401

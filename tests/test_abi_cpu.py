@@ -105,3 +105,28 @@ def test_tuned_gemm_table_is_well_formed():
     assert len({(r[0], r[1]) for r in ent}) == len(ent)
     # the 9600-row (64 ASTs x 150 nodes) encoder shapes of the train step are covered
     assert any("_9600_" in r[1] for r in ent)
+
+
+def test_every_shim_op_guards_its_tensors_device():
+    """The C++ op shim resolves PyTorch's current stream, whose default is the null handle; the library maps a
+    null stream to the calling thread's current device, so every registered op must make its tensors' device
+    current first (at::OptionalDeviceGuard), as codegen'd ATen ops do (ADVICE round 3)."""
+    src = open(os.path.join(ROOT, "code-structure-aware-transformer_amd", "csrc", "csa_torch.cpp")).read()
+    ops = re.findall(r'm\.impl\("(\w+)", &(\w+)\)', src)
+    assert len(ops) >= 7
+    for name, fn in ops:
+        body = re.search(r"\b" + fn + r"\([^;{]*\)\s*\{(.*?)\n\}", src, re.S)
+        assert body, fn
+        head = body.group(1).split("\n")[1]
+        assert "OptionalDeviceGuard" in head, f"{name}: first statement is not a device guard: {head.strip()}"
+
+
+def test_python_ops_call_the_library_on_the_tensors_device():
+    """The ctypes-bound glue / generator / optimizer ops wrap each library call in _lib.on_device."""
+    pkg = os.path.join(ROOT, "code-structure-aware-transformer_amd", "csa_amd")
+    for f in ("glue.py", "gen_ops.py", "train.py"):
+        lines = open(os.path.join(pkg, f)).read().split("\n")
+        calls = [i for i, ln in enumerate(lines) if re.match(r"\s*check\((L|lib\(\))\.csa_", ln)]
+        assert calls, f
+        for i in calls:
+            assert "with on_device(" in lines[i - 1], f"{f}:{i + 1} library call outside on_device"
