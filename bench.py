@@ -41,6 +41,46 @@ IDEAL_BYTES_PER_AST_F32IO = 3.739e6
 IDEAL_BYTES_PER_AST_BF16IO = 2.050e6
 
 
+PMC_TABLE = os.path.join(ROOT, "code-structure-aware-transformer_amd", "csa_amd", "pmc_gfx950.json")
+# the kernels of each profiled stage (csa_sbm.hip launch order)
+STAGE_KERNELS = {"prep": ("k_cluster_softmax", "k_frag_prep"), "proj_fwd": ("k_proj_fwd_l",),
+                 "attn_fwd": ("k_attn_fwd",), "attn_bwd_kv": ("k_attn_rowprep", "k_attn_bwd_kv"),
+                 "attn_bwd_q": ("k_attn_bwd_qg",), "proj_bwd": ("k_proj_bwd_s",),
+                 "reduce": ("k_reduce_slabs", "k_cluster_grad")}
+
+
+def pmc_table():
+    """The per-kernel HBM bytes / rocprof durations of the headline configuration (tools/pmc_traffic.py), shipped
+    inside the package so the driver's run on the GPU box carries them."""
+    if not os.path.exists(PMC_TABLE):
+        return None
+    with open(PMC_TABLE) as f:
+        return json.load(f)
+
+
+def traffic_evidence(table, B, stage_ms):
+    """north_star's "achieved HBM GB/s against MI355X peak for the masking/softmax/sampling kernels": counter
+    bytes per launch / the rocprof average duration of the same capture, per kernel, and the whole layer's
+    counter bytes against the ideal fused traffic (3.739 MB per AST)."""
+    ks = table["kernels"]
+    by = {}
+    for stage, names in STAGE_KERNELS.items():
+        for n in names:
+            t = ks.get(n)
+            if not t or not t.get("rocprof_avg_ns"):
+                continue
+            gbs = t["bytes"] / (t["rocprof_avg_ns"] * 1e-9) / 1e9
+            by[n] = {"stage": stage, "bytes": t["bytes"], "rocprof_avg_ms": round(t["rocprof_avg_ns"] * 1e-6, 4),
+                     "GB_s": round(gbs, 1), "frac_of_hbm_peak": round(gbs / PEAK_HBM_GBS, 4)}
+    total = sum(t["bytes"] for n, t in ks.items() if any(n in v for v in STAGE_KERNELS.values()))
+    live = {s: round(sum(by[n]["bytes"] for n in names if n in by) / (stage_ms[s] * 1e-3) / 1e9, 1)
+            for s, names in STAGE_KERNELS.items() if s in stage_ms and any(n in by for n in names)}
+    return {"traffic_by_kernel": by, "traffic_GB_s_by_live_stage": live,
+            "traffic_bytes_per_step": total, "ideal_bytes_per_step": round(IDEAL_BYTES_PER_AST_F32IO * B),
+            "wasted_traffic_ratio": round(total / (IDEAL_BYTES_PER_AST_F32IO * B), 3),
+            "pmc_table": os.path.relpath(PMC_TABLE, ROOT)}
+
+
 def stage_flops_per_ast(H, N, M, D, k):
     """Algorithmic FLOPs per AST (one batch element, all heads) per kernel stage. The attention
     backward's algorithmic work (dP, dV, dK, dT | dQ, dQh) is split as its kernels do it: k_attn_bwd_kv computes
@@ -298,7 +338,10 @@ def train_step_bench(world, rank, dev, steps, warmup, config="java", per_gpu_bat
     el = timed_region(world, dev, steps, lambda i: losses.append(step(*batches[i % nbatches])))
     mean_loss = float(torch.stack(losses).mean())
     nparam = sum(p.numel() for p in model.parameters())
-    return {"config": f"config/{config}.py CSATrans summary train step (DDP over RCCL)", "per_gpu_batch": per_gpu_batch,
+    wrapped = world > 1 or force_ddp
+    return {"config": f"config/{config}.py CSATrans summary train step" + (" (DDP over RCCL)" if wrapped else
+                                                                           " (one GPU, no DDP wrapper)"),
+            "per_gpu_batch": per_gpu_batch,
             "global_batch": per_gpu_batch * world, "steps": steps, "warmup": warmup,
             "ms_per_step": round(el * 1000 / steps, 3), "samples_per_s": round(world * per_gpu_batch * steps / el, 1),
             "params": nparam, "mean_loss": round(mean_loss, 4), "n_ranks": world,
@@ -426,7 +469,7 @@ def main():
         return
 
     from csa_amd import ops
-    from csa_amd._lib import STAGES, CsaProf, KERNEL_OF_STAGE
+    from csa_amd._lib import STAGES, CsaProf, KERNEL_OF_STAGE, loaded_source_hash
     from csa_amd.module.sbm_attn import FullAttention, SBMAttention
 
     B, H, N, d, k = args.batch, 8, args.seq_len, args.head_dim, args.clusters
@@ -539,13 +582,19 @@ def main():
         roofline = {"bound": "mfma", "kernel": kernel_of[dom], "achieved": round(ach, 2),
                     "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / PEAK_F32_MFMA_TFLOPS, 4),
                     "traffic": None, "avg_launch_ms": round(dom_ms, 4)}
-        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc):
-            with open(pmc) as f:
-                tr = json.load(f).get(kernel_of[dom])
-            if tr:  # HBM bytes per launch from the committed PMC passes (tools/pmc_traffic.py)
-                roofline["traffic"] = tr["bytes"]
-                roofline["traffic_unit"] = "bytes/launch (rocprofv3 2xFETCH_SIZE+WRITE_SIZE, profiles/pmc_traffic.json)"
+    headline = (B, N, d, k, args.precision, args.dense, args.eval) == (256, 150, 64, 10, "fp32", False, False)
+    table = pmc_table() if headline else None
+    if roofline and table:
+        tr = table["kernels"].get(kernel_of[dom])
+        if tr:  # HBM bytes per launch and rocprof duration from the shipped PMC table (tools/pmc_traffic.py)
+            roofline["traffic"] = tr["bytes"]
+            roofline["traffic_unit"] = ("bytes/launch (rocprofv3 2 x FETCH_SIZE + WRITE_SIZE, " +
+                                        os.path.relpath(PMC_TABLE, ROOT) + ")")
+            if tr.get("rocprof_avg_ns"):
+                ach_r = flops[dom] * B / (tr["rocprof_avg_ns"] * 1e-9) / 1e12
+                roofline["frac_rocprof"] = round(ach_r / PEAK_F32_MFMA_TFLOPS, 4)
+                roofline["rocprof_avg_launch_ms"] = round(tr["rocprof_avg_ns"] * 1e-6, 4)
+            roofline["pmc_table_matches_library"] = table["csa_source_hash"] == loaded_source_hash()
     total_flops = sum(flops.values()) * B
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "ASTs/s", "n_gpus": world, "steps": args.steps,
@@ -568,6 +617,8 @@ def main():
                                         for s, v in timed.items() if v > 0},
         "attn_bwd_schedule": "side stream (overlapped stage windows)" if overlapped else "in order",
     }
+    if table:
+        out.update(traffic_evidence(table, B, stage_ms))
     if args.precision == "fp32" and not args.no_bf16_leg and not args.dense and N <= 150:
         # the same layer with CSA_DTYPE_BF16 (north_star's bf16 variant): side measurement, same step
         progress("bf16-mode leg")

@@ -11,12 +11,12 @@ Extensions (all default to the reference behaviour):
   * ``module.uniforms``: optional (B,H,N,M) uniforms for the next forward's Bernoulli draws
     (host-supplied-draw parity mode, bit-identical to torch.bernoulli given the same draws).
   * ``config["attn_precision"]`` / ``module.attn_precision`` (default "fp32", the reference's
-    forced precision, sbm_attn.py:120-126): "bf16" runs QK^T, PV and their gradients on bf16 MFMA
-    (fp32 accumulation; the cluster projection, expA and the sampled graph stay fp32).
-  * ``module.bwd_schedule`` (default "auto"): "in_order" keeps the attention backward's two halves on
-    the current stream, "concurrent" puts the key half on a side stream beside the query half, "auto"
-    decides from the grid shape (csa_amd.train.wrap_ddp sets "in_order" beside RCCL). Bitwise-identical
-    results either way.
+    forced precision, sbm_attn.py:120-126): "bf16" runs QK^T, PV and their gradients, the projection MLP
+    and sigmoid(. C^T) (forward and backward) on bf16 MFMA with fp32 accumulation; T = Kh S^T, expA, the
+    sampling and all elementwise work stay fp32.
+  * ``module.bwd_schedule`` (default "auto"): accepted for the CSE attention's schedule vocabulary; the
+    SBM backward is one stream-ordered chain since ABI v6 (its query half consumes the ds / G tiles the
+    key half writes), so every value gives the same launches and bitwise-identical results.
   * ``Attention`` keeps W_q / W_k / W_v packed back to back (one QKV GEMM) from construction on and after
     every ``.to()`` / ``.cuda()``: the packing exists before DDP or an optimizer sees the parameters.
 """

@@ -18,7 +18,7 @@ from typing import List, Optional, Tuple
 import torch
 
 from . import _lib
-from ._lib import CSA_FLAG_DENSE, SCHEDULES, lib
+from ._lib import CSA_FLAG_DENSE, CSA_FLAG_FWD_ONLY, SCHEDULES, lib
 
 __all__ = ["sbm_attention", "dense_attention", "ste_sample", "ste_backward", "rel_attn", "SBMAttentionFunction"]
 
@@ -29,7 +29,7 @@ SHIM_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "lib
 _SCHEMAS = {
     "sbm_fwd": "(Tensor Q, Tensor K, Tensor V, Tensor? mask, Tensor? cluster_w, Tensor[] proj_w, Tensor[] proj_b, "
                "Tensor? uniforms, int k, int seed, int offset, float attn_p, float proj_p, bool dense, "
-               "bool bf16=False) -> (Tensor, Tensor, Tensor)",
+               "bool bf16=False, bool fwd_only=False) -> (Tensor, Tensor, Tensor)",
     "sbm_maps": "(Tensor Q, Tensor K, Tensor V, Tensor? mask, Tensor state, int k, bool dense) -> (Tensor, Tensor)",
     "sbm_bwd": "(Tensor Q, Tensor K, Tensor V, Tensor? mask, Tensor? cluster_w, Tensor[] proj_w, Tensor[] proj_b, "
                "int k, float attn_p, float proj_p, int seed, int offset, bool dense, Tensor state, Tensor X, "
@@ -135,15 +135,17 @@ def head_major_out(B, H, N, d, device):
 # ---------------------------------------------------------------------------------------
 # fake (meta) implementations of the C++ ops
 # ---------------------------------------------------------------------------------------
-def _state_bytes(B, H, N, M, d, k, dense):
-    return lib().csa_sbm_state_bytes(B, H, N, M, d, k, CSA_FLAG_DENSE if dense else 0)
+def _state_bytes(B, H, N, M, d, k, dense, fwd_only=False):
+    return lib().csa_sbm_state_bytes(B, H, N, M, d, k, (CSA_FLAG_DENSE if dense else 0) |
+                                     (CSA_FLAG_FWD_ONLY if fwd_only else 0))
 
 
 @torch.library.register_fake("csa::sbm_fwd")
-def _(Q, K, V, mask, cluster_w, proj_w, proj_b, uniforms, k, seed, offset, attn_p, proj_p, dense, bf16=False):
+def _(Q, K, V, mask, cluster_w, proj_w, proj_b, uniforms, k, seed, offset, attn_p, proj_p, dense, bf16=False,
+      fwd_only=False):
     B, H, N, d = Q.shape
     return (Q.new_empty(B, N, H, d).transpose(1, 2), Q.new_empty(0 if dense else H),
-            Q.new_empty(_state_bytes(B, H, N, K.shape[2], d, k, dense), dtype=torch.uint8))
+            Q.new_empty(_state_bytes(B, H, N, K.shape[2], d, k, dense, fwd_only), dtype=torch.uint8))
 
 
 @torch.library.register_fake("csa::sbm_maps")
@@ -193,8 +195,10 @@ class SBMAttentionFunction(torch.autograd.Function):
         seed = _draw_seed()
         pw = [] if dense else [w0, w1, w2]
         pb = [] if dense else [b0, b1, b2]
+        # no input needs a gradient (eval / no_grad): the forward skips the activations only the backward reads
+        fwd_only = not any(ctx.needs_input_grad)
         X, sp, state = torch.ops.csa.sbm_fwd(Q, K, V, mask, None if dense else cluster_w, pw, pb, uniforms, k, seed, 0,
-                                            attn_p, proj_p, dense, bf16)
+                                            attn_p, proj_p, dense, bf16, fwd_only)
         graph = attn = None
         if want_maps:
             graph, attn = torch.ops.csa.sbm_maps(Q, K, V, mask, state, k, dense)

@@ -9,7 +9,7 @@
 //        k_attn_fwd          expA tile, u < clamp(expA) sampling, online softmax
 //                            with graph-masked L1 renormalisation, dropout, PV    sbm_attn.py:55-64, STE.py:10-15
 //        k_sparsity_finish   integer edge counts -> head-wise sparsity            sbm_attn.py:64
-//   bwd: k_attn_gamma        gamma = rowsum(dX*X) (the F.normalize term)
+//   bwd: k_attn_rowprep      gamma = rowsum(dX*X) and the per-row constants of the elementwise backward
 //        k_attn_bwd_kv       S, dP, the elementwise backward once per element; dK (attention path),
 //                            dV, dT; ds and G tiles to the workspace
 //        k_attn_bwd_qg       dQ (attention path) = ds K, dQh = G T from those tiles
@@ -85,7 +85,7 @@ struct Layout {
   int64_t B, H, N, M, D, k, kp, KT, NQB, NKB, Mpad;
   size_t S, Qh, Kh, T, stats, Abits, Rbits, cnt, Wf[3], WfT[3], Cf, CfT, Sf, SfT, Act, total;
   // bwd workspace
-  size_t w_dQh, w_dT, w_slab, w_dS, w_dC, w_gx, w_dsg, w_total;
+  size_t w_dQh, w_dT, w_slab, w_dS, w_dC, w_gx, w_dsg, w_brow, w_total;
   int64_t G, slab_floats, w_dsg_plane;
 };
 
@@ -107,7 +107,8 @@ int64_t proj_bwd_groups(int64_t B, int64_t H, int64_t items_per_b, int wg_per_cu
   return best;
 }
 
-Layout make_layout(int64_t B, int64_t H, int64_t N, int64_t M, int64_t D, int64_t k, bool dense) {
+Layout make_layout(int64_t B, int64_t H, int64_t N, int64_t M, int64_t D, int64_t k, uint32_t flags) {
+  const bool dense = flags & CSA_FLAG_DENSE;
   Layout L;
   L.B = B; L.H = H; L.N = N; L.M = M; L.D = D; L.k = dense ? 0 : k;
   // kp (stored cluster width) is exactly 2*KPH of the instantiation used: 16, 32, 64 or 128
@@ -132,7 +133,8 @@ Layout make_layout(int64_t B, int64_t H, int64_t N, int64_t M, int64_t D, int64_
   L.Sf = take(sizeof(float) * H * KP32 * KP32);
   L.SfT = take(sizeof(float) * H * KP32 * KP32);
   // MLP activations of every 32-row item (h1 | h2 | po | hat), saved by k_proj_fwd for k_proj_bwd
-  L.Act = take(sizeof(float) * (dense ? 0 : B * H * (L.NQB + L.NKB) * (3 * D + KP32) * 32));
+  // (absent for CSA_FLAG_FWD_ONLY: only the backward reads them)
+  L.Act = take(sizeof(float) * ((dense || (flags & CSA_FLAG_FWD_ONLY)) ? 0 : B * H * (L.NQB + L.NKB) * (3 * D + KP32) * 32));
   L.total = o;
   // backward workspace
   // two workgroups per CU for d = 64 with KT = 1 (k_proj_bwd_s / k_proj_bwd<64, 1>: 80 / 64 KiB LDS)
@@ -149,6 +151,9 @@ Layout make_layout(int64_t B, int64_t H, int64_t N, int64_t M, int64_t D, int64_
   // 32 x 32 fp32 tiles [key][query]; G only with clusters
   L.w_dsg_plane = B * H * L.NQB * L.NKB * 1024;
   L.w_dsg = take(sizeof(float) * L.w_dsg_plane * (dense ? 1 : 2));
+  // per query row (NQB * 32 rows per (b,h), padded rows included) the constants of k_attn_bwd_kv's elementwise
+  // backward, written by k_attn_rowprep
+  L.w_brow = take(sizeof(float) * B * H * L.NQB * 32 * 4);
   L.w_total = o;
   return L;
 }
@@ -347,7 +352,7 @@ struct KArgs {
   const float* mask; int64_t mask_sb;
   const float* pb[3];  // proj biases
   const float *Wf[3], *WfT[3], *Cf, *CfT, *Sf, *SfT, *S;
-  float *Qh, *Kh, *T, *stats, *Act;
+  float *Qh, *Kh, *T, *stats, *Act;  // Act NULL for CSA_FLAG_FWD_ONLY (no activation blocks saved)
   uint32_t *Abits, *Rbits;
   unsigned long long* cnt;
   const float* U;
@@ -362,6 +367,7 @@ struct KArgs {
   float* gx;                               // dattn: per query row sum_j dattn_ij attn_ij (k_attn_gx)
   float *dQ, *dK, *dV, *dQh, *dT, *slab;
   float* dsg; int64_t gplane;  // ds | G tiles (Layout::w_dsg), G at dsg + gplane
+  float* brow;                 // per query row (c0, u, v, rho) of the elementwise backward (k_attn_rowprep)
   int64_t dx_sb, dx_sh, dx_sn, dq_sb, dq_sh, dq_sn, dk_sb, dk_sh, dk_sn, dv_sb, dv_sh, dv_sn;
   int G; int64_t slab_floats;
 };
@@ -677,7 +683,7 @@ __device__ __forceinline__ void proj_fwd_item(const KArgs& p, const FwdFrags& F,
   next();
 #endif
 #ifndef CSA_EXP_NO_ACT
-  {  // save the activations for k_proj_bwd (item r of this (b,h): Q blocks, then K blocks)
+  if (p.Act) {  // save the activations for k_proj_bwd (item r of this (b,h): Q blocks, then K blocks)
     constexpr int ABLK = (3 * D + 32 * KT) * 32;
     float* blk = p.Act + ((int64_t)bh * (p.NQB + p.NKB) + r) * ABLK;
     constexpr bool ABF = BF && (D == 64 || D == 96) && KT == 1;  // read back by k_proj_bwd_s<D, true>
@@ -792,6 +798,20 @@ __global__ __launch_bounds__((64 * ProjFwdLds<D, KT>::NW)) void k_proj_fwd_l(con
     printf("PHF d=%d w=%d layer0+act %llu layer1 %llu act1 %llu layer2 %llu hat %llu T+next %llu stores %llu\n", D, w,
            q[0], q[1], q[2], q[3], q[4], q[5], q[6]);
   }
+#endif
+}
+
+// fp32: k_attn_bwd_kv runs the elementwise backward once per element and hands the ds / G tiles to
+// k_attn_bwd_qg (which then recomputes neither S nor dP). bf16 mode: recomputing S and dP on the 16x faster bf16
+// MFMA costs less than moving the tiles through HBM, so k_attn_bwd_qr recomputes them (the round-3 design).
+// Same-box A/B (profiles/r04_ab_handoff.txt): fp32 layer step 1.329 (recompute) -> 1.275 ms (handoff); saving the
+// forward's S tiles for k_attn_bwd_kv as well measured 1.290 ms (+23 us forward stores, -22 us backward): not kept.
+template <bool BF>
+constexpr bool bwd_handoff() {
+#ifdef CSA_EXP_RECOMP  // experiment: the recompute pipeline for fp32 too
+  return false;
+#else
+  return !BF;
 #endif
 }
 
@@ -1203,7 +1223,7 @@ __global__ __launch_bounds__(64) void k_maps(const KArgs p, float* __restrict__ 
 
 // gx[b,h,i] = sum_j dattn[b,h,i,j] * attn[b,h,i,j] for an upstream gradient of the returned attn map
 // (sbm_attn.py:62 F.normalize backward needs sum_j G_ij attn_ij over the TOTAL gradient G of attn; the
-// dX V^T part is rowsum(dX * X), computed by k_attn_gamma). Recomputes attn like k_maps (S orientation:
+// dX V^T part is rowsum(dX * X), computed by k_attn_rowprep). Recomputes attn like k_maps (S orientation:
 // keys on lanes, queries in registers), one wave per (b, h, 32 queries); lane sums, then one reduction.
 template <int D, bool DENSE>
 __global__ __launch_bounds__(64) void k_attn_gx(const KArgs p) {
@@ -1255,26 +1275,42 @@ __global__ __launch_bounds__(64) void k_attn_gx(const KArgs p) {
   }
 }
 
-// gamma[b,h,i] = rowsum(dX * X) (+ gx) into stats[.][3], read by k_attn_bwd_kv's elementwise backward (the
-// F.normalize term of sbm_attn.py:62). Two lanes per row, each one half of the row (sequential fma over its
-// d/2 elements, then the two halves added). HBM-bound: 2 x 4d B per row.
+// Per query row of the backward (sbm_attn.py:59-63 autograd, oracle/closed_form.py), the row constants of
+// k_attn_bwd_kv's elementwise backward, so that per element it runs
+//   P = exp2(s log2e / sqrt(d) + c0 + kbias), dM = (keep ? dP : 0) u + v (the dM of an edge, A = 1),
+//   ds = ((A ? dM : 0) - rho) P / sqrt(d), G = A ? hardtanh(dM P + csp) : 0, attw = (A & keep) ? P u : 0
+// with gamma = rowsum(dX * X) (+ sum_j dattn attn, k_attn_gx) the F.normalize term and n = Zg / Z the row's
+// L1 norm of softmax * graph:
+//   c0 = -lse log2e, u = dscale / max(n, eps), v = -[n >= eps] gamma / max(n, eps), rho = [n < eps] gamma.
+// Rows past N (up to the query block's end) get c0 = -inf, u = v = rho = 0: P = 0, so they add nothing.
+// Two lanes per row, each one half of the dX . X dot product. HBM-bound: 2 x 4d B per row.
 template <int D>
-__global__ __launch_bounds__(256) void k_attn_gamma(const KArgs p) {
+__global__ __launch_bounds__(256) void k_attn_rowprep(const KArgs p) {
   constexpr int NS = D / 2;
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x, row = t >> 1;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x, row = t >> 1;  // row of the padded (bh, NQB*32)
   const int h = (int)(t & 1);
-  const bool rv = row < (int64_t)p.B * p.H * p.N;
+  const int NP = p.NQB * 32;
+  const bool rv = row < (int64_t)p.B * p.H * NP;
   const int64_t rc = rv ? row : 0;
-  const int i = (int)(rc % p.N), bh = (int)(rc / p.N), b = bh / p.H, hd = bh % p.H;
+  const int i = (int)(rc % NP), bh = (int)(rc / NP), b = bh / p.H, hd = bh % p.H;
+  const bool iv = rv && i < p.N;
+  const int ic = imin(i, p.N - 1);
   float dx[NS], xr[NS];
-  load_run<NS>(dx, p.dX + b * p.dx_sb + hd * p.dx_sh + (int64_t)i * p.dx_sn + h * NS, rv);
-  load_run<NS>(xr, p.X + b * p.x_sb + hd * p.x_sh + (int64_t)i * p.x_sn + h * NS, rv);
+  load_run<NS>(dx, p.dX + b * p.dx_sb + hd * p.dx_sh + (int64_t)ic * p.dx_sn + h * NS, iv);
+  load_run<NS>(xr, p.X + b * p.x_sb + hd * p.x_sh + (int64_t)ic * p.x_sn + h * NS, iv);
+  const f32x4 st = *reinterpret_cast<const f32x4*>(p.stats + ((int64_t)bh * p.N + ic) * 4);  // lse, 1/D, [n>=eps]
   float gp = 0.f;
 #pragma unroll
   for (int s = 0; s < NS; ++s) gp = fmaf(dx[s], xr[s], gp);
   float gamma = gp + __shfl_xor(gp, 1, 64);
-  if (p.dattn) gamma += p.gx[rc];
-  if (rv && h == 0) p.stats[rc * 4 + 3] = gamma;
+  if (p.dattn) gamma += p.gx[(int64_t)bh * p.N + ic];
+  const float dscale = p.attn_p > 0.f ? 1.f / (1.f - p.attn_p) : 1.f;
+  f32x4 rec;
+  rec[0] = iv ? -st[0] * LOG2E : NEG_INF;
+  rec[1] = iv ? dscale * st[1] : 0.f;
+  rec[2] = (iv && st[2] != 0.f) ? -gamma * st[1] : 0.f;
+  rec[3] = (iv && st[2] == 0.f) ? gamma : 0.f;
+  if (rv && h == 0) *reinterpret_cast<f32x4*>(p.brow + rc * 4) = rec;
 }
 
 // ------------------------------------------------------------------------------------
@@ -1316,7 +1352,10 @@ struct AttnBwdShape {
   // bwd_qg: K | T
   static constexpr int GK = 0, GT = IMG;
   static constexpr size_t G_BYTES = (size_t)IMG + NIMG;
-  // bwd_kv: Q | dX | Qh | stats (32 rows x 4)
+  // bwd_qr: K | V | T | key bias row (Mpad floats)
+  static constexpr int QK = 0, QV = IMG, QT = 2 * IMG, QB = 2 * IMG + NIMG;
+  static size_t r_bytes(int Mpad) { return (size_t)QB + 4 * (size_t)Mpad; }
+  // bwd_kv: Q | dX | Qh | row constants (32 rows x 4, k_attn_rowprep)
   static constexpr int KQ = 0, KX = IMG, KH = 2 * IMG, KS = 2 * IMG + NIMG;
   static constexpr size_t KV_BYTES = (size_t)KS + 32 * 16;
 };
@@ -1339,6 +1378,181 @@ __device__ __forceinline__ void store_mb4(float* __restrict__ out, int nrows, in
     for (int e = 0; e < 4; ++e) v[e] = d[4 * b + e] + d[8 + 4 * b + e];
     if (row < nrows) *reinterpret_cast<f32x4*>(out + (int64_t)row * kp + cl) = v;
   }
+}
+
+// ------------------------------------------------------------------------------------
+// B2 (bf16 mode): per (b,h, query block), S^T orientation: recompute S = QK^T and dP = dX V^T on bf16 MFMA,
+// the elementwise backward with the row constants of k_attn_rowprep (one record per lane: its query), then
+// dQ (attention path) = ds K, dQh = G T. The round-3 design, kept where recomputing is cheaper than the
+// k_attn_bwd_qg tile handoff (see bwd_handoff).
+// ------------------------------------------------------------------------------------
+// DG: an upstream gradient of the graph and / or attn output is present (p.dgraph, p.dattn)
+template <int D, int KPH, bool DENSE, bool DROP, bool DG, bool BF>
+__global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd_qr(const KArgs p) {
+  using SH = AttnBwdShape<D, KPH>;
+  constexpr int DT = D / 32, NS = D / 2, DP = SH::DP, KP = SH::KP, KPN = SH::KPN, KTA = SH::KTA;
+  constexpr bool SWZ = SH::SWZ;
+  constexpr bool MB4 = !DENSE && KP == 16;  // dQh on mfma4b (store_mb4)
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const uint32_t L0 = lds_offset(lds), Kl = L0 + SH::QK, Vl = L0 + SH::QV, Tl = L0 + SH::QT;
+  const int lane = lane_id(), c = lane & 31, h = lane >> 5;
+  const BhBlock xb = xcd_block(p.NQB, p.B * p.H);
+  if (!xb.valid) return;
+  const int qb = xb.blk, bh = xb.bh, b = bh / p.H, hd = bh % p.H;
+  const int i = qb * 32 + c;
+  const bool iv = i < p.N;
+  const int ic = imin(i, p.N - 1);
+  const int kld = (int)p.k_sn * 4, vld = (int)p.v_sn * 4;
+  const __amdgpu_buffer_rsrc_t kr = make_rsrc(p.K + b * p.k_sb + hd * p.k_sh, SWZ ? (p.M - 1) * kld + D * 4 : 0x7fffffff);
+  const __amdgpu_buffer_rsrc_t vr = make_rsrc(p.V + b * p.v_sb + hd * p.v_sh, SWZ ? (p.M - 1) * vld + D * 4 : 0x7fffffff);
+  const __amdgpu_buffer_rsrc_t tr = make_rsrc(DENSE ? p.K : p.T + (int64_t)bh * p.M * p.kp, p.M * p.kp * 4);
+  // rows past M are never fetched: zero the images once so they only ever hold finite data
+  if constexpr (SWZ) lds_zero<(2 * SH::IMG + SH::NIMG) / 4>(lds);
+  else if constexpr (!DENSE) lds_zero<SH::NIMG / 4>(lds + SH::QT / 4);
+  const DmaPat kpat = dma_pat(SW_BOTH, kld), vpat = dma_pat(SW_ROW, vld);
+#define CSA_ISSUE_BQ(row0)                          \
+  do {                                              \
+    if constexpr (SWZ) {                            \
+      dma64(Kl, kr, kpat, kld, (row0));             \
+      dma64(Vl, vr, vpat, vld, (row0));             \
+    } else {                                        \
+      dma_rows<D>(Kl, kr, kld, (row0), p.M);        \
+      dma_rows<D>(Vl, vr, vld, (row0), p.M);        \
+    }                                               \
+    if constexpr (!DENSE) dma_narrow(Tl, tr, (row0), KPN); \
+  } while (0)
+  const KeyMask km = key_mask_load(p, b);
+  CSA_ISSUE_BQ(0);
+  key_bias_store(lds + SH::QB / 4, p, b, km);
+  const int64_t wrow = ((int64_t)bh * p.NQB + qb) * p.Mpad + c;
+  uint32_t wAn = DENSE ? 0xffffffffu : p.Abits[wrow];
+  uint32_t wRn = DROP ? p.Rbits[wrow] : 0xffffffffu;
+  float q[NS], dx[NS];
+  load_run<NS>(q, p.Q + b * p.q_sb + hd * p.q_sh + (int64_t)ic * p.q_sn + h * NS, iv);
+  load_run<NS>(dx, p.dX + b * p.dx_sb + hd * p.dx_sh + (int64_t)ic * p.dx_sn + h * NS, iv);
+  // this lane's query row constants (c0, u, v, rho); a query past N has c0 = -inf: P = 0
+  const f32x4 rec = *reinterpret_cast<const f32x4*>(p.brow + ((int64_t)bh * p.NQB * 32 + i) * 4);
+  const float csp = (!DENSE && p.dsp) ? p.dsp[hd] / ((float)p.B * (float)p.N * (float)p.M) : 0.f;
+  const float c1 = p.scale * LOG2E;
+  f32x16 dq[DT], dqh[KTA];
+#pragma unroll
+  for (int t = 0; t < DT; ++t) dq[t] = zero16();
+#pragma unroll
+  for (int t = 0; t < KTA; ++t) dqh[t] = zero16();
+  for (int kt = 0; kt < p.NKB; ++kt) {
+    int ln = threadIdx.x;  // opaque per iteration: keeps the per-row LDS addresses out of the prologue
+    asm volatile("" : "+v"(ln));
+    const int c = ln & 31, h = (ln >> 5) & 1;
+    const int j0 = kt * 32;
+    wait_vm_all();  // tile kt's K/V/T images and its bit words have landed
+    const uint32_t wA = wAn, wR = wRn;
+    f32x16 sacc = zero16(), dpacc = zero16();
+    const int kb = SWZ ? row_base64(c, h, SW_BOTH) : 4 * (c * DP + NS * h);
+    const int vb = SH::QV + (SWZ ? row_base64(c, h, SW_ROW) : 4 * (c * DP + NS * h));
+    if constexpr (BF) {
+#pragma unroll
+      for (int j2 = 0; j2 < NS / 8; ++j2) {
+        const f32x4 k0 = lds_f4(lds, SWZ ? (kb ^ (32 * j2)) : kb + 32 * j2);
+        const f32x4 k1 = lds_f4(lds, SWZ ? (kb ^ (32 * j2 + 16)) : kb + 32 * j2 + 16);
+        sacc = mfma_bf(pack8(k0, k1), pack8(&q[8 * j2]), sacc);
+        const f32x4 v0 = lds_f4(lds, SWZ ? (vb ^ (32 * j2)) : vb + 32 * j2);
+        const f32x4 v1 = lds_f4(lds, SWZ ? (vb ^ (32 * j2 + 16)) : vb + 32 * j2 + 16);
+        dpacc = mfma_bf(pack8(v0, v1), pack8(&dx[8 * j2]), dpacc);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < NS / 4; ++j) {
+        const f32x4 kv = lds_f4(lds, SWZ ? (kb ^ (16 * j)) : kb + 16 * j);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sacc = mfma(kv[e], q[4 * j + e], sacc);
+      }
+#pragma unroll
+      for (int j = 0; j < NS / 4; ++j) {
+        const f32x4 vv = lds_f4(lds, SWZ ? (vb ^ (16 * j)) : vb + 16 * j);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dpacc = mfma(vv[e], dx[4 * j + e], dpacc);
+      }
+    }
+    // transposed operands of this tile's dQ / dQh products (lane d holds K[key crow(r,h)][d])
+    float kT[DT][16], tT[KTA][16];
+#pragma unroll
+    for (int t = 0; t < DT; ++t) {
+      const int tb = SWZ ? both_base64(t, c, h) : 4 * (32 * t + c) + 16 * DP * h;
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        kT[t][r] = SWZ ? both_read(lds, tb, r, SH::QK) : lds_f1(lds, tb + 4 * DP * crow(r, 0));
+    }
+    if constexpr (MB4) {  // lane (c, h): T[key crow(r,h)][cluster c & 15]
+#pragma unroll
+      for (int r = 0; r < 16; ++r) tT[0][r] = lds_f1(lds, SH::QT + narrow_elem(crow(r, h), c & 15, KPN));
+    } else if constexpr (!DENSE) {
+#pragma unroll
+      for (int at = 0; at < KTA; ++at)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float v = lds_f1(lds, SH::QT + narrow_elem(crow(r, h), imin(32 * at + c, KP - 1), KPN));
+          tT[at][r] = (KP >= 32 || c < KP) ? v : 0.f;
+        }
+    }
+    f32x4 bz[4];  // key bias of registers 4g..4g+3
+#pragma unroll
+    for (int g = 0; g < 4; ++g) bz[g] = lds_f4(lds, SH::QB + 4 * (j0 + 8 * g + 4 * h));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (kt + 1 < p.NKB) {  // tile kt+1 streams in under the elementwise work and the products below
+      CSA_ISSUE_BQ(j0 + 32);
+      if constexpr (!DENSE) wAn = p.Abits[wrow + j0 + 32];
+      if constexpr (DROP) wRn = p.Rbits[wrow + j0 + 32];
+    }
+    // Elementwise backward (k_attn_rowprep's formulas). A key past M has P = 0 (bias -inf) and A = 0.
+    float dsv[16], gv[16];
+    const int nvk = p.M - j0 - 4 * h;  // key crow(r,h) = j0 + crow(r,0) + 4h is < M iff crow(r,0) < nvk
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int jj = crow(r, h), j = j0 + jj;
+      const uint32_t a_w = DENSE ? 0xffffffffu : (uint32_t)__shfl((int)wA, jj, 64);
+      const uint32_t r_w = DROP ? (uint32_t)__shfl((int)wR, jj, 64) : 0xffffffffu;
+      const bool a = ((a_w >> c) & 1u) && crow(r, 0) < nvk;
+      const bool kp = (r_w >> c) & 1u;
+      const float P = __builtin_amdgcn_exp2f(fmaf(sacc[r], c1, bz[r >> 2][r & 3] + rec[0]));
+      float dM = fmaf(kp ? dpacc[r] : 0.f, rec[1], rec[2]);
+      float cg = csp;
+      if constexpr (DG) {
+        const bool inside = iv && (j < p.M);
+        const int64_t me = ((int64_t)bh * p.N + ic) * p.M + imin(j, p.M - 1);
+        if (p.dgraph) cg += ldz(p.dgraph, me, INT64_MAX, inside);
+        if (p.dattn) dM = fmaf(ldz(p.dattn, me, INT64_MAX, inside), rec[1] * (1.f - p.attn_p), dM);
+      }
+      dsv[r] = ((a ? dM : 0.f) - rec[3]) * (P * p.scale);
+      gv[r] = a ? __builtin_amdgcn_fmed3f(fmaf(dM, P, cg), -1.f, 1.f) : 0.f;  // STE.py:19 hardtanh(A * grad)
+    }
+    // dQ^T += K^T ds^T ; dQh^T += T^T G^T  (keys beyond M carry ds = G = 0)
+    if constexpr (BF) {
+      const bf16x8 s0 = pack8(&dsv[0]), s1 = pack8(&dsv[8]);
+#pragma unroll
+      for (int t = 0; t < DT; ++t) {
+        dq[t] = mfma_bf(pack8(&kT[t][0]), s0, dq[t]);
+        dq[t] = mfma_bf(pack8(&kT[t][8]), s1, dq[t]);
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < DT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dq[t] = mfma(kT[t][r], dsv[r], dq[t]);
+    }
+    if constexpr (MB4) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dqh[0] = mfma4b(tT[0][r], gv[r], dqh[0]);
+    } else if constexpr (!DENSE) {
+#pragma unroll
+      for (int at = 0; at < KTA; ++at)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dqh[at] = mfma(tT[at][r], gv[r], dqh[at]);
+    }
+  }
+#undef CSA_ISSUE_BQ
+  store_rows<DT>(p.dQ + b * p.dq_sb + hd * p.dq_sh + (int64_t)i * p.dq_sn, D, D, dq, iv);
+  if constexpr (MB4) store_mb4(p.dQh + ((int64_t)bh * p.N + qb * 32) * p.kp, p.N - qb * 32, p.kp, dqh[0]);
+  else if constexpr (!DENSE) store_rows<KTA>(p.dQh + ((int64_t)bh * p.N + i) * p.kp, p.kp, p.kp, dqh, iv);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1461,11 +1675,8 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
   using SH = AttnBwdShape<D, KPH>;
   constexpr int DT = D / 32, NS = D / 2, DP = SH::DP, KP = SH::KP, KPN = SH::KPN, KTA = SH::KTA;
   constexpr bool SWZ = SH::SWZ;
-#ifdef CSA_EXP_NO_MB4
-  constexpr bool MB4 = false;
-#else
   constexpr bool MB4 = !DENSE && KP == 16;  // dT on mfma4b (store_mb4)
-#endif
+  constexpr bool HO = bwd_handoff<BF>();    // ds / G tiles out for k_attn_bwd_qg (else k_attn_bwd_qr recomputes)
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const uint32_t L0 = lds_offset(lds), Ql = L0 + SH::KQ, Xl = L0 + SH::KX, Hl = L0 + SH::KH, Sl = L0 + SH::KS;
   const int lane = lane_id(), c = lane & 31, h = lane >> 5;
@@ -1479,7 +1690,7 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
   const __amdgpu_buffer_rsrc_t qr_ = make_rsrc(p.Q + b * p.q_sb + hd * p.q_sh, SWZ ? (p.N - 1) * qld + D * 4 : 0x7fffffff);
   const __amdgpu_buffer_rsrc_t xr_ = make_rsrc(p.dX + b * p.dx_sb + hd * p.dx_sh, SWZ ? (p.N - 1) * xld + D * 4 : 0x7fffffff);
   const __amdgpu_buffer_rsrc_t hr_ = make_rsrc(DENSE ? p.dX : p.Qh + (int64_t)bh * p.N * p.kp, p.N * p.kp * 4);
-  const __amdgpu_buffer_rsrc_t sr_ = make_rsrc(p.stats + (int64_t)bh * p.N * 4, p.N * 16);
+  const __amdgpu_buffer_rsrc_t sr_ = make_rsrc(p.brow + (int64_t)bh * p.NQB * 128, p.NQB * 512);
   // rows past N are never fetched: zero the images once so they only ever hold finite data
   if constexpr (SWZ) lds_zero<(int)(SH::KV_BYTES / 4)>(lds);
   else lds_zero<(SH::NIMG + 512) / 4>(lds + SH::KH / 4);
@@ -1499,7 +1710,7 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
   const float* mk = p.mask ? p.mask + b * p.mask_sb : nullptr;
   const float mval = mk ? mk[jc] : 0.f;
   const float kbias = (jv && mval == 0.f) ? 0.f : NEG_INF;  // this lane's key (sbm_attn.py:61)
-  const float jvf = jv ? 1.f : 0.f;  // G of a key past M is stored as 0 (its sampled bit may be set)
+  const uint32_t kvm = jv ? 0xffffffffu : 0u;  // a key past M counts as not sampled: its G is stored as 0
   // this lane's row (key j) of the ds / G tiles handed to k_attn_bwd_qg, tile (qb, kbi) at + qb * NKB * 1024
   float* dsw = p.dsg + ((int64_t)bh * p.NQB * p.NKB + kbi) * 1024 + c * 32 + 4 * h;
   float kr[NS], vr[NS];
@@ -1519,8 +1730,11 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
     const int c = ln & 31, h = (ln >> 5) & 1;
     const int i0 = qb * 32;
     const bool more = qb + 1 < p.NQB;
-    wait_vm_all();  // query block qb's Q / dX / Qh / stats images and bit words have landed
-    const uint32_t wA = wAn, wR = wRn;
+    wait_vm_all();  // query block qb's Q / dX / Qh / row-constant images and bit words have landed
+    // sampled / keep bits shifted so that register r's query is bit crow(r, 0); queries past N and keys past M
+    // count as not sampled
+    const uint32_t qvm = p.N - i0 >= 32 ? 0xffffffffu : (1u << (p.N - i0)) - 1u;
+    const uint32_t wAs = (wAn & qvm & kvm) >> (4 * h), wRs = wRn >> (4 * h);
     if (more) {
       if constexpr (!DENSE) wAn = p.Abits[wcol + (int64_t)(qb + 1) * p.Mpad];
       if constexpr (DROP) wRn = p.Rbits[wcol + (int64_t)(qb + 1) * p.Mpad];
@@ -1563,60 +1777,37 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
     // qb+1 are DMA'd in while the second half runs.
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
-      // Elementwise backward (bwd_elem's algebra) on register pairs: flags as float factors, so all but
-      // exp2, the P > 0 test, the clamp and the flag selects runs as packed fp32 (v_pk_*). A key past M
-      // computes lane-local garbage (its dK / dV / dT row is never stored); a query past N must add 0.
+      // Elementwise backward, once per element (k_attn_rowprep's row constants; scalar fp32: packed v_pk_* beside
+      // the MFMAs cost more issue cycles than they save). A query past N has c0 = -inf (P = 0) and A = 0; a key
+      // past M has kbias = -inf and A = 0; so every element outside [0,N) x [0,M) stores ds = G = attw = 0.
       float dsv[8], gv[8], awv[8];
 #pragma unroll
-      for (int rr = 0; rr < 8; rr += 2) {
-        f2 af, rmf, inf, lse2, invD2, big2, gam2;
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int r = 8 * half + rr + u;
-          const bool in = i0 + crow(r, h) < p.N;
-          const f32x4 st = lds_f4(lds, SH::KS + 16 * crow(r, h));
-          af[u] = (DENSE ? in : ((wA >> crow(r, h)) & 1u)) ? 1.f : 0.f;
-          rmf[u] = ((wR >> crow(r, h)) & 1u) ? dscale : 0.f;
-          inf[u] = in ? 1.f : 0.f;
-          lse2[u] = st[0]; invD2[u] = st[1]; big2[u] = st[2]; gam2[u] = st[3];
+      for (int rr = 0; rr < 8; ++rr) {
+        const int r = 8 * half + rr;
+        const f32x4 rec = lds_f4(lds, SH::KS + 16 * crow(r, h));  // (c0, u, v, rho) of query crow(r, h)
+        const bool a = (wAs >> crow(r, 0)) & 1u;
+        const bool kp = !DROP || ((wRs >> crow(r, 0)) & 1u);
+        const float P = __builtin_amdgcn_exp2f(fmaf(sacc[r], c1, rec[0] + kbias));
+        float dM = fmaf(kp ? dpacc[r] : 0.f, rec[1], rec[2]);
+        float cg = csp;
+        if constexpr (DG) {  // upstream gradients of the returned graph / attn maps
+          const int ii = i0 + crow(r, h);
+          const bool inside = (ii < p.N) && jv;
+          const int64_t me = ((int64_t)bh * p.N + imin(ii, p.N - 1)) * p.M + jc;
+          if (p.dgraph) cg += ldz(p.dgraph, me, INT64_MAX, inside);
+          if (p.dattn) dM = fmaf(ldz(p.dattn, me, INT64_MAX, inside), rec[1] * (1.f - p.attn_p), dM);
         }
-        const int r0 = 8 * half + rr;
-        const f2 s2 = {sacc[r0], sacc[r0 + 1]}, dpp2 = {dpacc[r0], dpacc[r0 + 1]};
-        const f2 x2 = __builtin_elementwise_fma(s2, (f2)c1, __builtin_elementwise_fma(lse2, (f2)(-LOG2E), (f2)kbias));
-        const f2 P2 = {__builtin_amdgcn_exp2f(x2[0]), __builtin_amdgcn_exp2f(x2[1])};
-        f2 dattn2 = dpp2 * rmf;
-        f2 dgr2 = {0.f, 0.f};
-        if constexpr (DG) {
-#pragma unroll
-          for (int u = 0; u < 2; ++u) {
-            const int ii = i0 + crow(r0 + u, h);
-            const bool inside = (ii < p.N) && jv;
-            const int64_t me = ((int64_t)bh * p.N + imin(ii, p.N - 1)) * p.M + jc;
-            dgr2[u] = p.dgraph ? ldz(p.dgraph, me, INT64_MAX, inside) : 0.f;
-            dattn2[u] += p.dattn ? ldz(p.dattn, me, INT64_MAX, inside) : 0.f;
-          }
-        }
-        const f2 gsel = gam2 * big2, rho = gam2 - gsel;  // big in {0, 1}: gamma goes to dM or to rho
-        const f2 mpos = {P2[0] > 0.f ? af[0] : 0.f, P2[1] > 0.f ? af[1] : 0.f};  // sign(M) of F.normalize
-        const f2 dM2 = __builtin_elementwise_fma(mpos, -gsel, dattn2) * invD2;
-        const f2 ds2 = P2 * (dM2 * af - rho) * (p.scale * inf);
-        const f2 dA2 = __builtin_elementwise_fma(dM2, P2, dgr2 + csp);
-        const f2 ain = af * inf * jvf;
-        const f2 aw2 = P2 * invD2 * rmf * ain;  // dropout(attn) weight for dV
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          dsv[rr + u] = ds2[u];
-          gv[rr + u] = __builtin_amdgcn_fmed3f(dA2[u], -1.f, 1.f) * ain[u];  // STE.py:19 hardtanh(A * grad)
-          awv[rr + u] = aw2[u];
+        dsv[rr] = ((a ? dM : 0.f) - rec[3]) * (P * p.scale);
+        gv[rr] = a ? __builtin_amdgcn_fmed3f(fmaf(dM, P, cg), -1.f, 1.f) : 0.f;  // STE.py:19 hardtanh(A * grad)
+        awv[rr] = (a && kp) ? P * rec[1] : 0.f;  // dropout(attn) weight for dV
 #ifdef CSA_EXP_NO_ELEM  // experiment: timing without the elementwise algebra (wrong results)
-          dsv[rr + u] = sacc[r0 + u] * dpacc[r0 + u];
-          gv[rr + u] = dpacc[r0 + u];
-          awv[rr + u] = sacc[r0 + u];
+        dsv[rr] = sacc[r] * dpacc[r];
+        gv[rr] = dpacc[r];
+        awv[rr] = sacc[r];
 #endif
-        }
       }
 #ifndef CSA_EXP_NO_DSG_STORE  // experiment: timing without the ds / G stores (wrong results)
-      {  // queries 16 half + 4 h + (0..3) and + 8: two f32x4 per tile, for ds and for G
+      if constexpr (HO) {  // queries 16 half + 4 h + (0..3) and + 8: two f32x4 per tile, for ds and for G
         float* w = dsw + (int64_t)qb * p.NKB * 1024 + 16 * half;
         // non-temporal: the tiles are read once, by the next kernel (same-box A/B: k_attn_bwd_qg 157 -> 134 us)
 #define CSA_ST4(ptr, val) __builtin_nontemporal_store((val), reinterpret_cast<f32x4*>(ptr))
@@ -2744,7 +2935,7 @@ KArgs make_kargs(const csa_sbm_fwd_args* a, const Layout& L) {
   p.S = (const float*)((char*)st + L.S);
   p.Qh = (float*)((char*)st + L.Qh); p.Kh = (float*)((char*)st + L.Kh); p.T = (float*)((char*)st + L.T);
   p.stats = (float*)((char*)st + L.stats);
-  p.Act = (float*)((char*)st + L.Act);
+  p.Act = (a->flags & CSA_FLAG_FWD_ONLY) ? nullptr : (float*)((char*)st + L.Act);
   p.Abits = (uint32_t*)((char*)st + L.Abits); p.Rbits = (uint32_t*)((char*)st + L.Rbits);
   p.cnt = (unsigned long long*)((char*)st + L.cnt);
   p.U = a->uniforms;
@@ -2891,25 +3082,34 @@ csa_status launch_fwd(const csa_sbm_fwd_args* a, const Layout& L, hipStream_t st
   return check_launch("csa_sbm_fwd");
 }
 
-// gamma, then k_attn_bwd_kv (the elementwise backward; ds / G tiles out), then k_attn_bwd_qg, in stream order.
+// the row constants, then k_attn_bwd_kv (the elementwise backward; ds / G tiles out), then k_attn_bwd_qg, in
+// stream order (bf16 mode: k_attn_bwd_qr recomputes the query side instead of reading tiles, bwd_handoff).
 template <int D, int KPH, bool DENSE, bool DROP, bool DG, bool BF>
 void launch_attn_bwd_v(const KArgs& p, int BH, const Layout& L, const csa_prof* pf, hipStream_t st) {
   using SH = AttnBwdShape<D, KPH>;
   {
     Stage sg(pf, CSA_STAGE_ATTN_BWD_KV, st);
-    const int64_t threads = 2LL * BH * p.N;
-    hipLaunchKernelGGL(k_attn_gamma<D>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, p);
+    const int64_t threads = 2LL * BH * L.NQB * 32;
+    hipLaunchKernelGGL(k_attn_rowprep<D>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, p);
     hipLaunchKernelGGL((k_attn_bwd_kv<D, KPH, DENSE, DROP, DG, BF>), dim3(xcd_grid((int)L.NKB, BH)), dim3(64),
                        SH::KV_BYTES, st, p);
   }
   Stage sg(pf, CSA_STAGE_ATTN_BWD_Q, st);
-  hipLaunchKernelGGL((k_attn_bwd_qg<D, KPH, DENSE, BF>), dim3(xcd_grid((int)L.NQB, BH)), dim3(64), SH::G_BYTES, st, p);
+  if constexpr (bwd_handoff<BF>()) {
+    hipLaunchKernelGGL((k_attn_bwd_qg<D, KPH, DENSE, BF>), dim3(xcd_grid((int)L.NQB, BH)), dim3(64), SH::G_BYTES,
+                       st, p);
+  } else {
+    const size_t r_lds = SH::r_bytes((int)L.Mpad);
+    if (r_lds > 64 * 1024) set_dyn_lds((const void*)k_attn_bwd_qr<D, KPH, DENSE, DROP, DG, BF>, (int)r_lds);
+    hipLaunchKernelGGL((k_attn_bwd_qr<D, KPH, DENSE, DROP, DG, BF>), dim3(xcd_grid((int)L.NQB, BH)), dim3(64), r_lds,
+                       st, p);
+  }
 }
 
 template <int D, int KPH, bool DENSE, bool BF>
 void launch_attn_bwd_b(const KArgs& p, int BH, const Layout& L, bool drop, const csa_prof* pf, hipStream_t st) {
   const bool dg = p.dgraph != nullptr || p.dattn != nullptr;
-  if (p.dattn)  // sum_j dattn_ij attn_ij per query row, added to gamma by k_attn_gamma
+  if (p.dattn)  // sum_j dattn_ij attn_ij per query row, added to gamma by k_attn_rowprep
     hipLaunchKernelGGL((k_attn_gx<D, DENSE>), dim3(xcd_grid((int)L.NQB, BH)), dim3(64), 0, st, p);
   if (drop) {
     if (dg) return launch_attn_bwd_v<D, KPH, DENSE, true, true, BF>(p, BH, L, pf, st);
@@ -2950,6 +3150,7 @@ csa_status launch_bwd(const csa_sbm_bwd_args* b, const Layout& L, hipStream_t st
   p.slab = (float*)((char*)b->workspace + L.w_slab);
   p.G = (int)L.G; p.slab_floats = L.slab_floats;
   p.dsg = (float*)((char*)b->workspace + L.w_dsg); p.gplane = L.w_dsg_plane;
+  p.brow = (float*)((char*)b->workspace + L.w_brow);
   const int BH = (int)(a->B * a->H);
   (void)dense;
   const csa_prof* pf = b->prof;
@@ -3011,17 +3212,17 @@ const char* csa_last_error_str(void) { return csa::get_error(); }
 int csa_sbm_supported(int64_t d, int64_t k, uint32_t flags) { return supported(d, k, flags) ? 1 : 0; }
 
 size_t csa_sbm_state_bytes(int64_t B, int64_t H, int64_t N, int64_t M, int64_t d, int64_t k, uint32_t flags) {
-  return make_layout(B, H, N, M, d, k, flags & CSA_FLAG_DENSE).total;
+  return make_layout(B, H, N, M, d, k, flags).total;
 }
 
 size_t csa_sbm_bwd_workspace_bytes(int64_t B, int64_t H, int64_t N, int64_t M, int64_t d, int64_t k, uint32_t flags) {
-  return make_layout(B, H, N, M, d, k, flags & CSA_FLAG_DENSE).w_total;
+  return make_layout(B, H, N, M, d, k, flags).w_total;
 }
 
 csa_status csa_sbm_fwd(const csa_sbm_fwd_args* a, void* stream) {
   csa_status s = validate_fwd(a);
   if (s != CSA_OK) return s;
-  const Layout L = make_layout(a->B, a->H, a->N, a->M, a->d, a->k, a->flags & CSA_FLAG_DENSE);
+  const Layout L = make_layout(a->B, a->H, a->N, a->M, a->d, a->k, a->flags);
   hipStream_t st = (hipStream_t)stream;
   const DeviceGuard guard(st);
   const bool dense = a->flags & CSA_FLAG_DENSE;
@@ -3043,7 +3244,7 @@ csa_status csa_sbm_maps(const csa_sbm_fwd_args* a, float* graph, float* attn, vo
   if (s != CSA_OK) return s;
   if (!graph && !attn) return CSA_OK;
   const bool dense = a->flags & CSA_FLAG_DENSE;
-  const Layout L = make_layout(a->B, a->H, a->N, a->M, a->d, a->k, dense);
+  const Layout L = make_layout(a->B, a->H, a->N, a->M, a->d, a->k, a->flags);
   KArgs p = make_kargs(a, L);
   hipStream_t st = (hipStream_t)stream;
   const DeviceGuard guard(st);
@@ -3077,7 +3278,8 @@ csa_status csa_sbm_bwd(const csa_sbm_bwd_args* b, void* stream) {
                  !b->dproj_b[1] || !b->dproj_b[2]))
     return fail(CSA_INVALID_ARG, "null parameter-gradient output");
   if (b->schedule > CSA_SCHED_CONCURRENT) return fail(CSA_INVALID_ARG, "schedule must be a CSA_SCHED_* value");
-  const Layout L = make_layout(a->B, a->H, a->N, a->M, a->d, a->k, dense);
+  if (a->flags & CSA_FLAG_FWD_ONLY) return fail(CSA_INVALID_ARG, "the forward ran with CSA_FLAG_FWD_ONLY: no backward state");
+  const Layout L = make_layout(a->B, a->H, a->N, a->M, a->d, a->k, a->flags);
   hipStream_t st = (hipStream_t)stream;
   const DeviceGuard guard(st);
   if (a->d == 64) {

@@ -146,17 +146,19 @@ std::tuple<Tensor, Tensor, Tensor> sbm_fwd(const Tensor& Q, const Tensor& K, con
                                            const optional<Tensor>& mask, const optional<Tensor>& cluster_w,
                                            at::TensorList proj_w, at::TensorList proj_b,
                                            const optional<Tensor>& uniforms, int64_t k, int64_t seed,
-                                           int64_t offset, double attn_p, double proj_p, bool dense, bool bf16) {
+                                           int64_t offset, double attn_p, double proj_p, bool dense, bool bf16,
+                                           bool fwd_only) {
   const at::OptionalDeviceGuard guard(at::device_of(Q));
   const SbmIn in = sbm_prep(Q, K, V, mask, cluster_w, proj_w, proj_b, uniforms);
   const int64_t B = in.Q.size(0), H = in.Q.size(1), N = in.Q.size(2), d = in.Q.size(3), M = in.K.size(2);
-  const uint32_t flags = dense ? CSA_FLAG_DENSE : 0u;
+  const uint32_t flags = (dense ? CSA_FLAG_DENSE : 0u) | (fwd_only ? CSA_FLAG_FWD_ONLY : 0u);
   TORCH_CHECK(csa_sbm_supported(d, k, flags), "csa::sbm_fwd: unsupported head_dim=", d, " / num_clusters=", k);
   const auto o = in.Q.options().dtype(at::kFloat);
   Tensor X = head_major_out(B, H, N, d, o);
   Tensor sp = at::empty({dense ? 0 : H}, o);
   Tensor state = at::empty({(int64_t)csa_sbm_state_bytes(B, H, N, M, d, k, flags)}, o.dtype(at::kByte));
   csa_sbm_fwd_args a = fwd_struct(in, k, seed, offset, attn_p, proj_p, dense, bf16);
+  a.flags = flags;
   a.X = fpw(X); a.x_sb = X.stride(0); a.x_sh = X.stride(1); a.x_sn = X.stride(2);
   if (!dense) a.sparsity = fpw(sp);
   a.state = state.data_ptr();

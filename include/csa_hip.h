@@ -54,6 +54,10 @@ typedef enum csa_status {
 
 /* flags */
 #define CSA_FLAG_DENSE 1u /* FullAttention (graph == 1, no cluster projection, no sampling) */
+/* ABI v6: the caller will not run csa_sbm_bwd on this forward's state (inference / no_grad): the state omits the
+ * projection MLP's saved activations, which only the backward reads (csa_sbm_state_bytes shrinks, the forward
+ * skips their stores); csa_sbm_bwd rejects such a state. */
+#define CSA_FLAG_FWD_ONLY 2u
 
 /* ABI v5: schedule of an attention backward's two halves (csa_rel_attn_bwd_args .schedule). The key half
  * may run on a caller-owned side stream beside the query half, forked from and joined back into `stream`

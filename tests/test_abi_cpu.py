@@ -49,6 +49,13 @@ def test_state_and_workspace_sizes_monotone():
     b = L.csa_sbm_state_bytes(4, 8, 150, 150, 64, 10, 0)
     assert 0 < a < b
     assert L.csa_sbm_bwd_workspace_bytes(256, 8, 150, 150, 64, 10, 0) > 0
+    # CSA_FLAG_FWD_ONLY drops exactly the projection MLP's activation blocks (B H (NQB + NKB) 32-row items of
+    # h1 | h2 | po | hat: (3 d + 32) x 32 fp32 each)
+    f = L.csa_sbm_state_bytes(4, 8, 150, 150, 64, 10, _lib.CSA_FLAG_FWD_ONLY)
+    assert b - f == 4 * 8 * 10 * (3 * 64 + 32) * 32 * 4
+    # the backward workspace holds the ds / G tiles (dense: ds only) and the per-row constants
+    dense = _lib.CSA_FLAG_DENSE
+    assert L.csa_sbm_bwd_workspace_bytes(4, 8, 150, 150, 64, 0, dense) >= 4 * 8 * 25 * 1024 * 4 + 4 * 8 * 160 * 16
 
 
 def test_invalid_args_rejected_without_gpu():

@@ -1,5 +1,7 @@
 """End-to-end: the caller model (csa_amd.model.CSATrans) on the HIP kernels vs the REFERENCE CSATrans
 (module/csa_trans.py) on identical weights, inputs and uniforms (tests/golden/csatrans_tiny.npz)."""
+import re
+
 import numpy as np
 import pytest
 import torch
@@ -326,3 +328,14 @@ def test_tuned_gemm_table_keeps_the_train_step():
                 bad.append((k, d / n))
     print("worst per-tensor gradient difference (tuned vs default GEMMs):", max(rel), f"({len(noise)} noise-level biases)")
     assert not bad, bad
+    # The exemption above covers exactly the biases whose exact gradient is 0, and nothing else. In every CSE
+    # layer's DisentangledAttn (module/disentangled_attn.py:44-65) the score of row x is
+    #   s[x, y] = (q_x . k_y + lq[rel[y,x]] . k_y + q_x . lk[rel[x,y]]) / sqrt(3 d_k), then softmax over y.
+    # A bias b of the lk projections (l_linear.1, t_linear.1) adds q_x . b to the whole row x; the key
+    # projection's bias (linear_layers.1) adds q_x . b as well (its lq . b part measured at rounding level in
+    # round 3). Softmax is shift-invariant per row, so d loss / d b = sum_x (sum_y g[x, y]) q_x = 0 with g the
+    # softmax input gradient, whose rows sum to 0. 4 CSE layers x 3 biases = 12 tensors.
+    zero = {k for k in g_d
+            if re.fullmatch(r"pegen\.layers\.\d+\.self_attn\.(l_linear\.1|t_linear\.1|linear_layers\.1)\.bias", k)}
+    assert len(zero) == 12, sorted(zero)
+    assert set(noise) == zero, (sorted(set(noise) - zero), sorted(zero - set(noise)))
