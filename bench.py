@@ -46,7 +46,7 @@ PMC_TABLE = os.path.join(ROOT, "code-structure-aware-transformer_amd", "csa_amd"
 STAGE_KERNELS = {"prep": ("k_cluster_softmax", "k_frag_prep"), "proj_fwd": ("k_proj_fwd_l",),
                  "attn_fwd": ("k_attn_fwd",), "attn_bwd_kv": ("k_attn_rowprep", "k_attn_bwd_kv"),
                  "attn_bwd_q": ("k_attn_bwd_qg",), "proj_bwd": ("k_proj_bwd_s",),
-                 "reduce": ("k_reduce_slabs", "k_cluster_grad")}
+                 "reduce": ("k_reduce_slabs", "k_cluster_grad")}  # (proj_bwd_k: k_proj_bwd_s as well)
 
 
 def pmc_table():
@@ -548,19 +548,29 @@ def main():
     flops = stage_flops_per_ast(H, N, N, d, 0 if args.dense else k)
     if args.dense:
         flops = {"attn_fwd": H * 4 * N * N * d, "attn_bwd_q": H * 2 * N * N * d, "attn_bwd_kv": H * 6 * N * N * d}
+    if "proj_bwd_k" in stage_ms:  # concurrent schedule: the projection backward's key / query items split
+        flops["proj_bwd_k"] = H * (N * (12 * d * d + 4 * k * d) + N * 4 * k * k)
+        flops["proj_bwd"] = H * N * (12 * d * d + 4 * k * d)
     timed = {s: v for s, v in stage_ms.items() if s in flops}
-    # side-stream backward (B=64 shapes): the bwd_kv window opens at the fork, before bwd_q ends (in
-    # order it opens after bwd_q's stop), so neither window is one kernel's launch and neither can be
-    # the roofline kernel
+    # side-stream backward: a stage window that overlaps another backward stage's window is not one kernel's
+    # launch alone on the device, so it cannot be the roofline kernel
     pb0 = profs[-1][1]
-    sq, skv = STAGES["attn_bwd_q"], STAGES["attn_bwd_kv"]
-    overlapped = bool(pb0.stop[sq] and pb0.start[skv]) and \
-        ev.elapsed_ms(ctypes.c_void_p(pb0.stop[sq]), ctypes.c_void_p(pb0.start[skv])) < 0
-    cand = {s: v for s, v in timed.items() if not (overlapped and s in ("attn_bwd_q", "attn_bwd_kv"))}
+    win = {}
+    base = None
+    for name in ("attn_bwd_kv", "attn_bwd_q", "proj_bwd_k", "proj_bwd", "reduce"):
+        s_ = STAGES[name]
+        if pb0.start[s_] and pb0.stop[s_]:
+            if base is None:
+                base = pb0.start[s_]
+            win[name] = (ev.elapsed_ms(ctypes.c_void_p(base), ctypes.c_void_p(pb0.start[s_])),
+                         ev.elapsed_ms(ctypes.c_void_p(base), ctypes.c_void_p(pb0.stop[s_])))
+    over = {a for a in win for b_ in win if a != b_ and win[a][0] < win[b_][1] - 1e-4 and win[b_][0] < win[a][1] - 1e-4}
+    overlapped = bool(over)
+    cand = {s: v for s, v in timed.items() if s not in over}
     dom = max(cand, key=cand.get) if cand else None
     kernel_of = dict(KERNEL_OF_STAGE)
     if not args.dense and d in (64, 96) and k <= 16:
-        kernel_of["proj_bwd"] = "k_proj_bwd_s"  # the k <= 16 projection-backward variant
+        kernel_of["proj_bwd"] = kernel_of["proj_bwd_k"] = "k_proj_bwd_s"  # the k <= 16 projection-backward variant
 
     # 2) timed region: events only around the dominant kernel (its live average launch duration)
     profs = make_profs(args.steps, [dom] if dom else [])
@@ -615,7 +625,8 @@ def main():
         # attention kernels side by side -- B=64 shapes, DESIGN §3 -- their stage windows overlap)
         "stage_frac_of_f32_mfma_peak": {s: round(flops[s] * B / (v * 1e-3) / 1e12 / PEAK_F32_MFMA_TFLOPS, 3)
                                         for s, v in timed.items() if v > 0},
-        "attn_bwd_schedule": "side stream (overlapped stage windows)" if overlapped else "in order",
+        "bwd_schedule": ("projection backward key-block items on a side stream beside k_attn_bwd_qg (overlapped "
+                         "stage windows: " + ", ".join(sorted(over)) + ")") if overlapped else "in order",
     }
     if table:
         out.update(traffic_evidence(table, B, stage_ms))

@@ -24,9 +24,10 @@ i64, u64, u32, f32, vp = ctypes.c_int64, ctypes.c_uint64, ctypes.c_uint32, ctype
 
 
 CSA_STAGE_COUNT = 8
-STAGES = {"prep": 0, "proj_fwd": 1, "attn_fwd": 2, "attn_bwd_q": 3, "attn_bwd_kv": 4, "proj_bwd": 5, "reduce": 6}
+STAGES = {"prep": 0, "proj_fwd": 1, "attn_fwd": 2, "attn_bwd_q": 3, "attn_bwd_kv": 4, "proj_bwd": 5, "reduce": 6,
+          "proj_bwd_k": 7}
 KERNEL_OF_STAGE = {"proj_fwd": "k_proj_fwd", "attn_fwd": "k_attn_fwd", "attn_bwd_q": "k_attn_bwd_qg",
-                   "attn_bwd_kv": "k_attn_bwd_kv", "proj_bwd": "k_proj_bwd"}
+                   "attn_bwd_kv": "k_attn_bwd_kv", "proj_bwd": "k_proj_bwd", "proj_bwd_k": "k_proj_bwd"}
 
 
 def on_device(device):

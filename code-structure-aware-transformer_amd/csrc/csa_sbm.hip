@@ -87,6 +87,7 @@ struct Layout {
   // bwd workspace
   size_t w_dQh, w_dT, w_slab, w_dS, w_dC, w_gx, w_dsg, w_brow, w_total;
   int64_t G, slab_floats, w_dsg_plane;
+  int64_t G_K, G_Q;  // k_proj_bwd_s split by item kind (concurrent schedule): workgroups per head of each launch
 };
 
 inline size_t al(size_t x) { return (x + 255) & ~size_t(255); }
@@ -139,11 +140,13 @@ Layout make_layout(int64_t B, int64_t H, int64_t N, int64_t M, int64_t D, int64_
   // backward workspace
   // two workgroups per CU for d = 64 with KT = 1 (k_proj_bwd_s / k_proj_bwd<64, 1>: 80 / 64 KiB LDS)
   L.G = dense ? 0 : proj_bwd_groups(B, H, L.NQB + L.NKB, (D == 64 && L.KT == 1) ? 2 : 1);
+  L.G_K = dense ? 0 : proj_bwd_groups(B, H, L.NKB, (D == 64 && L.KT == 1) ? 2 : 1);
+  L.G_Q = dense ? 0 : proj_bwd_groups(B, H, L.NQB, (D == 64 && L.KT == 1) ? 2 : 1);
   L.slab_floats = dense ? 0 : (3 * D * D + 3 * D + KP32 * D + KP32 * KP32);
   o = 0;
   L.w_dQh = take(sizeof(float) * B * H * N * L.kp);
   L.w_dT = take(sizeof(float) * B * H * M * L.kp);
-  L.w_slab = take(sizeof(float) * H * L.G * L.slab_floats);
+  L.w_slab = take(sizeof(float) * H * std::max(L.G, L.G_K + L.G_Q) * L.slab_floats);
   L.w_dS = take(sizeof(float) * H * KP32 * KP32);
   L.w_dC = take(sizeof(float) * H * KP32 * D);
   L.w_gx = take(sizeof(float) * B * H * N);  // used only when an attn-map gradient is passed
@@ -370,6 +373,7 @@ struct KArgs {
   float* brow;                 // per query row (c0, u, v, rho) of the elementwise backward (k_attn_rowprep)
   int64_t dx_sb, dx_sh, dx_sn, dq_sb, dq_sh, dq_sn, dk_sb, dk_sh, dk_sn, dv_sb, dv_sh, dv_sn;
   int G; int64_t slab_floats;
+  int pb_kind, pb_goff;  // k_proj_bwd_s items: 0 all, 1 key blocks, 2 query blocks; its first slab of the head's G
 };
 
 // One 16-bit uniform per element: Philox word e/2, low half for even e.
@@ -397,6 +401,13 @@ __device__ __forceinline__ void mlp_act(const KArgs& p, f32x16 (&a)[D / 32], int
       if (drop)
         u = philox4x32(u32x4{(uint32_t)row, (uint32_t)(4 * ot + 2 * gp + h) | (layer << 16) | (isK << 20),
                              (uint32_t)bh, (RNG_PROJ_DROP << 28) ^ p.off}, p.seed_lo, p.seed_hi);
+#ifdef CSA_EXP_RNG24_COST  // experiment: the half extra Philox call per 8 uniforms of 24-bit draws
+      if (drop && gp == 0) {
+        const u32x4 x = philox4x32(u32x4{(uint32_t)row, (uint32_t)(4 * ot + h) | (layer << 16) | (isK << 20),
+                                         (uint32_t)bh, 0x50000000u ^ p.off}, p.seed_lo, p.seed_hi);
+        u.x ^= ((x.x ^ x.y ^ x.z ^ x.w) == 0x9e3779b9u) ? 1u : 0u;
+      }
+#endif
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         float v = a[ot][8 * gp + e];
@@ -1009,6 +1020,14 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd
           r_drop[gp] = philox4x32(u32x4{(uint32_t)i, (uint32_t)(8 * kt + 4 * gp + h), (uint32_t)bh,
                                         (RNG_ATTN_DROP << 28) ^ p.off}, sk0, sk1);
       }
+#ifdef CSA_EXP_RNG24_COST  // experiment: the two extra Philox calls per tile that 24-bit uniforms would need
+      {
+        const u32x4 x1 = philox4x32(u32x4{(uint32_t)i, (uint32_t)(8 * kt + h), (uint32_t)bh, 0x70000000u ^ p.off}, sk0, sk1);
+        const u32x4 x2 = philox4x32(u32x4{(uint32_t)i, (uint32_t)(8 * kt + 4 + h), (uint32_t)bh, 0x60000000u ^ p.off}, sk0, sk1);
+        const uint32_t z = x1.x ^ x1.y ^ x1.z ^ x1.w ^ x2.x ^ x2.y ^ x2.z ^ x2.w;
+        r_drop[0].x ^= (z == 0x9e3779b9u) ? 1u : 0u;  // never changes a result in practice; keeps the calls live
+      }
+#endif
     }
     // S^T = K Q^T : A operand = K rows from the image (row c, lin-perm chunks of half h)
     f32x16 sacc = zero16();
@@ -2409,9 +2428,11 @@ __global__ __launch_bounds__(256, ProjBwdSmallShape<D>::LCS ? 1 : 2) void k_proj
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int hd = blockIdx.y, g = blockIdx.x, G = gridDim.x;
   const int per_b = p.NQB + p.NKB;
-  const int i_lo = (int)((int64_t)g * p.B * per_b / G), i_hi = (int)((int64_t)(g + 1) * p.B * per_b / G);
-  const int n_items = i_hi - i_lo;  // this workgroup's items: i_lo .. i_hi - 1 of the head
-  float* slab = p.slab + ((int64_t)hd * G + g) * p.slab_floats;
+  // this launch's items of the head, per batch element: all (Q blocks, then K blocks), or one kind only
+  const int ipb = p.pb_kind == 1 ? p.NKB : p.pb_kind == 2 ? p.NQB : per_b, roff = p.pb_kind == 1 ? p.NQB : 0;
+  const int i_lo = (int)((int64_t)g * p.B * ipb / G), i_hi = (int)((int64_t)(g + 1) * p.B * ipb / G);
+  const int n_items = i_hi - i_lo;  // this workgroup's items: i_lo .. i_hi - 1 of the launch's items
+  float* slab = p.slab + ((int64_t)hd * p.G + p.pb_goff + g) * p.slab_floats;
   const float ks = p.proj_p > 0.f ? 1.f / (1.f - p.proj_p) : 1.f;
   const float* CfT = p.CfT + (size_t)hd * 32 * D;
   const float* SfT = p.SfT + (size_t)hd * 32 * 32;
@@ -2442,8 +2463,8 @@ __global__ __launch_bounds__(256, ProjBwdSmallShape<D>::LCS ? 1 : 2) void k_proj
     Item it;
     const int item = grp * 4 + w;
     it.has = item < n_items;
-    it.b = it.has ? (i_lo + item) / per_b : 0;
-    it.r = it.has ? (i_lo + item) % per_b : 0;
+    it.b = it.has ? (i_lo + item) / ipb : 0;
+    it.r = it.has ? roff + (i_lo + item) % ipb : 0;
     it.isK = it.r >= p.NQB;
     it.rb = it.isK ? it.r - p.NQB : it.r;
     it.nrows = it.isK ? p.M : p.N;
@@ -3084,8 +3105,10 @@ csa_status launch_fwd(const csa_sbm_fwd_args* a, const Layout& L, hipStream_t st
 
 // the row constants, then k_attn_bwd_kv (the elementwise backward; ds / G tiles out), then k_attn_bwd_qg, in
 // stream order (bf16 mode: k_attn_bwd_qr recomputes the query side instead of reading tiles, bwd_handoff).
-template <int D, int KPH, bool DENSE, bool DROP, bool DG, bool BF>
-void launch_attn_bwd_v(const KArgs& p, int BH, const Layout& L, const csa_prof* pf, hipStream_t st) {
+// mid(): enqueued between the key half and the query half (the concurrent schedule forks the projection
+// backward's key-block items there).
+template <int D, int KPH, bool DENSE, bool DROP, bool DG, bool BF, typename MID>
+void launch_attn_bwd_v(const KArgs& p, int BH, const Layout& L, const csa_prof* pf, hipStream_t st, MID mid) {
   using SH = AttnBwdShape<D, KPH>;
   {
     Stage sg(pf, CSA_STAGE_ATTN_BWD_KV, st);
@@ -3094,6 +3117,7 @@ void launch_attn_bwd_v(const KArgs& p, int BH, const Layout& L, const csa_prof* 
     hipLaunchKernelGGL((k_attn_bwd_kv<D, KPH, DENSE, DROP, DG, BF>), dim3(xcd_grid((int)L.NKB, BH)), dim3(64),
                        SH::KV_BYTES, st, p);
   }
+  mid();
   Stage sg(pf, CSA_STAGE_ATTN_BWD_Q, st);
   if constexpr (bwd_handoff<BF>()) {
     hipLaunchKernelGGL((k_attn_bwd_qg<D, KPH, DENSE, BF>), dim3(xcd_grid((int)L.NQB, BH)), dim3(64), SH::G_BYTES,
@@ -3106,25 +3130,39 @@ void launch_attn_bwd_v(const KArgs& p, int BH, const Layout& L, const csa_prof* 
   }
 }
 
-template <int D, int KPH, bool DENSE, bool BF>
-void launch_attn_bwd_b(const KArgs& p, int BH, const Layout& L, bool drop, const csa_prof* pf, hipStream_t st) {
+template <int D, int KPH, bool DENSE, bool BF, typename MID>
+void launch_attn_bwd_b(const KArgs& p, int BH, const Layout& L, bool drop, const csa_prof* pf, hipStream_t st, MID mid) {
   const bool dg = p.dgraph != nullptr || p.dattn != nullptr;
   if (p.dattn)  // sum_j dattn_ij attn_ij per query row, added to gamma by k_attn_rowprep
     hipLaunchKernelGGL((k_attn_gx<D, DENSE>), dim3(xcd_grid((int)L.NQB, BH)), dim3(64), 0, st, p);
   if (drop) {
-    if (dg) return launch_attn_bwd_v<D, KPH, DENSE, true, true, BF>(p, BH, L, pf, st);
-    return launch_attn_bwd_v<D, KPH, DENSE, true, false, BF>(p, BH, L, pf, st);
+    if (dg) return launch_attn_bwd_v<D, KPH, DENSE, true, true, BF>(p, BH, L, pf, st, mid);
+    return launch_attn_bwd_v<D, KPH, DENSE, true, false, BF>(p, BH, L, pf, st, mid);
   }
-  if (dg) return launch_attn_bwd_v<D, KPH, DENSE, false, true, BF>(p, BH, L, pf, st);
-  return launch_attn_bwd_v<D, KPH, DENSE, false, false, BF>(p, BH, L, pf, st);
+  if (dg) return launch_attn_bwd_v<D, KPH, DENSE, false, true, BF>(p, BH, L, pf, st, mid);
+  return launch_attn_bwd_v<D, KPH, DENSE, false, false, BF>(p, BH, L, pf, st, mid);
 }
 
-template <int D, int KPH, bool DENSE>
-void launch_attn_bwd(const KArgs& p, int BH, const Layout& L, bool drop, const csa_prof* pf, hipStream_t st) {
+template <int D, int KPH, bool DENSE, typename MID>
+void launch_attn_bwd(const KArgs& p, int BH, const Layout& L, bool drop, const csa_prof* pf, hipStream_t st, MID mid) {
   if constexpr (KPH <= 8) {
-    if (p.bf16) return launch_attn_bwd_b<D, KPH, DENSE, true>(p, BH, L, drop, pf, st);
+    if (p.bf16) return launch_attn_bwd_b<D, KPH, DENSE, true>(p, BH, L, drop, pf, st, mid);
   }
-  return launch_attn_bwd_b<D, KPH, DENSE, false>(p, BH, L, drop, pf, st);
+  return launch_attn_bwd_b<D, KPH, DENSE, false>(p, BH, L, drop, pf, st, mid);
+}
+
+// k_proj_bwd_s over one kind of items (0 all, 1 key blocks, 2 query blocks) on stream s
+template <int D>
+void launch_proj_bwd_s(KArgs p, int kind, int G, int goff, int Gtot, int H, hipStream_t s) {
+  using Ss = ProjBwdSmallShape<D>;
+  p.pb_kind = kind; p.pb_goff = goff; p.G = Gtot;
+  if (p.bf16) {  // CSA_DTYPE_BF16: projection contractions on bf16 MFMA
+    set_dyn_lds((const void*)k_proj_bwd_s<D, true>, (int)Ss::LDS_BYTES);
+    hipLaunchKernelGGL((k_proj_bwd_s<D, true>), dim3(G, H), dim3(256), Ss::LDS_BYTES, s, p);
+  } else {
+    set_dyn_lds((const void*)k_proj_bwd_s<D>, (int)Ss::LDS_BYTES);
+    hipLaunchKernelGGL((k_proj_bwd_s<D>), dim3(G, H), dim3(256), Ss::LDS_BYTES, s, p);
+  }
 }
 
 template <int D, int KPH, int KT>
@@ -3155,25 +3193,39 @@ csa_status launch_bwd(const csa_sbm_bwd_args* b, const Layout& L, hipStream_t st
   (void)dense;
   const csa_prof* pf = b->prof;
   if constexpr (KT > 0) {
-    launch_attn_bwd<D, KPH, false>(p, BH, L, a->attn_dropout > 0.f, pf, st);
+    // Concurrent schedule (k <= 16): the projection backward's key-block items need only dT and dK, which the
+    // key half has written, so they run on the caller's side stream beside k_attn_bwd_qg (HBM / latency bound)
+    // and the query-block items follow it on this stream. Separate slab sets, summed in a fixed order: the
+    // results are bitwise those of the in-order schedule.
+    constexpr bool SPLIT = (D == 64 || D == 96) && KPH == 8;
+    const bool conc = SPLIT && b->side_stream && b->side_fork && b->side_join && b->schedule != CSA_SCHED_IN_ORDER;
+    const SideLane lane{(hipStream_t)b->side_stream, (hipEvent_t)b->side_fork, (hipEvent_t)b->side_join};
+    const int Gtot = (int)(L.G_K + L.G_Q);
+    bool forked = false;
+    auto mid = [&]() {
+      if (!conc || !lane.fork(st)) return;
+      forked = true;
+      Stage sg(pf, CSA_STAGE_PROJ_BWD_K, lane.s);
+      if constexpr (SPLIT) launch_proj_bwd_s<D>(p, 1, (int)L.G_K, 0, Gtot, (int)a->H, lane.s);
+    };
+    launch_attn_bwd<D, KPH, false>(p, BH, L, a->attn_dropout > 0.f, pf, st, mid);
+    if (conc && !forked) return fail_hip("csa_sbm_bwd: side-stream fork");
     using Sh = ProjBwdShape<D, KT>;
     if (!Sh::REGACC && hipMemsetAsync(p.slab, 0, sizeof(float) * a->H * L.G * L.slab_floats, st) != hipSuccess)
       return check_launch("memset slabs");
     {
       Stage sg(pf, CSA_STAGE_PROJ_BWD, st);
-      if constexpr ((D == 64 || D == 96) && KPH == 8) {  // k <= 16
-        using Ss = ProjBwdSmallShape<D>;
-        if (p.bf16) {  // CSA_DTYPE_BF16: projection contractions on bf16 MFMA
-          set_dyn_lds((const void*)k_proj_bwd_s<D, true>, (int)Ss::LDS_BYTES);
-          hipLaunchKernelGGL((k_proj_bwd_s<D, true>), dim3(L.G, a->H), dim3(256), Ss::LDS_BYTES, st, p);
-        } else {
-          set_dyn_lds((const void*)k_proj_bwd_s<D>, (int)Ss::LDS_BYTES);
-          hipLaunchKernelGGL((k_proj_bwd_s<D>), dim3(L.G, a->H), dim3(256), Ss::LDS_BYTES, st, p);
-        }
+      if constexpr (SPLIT) {  // k <= 16
+        if (forked) launch_proj_bwd_s<D>(p, 2, (int)L.G_Q, (int)L.G_K, Gtot, (int)a->H, st);
+        else launch_proj_bwd_s<D>(p, 0, (int)L.G, 0, (int)L.G, (int)a->H, st);
       } else {
         set_dyn_lds((const void*)k_proj_bwd<D, KT>, (int)Sh::LDS_BYTES);
         hipLaunchKernelGGL((k_proj_bwd<D, KT>), dim3(L.G, a->H), dim3(256), Sh::LDS_BYTES, st, p);
       }
+    }
+    if (forked) {
+      if (!lane.join(st)) return fail_hip("csa_sbm_bwd: side-stream join");
+      p.G = Gtot;  // the reduction sums both launches' slabs
     }
     Stage sr(pf, CSA_STAGE_REDUCE, st);
     const int KP32 = 32 * KT;
@@ -3186,7 +3238,7 @@ csa_status launch_bwd(const csa_sbm_bwd_args* b, const Layout& L, hipStream_t st
     hipLaunchKernelGGL(k_cluster_grad, dim3((unsigned)a->k, (unsigned)a->H), dim3(128), 0, st, p.S, (const float*)dS_ws,
                        (const float*)dC_ws, a->cluster_w, b->dcluster_w, (int)a->k, D, KP32);
   } else {
-    launch_attn_bwd<D, 0, true>(p, BH, L, a->attn_dropout > 0.f, pf, st);
+    launch_attn_bwd<D, 0, true>(p, BH, L, a->attn_dropout > 0.f, pf, st, [] {});
   }
   return check_launch("csa_sbm_bwd");
 }

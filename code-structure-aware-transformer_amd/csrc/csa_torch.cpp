@@ -243,8 +243,10 @@ std::vector<Tensor> sbm_bwd(const Tensor& Q, const Tensor& K, const Tensor& V, c
     }
   }
   b.prof = g_prof_bwd;
-  b.schedule = (uint32_t)schedule;  // ABI v6: validated, no side lane (the SBM backward runs in order)
-  check(csa_sbm_bwd(&b, cur_stream(in.Q)), "csa_sbm_bwd");
+  {
+    const std::unique_lock<std::mutex> lane_lock = set_side_lane(b, in.Q, schedule);
+    check(csa_sbm_bwd(&b, cur_stream(in.Q)), "csa_sbm_bwd");
+  }
   return outs;
 }
 

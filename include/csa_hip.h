@@ -63,8 +63,9 @@ typedef enum csa_status {
  * may run on a caller-owned side stream beside the query half, forked from and joined back into `stream`
  * with two caller-owned events (capture-safe); outputs are bitwise the same either way. AUTO uses the side
  * stream when the query half's grid leaves a partial last round of workgroups on the device (side_stream
- * must be set, else it runs in order). ABI v6: the SBM backward's query half consumes the ds / G tiles
- * its key half writes, so csa_sbm_bwd always runs in order (its schedule fields are accepted and unused). */
+ * must be set, else it runs in order). ABI v6, csa_sbm_bwd: the projection backward's key-block items (they
+ * need only the key half's dT) run on the side stream beside the query half (k_attn_bwd_qg) and its query-
+ * block items; AUTO = CONCURRENT whenever a side lane is given. Bitwise-identical results either way. */
 #define CSA_SCHED_AUTO 0u
 #define CSA_SCHED_IN_ORDER 1u
 #define CSA_SCHED_CONCURRENT 2u /* needs side_stream / side_fork / side_join */
@@ -87,10 +88,11 @@ enum {
   CSA_STAGE_PREP = 0,       /* cluster softmax + fragment prep */
   CSA_STAGE_PROJ_FWD = 1,   /* k_proj_fwd */
   CSA_STAGE_ATTN_FWD = 2,   /* k_attn_fwd */
-  CSA_STAGE_ATTN_BWD_Q = 3, /* k_attn_bwd_q */
-  CSA_STAGE_ATTN_BWD_KV = 4,/* k_attn_bwd_kv */
-  CSA_STAGE_PROJ_BWD = 5,   /* k_proj_bwd */
+  CSA_STAGE_ATTN_BWD_Q = 3, /* k_attn_bwd_qg (bf16 mode: k_attn_bwd_qr) */
+  CSA_STAGE_ATTN_BWD_KV = 4,/* k_attn_rowprep + k_attn_bwd_kv */
+  CSA_STAGE_PROJ_BWD = 5,   /* k_proj_bwd (concurrent schedule: its query-block items only) */
   CSA_STAGE_REDUCE = 6,     /* slab reduction + cluster grad */
+  CSA_STAGE_PROJ_BWD_K = 7, /* concurrent schedule: k_proj_bwd's key-block items, on the side stream */
   CSA_STAGE_COUNT = 8
 };
 typedef struct csa_prof {
@@ -138,8 +140,8 @@ typedef struct csa_sbm_bwd_args {
   /* ABI v4: (B,H,N,M) contiguous upstream gradient of the returned attn map (sbm_attn.py:62, the tensor the
    * reference returns), or NULL. */
   const float* dattn;
-  /* ABI v5: CSA_SCHED_* and a side lane (hipStream_t + two hipEvent_t). ABI v6: validated (schedule must be
-   * a CSA_SCHED_* value) and otherwise unused: the SBM backward is one stream-ordered chain. */
+  /* ABI v5: CSA_SCHED_* and the caller's side lane: a hipStream_t of the same device as `stream` and two
+   * hipEvent_t (hipEventDisableTiming) used only between this call's fork and join. NULL = in order. */
   uint32_t schedule;
   void* side_stream; void* side_fork; void* side_join;
 } csa_sbm_bwd_args;
