@@ -203,6 +203,7 @@ struct RelArgs {
   const float* RB;  // tile-major relation bias (written by k_rel_fwd_f)
   int bf16;         // CSA_DTYPE_BF16: bf16 MFMA for c2c, PV and their gradients
   float *dk, *dv, *gc2p, *gp2ct, *qstat;
+  float* gt;  // fp32 16-row path: softmax-input gradient tiles k_rel_bwd_kh -> k_rel_bwd_qg ([key][query] 32 x 32)
   const float *lq, *lk;
   int qstat_pre;  // qstat written by k_rel_qstat (concurrent backward): k_rel_bwd_qf leaves it alone
   int LB16, Q4;   // 16-row bins (k_rel_bwd_qh / kh): row stride and the per-lane-group K range
@@ -1215,6 +1216,8 @@ __device__ __forceinline__ void bins_store16(float* __restrict__ outT, int64_t l
 // LDS of the 16-row kernels: images | (key side: 512 B of query stats) | 4 KB bias tile | 2 x 16-row bins
 __host__ __device__ constexpr int rel16_bins_off(bool key_side) { return 2 * 32 * 64 * 4 + (key_side ? 512 : 0) + 4096; }
 
+typedef uint32_t u32x4v_t __attribute__((ext_vector_type(4)));
+
 // Query side, 16-row waves: workgroup = (b,h, 32-query block), wave w = queries 16 w .. 16 w + 15.
 // Same algebra and outputs as k_rel_bwd_qf.
 __global__ __launch_bounds__(128, 2) void k_rel_bwd_qh(const RelArgs p) {
@@ -1457,6 +1460,14 @@ __global__ __launch_bounds__(128, 2) void k_rel_bwd_kh(const RelArgs p) {
       Pv[e] = P;
       gv[e] = (inside && !msk) ? P * (dpa - dl[e]) * p.inv_scale : 0.f;
     }
+    if (p.gt) {  // this key's row of tile (qb, kbi) for k_rel_bwd_qg: queries 16 st + 4 g .. + 3 (read once: non-temporal)
+      const __amdgpu_buffer_rsrc_t gr = make_rsrc(p.gt + (int64_t)bh * p.NQB * p.NKB * 1024, p.NQB * p.NKB * 4096);
+#pragma unroll
+      for (int st = 0; st < 2; ++st)
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(u32x4v_t, f32x4{gv[4 * st], gv[4 * st + 1], gv[4 * st + 2], gv[4 * st + 3]}), gr,
+            4 * (yr * 32 + 4 * g + 16 * st), (qb * p.NKB + kbi) * 4096, 2);
+    }
     float xc[4][8], qc[4][8];  // A operands of dv / dk: X[query 16 st + 4 g + i][d = 16 t + x16]
 #pragma unroll
     for (int t = 0; t < 4; ++t)
@@ -1502,6 +1513,80 @@ __global__ __launch_bounds__(128, 2) void k_rel_bwd_kh(const RelArgs p) {
     }
   }
   bins_store16(p.gp2ct + ((int64_t)hd * p.B + b) * p.Lp * p.ldx, p.ldx, j, bins, p.LB16, p.Q4, p.Lp, jv);
+}
+
+// Query side, 16-row waves, from the key side's g tiles (fp32): workgroup = (b,h, 32-query block), wave w =
+// queries 16 w .. 16 w + 15. k_rel_bwd_kh stored the softmax-input gradient g = P (dP - delta) / sqrt(3 d)
+// of every element as [key][query] tiles, so this kernel neither recomputes the scores (no V image, no bias
+// tile, no exp) nor dP: dq = g K (16x16x4 MFMA, K image by LDS-DMA) and the c2p gather backward
+// (G_c2p bins, then dq += G_c2p LK), with k_rel_bwd_qh's operand layouts and summation orders.
+__global__ __launch_bounds__(128, 2) void k_rel_bwd_qg(const RelArgs p) {
+  constexpr int D = 64, IMG = 32 * D * 4;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const uint32_t Kl = lds_offset(lds);
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int lane = lane_id(), x16 = lane & 15, g = lane >> 4;
+  float* bins = lds + rel16_bins_off(false) / 4 + w * 16 * p.LB16;
+  const BhBlock xb = xcd_block(p.NQB, p.B * p.H);
+  if (!xb.valid) return;  // whole workgroup
+  const int qb = xb.blk, bh = xb.bh, b = bh / p.H, hd = bh % p.H;
+  const int xr = 16 * w + x16, i = qb * 32 + xr;
+  const bool iv = i < p.N;
+  const int ic = imin(i, p.N - 1);
+  const int kld = (int)p.k_sn * 4;
+  const __amdgpu_buffer_rsrc_t kr = make_rsrc(p.k + b * p.k_sb + hd * p.k_sh, (p.N - 1) * kld + D * 4);
+  // rows past N are never fetched: the image holds zeros there (zeroed before any DMA can land)
+  for (int e = (int)threadIdx.x; e < IMG / 16; e += 128) reinterpret_cast<f32x4*>(lds)[e] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int e = lane; e < 16 * p.LB16; e += 64) bins[e] = 0.f;
+  __syncthreads();
+  const DmaPat kpat = dma_pat(SW_BOTH, kld);
+  const uint16_t* rmrow = prep_row(p, p.RM, b, hd, ic);
+  Codes8 cm = load_codes8(rmrow, 0);
+  // element e = 4 st + i of tile kt (key 16 st + 4 g + i, query xr): tg + kt * 1024 + 32 (16 st + 4 g + i)
+  const float* tg = p.gt + ((int64_t)bh * p.NQB + qb) * p.NKB * 1024 + 128 * g + xr;
+  float gn[8];
+  auto load_g = [&](int kt) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) gn[e] = tg[kt * 1024 + 32 * (16 * (e >> 2) + (e & 3))];
+  };
+  dma64(Kl, kr, kpat, kld, 0, 4 * w, 4 * w + 4);  // wave w fetches rows 16 w .. 16 w + 15
+  load_g(0);
+  f32x4 dq[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) dq[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int kt = 0; kt < p.NKB; ++kt) {
+    const int j0 = kt * 32;
+    wait_vm_all();
+    __syncthreads();  // both waves' pieces of tile kt landed
+    float gv[8];
+    uint32_t col[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { gv[e] = gn[e]; col[e] = code8(cm, e) & 0xffu; }  // rel[x][y]: the c2p column
+    float kT[4][8];  // A operands of dq: K[key 16 st + 4 g + i][d = 16 t + x16]
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) kT[t][e] = lds_f1(lds, img_elem(16 * (e >> 2) + 4 * g + (e & 3), 16 * t + x16, SW_BOTH));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();  // both waves read tile kt out: refill
+    if (kt + 1 < p.NKB) {
+      dma64(Kl, kr, kpat, kld, j0 + 32, 4 * w, 4 * w + 4);
+      cm = load_codes8(rmrow, kt + 1);
+      load_g(kt + 1);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) dq[t] = mfma16(kT[t][e], gv[e], dq[t]);
+    bins_scatter16(bins, p.LB16, gv, col);
+  }
+  bins_times16(dq, bins, p.LB16, p.Q4, p.lk + (int64_t)hd * p.L * D, p.L);
+  if (iv) {
+    float* dst = p.dq + b * p.dq_sb + hd * p.dq_sh + (int64_t)i * p.dq_sn + 4 * g;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) *reinterpret_cast<f32x4*>(dst + 16 * t) = dq[t];
+  }
+  bins_store16(p.gc2p + ((int64_t)hd * p.B + b) * p.Lp * p.ldx, p.ldx, i, bins, p.LB16, p.Q4, p.Lp, iv);
 }
 
 // Relation-embedding gradients of the fused path, split over the batch (deterministic):
@@ -1618,7 +1703,7 @@ struct RelLayout {
   int RS;                                    // batch splits of the dlq / dlk reductions
   bool fused;                                // d_k = 64: prepared planes + in-kernel gather backward
   size_t c2p, p2ct, RM, RT, RB, state_total;  // forward state
-  size_t G, P, gc2p, gp2ct, part, qstat, ws_total;  // backward workspace
+  size_t G, P, gc2p, gp2ct, part, qstat, gt, ws_total;  // backward workspace
 };
 
 inline size_t ral(size_t x) { return (x + 255) & ~size_t(255); }
@@ -1651,6 +1736,7 @@ RelLayout rel_layout(int64_t B, int64_t H, int64_t N, int64_t L, int64_t d) {
   R.gp2ct = take(R.fused ? sizeof(float) * H * B * R.Lp * R.ldx : sizeof(float) * B * H * N * R.Lp);
   R.part = take(sizeof(float) * (R.fused ? 2 : 1) * R.RS * H * L * d);  // fused: dlk and dlq partials
   R.qstat = take(R.fused ? sizeof(float) * B * H * N * 4 : 0);
+  R.gt = take(R.fused ? sizeof(float) * B * H * R.NP * R.NP : 0);
   R.ws_total = o;
   return R;
 }
@@ -1731,6 +1817,16 @@ inline bool rel_use16(const RelArgs& p) {
   return false;
 #else
   return !p.bf16;
+#endif
+}
+
+// fp32 16-row backward: the key side hands its g tiles to k_rel_bwd_qg (no score / dP recompute on the query
+// side). CSA_EXP_REL_RECOMP: experiment build with the round-3 recomputing query kernel (DESIGN.md §3 CSE A/B).
+inline bool rel_handoff() {
+#ifdef CSA_EXP_REL_RECOMP
+  return false;
+#else
+  return true;
 #endif
 }
 
@@ -1903,7 +1999,16 @@ csa_status csa_rel_attn_bwd(const csa_rel_attn_bwd_args* b, void* stream) {
         hipLaunchKernelGGL((k_rel_bwd_kf<64, false>), gk, blk, lk_bytes, s_, p);
       }
     };
-    if (side) {  // fork: row statistics + key side on the side stream, query side here, join before the lgrad
+    if (w16 && rel_handoff()) {  // fp32: row statistics, key side (g tiles out), query side from the tiles
+      p.qstat_pre = 1;
+      p.gt = (float*)((char*)ws + R.gt);
+      const int64_t threads = 4LL * B * H * N;
+      hipLaunchKernelGGL(k_rel_qstat<4>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, p);
+      launch_k(st);
+      const size_t lg_bytes = rel16_bins_off(false) + bins16_lds_bytes(p);
+      set_dyn_lds((const void*)k_rel_bwd_qg, (int)lg_bytes);
+      hipLaunchKernelGGL(k_rel_bwd_qg, gq, blk, lg_bytes, st, p);
+    } else if (side) {  // fork: row statistics + key side on the side stream, query side here, join before the lgrad
       if (!side->fork(st)) return rfail_hip("csa_rel_attn_bwd: side-stream fork");
       p.qstat_pre = 1;
       const int parts = w16 ? 4 : 2;

@@ -18,3 +18,9 @@ for i in 1 2; do
   run rng24c $LIB/libcsa_RNG24C.so "" || exit 1
 done
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 tools/ddp_one_gpu.py 8 > gpurun_out/ddp_one_gpu.log 2>&1; rc=$?; grep '^{' gpurun_out/ddp_one_gpu.log; echo "ddp rc=$rc"
+# CSE: the g-tile handoff vs the recomputing query kernel (java layer shape, B=64), same box, alternating
+for i in 1 2 3; do
+  for v in hip RELRECOMP; do
+    echo -n "cse $v: "; CSA_HIP_LIB=$LIB/libcsa_$v.so timeout -k 10 120 python tools/cse_bench.py 64 20 2>&1 | tail -1 || exit 1
+  done
+done
