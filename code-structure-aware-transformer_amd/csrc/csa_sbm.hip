@@ -3215,18 +3215,16 @@ csa_status launch_bwd(const csa_sbm_bwd_args* b, const Layout& L, hipStream_t st
       return check_launch("memset slabs");
     {
       Stage sg(pf, CSA_STAGE_PROJ_BWD, st);
-      if constexpr (SPLIT) {  // k <= 16
-        if (forked) launch_proj_bwd_s<D>(p, 2, (int)L.G_Q, (int)L.G_K, Gtot, (int)a->H, st);
-        else launch_proj_bwd_s<D>(p, 0, (int)L.G, 0, (int)L.G, (int)a->H, st);
+      if constexpr (SPLIT) {  // k <= 16: the same two launches and slab sets on every schedule
+        if (!forked) launch_proj_bwd_s<D>(p, 1, (int)L.G_K, 0, Gtot, (int)a->H, st);
+        launch_proj_bwd_s<D>(p, 2, (int)L.G_Q, (int)L.G_K, Gtot, (int)a->H, st);
       } else {
         set_dyn_lds((const void*)k_proj_bwd<D, KT>, (int)Sh::LDS_BYTES);
         hipLaunchKernelGGL((k_proj_bwd<D, KT>), dim3(L.G, a->H), dim3(256), Sh::LDS_BYTES, st, p);
       }
     }
-    if (forked) {
-      if (!lane.join(st)) return fail_hip("csa_sbm_bwd: side-stream join");
-      p.G = Gtot;  // the reduction sums both launches' slabs
-    }
+    if (forked && !lane.join(st)) return fail_hip("csa_sbm_bwd: side-stream join");
+    if constexpr (SPLIT) p.G = Gtot;  // the reduction sums both launches' slabs
     Stage sr(pf, CSA_STAGE_REDUCE, st);
     const int KP32 = 32 * KT;
     float* dS_ws = (float*)((char*)b->workspace + L.w_dS);
