@@ -3196,9 +3196,11 @@ csa_status launch_bwd(const csa_sbm_bwd_args* b, const Layout& L, hipStream_t st
     // Concurrent schedule (k <= 16): the projection backward's key-block items need only dT and dK, which the
     // key half has written, so they run on the caller's side stream beside k_attn_bwd_qg (HBM / latency bound)
     // and the query-block items follow it on this stream. Separate slab sets, summed in a fixed order: the
-    // results are bitwise those of the in-order schedule.
+    // results are bitwise those of the in-order schedule. Only on an explicit CSA_SCHED_CONCURRENT: AUTO runs in
+    // order, measured 0.06 ms per step faster at the headline shape (the two kernels contend for the same CUs;
+    // profiles/r04_ab_concurrent.txt).
     constexpr bool SPLIT = (D == 64 || D == 96) && KPH == 8;
-    const bool conc = SPLIT && b->side_stream && b->side_fork && b->side_join && b->schedule != CSA_SCHED_IN_ORDER;
+    const bool conc = SPLIT && b->side_stream && b->side_fork && b->side_join && b->schedule == CSA_SCHED_CONCURRENT;
     const SideLane lane{(hipStream_t)b->side_stream, (hipEvent_t)b->side_fork, (hipEvent_t)b->side_join};
     const int Gtot = (int)(L.G_K + L.G_Q);
     bool forked = false;

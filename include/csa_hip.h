@@ -65,7 +65,8 @@ typedef enum csa_status {
  * stream when the query half's grid leaves a partial last round of workgroups on the device (side_stream
  * must be set, else it runs in order). ABI v6, csa_sbm_bwd: the projection backward's key-block items (they
  * need only the key half's dT) run on the side stream beside the query half (k_attn_bwd_qg) and its query-
- * block items; AUTO = CONCURRENT whenever a side lane is given. Bitwise-identical results either way. */
+ * block items on CSA_SCHED_CONCURRENT only (AUTO runs in order: faster at the headline shape, measured).
+ * Bitwise-identical results either way. */
 #define CSA_SCHED_AUTO 0u
 #define CSA_SCHED_IN_ORDER 1u
 #define CSA_SCHED_CONCURRENT 2u /* needs side_stream / side_fork / side_join */

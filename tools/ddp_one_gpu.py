@@ -48,7 +48,7 @@ def main():
         out, sp = model(x)[:2]
         loss = label_smoothing_loss(out, y) + 1e-2 * sp
         loss.backward()
-        return float(loss)
+        return float(loss.detach())
 
     t0 = time.time()
     ddp = wrap_ddp(build(), dev)
