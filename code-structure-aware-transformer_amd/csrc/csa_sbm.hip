@@ -373,7 +373,9 @@ struct KArgs {
   float* brow;                 // per query row (c0, u, v, rho) of the elementwise backward (k_attn_rowprep)
   int64_t dx_sb, dx_sh, dx_sn, dq_sb, dq_sh, dq_sn, dk_sb, dk_sh, dk_sn, dv_sb, dv_sh, dv_sn;
   int G; int64_t slab_floats;
-  int pb_kind, pb_goff;  // k_proj_bwd_s items: 0 all, 1 key blocks, 2 query blocks; its first slab of the head's G
+  // k_proj_bwd_s items: 0 all, 1 key blocks, 2 query blocks, 3 both in one launch (workgroups [0, pb_gk) key
+  // blocks, the rest query blocks); pb_goff: the launch's first slab of the head's G
+  int pb_kind, pb_goff, pb_gk;
 };
 
 // One 16-bit uniform per element: Philox word e/2, low half for even e.
@@ -817,6 +819,14 @@ __global__ __launch_bounds__((64 * ProjFwdLds<D, KT>::NW)) void k_proj_fwd_l(con
 // MFMA costs less than moving the tiles through HBM, so k_attn_bwd_qr recomputes them (the round-3 design).
 // Same-box A/B (profiles/r04_ab_handoff.txt): fp32 layer step 1.329 (recompute) -> 1.275 ms (handoff); saving the
 // forward's S tiles for k_attn_bwd_kv as well measured 1.290 ms (+23 us forward stores, -22 us backward): not kept.
+// One-plane handoff (no upstream map gradients): the key side stores w = dM P for an edge (A = 1) and the bit
+// pattern W_NO_EDGE (a signalling NaN, which no arithmetic produces) for a non-edge, so the query side rebuilds
+//   ds = ((A ? w : 0) - rho P) / sqrt(d),  G = A ? hardtanh(w + csp) : 0
+// from one float per element: rho = [n < eps] gamma is 0 on every row whose normaliser is not degenerate, and
+// only tiles holding a row with rho != 0 also store P (in the second plane). Half the handoff bytes of the
+// two-plane ds | G format, which the map-gradient variant (DG: per-element dgraph / dattn terms) keeps.
+constexpr uint32_t W_NO_EDGE = 0x7f800001u;
+
 template <bool BF>
 constexpr bool bwd_handoff() {
 #ifdef CSA_EXP_RECOMP  // experiment: the recompute pipeline for fp32 too
@@ -1585,7 +1595,7 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
 // LDS per wave): the ds / G registers are refilled right behind the MFMAs that read them and the K / T
 // operands are read from LDS just before their MFMAs, and the other waves' MFMAs cover the load latency.
 // ------------------------------------------------------------------------------------
-template <int D, int KPH, bool DENSE, bool BF>
+template <int D, int KPH, bool DENSE, bool BF, bool W1>
 __global__ __launch_bounds__(64, (D <= 64 && KPH <= 8) ? 4 : 2) void k_attn_bwd_qg(const KArgs p) {
   using SH = AttnBwdShape<D, KPH>;
   constexpr int DT = D / 32, DP = SH::DP, KP = SH::KP, KPN = SH::KPN, KTA = SH::KTA;
@@ -1615,14 +1625,17 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 8) ? 4 : 2) void k_attn_bwd_
   } while (0)
   // element (key crow(r,h), query c) of tile kt: tb + kt * 1024 + 32 crow(r,h)
   const float* tb = p.dsg + ((int64_t)bh * p.NQB + qb) * p.NKB * 1024 + c;
-  float dsv[16], gv[16];
+  float dsv[16], gv[16];  // W1: dsv holds the tile's w values until the top of its iteration
   auto load_tile = [&](int kt) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       dsv[r] = tb[kt * 1024 + 32 * crow(r, h)];
-      if constexpr (!DENSE) gv[r] = tb[p.gplane + kt * 1024 + 32 * crow(r, h)];
+      if constexpr (!DENSE && !W1) gv[r] = tb[p.gplane + kt * 1024 + 32 * crow(r, h)];
     }
   };
+  // W1: this lane's rho (k_attn_rowprep) and the STE term; ds is summed unscaled and dQ scaled at the end
+  const float rho = W1 ? p.brow[(((int64_t)bh * p.NQB + qb) * 32 + c) * 4 + 3] : 0.f;
+  const float csp = (W1 && p.dsp) ? p.dsp[hd] / ((float)p.B * (float)p.N * (float)p.M) : 0.f;
   CSA_ISSUE_BQ(0);
   load_tile(0);
   f32x16 dq[DT], dqh[KTA];
@@ -1636,6 +1649,19 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 8) ? 4 : 2) void k_attn_bwd_
     const int c = ln & 31, h = (ln >> 5) & 1;
     const bool more = kt + 1 < p.NKB;
     wait_vm_all();  // tile kt's K / T images and ds / G values have landed
+    if constexpr (W1) {  // k_attn_bwd_kv's expressions (W_NO_EDGE)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const bool a = __float_as_uint(dsv[r]) != W_NO_EDGE;
+        const float w = a ? dsv[r] : 0.f;
+        gv[r] = a ? __builtin_amdgcn_fmed3f(w + csp, -1.f, 1.f) : 0.f;
+        dsv[r] = w;
+      }
+      if (rho != 0.f) {  // rare: a degenerate row (n < eps) also takes -rho P from the second plane
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dsv[r] = fmaf(-rho, tb[p.gplane + kt * 1024 + 32 * crow(r, h)], dsv[r]);
+      }
+    }
     // dQ^T += K^T ds^T (lane d holds K[key crow(r,h)][d], read from the SW_COL / padded image per K-step)
 #pragma unroll
     for (int t = 0; t < DT; ++t) {
@@ -1678,6 +1704,12 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 8) ? 4 : 2) void k_attn_bwd_
     }
   }
 #undef CSA_ISSUE_BQ
+  if constexpr (W1) {
+#pragma unroll
+    for (int t = 0; t < DT; ++t)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) dq[t][e] *= p.scale;
+  }
   store_rows<DT>(p.dQ + b * p.dq_sb + hd * p.dq_sh + (int64_t)i * p.dq_sn, D, D, dq, iv);
   if constexpr (MB4) store_mb4(p.dQh + ((int64_t)bh * p.N + qb * 32) * p.kp, p.N - qb * 32, p.kp, dqh[0]);
   else if constexpr (!DENSE) store_rows<KTA>(p.dQh + ((int64_t)bh * p.N + i) * p.kp, p.kp, p.kp, dqh, iv);
@@ -1696,6 +1728,7 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
   constexpr bool SWZ = SH::SWZ;
   constexpr bool MB4 = !DENSE && KP == 16;  // dT on mfma4b (store_mb4)
   constexpr bool HO = bwd_handoff<BF>();    // ds / G tiles out for k_attn_bwd_qg (else k_attn_bwd_qr recomputes)
+  constexpr bool W1 = HO && !DENSE && !DG;  // one-plane w tiles (W_NO_EDGE)
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const uint32_t L0 = lds_offset(lds), Ql = L0 + SH::KQ, Xl = L0 + SH::KX, Hl = L0 + SH::KH, Sl = L0 + SH::KS;
   const int lane = lane_id(), c = lane & 31, h = lane >> 5;
@@ -1750,6 +1783,8 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
     const int i0 = qb * 32;
     const bool more = qb + 1 < p.NQB;
     wait_vm_all();  // query block qb's Q / dX / Qh / row-constant images and bit words have landed
+    // W1: does a row of this query block have rho != 0 (its query side then needs P as well)?
+    const bool rho_any = W1 && __builtin_amdgcn_ballot_w64(lds_f1(lds, SH::KS + 16 * c + 12) != 0.f) != 0;
     // sampled / keep bits shifted so that register r's query is bit crow(r, 0); queries past N and keys past M
     // count as not sampled
     const uint32_t qvm = p.N - i0 >= 32 ? 0xffffffffu : (1u << (p.N - i0)) - 1u;
@@ -1799,7 +1834,9 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
       // Elementwise backward, once per element (k_attn_rowprep's row constants; scalar fp32: packed v_pk_* beside
       // the MFMAs cost more issue cycles than they save). A query past N has c0 = -inf (P = 0) and A = 0; a key
       // past M has kbias = -inf and A = 0; so every element outside [0,N) x [0,M) stores ds = G = attw = 0.
-      float dsv[8], gv[8], awv[8];
+      float dsv[8], gv[8], awv[8], wv[4];
+      // this half's queries 16 half + 4 h + (0..3) and + 8 of the tile: two f32x4 per plane
+      float* const wst = dsw + (int64_t)qb * p.NKB * 1024 + 16 * half;
 #pragma unroll
       for (int rr = 0; rr < 8; ++rr) {
         const int r = 8 * half + rr;
@@ -1816,9 +1853,22 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
           if (p.dgraph) cg += ldz(p.dgraph, me, INT64_MAX, inside);
           if (p.dattn) dM = fmaf(ldz(p.dattn, me, INT64_MAX, inside), rec[1] * (1.f - p.attn_p), dM);
         }
-        dsv[rr] = ((a ? dM : 0.f) - rec[3]) * (P * p.scale);
-        gv[rr] = a ? __builtin_amdgcn_fmed3f(fmaf(dM, P, cg), -1.f, 1.f) : 0.f;  // STE.py:19 hardtanh(A * grad)
+        if constexpr (W1) {  // the query side's expressions exactly (k_attn_bwd_qg)
+          const float w = dM * P;
+          wv[rr & 3] = __uint_as_float(a ? __float_as_uint(w) : W_NO_EDGE);
+          dsv[rr] = fmaf(-rec[3], P, a ? w : 0.f) * p.scale;
+          gv[rr] = a ? __builtin_amdgcn_fmed3f(w + cg, -1.f, 1.f) : 0.f;
+        } else {
+          dsv[rr] = ((a ? dM : 0.f) - rec[3]) * (P * p.scale);
+          gv[rr] = a ? __builtin_amdgcn_fmed3f(fmaf(dM, P, cg), -1.f, 1.f) : 0.f;  // STE.py:19 hardtanh(A * grad)
+        }
         awv[rr] = (a && kp) ? P * rec[1] : 0.f;  // dropout(attn) weight for dV
+#ifndef CSA_EXP_NO_DSG_STORE
+        if constexpr (W1) {  // stored as soon as four are ready (fewer live registers); non-temporal, see below
+          if ((rr & 3) == 3)
+            __builtin_nontemporal_store((f32x4{wv[0], wv[1], wv[2], wv[3]}), reinterpret_cast<f32x4*>(wst + 2 * (rr & 4)));
+        }
+#endif
 #ifdef CSA_EXP_NO_ELEM  // experiment: timing without the elementwise algebra (wrong results)
         dsv[rr] = sacc[r] * dpacc[r];
         gv[rr] = dpacc[r];
@@ -1827,12 +1877,25 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
       }
 #ifndef CSA_EXP_NO_DSG_STORE  // experiment: timing without the ds / G stores (wrong results)
       if constexpr (HO) {  // queries 16 half + 4 h + (0..3) and + 8: two f32x4 per tile, for ds and for G
-        float* w = dsw + (int64_t)qb * p.NKB * 1024 + 16 * half;
+        float* const w = wst;
         // non-temporal: the tiles are read once, by the next kernel (same-box A/B: k_attn_bwd_qg 157 -> 134 us)
 #define CSA_ST4(ptr, val) __builtin_nontemporal_store((val), reinterpret_cast<f32x4*>(ptr))
-        CSA_ST4(w, (f32x4{dsv[0], dsv[1], dsv[2], dsv[3]}));
-        CSA_ST4(w + 8, (f32x4{dsv[4], dsv[5], dsv[6], dsv[7]}));
-        if constexpr (!DENSE) {
+        if constexpr (W1) {  // (the w values are stored in the elementwise loop)
+          if (rho_any) {  // rare (a degenerate row): P of the half's elements, recomputed, into the second plane
+            float pv[8];
+#pragma unroll
+            for (int rr = 0; rr < 8; ++rr) {
+              const f32x4 rec = lds_f4(lds, SH::KS + 16 * crow(8 * half + rr, h));
+              pv[rr] = __builtin_amdgcn_exp2f(fmaf(sacc[8 * half + rr], c1, rec[0] + kbias));
+            }
+            CSA_ST4(w + p.gplane, (f32x4{pv[0], pv[1], pv[2], pv[3]}));
+            CSA_ST4(w + p.gplane + 8, (f32x4{pv[4], pv[5], pv[6], pv[7]}));
+          }
+        } else {
+          CSA_ST4(w, (f32x4{dsv[0], dsv[1], dsv[2], dsv[3]}));
+          CSA_ST4(w + 8, (f32x4{dsv[4], dsv[5], dsv[6], dsv[7]}));
+        }
+        if constexpr (!DENSE && !W1) {
           CSA_ST4(w + p.gplane, (f32x4{gv[0], gv[1], gv[2], gv[3]}));
           CSA_ST4(w + p.gplane + 8, (f32x4{gv[4], gv[5], gv[6], gv[7]}));
         }
@@ -2426,13 +2489,19 @@ __global__ __launch_bounds__(256, ProjBwdSmallShape<D>::LCS ? 1 : 2) void k_proj
   float* IN = lds + 4 * REG;
   const int lane = lane_id(), c = lane & 31, h = lane >> 5, c16 = lane & 15, g4 = lane >> 4;
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const int hd = blockIdx.y, g = blockIdx.x, G = gridDim.x;
+  const int hd = blockIdx.y;
   const int per_b = p.NQB + p.NKB;
-  // this launch's items of the head, per batch element: all (Q blocks, then K blocks), or one kind only
-  const int ipb = p.pb_kind == 1 ? p.NKB : p.pb_kind == 2 ? p.NQB : per_b, roff = p.pb_kind == 1 ? p.NQB : 0;
+  // this workgroup's item kind, its index among the workgroups of that kind and their count, its slab
+  int kind = p.pb_kind, g = blockIdx.x, G = gridDim.x, gs = p.pb_goff + g;
+  if (kind == 3) {
+    const bool key = g < p.pb_gk;
+    kind = key ? 1 : 2; gs = g; G = key ? p.pb_gk : G - p.pb_gk; g = key ? g : g - p.pb_gk;
+  }
+  // items of the head, per batch element: all (Q blocks, then K blocks), or one kind only
+  const int ipb = kind == 1 ? p.NKB : kind == 2 ? p.NQB : per_b, roff = kind == 1 ? p.NQB : 0;
   const int i_lo = (int)((int64_t)g * p.B * ipb / G), i_hi = (int)((int64_t)(g + 1) * p.B * ipb / G);
-  const int n_items = i_hi - i_lo;  // this workgroup's items: i_lo .. i_hi - 1 of the launch's items
-  float* slab = p.slab + ((int64_t)hd * p.G + p.pb_goff + g) * p.slab_floats;
+  const int n_items = i_hi - i_lo;  // this workgroup's items: i_lo .. i_hi - 1 of its kind's items
+  float* slab = p.slab + ((int64_t)hd * p.G + gs) * p.slab_floats;
   const float ks = p.proj_p > 0.f ? 1.f / (1.f - p.proj_p) : 1.f;
   const float* CfT = p.CfT + (size_t)hd * 32 * D;
   const float* SfT = p.SfT + (size_t)hd * 32 * 32;
@@ -3120,7 +3189,7 @@ void launch_attn_bwd_v(const KArgs& p, int BH, const Layout& L, const csa_prof* 
   mid();
   Stage sg(pf, CSA_STAGE_ATTN_BWD_Q, st);
   if constexpr (bwd_handoff<BF>()) {
-    hipLaunchKernelGGL((k_attn_bwd_qg<D, KPH, DENSE, BF>), dim3(xcd_grid((int)L.NQB, BH)), dim3(64), SH::G_BYTES,
+    hipLaunchKernelGGL((k_attn_bwd_qg<D, KPH, DENSE, BF, !DENSE && !DG>), dim3(xcd_grid((int)L.NQB, BH)), dim3(64), SH::G_BYTES,
                        st, p);
   } else {
     const size_t r_lds = SH::r_bytes((int)L.Mpad);
@@ -3151,11 +3220,11 @@ void launch_attn_bwd(const KArgs& p, int BH, const Layout& L, bool drop, const c
   return launch_attn_bwd_b<D, KPH, DENSE, false>(p, BH, L, drop, pf, st, mid);
 }
 
-// k_proj_bwd_s over one kind of items (0 all, 1 key blocks, 2 query blocks) on stream s
+// k_proj_bwd_s over items of `kind` (KArgs::pb_kind) with G workgroups per head, on stream s
 template <int D>
-void launch_proj_bwd_s(KArgs p, int kind, int G, int goff, int Gtot, int H, hipStream_t s) {
+void launch_proj_bwd_s(KArgs p, int kind, int G, int goff, int gk, int Gtot, int H, hipStream_t s) {
   using Ss = ProjBwdSmallShape<D>;
-  p.pb_kind = kind; p.pb_goff = goff; p.G = Gtot;
+  p.pb_kind = kind; p.pb_goff = goff; p.pb_gk = gk; p.G = Gtot;
   if (p.bf16) {  // CSA_DTYPE_BF16: projection contractions on bf16 MFMA
     set_dyn_lds((const void*)k_proj_bwd_s<D, true>, (int)Ss::LDS_BYTES);
     hipLaunchKernelGGL((k_proj_bwd_s<D, true>), dim3(G, H), dim3(256), Ss::LDS_BYTES, s, p);
@@ -3208,7 +3277,7 @@ csa_status launch_bwd(const csa_sbm_bwd_args* b, const Layout& L, hipStream_t st
       if (!conc || !lane.fork(st)) return;
       forked = true;
       Stage sg(pf, CSA_STAGE_PROJ_BWD_K, lane.s);
-      if constexpr (SPLIT) launch_proj_bwd_s<D>(p, 1, (int)L.G_K, 0, Gtot, (int)a->H, lane.s);
+      if constexpr (SPLIT) launch_proj_bwd_s<D>(p, 1, (int)L.G_K, 0, 0, Gtot, (int)a->H, lane.s);
     };
     launch_attn_bwd<D, KPH, false>(p, BH, L, a->attn_dropout > 0.f, pf, st, mid);
     if (conc && !forked) return fail_hip("csa_sbm_bwd: side-stream fork");
@@ -3217,9 +3286,10 @@ csa_status launch_bwd(const csa_sbm_bwd_args* b, const Layout& L, hipStream_t st
       return check_launch("memset slabs");
     {
       Stage sg(pf, CSA_STAGE_PROJ_BWD, st);
-      if constexpr (SPLIT) {  // k <= 16: the same two launches and slab sets on every schedule
-        if (!forked) launch_proj_bwd_s<D>(p, 1, (int)L.G_K, 0, Gtot, (int)a->H, st);
-        launch_proj_bwd_s<D>(p, 2, (int)L.G_Q, (int)L.G_K, Gtot, (int)a->H, st);
+      if constexpr (SPLIT) {  // k <= 16: the same workgroup items and slab sets on every schedule
+        // in order: both kinds in one launch, each workgroup's items and slab as in the concurrent form
+        if (forked) launch_proj_bwd_s<D>(p, 2, (int)L.G_Q, (int)L.G_K, 0, Gtot, (int)a->H, st);
+        else launch_proj_bwd_s<D>(p, 3, Gtot, 0, (int)L.G_K, Gtot, (int)a->H, st);
       } else {
         set_dyn_lds((const void*)k_proj_bwd<D, KT>, (int)Sh::LDS_BYTES);
         hipLaunchKernelGGL((k_proj_bwd<D, KT>), dim3(L.G, a->H), dim3(256), Sh::LDS_BYTES, st, p);

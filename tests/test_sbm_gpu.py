@@ -70,6 +70,78 @@ def test_sbm_forward_backward_matches_reference(golden, case):
             np.testing.assert_allclose(p.grad.cpu().numpy(), z["g:" + pn], rtol=RTOL, atol=ATOL, err_msg=pn + " (ref)")
 
 
+def _sbm_vs_oracle(z, Qn, Kn, u, k):
+    """Forward + backward of the module with host-supplied uniforms against the closed-form oracle."""
+    m = make_module(z, k)
+    Q, K, V = dev(Qn, True), dev(Kn, True), dev(z["V"], True)
+    m.uniforms = dev(u)
+    X, sp, graph, attn = m(Q, K, V, dev(z["mask"]))
+    g = graph.detach().cpu().numpy().astype(np.uint8)
+    params = {kk[2:]: torch.from_numpy(v) for kk, v in z.items() if kk.startswith("p:")}
+    ref, rg = closed_form.sbm_fwd_bwd(torch.from_numpy(Qn), torch.from_numpy(Kn), torch.from_numpy(z["V"]),
+                                     torch.from_numpy(z["mask"]), params, torch.from_numpy(u), k, torch.from_numpy(z["dX"]),
+                                     torch.from_numpy(z["dsparsity"]), graph_override=torch.from_numpy(g.astype(np.float32)))
+    np.testing.assert_allclose(X.detach().cpu().numpy(), ref["X"].numpy(), rtol=RTOL, atol=ATOL)
+    ((X * dev(z["dX"])).sum() + (sp * dev(z["dsparsity"])).sum()).backward()
+    for name, t, key in (("dQ", Q, "Q"), ("dK", K, "K"), ("dV", V, "V")):
+        np.testing.assert_allclose(t.grad.cpu().numpy(), rg[key].numpy(), rtol=RTOL, atol=ATOL, err_msg=name)
+    for pn, p in m.named_parameters():
+        np.testing.assert_allclose(p.grad.cpu().numpy(), rg[pn].numpy(), rtol=RTOL, atol=ATOL, err_msg=pn)
+    return g, X.detach().cpu().numpy()
+
+
+@pytest.mark.skipif(not has_gpu(), reason="needs GPU")
+def test_sbm_rows_without_edges_match_oracle(golden):
+    """Query rows that sample no key (u = 1 never samples; host-supplied uniforms) in three of the five query
+    blocks, the last, partial one included: their attn row and X row are zero (F.normalize's clamp), and
+    every element of theirs is W_NO_EDGE in the backward's one-plane tiles."""
+    z = golden("sbm_n150")
+    k = int(z["meta"][4])
+    u = z["u"].copy()
+    rows = [3, 40, 41, 77, 149]
+    u[:, :, rows, :] = 1.0
+    g, X = _sbm_vs_oracle(z, z["Q"], z["K"], u, k)
+    assert not g[:, :, rows, :].any() and not X[:, :, rows, :].any()
+
+
+@pytest.mark.skipif(not has_gpu(), reason="needs GPU")
+def test_sbm_degenerate_normaliser_rows_match_oracle(golden):
+    """A query row whose sampled keys carry almost no softmax mass (n = sum_j P A < eps = 1e-12, so
+    F.normalize divides by eps, not n) has rho = gamma != 0: ds = (A dM - rho) P / sqrt(d) on every key, the
+    case where the one-plane backward handoff (W_NO_EDGE) also stores P in the tile's second plane. Built by
+    giving query row i and key j one dominant score (Q_i = K_j = t 1, t bisected so that n ~ 1e-13) and
+    leaving key j unsampled (u = 1) while every other key of the row is sampled (u = 0)."""
+    z = golden("sbm_n150")
+    B, H, N, d, k = (int(v) for v in z["meta"])
+    Qn, Kn, u = z["Q"].copy(), z["K"].copy(), z["u"].copy()
+    i, j = 40, 77
+    valid = z["mask"] == 0  # (B, N): keys that take part (sbm_attn.py:61)
+    assert valid[:, j].all()
+
+    def mass(t):  # the largest n over (b, h) of row i when Q_i = K_j = t 1 (float64)
+        q, kk = Qn.astype(np.float64), Kn.astype(np.float64)
+        q[:, :, i, :], kk[:, :, j, :] = t, t
+        s = np.einsum("bhd,bhnd->bhn", q[:, :, i, :], kk) / np.sqrt(d)
+        s = np.where(valid[:, None, :], s, -np.inf)
+        p = np.exp(s - s.max(-1, keepdims=True))
+        p /= p.sum(-1, keepdims=True)
+        p[:, :, j] = 0.0
+        return p.sum(-1)
+
+    lo, hi = 0.5, 6.0  # n(t) falls as t grows
+    for _ in range(60):
+        mid = 0.5 * (lo + hi)
+        lo, hi = (mid, hi) if mass(mid).max() > 1e-13 else (lo, mid)
+    t = hi
+    n = mass(t)
+    assert n.max() <= 1e-13 and n.min() > 1e-18
+    Qn[:, :, i, :], Kn[:, :, j, :] = t, t
+    u[:, :, i, :] = 0.0
+    u[:, :, i, j] = 1.0
+    g, X = _sbm_vs_oracle(z, Qn, Kn, u, k)
+    assert not g[:, :, i, j].any() and g[:, :, i, :].sum() == B * H * (N - 1) and np.abs(X[:, :, i, :]).max() > 0
+
+
 @pytest.mark.skipif(not has_gpu(), reason="needs GPU")
 @pytest.mark.parametrize("case", ["sbm_n37_mapgrad", "sbm_n33_d96_mapgrad"])
 def test_sbm_map_gradients_match_reference(golden, case):
