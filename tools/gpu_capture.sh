@@ -22,5 +22,5 @@ import json, sys
 t = json.load(open(sys.argv[1]))
 for n, v in sorted(t["kernels"].items(), key=lambda kv: -(kv[1]["rocprof_avg_ns"] or 0)):
     if v["rocprof_avg_ns"]:
-        print(f"{n:22s} {v['rocprof_avg_ns']/1000:8.1f} us  {v['bytes']/1e6:8.1f} MB  {v['bytes']/v['rocprof_avg_ns']:6.2f} TB/s")
+        print(f"{n:22s} {v['rocprof_avg_ns']/1000:8.1f} us  {v['bytes']/1e6:8.1f} MB  {v['bytes']/v['rocprof_avg_ns']:7.1f} GB/s")
 PY
