@@ -859,7 +859,7 @@ __device__ __forceinline__ uint32_t writelane_batch(uint32_t dst, const unsigned
     "s"((uint32_t)b[R0 + 6]), "s"((uint32_t)(b[R0 + 6] >> 32)), "s"((uint32_t)b[R0 + 7]),                \
     "s"((uint32_t)(b[R0 + 7] >> 32))
   if constexpr (R0 == 0)
-    asm("s_nop 4\n\t"
+    asm volatile("s_nop 4\n\t"
       "v_writelane_b32 %0, %1, 0\n\t"
       "v_writelane_b32 %0, %2, 4\n\t"
       "v_writelane_b32 %0, %3, 1\n\t"
@@ -878,7 +878,7 @@ __device__ __forceinline__ uint32_t writelane_batch(uint32_t dst, const unsigned
       "v_writelane_b32 %0, %16, 15"
         CSA_WL_OPS);
   else
-    asm("s_nop 4\n\t"
+    asm volatile("s_nop 4\n\t"
       "v_writelane_b32 %0, %1, 16\n\t"
       "v_writelane_b32 %0, %2, 20\n\t"
       "v_writelane_b32 %0, %3, 17\n\t"
@@ -899,13 +899,16 @@ __device__ __forceinline__ uint32_t writelane_batch(uint32_t dst, const unsigned
 #undef CSA_WL_OPS
   return dst;
 }
-__device__ __forceinline__ uint32_t pack_bits(const bool (&v)[16]) {
+// One batch of 8 registers of a mask into the packed word (layout above): batch bt covers registers
+// 8 bt .. 8 bt + 7, i.e. keys (crow(r,0), crow(r,1)) -> lanes 0..15 (bt = 0) or 16..31 (bt = 1).
+__device__ __forceinline__ uint32_t pack_batch(uint32_t w, int bt, const bool (&v)[8]) {
   unsigned long long b[16];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) b[r] = __ballot(v[r]);
-  uint32_t w = 0;
-  w = writelane_batch<0>(w, b);
-  return writelane_batch<8>(w, b);
+  for (int e = 0; e < 8; ++e) b[8 * bt + e] = __ballot(v[e]);
+  return bt == 0 ? writelane_batch<0>(w, b) : writelane_batch<8>(w, b);
+}
+__device__ __forceinline__ void pin(u32x4& x) {
+  asm volatile("" : "+v"(x.x), "+v"(x.y), "+v"(x.z), "+v"(x.w));
 }
 
 template <int D, int KPH>
@@ -1021,6 +1024,10 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd
     {
       uint32_t sk0 = p.seed_lo, sk1 = p.seed_hi;  // opaque per tile: round keys are not held across the loop
       asm volatile("" : "+s"(sk0), "+s"(sk1));
+#ifdef CSA_EXP_FWD_NO_RNG  // experiment: timing without the tile's Philox calls (wrong masks)
+      r_ste[0] = r_ste[1] = r_drop[0] = r_drop[1] = u32x4{(uint32_t)i * 2654435761u, sk0 ^ (uint32_t)kt, sk1, (uint32_t)bh};
+      if (false)
+#endif
 #pragma unroll
       for (int gp = 0; gp < 2; ++gp) {
         if constexpr (!DENSE && !HAS_U)
@@ -1085,49 +1092,6 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd
       s[r] = fmaf(sacc[r], p.scale, bz[r >> 2][r & 3]);
       tmax = fmaxf(tmax, s[r]);
     }
-    bool av[16], keep[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) { av[r] = true; keep[r] = true; }
-    if constexpr (!DENSE) {
-      if constexpr (HAS_U) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int j = j0 + crow(r, h);
-          const float v = p.U[((int64_t)bh * p.N + ic) * p.M + imin(j, p.M - 1)];
-          const float uu = (iv && j < p.M) ? v : 2.f;
-          av[r] = uu < fminf(fmaxf(eacc[r], 0.01f), 0.99f);  // STE.py:11-13
-        }
-      } else {
-#pragma unroll
-        for (int gp = 0; gp < 2; ++gp) {
-          const u32x4 rr = r_ste[gp];
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const int r = 8 * gp + e;
-            av[r] = (float)u16_of(rr, e) < __builtin_amdgcn_fmed3f(eacc[r], 0.01f * ESC, 0.99f * ESC);
-          }
-        }
-      }
-    }
-    if constexpr (DROP) {
-#pragma unroll
-      for (int gp = 0; gp < 2; ++gp) {
-        const u32x4 rr = r_drop[gp];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) keep[8 * gp + e] = u16_of(rr, e) >= p.drop_thr;
-      }
-    }
-    // bit-pack the sampled graph / dropout keep mask: word [qb][key] holds 32 query bits (lanes 0..31)
-    if constexpr (!DENSE || DROP) {
-      const uint32_t myA = DENSE ? 0u : pack_bits(av);
-      const uint32_t myR = DROP ? pack_bits(keep) : 0u;
-      const int64_t widx = ((int64_t)bh * p.NQB + qb) * p.Mpad + j0 + c;
-      if constexpr (!DENSE) {
-        if (h == 0) p.Abits[widx] = myA;
-        if (j0 + c < p.M) cntl += __popc(myA & qmask);  // sampled edges inside [0,N) x [0,M)
-      }
-      if constexpr (DROP) if (h == 0) p.Rbits[widx] = myR;
-    }
     // online softmax update (exp(-inf - m) = 0 covers masked keys; m_use keeps an all-masked prefix finite)
     tmax = xhalf_max(tmax);
     const float m_new = fmaxf(m_run, tmax);
@@ -1135,18 +1099,66 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd
     const float alpha = __expf(m_run - m_use);
     zp *= alpha;
     zgp *= alpha;
+    if (__builtin_amdgcn_ballot_w64(alpha != 1.f)) {  // the running max moved for some query (o *= 1 is exact)
 #pragma unroll
-    for (int t = 0; t < DT; ++t)
+      for (int t = 0; t < DT; ++t)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
-    float w[16];
+        for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
+    }
+    float ex[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const float e = __expf(s[r] - m_use);
-      zp += e;
-      const float wa = av[r] ? e : 0.f;
-      zgp += wa;
-      w[r] = keep[r] ? wa : 0.f;
+      ex[r] = __expf(s[r] - m_use);
+      zp += ex[r];
+    }
+    // Sampled graph / dropout keep masks, applied and bit-packed (word [qb][key] holds 32 query bits, lanes
+    // 0..31) in two batches of 8 registers: each batch's compare masks (SGPR pairs) are consumed right away by
+    // the selects and its writelane batch, so at most 16 mask SGPRs are live at once (taking all 32 masks
+    // first spilled ~30 SGPRs to VGPR lanes, ~45 v_readlane per tile). pin() makes batch 1's operands opaque
+    // after batch 0's writelanes (asm volatile), so the compiler cannot hoist its compares.
+    float w[16];
+    uint32_t myA = 0u, myR = 0u;
+#pragma unroll
+    for (int bt = 0; bt < 2; ++bt) {
+      if (bt == 1) {
+        if constexpr (!DENSE && !HAS_U) {
+          pin(r_ste[1]);
+#pragma unroll
+          for (int r = 8; r < 16; ++r) asm volatile("" : "+v"(eacc[r]));
+        }
+        if constexpr (DROP) pin(r_drop[1]);
+      }
+      bool av[8], keep[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int r = 8 * bt + e;
+        av[e] = true;
+        keep[e] = true;
+        if constexpr (!DENSE) {
+          if constexpr (HAS_U) {
+            const int j = j0 + crow(r, h);
+            const float v = p.U[((int64_t)bh * p.N + ic) * p.M + imin(j, p.M - 1)];
+            const float uu = (iv && j < p.M) ? v : 2.f;
+            av[e] = uu < fminf(fmaxf(eacc[r], 0.01f), 0.99f);  // STE.py:11-13
+          } else {
+            av[e] = (float)u16_of(r_ste[bt], e) < __builtin_amdgcn_fmed3f(eacc[r], 0.01f * ESC, 0.99f * ESC);
+          }
+        }
+        if constexpr (DROP) keep[e] = u16_of(r_drop[bt], e) >= p.drop_thr;
+        const float wa = av[e] ? ex[r] : 0.f;
+        zgp += wa;
+        w[r] = keep[e] ? wa : 0.f;
+      }
+      if constexpr (!DENSE) myA = pack_batch(myA, bt, av);
+      if constexpr (DROP) myR = pack_batch(myR, bt, keep);
+    }
+    if constexpr (!DENSE || DROP) {
+      const int64_t widx = ((int64_t)bh * p.NQB + qb) * p.Mpad + j0 + c;
+      if constexpr (!DENSE) {
+        if (h == 0) p.Abits[widx] = myA;
+        if (j0 + c < p.M) cntl += __popc(myA & qmask);  // sampled edges inside [0,N) x [0,M)
+      }
+      if constexpr (DROP) if (h == 0) p.Rbits[widx] = myR;
     }
     m_run = m_new;
     // O^T += V^T W^T (keys beyond M carry w = 0)

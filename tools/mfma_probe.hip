@@ -75,6 +75,17 @@ __global__ void k_rate(float* out, long long* cyc, int n) {
       d3 = __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, d3, 0, 0, 0);
     }
     s = d0[0] + d1[1] + d2[2] + d3[3];
+  } else if constexpr (W == 5) {
+    f32x16 d0 = {};  // one dependent chain of 32x32x2 (W == 6: the same at two waves per SIMD)
+    for (int i = 0; i < 4 * n; ++i) d0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, d0, 0, 0, 0);
+    s = d0[0];
+  } else if constexpr (W == 7) {
+    f32x16 d0 = {}, d1 = {};  // two interleaved chains of 32x32x2
+    for (int i = 0; i < 2 * n; ++i) {
+      d0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, d0, 0, 0, 0);
+      d1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, d1, 0, 0, 0);
+    }
+    s = d0[0] + d1[1];
   } else {
     f32x16 d0 = {};  // one dependent chain of 16x16x1_4b
     for (int i = 0; i < 4 * n; ++i) d0 = __builtin_amdgcn_mfma_f32_16x16x1f32(a, b, d0, 0, 0, 0);
@@ -123,8 +134,9 @@ int main() {
     }
   }
   const char* rn[] = {"16x16x1_4b x4 indep", "32x32x2 x4 indep", "16x16x4 x4 indep", "4x4x1_16b x4 indep",
-                      "16x16x1_4b dependent chain"};
-  for (int w = 0; w < 5; ++w) {
+                      "16x16x1_4b dependent chain", "32x32x2 dependent chain", "32x32x2 dep, 2 waves/SIMD",
+                      "32x32x2 two chains"};
+  for (int w = 0; w < 8; ++w) {
     const int n = 4096;
     for (int rep = 0; rep < 2; ++rep) {
       if (w == 0) k_rate<0><<<256, 256>>>(d, c, n);
@@ -132,6 +144,9 @@ int main() {
       if (w == 2) k_rate<2><<<256, 256>>>(d, c, n);
       if (w == 3) k_rate<3><<<256, 256>>>(d, c, n);
       if (w == 4) k_rate<4><<<256, 256>>>(d, c, n);
+      if (w == 5) k_rate<5><<<256, 256>>>(d, c, n);
+      if (w == 6) k_rate<5><<<256, 512>>>(d, c, n);
+      if (w == 7) k_rate<7><<<256, 256>>>(d, c, n);
     }
     long long hc[256];
     hipMemcpy(hc, c, sizeof(hc), hipMemcpyDeviceToHost);
