@@ -1,0 +1,16 @@
+#!/bin/bash
+# Same-box A/B: the tree (one-plane w handoff, single-launch key/query projection backward, batched mask
+# packing) vs commit 58bfec7 (two-plane ds | G handoff, two in-order projection-backward launches).
+set -o pipefail
+export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+LIB=$R/code-structure-aware-transformer_amd/csa_amd/lib
+mkdir -p $R/gpurun_out
+run() {  # tag lib
+  CSA_HIP_LIB=$2 timeout -k 10 120 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-train --no-cpu-config1 > gpurun_out/bench_n.json || exit $?
+  python3 -c "import json; d=json.load(open('gpurun_out/bench_n.json')); print('$1', d['ms_per_step'], d['step_frac_of_f32_mfma_peak'], {k: round(v,4) for k,v in d['stage_ms'].items()}, d['bf16_mode']['ms_per_step'])"
+}
+for i in 1 2 3; do
+  run tree $LIB/libcsa_hip.so || exit 1
+  run r58 $LIB/libcsa_R58.so || exit 1
+done
