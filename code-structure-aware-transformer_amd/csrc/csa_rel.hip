@@ -597,55 +597,83 @@ __device__ __forceinline__ void bins_store_t(float* __restrict__ outT, int64_t l
   for (int r = KB2 * h; r < r1; ++r) outT[(int64_t)r * ldx + row] = brow[r];
 }
 
-// Relation logits C2P = Q LK_h^T and P2CT = K LQ_h^T, (B,H,N,Lp) each: one wave per (b,h, 32 rows,
-// table). The wave's 32 rows stay in registers; the 32-row slabs of LK / LQ (L2-resident, shared by
-// the whole batch) come in by LDS-DMA into two SW_ROW images, slab lt+1 in flight while slab lt's 32
-// MFMAs run (per-lane row loads from global would touch 64 cache lines per instruction); stores are
-// coalesced along the relation index.
+// One l-tile of k_rel_logits: both chains from the slab image (TWO: the pair's second block exists; a
+// wave-uniform choice of body, so the single-block tail wave issues half the MFMAs), the refill, the stores.
+template <int D, bool TWO>
+__device__ __forceinline__ void logits_tile(const RelArgs& p, const float* lds, uint32_t L0, __amdgpu_buffer_rsrc_t lr,
+                                            const DmaPat& pat, int rbase, const float (&xr0)[D / 2],
+                                            const float (&xr1)[D / 2], float* out, int rp, int lt, int NLT, int lane) {
+  constexpr int NS = D / 2;
+  const int c = lane & 31, h = lane >> 5;
+  const int l = lt * 32 + c;
+  // slab lt has landed: vector memory operations retire in issue order, so waiting until only the previous
+  // tile's stores (issued after slab lt's DMA) are outstanding suffices
+  if (lt == 0) wait_vm_all();
+  else if constexpr (TWO) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  f32x16 acc0 = zero16(), acc1 = zero16();
+#pragma unroll
+  for (int j = 0; j < NS / 4; ++j) {
+    const f32x4 lv = lds_f4(lds, rbase ^ (16 * j));
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      acc0 = mfma(xr0[4 * j + e], lv[e], acc0);  // D[x][l]
+      if constexpr (TWO) acc1 = mfma(xr1[4 * j + e], lv[e], acc1);
+    }
+  }
+  if (lt + 1 < NLT) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slab lt read out before it is refilled
+    dma64(L0, lr, pat, D * 4, (lt + 1) * 32);
+  }
+  // buffer stores: rows past N fall outside the descriptor and columns past L get an out-of-range offset, so
+  // the range check drops both (no per-element branches); the row part of the offset is wave-uniform (soffset)
+  const __amdgpu_buffer_rsrc_t orr = make_rsrc(out, p.N * p.Lp * 4);
+  const int voff = l < p.L ? ((64 * rp + 4 * h) * p.Lp + l) * 4 : 0x40000000;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int soff = crow(r, 0) * p.Lp * 4;
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc0[r]), orr, voff, soff, 0);
+    if constexpr (TWO) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc1[r]), orr, voff, soff + 32 * p.Lp * 4, 0);
+  }
+}
+
+// Relation logits C2P = Q LK_h^T and P2CT = K LQ_h^T, (B,H,N,Lp) each: one wave per (b,h, table, pair of
+// 32-row blocks). The wave's 2 x 32 rows stay in registers as the A operands of two independent accumulator
+// chains; each 32-row slab of LK / LQ (L2-resident, shared by the whole batch) comes in by LDS-DMA into one
+// SW_ROW image and feeds both chains (64 MFMAs per slab; per-lane row loads from global would touch 64 cache
+// lines per instruction). One 8 KiB image per wave (not two): the refill waits for the slab's reads, and the
+// other waves of the SIMD (<= 20 per CU by LDS, ~100 VGPRs) cover it, so the grid (2 x ceil(NQB / 2) x B x H
+// waves) runs in one round. Stores are coalesced along the relation index.
 template <int D>
-__global__ __launch_bounds__(64) void k_rel_logits(const RelArgs p, float* __restrict__ c2p, float* __restrict__ p2ct) {
-  constexpr int NS = D / 2, IMG = 32 * D * 4;
+__global__ __launch_bounds__(64, 4) void k_rel_logits(const RelArgs p, float* __restrict__ c2p, float* __restrict__ p2ct) {
+  constexpr int NS = D / 2;
   static_assert(D == 64, "fused CSE path is d_k = 64");
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const uint32_t L0 = lds_offset(lds);
   const int lane = lane_id(), c = lane & 31, h = lane >> 5;
-  const BhBlock xb = xcd_block(2 * p.NQB, p.B * p.H);
+  const int NRP = (p.NQB + 1) / 2;  // pairs of row blocks
+  const BhBlock xb = xcd_block(2 * NRP, p.B * p.H);
   if (!xb.valid) return;
-  const int which = xb.blk & 1, rb = xb.blk >> 1, bh = xb.bh, b = bh / p.H, hd = bh % p.H;
-  const int x = rb * 32 + c;
-  const int xc = imin(x, p.N - 1);
-  const float* X = which ? p.k + b * p.k_sb + hd * p.k_sh + (int64_t)xc * p.k_sn
-                         : p.q + b * p.q_sb + hd * p.q_sh + (int64_t)xc * p.q_sn;
+  const int which = xb.blk & 1, rp = xb.blk >> 1, bh = xb.bh, b = bh / p.H, hd = bh % p.H;
+  const bool two = 2 * rp + 1 < p.NQB;  // (wave-uniform) the pair's second block exists
+  const float* X0 = which ? p.k + b * p.k_sb + hd * p.k_sh : p.q + b * p.q_sb + hd * p.q_sh;
+  const int64_t xs = which ? p.k_sn : p.q_sn;
+  const int x0 = 64 * rp + c, x1 = x0 + 32;
   const float* Lm = (which ? p.lq : p.lk) + (int64_t)hd * p.L * D;
   const __amdgpu_buffer_rsrc_t lr = make_rsrc(Lm, p.L * D * 4);
-  lds_zero<2 * IMG / 4>(lds);
+  lds_zero<32 * D>(lds);
   const DmaPat pat = dma_pat(SW_ROW, D * 4);
   dma64(L0, lr, pat, D * 4, 0);
-  float xr[NS];
-  load_run<NS>(xr, X + h * NS, x < p.N);
+  float xr0[NS], xr1[NS];
+  load_run<NS>(xr0, X0 + (int64_t)imin(x0, p.N - 1) * xs + h * NS, x0 < p.N);
+  load_run<NS>(xr1, X0 + (int64_t)imin(x1, p.N - 1) * xs + h * NS, two && x1 < p.N);
   float* out = (which ? p2ct : c2p) + (int64_t)bh * p.N * p.Lp;
   const int NLT = (p.L + 31) / 32;
   const int rbase = row_base64(c, h);
-  for (int lt = 0; lt < NLT; ++lt) {
-    const int l = lt * 32 + c;
-    const int cur = lt & 1;
-    wait_vm_all();
-    if (lt + 1 < NLT) dma64(L0 + IMG * (cur ^ 1), lr, pat, D * 4, (lt + 1) * 32);
-    f32x16 acc = zero16();
-#pragma unroll
-    for (int j = 0; j < NS / 4; ++j) {
-      const f32x4 lv = lds_f4(lds, IMG * cur + (rbase ^ (16 * j)));
-#pragma unroll
-      for (int e = 0; e < 4; ++e) acc = mfma(xr[4 * j + e], lv[e], acc);  // D[x][l]
-    }
-    if (l < p.L) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int xx = rb * 32 + crow(r, h);
-        if (xx < p.N) out[(int64_t)xx * p.Lp + l] = acc[r];
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slab lt read out before it is refilled
+  if (two) {
+    for (int lt = 0; lt < NLT; ++lt) logits_tile<D, true>(p, lds, L0, lr, pat, rbase, xr0, xr1, out, rp, lt, NLT, lane);
+  } else {
+    for (int lt = 0; lt < NLT; ++lt) logits_tile<D, false>(p, lds, L0, lr, pat, rbase, xr0, xr1, out, rp, lt, NLT, lane);
   }
 }
 
@@ -1911,8 +1939,8 @@ csa_status csa_rel_attn_fwd(const csa_rel_attn_args* a, void* stream) {
   RelArgs p = make_rel(a, R);
   const dim3 grid(xcd_grid(p.NQB, (int)(a->B * a->H)));
   if (R.fused) {
-    hipLaunchKernelGGL(k_rel_logits<64>, dim3(xcd_grid(2 * p.NQB, (int)(a->B * a->H))), dim3(64), 2 * 32 * 64 * 4,
-                       st, p, (float*)p.c2p, (float*)p.p2ct);
+    hipLaunchKernelGGL(k_rel_logits<64>, dim3(xcd_grid(2 * (int)((p.NQB + 1) / 2), (int)(a->B * a->H))), dim3(64),
+                       32 * 64 * 4, st, p, (float*)p.c2p, (float*)p.p2ct);
     const int NT = (int)(R.NP / 32);
     hipLaunchKernelGGL(k_rel_prep, dim3((unsigned)(NT * NT), (unsigned)(a->B * p.P_)), dim3(256), 0, st, p,
                        (uint16_t*)p.RM, (uint16_t*)p.RT);
