@@ -477,8 +477,11 @@ __global__ __launch_bounds__(64) void k_rel_scatter(const RelArgs p, float* __re
 // (asymmetric) mask stays exact. Entries outside [0,N)^2 hold 0x0100.
 __host__ __device__ constexpr int tile_pos(int j) { return 16 * ((j >> 2) & 1) + (j & 3) + 4 * (j >> 3); }
 
+// One 32 x 32 tile of one plane per workgroup; a thread codes 4 consecutive columns of one row, which
+// tile_pos keeps contiguous (positions 16 (k & 1) + 4 (k >> 1) + 0..3 for column group k), so RM and RT
+// take one 8-B store per thread (RT through the LDS transpose).
 __global__ __launch_bounds__(256) void k_rel_prep(const RelArgs p, uint16_t* __restrict__ RM, uint16_t* __restrict__ RT) {
-  __shared__ uint16_t tile[32][33];
+  __shared__ uint16_t tile[32][36];  // [row a][column b] of the tile's codes (36: 8-B aligned rows)
   const int NT = p.NP / 32, at = (int)blockIdx.x / NT, bt = (int)blockIdx.x % NT;
   const int bp = blockIdx.y, b = bp / p.P_, pl = bp % p.P_;
   const int hd = p.group > 0 ? (pl == 0 ? 0 : p.group) : pl;  // a head that reads plane pl
@@ -486,22 +489,27 @@ __global__ __launch_bounds__(256) void k_rel_prep(const RelArgs p, uint16_t* __r
   const uint8_t* mp = p.mask + plane_off(p, b, hd, p.mask_sb, p.mask_sh);
   uint16_t* rm = RM + (size_t)bp * p.NP * p.NP;
   uint16_t* rt = RT + (size_t)bp * p.NP * p.NP;
-  for (int e = threadIdx.x; e < 1024; e += 256) {
-    const int al = e >> 5, bl = e & 31, a = at * 32 + al, bb = bt * 32 + bl;
-    uint16_t code = 0x0100;
+  const int t = (int)threadIdx.x, rl = t >> 3, k = t & 7, pos = 16 * (k & 1) + 4 * (k >> 1);
+  const int a = at * 32 + rl;
+  uint16_t code[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int bb = bt * 32 + 4 * k + i;
+    code[i] = 0x0100;
     if (a < p.N && bb < p.N) {
       int r = rp[(int64_t)a * p.N + bb];
       r = r < p.L ? r : p.L - 1;  // memory safety; the reference requires rel < L
-      code = (uint16_t)(r | (mp[(int64_t)a * p.N + bb] ? 0x100 : 0));
+      code[i] = (uint16_t)(r | (mp[(int64_t)a * p.N + bb] ? 0x100 : 0));
     }
-    rm[(size_t)a * p.NP + bt * 32 + tile_pos(bl)] = code;
-    tile[al][bl] = code;
+    tile[rl][4 * k + i] = code[i];
   }
+  *reinterpret_cast<uint2*>(rm + (size_t)a * p.NP + bt * 32 + pos) =
+      uint2{(uint32_t)code[0] | ((uint32_t)code[1] << 16), (uint32_t)code[2] | ((uint32_t)code[3] << 16)};
   __syncthreads();
-  for (int e = threadIdx.x; e < 1024; e += 256) {
-    const int bl = e >> 5, al = e & 31;
-    rt[(size_t)(bt * 32 + bl) * p.NP + at * 32 + tile_pos(al)] = tile[al][bl];
-  }
+  // RT row bt * 32 + rl, columns a = at * 32 + 4 k + i: tile[4 k + i][rl]
+  *reinterpret_cast<uint2*>(rt + (size_t)(bt * 32 + rl) * p.NP + at * 32 + pos) =
+      uint2{(uint32_t)tile[4 * k][rl] | ((uint32_t)tile[4 * k + 1][rl] << 16),
+            (uint32_t)tile[4 * k + 2][rl] | ((uint32_t)tile[4 * k + 3][rl] << 16)};
 }
 
 struct Codes { uint32_t w[8]; };
