@@ -859,7 +859,7 @@ __device__ __forceinline__ uint32_t writelane_batch(uint32_t dst, const unsigned
     "s"((uint32_t)b[R0 + 6]), "s"((uint32_t)(b[R0 + 6] >> 32)), "s"((uint32_t)b[R0 + 7]),                \
     "s"((uint32_t)(b[R0 + 7] >> 32))
   if constexpr (R0 == 0)
-    asm volatile("s_nop 4\n\t"
+    asm("s_nop 4\n\t"
       "v_writelane_b32 %0, %1, 0\n\t"
       "v_writelane_b32 %0, %2, 4\n\t"
       "v_writelane_b32 %0, %3, 1\n\t"
@@ -878,7 +878,7 @@ __device__ __forceinline__ uint32_t writelane_batch(uint32_t dst, const unsigned
       "v_writelane_b32 %0, %16, 15"
         CSA_WL_OPS);
   else
-    asm volatile("s_nop 4\n\t"
+    asm("s_nop 4\n\t"
       "v_writelane_b32 %0, %1, 16\n\t"
       "v_writelane_b32 %0, %2, 20\n\t"
       "v_writelane_b32 %0, %3, 17\n\t"
@@ -899,16 +899,13 @@ __device__ __forceinline__ uint32_t writelane_batch(uint32_t dst, const unsigned
 #undef CSA_WL_OPS
   return dst;
 }
-// One batch of 8 registers of a mask into the packed word (layout above): batch bt covers registers
-// 8 bt .. 8 bt + 7, i.e. keys (crow(r,0), crow(r,1)) -> lanes 0..15 (bt = 0) or 16..31 (bt = 1).
-__device__ __forceinline__ uint32_t pack_batch(uint32_t w, int bt, const bool (&v)[8]) {
+__device__ __forceinline__ uint32_t pack_bits(const bool (&v)[16]) {
   unsigned long long b[16];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) b[8 * bt + e] = __ballot(v[e]);
-  return bt == 0 ? writelane_batch<0>(w, b) : writelane_batch<8>(w, b);
-}
-__device__ __forceinline__ void pin(u32x4& x) {
-  asm volatile("" : "+v"(x.x), "+v"(x.y), "+v"(x.z), "+v"(x.w));
+  for (int r = 0; r < 16; ++r) b[r] = __ballot(v[r]);
+  uint32_t w = 0;
+  w = writelane_batch<0>(w, b);
+  return writelane_batch<8>(w, b);
 }
 
 template <int D, int KPH>
@@ -1092,6 +1089,49 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd
       s[r] = fmaf(sacc[r], p.scale, bz[r >> 2][r & 3]);
       tmax = fmaxf(tmax, s[r]);
     }
+    bool av[16], keep[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { av[r] = true; keep[r] = true; }
+    if constexpr (!DENSE) {
+      if constexpr (HAS_U) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int j = j0 + crow(r, h);
+          const float v = p.U[((int64_t)bh * p.N + ic) * p.M + imin(j, p.M - 1)];
+          const float uu = (iv && j < p.M) ? v : 2.f;
+          av[r] = uu < fminf(fmaxf(eacc[r], 0.01f), 0.99f);  // STE.py:11-13
+        }
+      } else {
+#pragma unroll
+        for (int gp = 0; gp < 2; ++gp) {
+          const u32x4 rr = r_ste[gp];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const int r = 8 * gp + e;
+            av[r] = (float)u16_of(rr, e) < __builtin_amdgcn_fmed3f(eacc[r], 0.01f * ESC, 0.99f * ESC);
+          }
+        }
+      }
+    }
+    if constexpr (DROP) {
+#pragma unroll
+      for (int gp = 0; gp < 2; ++gp) {
+        const u32x4 rr = r_drop[gp];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) keep[8 * gp + e] = u16_of(rr, e) >= p.drop_thr;
+      }
+    }
+    // bit-pack the sampled graph / dropout keep mask: word [qb][key] holds 32 query bits (lanes 0..31)
+    if constexpr (!DENSE || DROP) {
+      const uint32_t myA = DENSE ? 0u : pack_bits(av);
+      const uint32_t myR = DROP ? pack_bits(keep) : 0u;
+      const int64_t widx = ((int64_t)bh * p.NQB + qb) * p.Mpad + j0 + c;
+      if constexpr (!DENSE) {
+        if (h == 0) p.Abits[widx] = myA;
+        if (j0 + c < p.M) cntl += __popc(myA & qmask);  // sampled edges inside [0,N) x [0,M)
+      }
+      if constexpr (DROP) if (h == 0) p.Rbits[widx] = myR;
+    }
     // online softmax update (exp(-inf - m) = 0 covers masked keys; m_use keeps an all-masked prefix finite)
     tmax = xhalf_max(tmax);
     const float m_new = fmaxf(m_run, tmax);
@@ -1099,66 +1139,18 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd
     const float alpha = __expf(m_run - m_use);
     zp *= alpha;
     zgp *= alpha;
-    if (__builtin_amdgcn_ballot_w64(alpha != 1.f)) {  // the running max moved for some query (o *= 1 is exact)
 #pragma unroll
-      for (int t = 0; t < DT; ++t)
+    for (int t = 0; t < DT; ++t)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
-    }
-    float ex[16];
+      for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
+    float w[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      ex[r] = __expf(s[r] - m_use);
-      zp += ex[r];
-    }
-    // Sampled graph / dropout keep masks, applied and bit-packed (word [qb][key] holds 32 query bits, lanes
-    // 0..31) in two batches of 8 registers: each batch's compare masks (SGPR pairs) are consumed right away by
-    // the selects and its writelane batch, so at most 16 mask SGPRs are live at once (taking all 32 masks
-    // first spilled ~30 SGPRs to VGPR lanes, ~45 v_readlane per tile). pin() makes batch 1's operands opaque
-    // after batch 0's writelanes (asm volatile), so the compiler cannot hoist its compares.
-    float w[16];
-    uint32_t myA = 0u, myR = 0u;
-#pragma unroll
-    for (int bt = 0; bt < 2; ++bt) {
-      if (bt == 1) {
-        if constexpr (!DENSE && !HAS_U) {
-          pin(r_ste[1]);
-#pragma unroll
-          for (int r = 8; r < 16; ++r) asm volatile("" : "+v"(eacc[r]));
-        }
-        if constexpr (DROP) pin(r_drop[1]);
-      }
-      bool av[8], keep[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int r = 8 * bt + e;
-        av[e] = true;
-        keep[e] = true;
-        if constexpr (!DENSE) {
-          if constexpr (HAS_U) {
-            const int j = j0 + crow(r, h);
-            const float v = p.U[((int64_t)bh * p.N + ic) * p.M + imin(j, p.M - 1)];
-            const float uu = (iv && j < p.M) ? v : 2.f;
-            av[e] = uu < fminf(fmaxf(eacc[r], 0.01f), 0.99f);  // STE.py:11-13
-          } else {
-            av[e] = (float)u16_of(r_ste[bt], e) < __builtin_amdgcn_fmed3f(eacc[r], 0.01f * ESC, 0.99f * ESC);
-          }
-        }
-        if constexpr (DROP) keep[e] = u16_of(r_drop[bt], e) >= p.drop_thr;
-        const float wa = av[e] ? ex[r] : 0.f;
-        zgp += wa;
-        w[r] = keep[e] ? wa : 0.f;
-      }
-      if constexpr (!DENSE) myA = pack_batch(myA, bt, av);
-      if constexpr (DROP) myR = pack_batch(myR, bt, keep);
-    }
-    if constexpr (!DENSE || DROP) {
-      const int64_t widx = ((int64_t)bh * p.NQB + qb) * p.Mpad + j0 + c;
-      if constexpr (!DENSE) {
-        if (h == 0) p.Abits[widx] = myA;
-        if (j0 + c < p.M) cntl += __popc(myA & qmask);  // sampled edges inside [0,N) x [0,M)
-      }
-      if constexpr (DROP) if (h == 0) p.Rbits[widx] = myR;
+      const float e = __expf(s[r] - m_use);
+      zp += e;
+      const float wa = av[r] ? e : 0.f;
+      zgp += wa;
+      w[r] = keep[r] ? wa : 0.f;
     }
     m_run = m_new;
     // O^T += V^T W^T (keys beyond M carry w = 0)
@@ -2874,12 +2866,15 @@ __global__ __launch_bounds__(256, ProjBwdSmallShape<D>::LCS ? 1 : 2) void k_proj
 // coalesced 256 B row of one slab), then the 4 wave partials are combined in a fixed order.
 // The summation order depends only on (H, G), never on timing -> bitwise deterministic.
 // ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_reduce_slabs(const KArgs p, int D, int KP32, float* __restrict__ dW0,
+// 16 waves per 64 slab elements: the shared weight elements sum H x G slabs each (432 at B = 256), and with
+// four waves only ~200 workgroups (one per CU) held the whole 20 MB of their reads in flight.
+constexpr int RS_WAVES = 16;
+__global__ __launch_bounds__(64 * RS_WAVES) void k_reduce_slabs(const KArgs p, int D, int KP32, float* __restrict__ dW0,
                                                       float* __restrict__ dW1, float* __restrict__ dW2,
                                                       float* __restrict__ db0, float* __restrict__ db1,
                                                       float* __restrict__ db2, float* __restrict__ dS_ws,
                                                       float* __restrict__ dC_ws) {
-  __shared__ float red[4][64];
+  __shared__ float red[RS_WAVES][64];
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t e = (int64_t)blockIdx.x * 64 + l;
   const int G = p.G;
@@ -2901,17 +2896,19 @@ __global__ __launch_bounds__(256) void k_reduce_slabs(const KArgs p, int D, int 
 #pragma unroll
   for (int a = 0; a < 8; ++a) acc[a] = 0.f;
   int i = w;
-  for (; i + 28 < ns; i += 32) {
+  for (; i + RS_WAVES * 7 < ns; i += RS_WAVES * 8) {
 #pragma unroll
-    for (int a = 0; a < 8; ++a) acc[a] += src[(int64_t)(i + 4 * a) * p.slab_floats];
+    for (int a = 0; a < 8; ++a) acc[a] += src[(int64_t)(i + RS_WAVES * a) * p.slab_floats];
   }
 #pragma unroll
   for (int a = 0; a < 8; ++a)
-    if (i + 4 * a < ns) acc[a] += src[(int64_t)(i + 4 * a) * p.slab_floats];
+    if (i + RS_WAVES * a < ns) acc[a] += src[(int64_t)(i + RS_WAVES * a) * p.slab_floats];
   red[w][l] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   __syncthreads();
   if (w != 0 || ns == 0) return;
-  const float s = (red[0][l] + red[1][l]) + (red[2][l] + red[3][l]);
+  float s = 0.f;  // the waves' partials in wave order (fixed: deterministic)
+#pragma unroll
+  for (int v = 0; v < RS_WAVES; ++v) s += red[v][l];
   if (e < nW) {
     const int64_t DD = (int64_t)D * D;
     if (e < DD) dW0[e] = s;
@@ -3314,7 +3311,7 @@ csa_status launch_bwd(const csa_sbm_bwd_args* b, const Layout& L, hipStream_t st
     float* dS_ws = (float*)((char*)b->workspace + L.w_dS);
     float* dC_ws = (float*)((char*)b->workspace + L.w_dC);
     const int64_t total = 3LL * D * D + 3LL * D + (int64_t)a->H * KP32 * D + (int64_t)a->H * KP32 * KP32;
-    hipLaunchKernelGGL(k_reduce_slabs, dim3((unsigned)((total + 63) / 64)), dim3(256), 0, st, p, D, KP32,
+    hipLaunchKernelGGL(k_reduce_slabs, dim3((unsigned)((total + 63) / 64)), dim3(64 * RS_WAVES), 0, st, p, D, KP32,
                        b->dproj_w[0], b->dproj_w[1], b->dproj_w[2], b->dproj_b[0], b->dproj_b[1], b->dproj_b[2],
                        dS_ws, dC_ws);
     hipLaunchKernelGGL(k_cluster_grad, dim3((unsigned)a->k, (unsigned)a->H), dim3(128), 0, st, p.S, (const float*)dS_ws,
