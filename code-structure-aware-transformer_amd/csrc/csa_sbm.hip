@@ -831,6 +831,8 @@ template <bool BF>
 constexpr bool bwd_handoff() {
 #ifdef CSA_EXP_RECOMP  // experiment: the recompute pipeline for fp32 too
   return false;
+#elif defined(CSA_EXP_BF_HANDOFF)  // experiment: the (one-plane) handoff in bf16 mode too
+  return true;
 #else
   return !BF;
 #endif
