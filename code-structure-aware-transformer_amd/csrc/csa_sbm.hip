@@ -2,20 +2,21 @@
 //
 // CSA_EXP_* macros select throw-away experiment builds (tools/build_variant.py);
 // the shipped library is built without them.
-// Pipeline (one forward + one backward = 9 launches, all stream-ordered, no host sync):
-//   fwd: k_cluster_softmax   S_h = softmax_{k^2}(C_h C_h^T)                      sbm_attn.py:37-39
-//        k_frag_prep         weights -> MFMA-operand-major fragments (L2-resident)
-//        k_proj_fwd          Qh = sigmoid(MLP(Q) C^T), Kh likewise, T = Kh S^T    sbm_attn.py:41-53
+// Pipeline (one forward + one backward = 10 launches, all stream-ordered, no host sync):
+//   fwd: k_prep              S_h = softmax_{k^2}(C_h C_h^T) (sbm_attn.py:37-39) and the weights ->
+//                            MFMA-operand-major fragments (L2-resident), one launch
+//        k_proj_fwd_l        Qh = sigmoid(MLP(Q) C^T), Kh likewise, T = Kh S^T    sbm_attn.py:41-53
 //        k_attn_fwd          expA tile, u < clamp(expA) sampling, online softmax
 //                            with graph-masked L1 renormalisation, dropout, PV    sbm_attn.py:55-64, STE.py:10-15
 //        k_sparsity_finish   integer edge counts -> head-wise sparsity            sbm_attn.py:64
 //   bwd: k_attn_rowprep      gamma = rowsum(dX*X) and the per-row constants of the elementwise backward
 //        k_attn_bwd_kv       S, dP, the elementwise backward once per element; dK (attention path),
-//                            dV, dT; ds and G tiles to the workspace
-//        k_attn_bwd_qg       dQ (attention path) = ds K, dQh = G T from those tiles
-//        k_proj_bwd          STE/sigmoid/cluster/MLP backward (+dQ, +dK second path),
+//                            dV, dT; one float per element (w, or W_NO_EDGE) to the workspace
+//        k_attn_bwd_qg       dQ (attention path) = ds K, dQh = G T, ds and G rebuilt from those tiles
+//        k_proj_bwd_s        STE/sigmoid/cluster/MLP backward (+dQ, +dK second path),
 //                            per-workgroup fixed-order partial slabs for dW, db, dC, dS
-//        k_param_reduce      fixed-order slab reduction, softmax_{k^2} backward -> dC
+//        k_reduce_slabs      fixed-order slab reduction
+//        k_cluster_grad      softmax_{k^2} backward -> dC
 // The N x N intermediates of the reference (expA, graph, dot, softmax, attn: ~11 fp32
 // (B,H,N,M) tensors) are never materialised: the sampled graph and the dropout keep-mask
 // are kept as 1 bit per edge for the backward, and the optional attn/graph maps are
@@ -248,13 +249,53 @@ __device__ __forceinline__ void frag_chain(const float* __restrict__ frag, int n
 }
 
 // ------------------------------------------------------------------------------------
+// Fragment prep: dst(it, s, lane) = Mat[32 it + c][kperm(s, h)] (or Mat^T), 0 outside.
+// ------------------------------------------------------------------------------------
+struct FragJob {
+  const float* src; float* dst;
+  int rows, cols, ld;         // source matrix (rows x cols, row stride ld)
+  int transpose;              // value = src[kk][r] instead of src[r][kk]
+  int acc_perm;               // kperm: 0 = lin (k = s + nsteps*h), 1 = acc (k = 32(s/16)+crow(s%16,h))
+  int nit, nsteps;            // output tiles x K-steps
+  int batch; int64_t src_bstride, dst_bstride;  // repeated per head
+};
+struct FragJobs { FragJob j[12]; int n; };
+
+// element e of job J (e = batch index * per-batch elements + position in the fragment array)
+__device__ __forceinline__ void frag_elem(const FragJob& J, int64_t e) {
+  const int64_t per = (int64_t)J.nit * J.nsteps * 64;
+  const int64_t bidx = e / per, rem = e % per;
+  const int s4 = (int)(rem / 256) % (J.nsteps / 4);
+  const int it = (int)(rem / 256) / (J.nsteps / 4);
+  const int lane = (int)(rem / 4) % 64, s = s4 * 4 + (int)(rem % 4);
+  const int c = lane & 31, h = lane >> 5;
+  const int r = 32 * it + c;
+  const int kk = J.acc_perm ? 32 * (s / 16) + crow(s % 16, h) : s + J.nsteps * h;
+  const float* src = J.src + bidx * J.src_bstride;
+  float v = 0.f;
+  if (r < J.rows && kk < J.cols) v = J.transpose ? src[(int64_t)kk * J.ld + r] : src[(int64_t)r * J.ld + kk];
+  J.dst[bidx * J.dst_bstride + rem] = v;
+}
+
+// ------------------------------------------------------------------------------------
 // F1: S_h = softmax over all k^2 entries of C_h C_h^T, zero-padded to (32KT x 32KT)
 // ------------------------------------------------------------------------------------
 // MAXE = ceil(k^2 / 256) rounded up to 1, 4, 16 or 64 (host-selected instantiation)
+// The forward's prep stage in one launch: blocks 0 .. H-1 compute S_h (one head each) and then lay out S_h's
+// fragments (jobs [0, nS), batch index = the head); blocks H .. run the weight / cluster fragment jobs
+// [nS, n), which do not depend on S, grid-stride.
 template <int MAXE>
-__global__ __launch_bounds__(256) void k_cluster_softmax(const float* __restrict__ C, float* __restrict__ S,
-                                                         int k, int D, int KP32, unsigned long long* __restrict__ cnt,
-                                                         int H) {
+__global__ __launch_bounds__(256) void k_prep(const float* __restrict__ C, float* __restrict__ S, int k, int D, int KP32,
+                                              unsigned long long* __restrict__ cnt, int H, const FragJobs jobs, int nS) {
+  if ((int)blockIdx.x >= H) {
+    const int64_t t0 = (int64_t)(blockIdx.x - H) * 256 + threadIdx.x, stride = (int64_t)(gridDim.x - H) * 256;
+    for (int j = nS; j < jobs.n; ++j) {
+      const FragJob& J = jobs.j[j];
+      const int64_t total = (int64_t)J.nit * J.nsteps * 64 * J.batch;
+      for (int64_t e = t0; e < total; e += stride) frag_elem(J, e);
+    }
+    return;
+  }
   // C_h (k x D <= 128 x 96) staged in LDS; each thread keeps its (up to MAXE) logits in registers
   // across the max / sum / normalise passes (one dot product per entry instead of three).
   const int hd = blockIdx.x, tid = threadIdx.x;
@@ -312,37 +353,11 @@ __global__ __launch_bounds__(256) void k_cluster_softmax(const float* __restrict
     const int e = tid + 256 * q;
     if (e < kk) Sh[(e / k) * KP32 + e % k] = v[q] / sm;
   }
-}
-
-// ------------------------------------------------------------------------------------
-// Fragment prep: dst(it, s, lane) = Mat[32 it + c][kperm(s, h)] (or Mat^T), 0 outside.
-// ------------------------------------------------------------------------------------
-struct FragJob {
-  const float* src; float* dst;
-  int rows, cols, ld;         // source matrix (rows x cols, row stride ld)
-  int transpose;              // value = src[kk][r] instead of src[r][kk]
-  int acc_perm;               // kperm: 0 = lin (k = s + nsteps*h), 1 = acc (k = 32(s/16)+crow(s%16,h))
-  int nit, nsteps;            // output tiles x K-steps
-  int batch; int64_t src_bstride, dst_bstride;  // repeated per head
-};
-struct FragJobs { FragJob j[12]; int n; };
-
-__global__ __launch_bounds__(256) void k_frag_prep(const FragJobs jobs) {
-  const FragJob J = jobs.j[blockIdx.y];
-  const int64_t per = (int64_t)J.nit * J.nsteps * 64;
-  const int64_t total = per * J.batch;
-  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
-    const int64_t bidx = e / per, rem = e % per;
-    const int s4 = (int)(rem / 256) % (J.nsteps / 4);
-    const int it = (int)(rem / 256) / (J.nsteps / 4);
-    const int lane = (int)(rem / 4) % 64, s = s4 * 4 + (int)(rem % 4);
-    const int c = lane & 31, h = lane >> 5;
-    const int r = 32 * it + c;
-    const int kk = J.acc_perm ? 32 * (s / 16) + crow(s % 16, h) : s + J.nsteps * h;
-    const float* src = J.src + bidx * J.src_bstride;
-    float v = 0.f;
-    if (r < J.rows && kk < J.cols) v = J.transpose ? src[(int64_t)kk * J.ld + r] : src[(int64_t)r * J.ld + kk];
-    J.dst[bidx * J.dst_bstride + rem] = v;
+  __syncthreads();  // S_h complete (the workgroup's global writes are visible to it after the barrier)
+  for (int j = 0; j < nS; ++j) {
+    const FragJob& J = jobs.j[j];
+    const int64_t per = (int64_t)J.nit * J.nsteps * 64;
+    for (int64_t e = tid; e < per; e += 256) frag_elem(J, hd * per + e);
   }
 }
 
@@ -3124,15 +3139,14 @@ csa_status launch_fwd(const csa_sbm_fwd_args* a, const Layout& L, hipStream_t st
     float* S = (float*)((char*)a->state + L.S);
     {
     Stage sg(a->prof, CSA_STAGE_PREP, st);
-    {
-      const int kk = (int)(a->k * a->k);
-      auto csm = kk <= 256 ? k_cluster_softmax<1> : kk <= 1024 ? k_cluster_softmax<4>
-               : kk <= 4096 ? k_cluster_softmax<16> : k_cluster_softmax<64>;
-      hipLaunchKernelGGL(csm, dim3(a->H), dim3(256), 0, st, a->cluster_w, S, (int)a->k, D, KP32, p.cnt, (int)a->H);
-    }
     FragJobs J;
     memset(&J, 0, sizeof(J));
     int n = 0;
+    J.j[n++] = FragJob{S, (float*)p.Sf, KP32, KP32, KP32, 0, 1, KT, 16 * KT, (int)a->H, (int64_t)KP32 * KP32,
+                       (int64_t)KP32 * KP32};
+    J.j[n++] = FragJob{S, (float*)p.SfT, KP32, KP32, KP32, 1, 1, KT, 16 * KT, (int)a->H, (int64_t)KP32 * KP32,
+                       (int64_t)KP32 * KP32};
+    const int nS = n;  // S_h's fragments: laid out by the head's softmax block
     for (int l = 0; l < 3; ++l) {  // forward weights: A[o][i] = W[o][i]; l=0 lin-perm, else acc-perm
       J.j[n++] = FragJob{a->proj_w[l], (float*)p.Wf[l], D, D, D, 0, l == 0 ? 0 : 1, D / 32, D / 2, 1, 0, 0};
     }
@@ -3143,12 +3157,11 @@ csa_status launch_fwd(const csa_sbm_fwd_args* a, const Layout& L, hipStream_t st
                        (int64_t)KP32 * D};
     J.j[n++] = FragJob{a->cluster_w, (float*)p.CfT, D, (int)a->k, D, 1, 1, D / 32, 16 * KT, (int)a->H, a->k * D,
                        (int64_t)KP32 * D};
-    J.j[n++] = FragJob{S, (float*)p.Sf, KP32, KP32, KP32, 0, 1, KT, 16 * KT, (int)a->H, (int64_t)KP32 * KP32,
-                       (int64_t)KP32 * KP32};
-    J.j[n++] = FragJob{S, (float*)p.SfT, KP32, KP32, KP32, 1, 1, KT, 16 * KT, (int)a->H, (int64_t)KP32 * KP32,
-                       (int64_t)KP32 * KP32};
     J.n = n;
-    hipLaunchKernelGGL(k_frag_prep, dim3(16, n), dim3(256), 0, st, J);
+    const int kk = (int)(a->k * a->k);
+    auto prep = kk <= 256 ? k_prep<1> : kk <= 1024 ? k_prep<4> : kk <= 4096 ? k_prep<16> : k_prep<64>;
+    hipLaunchKernelGGL(prep, dim3((unsigned)a->H + 128), dim3(256), 0, st, a->cluster_w, S, (int)a->k, D, KP32, p.cnt,
+                       (int)a->H, J, nS);
     }
     {
       Stage sg(a->prof, CSA_STAGE_PROJ_FWD, st);
