@@ -98,8 +98,8 @@ inline size_t al(size_t x) { return (x + 255) & ~size_t(255); }
 // (dispatch rounds over the 256 CUs) x (groups of 4 items per workgroup); the smallest G wins ties
 // (fewer slabs to reduce). java B = 64, H = 8, 10 items per AST, 1 workgroup per CU: G = 32, one round
 // of 5 full groups (a whole-batch split, G = 64, ran two rounds of 3 groups, the last half empty).
-int64_t proj_bwd_groups(int64_t B, int64_t H, int64_t items_per_b, int wg_per_cu) {
-  const int64_t I = B * items_per_b, slots = 256LL * wg_per_cu;
+int64_t proj_bwd_groups(int64_t B, int64_t H, int64_t items_per_b, int wg_per_cu, int share = 1) {
+  const int64_t I = B * items_per_b, slots = std::max<int64_t>(1, 256LL * wg_per_cu / share);
   const int64_t gmax = std::min<int64_t>(I, std::max<int64_t>(1, 4 * slots / H));
   int64_t best = 1, best_cost = INT64_MAX;
   for (int64_t G = 1; G <= gmax; ++G) {
@@ -141,8 +141,11 @@ Layout make_layout(int64_t B, int64_t H, int64_t N, int64_t M, int64_t D, int64_
   // backward workspace
   // two workgroups per CU for d = 64 with KT = 1 (k_proj_bwd_s / k_proj_bwd<64, 1>: 80 / 64 KiB LDS)
   L.G = dense ? 0 : proj_bwd_groups(B, H, L.NQB + L.NKB, (D == 64 && L.KT == 1) ? 2 : 1);
-  L.G_K = dense ? 0 : proj_bwd_groups(B, H, L.NKB, (D == 64 && L.KT == 1) ? 2 : 1);
-  L.G_Q = dense ? 0 : proj_bwd_groups(B, H, L.NQB, (D == 64 && L.KT == 1) ? 2 : 1);
+  // the key / query split (k_proj_bwd_s kinds 1 and 2, or both in one launch) sizes each kind for half the
+  // workgroup slots, so the two together take the machine once (each sized for all of it: 2 rounds, and at
+  // java dims 3 groups of 4 items per workgroup where the unsplit grid had 5 in one round: 210 -> 256 us)
+  L.G_K = dense ? 0 : proj_bwd_groups(B, H, L.NKB, (D == 64 && L.KT == 1) ? 2 : 1, 2);
+  L.G_Q = dense ? 0 : proj_bwd_groups(B, H, L.NQB, (D == 64 && L.KT == 1) ? 2 : 1, 2);
   L.slab_floats = dense ? 0 : (3 * D * D + 3 * D + KP32 * D + KP32 * KP32);
   o = 0;
   L.w_dQh = take(sizeof(float) * B * H * N * L.kp);
