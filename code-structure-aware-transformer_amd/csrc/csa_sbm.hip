@@ -1851,8 +1851,8 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
       return SWZ ? both_read(lds, cb[t], r, off) : lds_f1(lds, off + cb[t] + 4 * DP * crow(r, 0));
     };
     // Two halves of the query block (registers r = 8 half .. 8 half + 7 = rows 16 half .. 16 half + 15):
-    // elementwise, then the dV / dK / dT K-steps of those rows, then (SWZ) those rows of query block
-    // qb+1 are DMA'd in while the second half runs.
+    // elementwise, then the dV / dK / dT K-steps of those rows; query block qb+1's images are DMA'd in
+    // after the second half.
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
       // Elementwise backward, once per element (k_attn_rowprep's row constants; scalar fp32: packed v_pk_* beside
@@ -1966,12 +1966,17 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
 #else
       if (more) {
 #endif
-        if constexpr (SWZ) {  // rows 16 half .. 16 half + 15 of every image are free again
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          dma64(Xl, xr_, xpat, xld, i0 + 32, 4 * half, 4 * half + 4);
-          dma64(Ql, qr_, qpat, qld, i0 + 32, 4 * half, 4 * half + 4);
-          if constexpr (!DENSE) dma_narrow(Hl, hr_, i0 + 32, KPN, half, half + 1);
-          dma_tile_contig<4>(Sl, sr_, i0 + 32, half, half + 1);
+        // the whole refill after the second half: no mid-tile wait on the first half's reads, so the second
+        // half's elementwise can be scheduled among the first half's MFMAs (a per-half rolling refill measured
+        // 4 us slower, profiles/r04_ab_kv_refill.txt)
+        if constexpr (SWZ) {
+          if (half == 1) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            dma64(Xl, xr_, xpat, xld, i0 + 32);
+            dma64(Ql, qr_, qpat, qld, i0 + 32);
+            if constexpr (!DENSE) dma_narrow(Hl, hr_, i0 + 32, KPN);
+            dma_tile_contig<4>(Sl, sr_, i0 + 32);
+          }
         } else if (half == 1) {
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           dma_rows<D>(Xl, xr_, xld, i0 + 32, p.N);
