@@ -44,7 +44,7 @@ IDEAL_BYTES_PER_AST_BF16IO = 2.050e6
 PMC_TABLE = os.path.join(ROOT, "code-structure-aware-transformer_amd", "csa_amd", "pmc_gfx950.json")
 # the kernels of each profiled stage (csa_sbm.hip launch order)
 STAGE_KERNELS = {"prep": ("k_prep",), "proj_fwd": ("k_proj_fwd_l",),
-                 "attn_fwd": ("k_attn_fwd",), "attn_bwd_kv": ("k_attn_rowprep", "k_attn_bwd_kv"),
+                 "attn_fwd": ("k_attn_fwd",), "attn_rowprep": ("k_attn_rowprep",), "attn_bwd_kv": ("k_attn_bwd_kv",),
                  "attn_bwd_q": ("k_attn_bwd_qg",), "proj_bwd": ("k_proj_bwd_s",),
                  "reduce": ("k_reduce_slabs", "k_cluster_grad")}  # (proj_bwd_k: k_proj_bwd_s as well)
 
@@ -557,7 +557,7 @@ def main():
     pb0 = profs[-1][1]
     win = {}
     base = None
-    for name in ("attn_bwd_kv", "attn_bwd_q", "proj_bwd_k", "proj_bwd", "reduce"):
+    for name in ("attn_rowprep", "attn_bwd_kv", "attn_bwd_q", "proj_bwd_k", "proj_bwd", "reduce"):
         s_ = STAGES[name]
         if pb0.start[s_] and pb0.stop[s_]:
             if base is None:

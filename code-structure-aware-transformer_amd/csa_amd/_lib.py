@@ -12,7 +12,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CSA_HIP_LIB", os.path.join(_HERE, "lib", "libcsa_hip.so"))
 
-CSA_ABI_VERSION = 6
+CSA_ABI_VERSION = 7
 CSA_FLAG_DENSE = 1
 CSA_FLAG_FWD_ONLY = 2
 CSA_SCHED_AUTO, CSA_SCHED_IN_ORDER, CSA_SCHED_CONCURRENT = 0, 1, 2
@@ -23,11 +23,12 @@ STATUS = {0: "CSA_OK", 1: "CSA_INVALID_ARG", 2: "CSA_UNSUPPORTED_SHAPE", 3: "CSA
 i64, u64, u32, f32, vp = ctypes.c_int64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_float, ctypes.c_void_p
 
 
-CSA_STAGE_COUNT = 8
+CSA_STAGE_COUNT = 9
 STAGES = {"prep": 0, "proj_fwd": 1, "attn_fwd": 2, "attn_bwd_q": 3, "attn_bwd_kv": 4, "proj_bwd": 5, "reduce": 6,
-          "proj_bwd_k": 7}
+          "proj_bwd_k": 7, "attn_rowprep": 8}
 KERNEL_OF_STAGE = {"proj_fwd": "k_proj_fwd", "attn_fwd": "k_attn_fwd", "attn_bwd_q": "k_attn_bwd_qg",
-                   "attn_bwd_kv": "k_attn_bwd_kv", "proj_bwd": "k_proj_bwd", "proj_bwd_k": "k_proj_bwd"}
+                   "attn_bwd_kv": "k_attn_bwd_kv", "proj_bwd": "k_proj_bwd", "proj_bwd_k": "k_proj_bwd",
+                   "attn_rowprep": "k_attn_rowprep"}
 
 
 def on_device(device):

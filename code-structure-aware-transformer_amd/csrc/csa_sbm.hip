@@ -3212,9 +3212,12 @@ template <int D, int KPH, bool DENSE, bool DROP, bool DG, bool BF, typename MID>
 void launch_attn_bwd_v(const KArgs& p, int BH, const Layout& L, const csa_prof* pf, hipStream_t st, MID mid) {
   using SH = AttnBwdShape<D, KPH>;
   {
-    Stage sg(pf, CSA_STAGE_ATTN_BWD_KV, st);
+    Stage sg(pf, CSA_STAGE_ATTN_ROWPREP, st);
     const int64_t threads = 2LL * BH * L.NQB * 32;
     hipLaunchKernelGGL(k_attn_rowprep<D>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, p);
+  }
+  {
+    Stage sg(pf, CSA_STAGE_ATTN_BWD_KV, st);
     hipLaunchKernelGGL((k_attn_bwd_kv<D, KPH, DENSE, DROP, DG, BF>), dim3(xcd_grid((int)L.NKB, BH)), dim3(64),
                        SH::KV_BYTES, st, p);
   }

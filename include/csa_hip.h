@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define CSA_ABI_VERSION 6
+#define CSA_ABI_VERSION 7
 
 typedef enum csa_status {
   CSA_OK = 0,
@@ -90,11 +90,12 @@ enum {
   CSA_STAGE_PROJ_FWD = 1,   /* k_proj_fwd */
   CSA_STAGE_ATTN_FWD = 2,   /* k_attn_fwd */
   CSA_STAGE_ATTN_BWD_Q = 3, /* k_attn_bwd_qg (bf16 mode: k_attn_bwd_qr) */
-  CSA_STAGE_ATTN_BWD_KV = 4,/* k_attn_rowprep + k_attn_bwd_kv */
+  CSA_STAGE_ATTN_BWD_KV = 4,/* k_attn_bwd_kv */
   CSA_STAGE_PROJ_BWD = 5,   /* k_proj_bwd (concurrent schedule: its query-block items only) */
   CSA_STAGE_REDUCE = 6,     /* slab reduction + cluster grad */
   CSA_STAGE_PROJ_BWD_K = 7, /* concurrent schedule: k_proj_bwd's key-block items, on the side stream */
-  CSA_STAGE_COUNT = 8
+  CSA_STAGE_ATTN_ROWPREP = 8, /* ABI v7: k_attn_rowprep, timed apart from k_attn_bwd_kv */
+  CSA_STAGE_COUNT = 9
 };
 typedef struct csa_prof {
   void* start[CSA_STAGE_COUNT];
