@@ -1336,34 +1336,50 @@ __global__ __launch_bounds__(64) void k_attn_gx(const KArgs p) {
 // L1 norm of softmax * graph:
 //   c0 = -lse log2e, u = dscale / max(n, eps), v = -[n >= eps] gamma / max(n, eps), rho = [n < eps] gamma.
 // Rows past N (up to the query block's end) get c0 = -inf, u = v = rho = 0: P = 0, so they add nothing.
-// Two lanes per row, each one half of the dX . X dot product. HBM-bound: 2 x 4d B per row.
+// LPR lanes per row (16 for d = 64, 32 for d = 96), one 16-B chunk of dX and of X each: a wave-instruction
+// reads whole rows (1 KiB contiguous at d = 64) instead of 64 lanes each on its own 128-B line; the dot
+// product's partial sums meet by lane shuffles, and the row's first lane writes its record. A wave covers
+// RPW rows (4 instructions per operand in flight). HBM-bound: 2 x 4d B per row.
 template <int D>
 __global__ __launch_bounds__(256) void k_attn_rowprep(const KArgs p) {
-  constexpr int NS = D / 2;
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x, row = t >> 1;  // row of the padded (bh, NQB*32)
-  const int h = (int)(t & 1);
-  const int NP = p.NQB * 32;
-  const bool rv = row < (int64_t)p.B * p.H * NP;
-  const int64_t rc = rv ? row : 0;
-  const int i = (int)(rc % NP), bh = (int)(rc / NP), b = bh / p.H, hd = bh % p.H;
-  const bool iv = rv && i < p.N;
-  const int ic = imin(i, p.N - 1);
-  float dx[NS], xr[NS];
-  load_run<NS>(dx, p.dX + b * p.dx_sb + hd * p.dx_sh + (int64_t)ic * p.dx_sn + h * NS, iv);
-  load_run<NS>(xr, p.X + b * p.x_sb + hd * p.x_sh + (int64_t)ic * p.x_sn + h * NS, iv);
-  const f32x4 st = *reinterpret_cast<const f32x4*>(p.stats + ((int64_t)bh * p.N + ic) * 4);  // lse, 1/D, [n>=eps]
-  float gp = 0.f;
+  constexpr int CPR = D / 4, LPR = CPR <= 16 ? 16 : 32, RPI = 64 / LPR, RPW = 4 * RPI;
+  const int lane = lane_id(), sub = lane % LPR;
+  const int64_t NP = (int64_t)p.NQB * 32, total = (int64_t)p.B * p.H * NP;
+  const int64_t r0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + lane / LPR;
+  float part[4];
 #pragma unroll
-  for (int s = 0; s < NS; ++s) gp = fmaf(dx[s], xr[s], gp);
-  float gamma = gp + __shfl_xor(gp, 1, 64);
-  if (p.dattn) gamma += p.gx[(int64_t)bh * p.N + ic];
+  for (int u = 0; u < 4; ++u) {
+    const int64_t rc = r0 + u * RPI < total ? r0 + u * RPI : total - 1;
+    const int i = (int)(rc % NP), bh = (int)(rc / NP), b = bh / p.H, hd = bh % p.H;
+    const bool ld = i < p.N && sub < CPR;
+    const int ic = imin(i, p.N - 1), ch = imin(sub, CPR - 1);
+    const f32x4 dx = *reinterpret_cast<const f32x4*>(p.dX + b * p.dx_sb + hd * p.dx_sh + (int64_t)ic * p.dx_sn + 4 * ch);
+    const f32x4 xr = *reinterpret_cast<const f32x4*>(p.X + b * p.x_sb + hd * p.x_sh + (int64_t)ic * p.x_sn + 4 * ch);
+    const float v = fmaf(dx[0], xr[0], fmaf(dx[1], xr[1], fmaf(dx[2], xr[2], dx[3] * xr[3])));
+    part[u] = ld ? v : 0.f;
+  }
   const float dscale = p.attn_p > 0.f ? 1.f / (1.f - p.attn_p) : 1.f;
-  f32x4 rec;
-  rec[0] = iv ? -st[0] * LOG2E : NEG_INF;
-  rec[1] = iv ? dscale * st[1] : 0.f;
-  rec[2] = (iv && st[2] != 0.f) ? -gamma * st[1] : 0.f;
-  rec[3] = (iv && st[2] == 0.f) ? gamma : 0.f;
-  if (rv && h == 0) *reinterpret_cast<f32x4*>(p.brow + rc * 4) = rec;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    float g = part[u];
+#pragma unroll
+    for (int o = 1; o < LPR; o <<= 1) g += __shfl_xor(g, o, 64);
+    const int64_t row = r0 + u * RPI;
+    if (sub == 0 && row < total) {
+      const int i = (int)(row % NP), bh = (int)(row / NP);
+      const bool iv = i < p.N;
+      const int ic = imin(i, p.N - 1);
+      const f32x4 st = *reinterpret_cast<const f32x4*>(p.stats + ((int64_t)bh * p.N + ic) * 4);  // lse, 1/D, [n>=eps]
+      float gamma = g;
+      if (p.dattn) gamma += p.gx[(int64_t)bh * p.N + ic];
+      f32x4 rec;
+      rec[0] = iv ? -st[0] * LOG2E : NEG_INF;
+      rec[1] = iv ? dscale * st[1] : 0.f;
+      rec[2] = (iv && st[2] != 0.f) ? -gamma * st[1] : 0.f;
+      rec[3] = (iv && st[2] == 0.f) ? gamma : 0.f;
+      *reinterpret_cast<f32x4*>(p.brow + row * 4) = rec;
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------
@@ -3213,8 +3229,9 @@ void launch_attn_bwd_v(const KArgs& p, int BH, const Layout& L, const csa_prof* 
   using SH = AttnBwdShape<D, KPH>;
   {
     Stage sg(pf, CSA_STAGE_ATTN_ROWPREP, st);
-    const int64_t threads = 2LL * BH * L.NQB * 32;
-    hipLaunchKernelGGL(k_attn_rowprep<D>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, p);
+    constexpr int RPW = 4 * (64 / (D / 4 <= 16 ? 16 : 32));  // rows per wave (k_attn_rowprep)
+    const int64_t rows = (int64_t)BH * L.NQB * 32, per_block = 4LL * RPW;
+    hipLaunchKernelGGL(k_attn_rowprep<D>, dim3((unsigned)((rows + per_block - 1) / per_block)), dim3(256), 0, st, p);
   }
   {
     Stage sg(pf, CSA_STAGE_ATTN_BWD_KV, st);
