@@ -1,0 +1,16 @@
+#!/bin/bash
+# k_attn_bwd_qg: same-box A/B of plain vs non-temporal loads of the w tiles (CSA_EXP_QG_NT_LOAD).
+set -o pipefail
+export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+LIB=$R/code-structure-aware-transformer_amd/csa_amd/lib
+mkdir -p $R/gpurun_out
+CSA_HIP_LIB=$LIB/libcsa_QGNT.so timeout -k 10 300 python -u -m pytest tests/test_sbm_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pt_w.log 2>&1; rc=$?; tail -2 gpurun_out/pt_w.log; [ $rc -eq 0 ] || exit $rc
+run() {  # tag lib
+  CSA_HIP_LIB=$2 timeout -k 10 120 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-train --no-cpu-config1 --no-bf16-leg > gpurun_out/bench_w.json || exit $?
+  python3 -c "import json; d=json.load(open('gpurun_out/bench_w.json')); print('$1', d['ms_per_step'], {k: round(v,4) for k,v in d['stage_ms'].items()})"
+}
+for i in 1 2 3; do
+  run tree $LIB/libcsa_hip.so || exit 1
+  run qgnt $LIB/libcsa_QGNT.so || exit 1
+done
