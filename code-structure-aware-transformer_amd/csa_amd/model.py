@@ -126,7 +126,8 @@ class CSE(nn.Module):
         self.norm = LayerNorm(hidden_size)
 
     def build_rel_emb(self):
-        return [torch.stack([self.L_q.weight, self.T_q.weight])]
+        # the reference's torch.stack([L_q.weight, T_q.weight]), kept as the pair its layers unbind
+        return [(self.L_q.weight, self.T_q.weight)]
 
     def forward(self, data):
         out = data.src_pe_emb

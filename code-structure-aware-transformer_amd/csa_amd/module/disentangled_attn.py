@@ -53,9 +53,12 @@ class DisentangledAttn(nn.Module):
         else:
             query, key, value = [transpose_for_scores(l(x), self.h)
                                  for l, x in zip(self.linear_layers, (query, key, value))]
-        lq = rel_emb[0]
-        l = lq[0].unsqueeze(0)  # 1, L, d
-        t = lq[1].unsqueeze(0)
+        # rel_emb[0]: the (L_q, T_q) embedding tables (the reference stacks them and selects each back out;
+        # unbind takes both at once, so the backward is one stack instead of two zero-filled select
+        # gradients accumulated into the stack's gradient, per layer)
+        tables = rel_emb[0]
+        l, t = (tables.unbind(0) if torch.is_tensor(tables) else tables)
+        l, t = l.unsqueeze(0), t.unsqueeze(0)  # 1, L, d
         lq, lk = [transpose_for_scores(lin(x), 4) for lin, x in zip(self.l_linear, (l, l))]
         tq, tk = [transpose_for_scores(lin(x), 4) for lin, x in zip(self.t_linear, (t, t))]
         lq = torch.cat([lq, tq], dim=1)  # 1, 8, L, d

@@ -75,6 +75,6 @@ def rel_attn(q, k, v, lq, lk, rel, mask, bf16=False, schedule="auto"):
     schedule: the backward's "auto" | "in_order" | "concurrent" (CSA_SCHED_*; bitwise-identical results)."""
     H = q.shape[1]
     rel, mask, group = _planes(rel, mask, H)
-    if lq.dim() == 4:
-        lq, lk = lq[0], lk[0]
+    if lq.dim() == 4:  # (1,H,L,d): a view (select's backward would zero-fill a (1,H,L,d) gradient)
+        lq, lk = lq.squeeze(0), lk.squeeze(0)
     return RelAttnFunction.apply(q, k, v, lq, lk, rel, mask, group, bool(bf16), schedule_code(schedule))
