@@ -19,6 +19,29 @@ def test_bias_grad_matches_column_sums(rows, cols):
     assert torch.equal(out, bias_grad(dy.float().cuda())), "deterministic"
 
 
+def test_bias_grad_back_to_back_on_two_streams():
+    """The one-launch path's per-stream arrival counters: many launches of different shapes queued back to
+    back (no synchronisation between them) on the default stream and on a side stream at once, each sum
+    checked. A counter not returned to 0 by its last workgroup would finish a later launch early."""
+    from csa_amd.glue import bias_grad
+    shapes = [(9600, 512), (300, 2048), (9600, 64), (1, 40), (2500, 130), (16384, 96)] * 3
+    g = torch.Generator().manual_seed(11)
+    dys = [torch.randn(r, c, generator=g) for r, c in shapes]
+    side = torch.cuda.Stream()
+    outs = []
+    for i, dy in enumerate(dys):
+        d = dy.cuda()
+        st = side if i % 2 else torch.cuda.current_stream()
+        st.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(st):
+            outs.append(bias_grad(d))
+            d.record_stream(st)
+    torch.cuda.synchronize()
+    for dy, out in zip(dys, outs):
+        ref = dy.double().sum(0)
+        np.testing.assert_allclose(out.cpu().numpy(), ref.numpy(), rtol=1e-4, atol=1e-5 * np.sqrt(dy.shape[0]))
+
+
 def test_glue_linear_matches_nn_linear():
     from csa_amd.glue import Linear
     torch.manual_seed(3)
