@@ -1641,7 +1641,9 @@ struct LgradArgs {
   int64_t ldx; int Lp, L, NP, B, N, H, nsplit;
 };
 // Workgroup = one wave per 32-row l tile (all of L), grid (H, 2 splits-sets): the chunk's X image is shared
-// by the waves (each DMAs some of its eight 1 KiB pieces; a barrier per chunk publishes it).
+// by the waves (each DMAs some of its eight 1 KiB pieces; a barrier per chunk publishes it). One wave per
+// (l tile, head, split) workgroup, each DMAing whole images with no barrier, measured 47 -> 77 us
+// (profiles/r04_ab_lgrad.txt).
 __global__ __launch_bounds__(512) void k_rel_lgrad(const LgradArgs g) {
   constexpr int D = 64, IMG = 32 * D * 4;
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -1662,10 +1664,20 @@ __global__ __launch_bounds__(512) void k_rel_lgrad(const LgradArgs g) {
   __syncthreads();
   // chunk ch: this wave's pieces of rows n0 .. n0 + 31 of batch element b into image buf, and its G runs
   // G[l][x0 + 8 q + 4 h + e] = the A operand of K-step r = 4 q + e (acc perm: x = x0 + crow(r, h))
-  auto issue = [&](int ch, int buf, f32x4 (&a4)[4]) {
+  // piece q (rows 4q .. 4q + 3) of a chunk: the lane's pattern entry q & 3 picked by selects (q is a runtime
+  // value here; dma64's array index would put the pattern in scratch and a scratch load before every piece)
+  auto piece = [&](uint32_t img, __amdgpu_buffer_rsrc_t xr, int n0, int q) {
+    const int m = q & 3;
+    const int pv = m == 0 ? pat.v[0] : m == 1 ? pat.v[1] : m == 2 ? pat.v[2] : pat.v[3];
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, lds_at(img + 1024 * q), 16, pv + (n0 + 4 * q) * ld, 0, 0, 0);
+  };
+  auto issue_x = [&](int ch, int buf) {
     const int b = ch / cpb, n0 = (ch % cpb) * 32;
     const __amdgpu_buffer_rsrc_t xr = make_rsrc(X + b * x_sb, (N - 1) * ld + D * 4);
-    for (int q = lt; q < 8; q += NW) dma64(L0 + IMG * buf, xr, pat, ld, n0, q, q + 1);
+    for (int q = lt; q < 8; q += NW) piece(L0 + IMG * buf, xr, n0, q);
+  };
+  auto issue_g = [&](int ch, f32x4 (&a4)[4]) {
+    const int b = ch / cpb, n0 = (ch % cpb) * 32;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
       a4[q] = *reinterpret_cast<const f32x4*>(arow + (int64_t)b * g.Lp * g.ldx + n0 + 8 * q + 4 * h);
@@ -1674,13 +1686,14 @@ __global__ __launch_bounds__(512) void k_rel_lgrad(const LgradArgs g) {
 #pragma unroll
   for (int t = 0; t < 2; ++t) vb[t] = col_base64(t, c, h);
   f32x16 acc[2] = {zero16(), zero16()};
+#ifdef CSA_EXP_LGRAD_G1  // experiment: the G runs one chunk ahead only (the round-3 form)
   f32x4 a4[4], an[4];
-  if (c0 < c1) issue(c0, 0, a4);
+  if (c0 < c1) { issue_x(c0, 0); issue_g(c0, a4); }
   for (int ch = c0; ch < c1; ++ch) {
     const int cur = (ch - c0) & 1, n0 = (ch % cpb) * 32;
     wait_vm_all();     // this wave's pieces of chunk ch and its G runs have landed
     __syncthreads();   // every wave's pieces landed; every wave read out image cur ^ 1 (chunk ch - 1)
-    if (ch + 1 < c1) issue(ch + 1, cur ^ 1, an);
+    if (ch + 1 < c1) { issue_x(ch + 1, cur ^ 1); issue_g(ch + 1, an); }
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -1691,6 +1704,47 @@ __global__ __launch_bounds__(512) void k_rel_lgrad(const LgradArgs g) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) a4[q] = an[q];
   }
+#else
+  // The G runs (the kernel's HBM stream: 100 MB at B = 64) are loaded two chunks ahead into a ring of three
+  // register buffers (the loop unrolled by three, so no buffer is copied while its loads are in flight), the
+  // X images one chunk ahead. Issue order per chunk: X pieces of chunk ch + 1, then the G runs of ch + 2
+  // (compiler fences keep the order; past the split's last chunk the last chunk's runs are loaded again, so
+  // every chunk issues exactly four G loads), and the vmcnt(4) at the top of the next chunk retires
+  // everything but those last four (vmcnt counts in issue order).
+  f32x4 B0[4], B1[4], B2[4];
+  auto step = [&](int ch, const f32x4 (&use)[4], f32x4 (&nxt)[4]) {
+    const int cur = (ch - c0) & 1, n0 = (ch % cpb) * 32;
+    // vmcnt(4) as the builtin (0x0f74: lgkmcnt / expcnt left open), which the compiler's wait insertion sees:
+    // behind an inline-asm wait it would still count the older loads as pending and wait for them again
+    __builtin_amdgcn_s_waitcnt(0x0f74);
+    __syncthreads();   // every wave's pieces landed; every wave read out image cur ^ 1 (chunk ch - 1)
+    if (ch + 1 < c1) issue_x(ch + 1, cur ^ 1);
+    asm volatile("" ::: "memory");
+    issue_g(imin(ch + 2, c1 - 1), nxt);
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float a = (n0 + crow(r, h) < N) ? use[r >> 2][r & 3] : 0.f;
+        acc[t] = mfma(a, lds_f1(lds, IMG * cur + vb[t] + 256 * crow(r, 0)), acc[t]);
+      }
+  };
+  if (c0 < c1) {
+    issue_x(c0, 0);
+    asm volatile("" ::: "memory");
+    issue_g(c0, B0);
+    issue_g(imin(c0 + 1, c1 - 1), B1);
+    asm volatile("" ::: "memory");
+  }
+  for (int ch = c0; ch < c1; ch += 3) {
+    step(ch, B0, B2);
+    if (ch + 1 >= c1) break;
+    step(ch + 1, B1, B0);
+    if (ch + 2 >= c1) break;
+    step(ch + 2, B2, B1);
+  }
+#endif
   float* out = g.part[which] + ((int64_t)sp * g.H + hd) * g.L * D;
 #pragma unroll
   for (int t = 0; t < 2; ++t)
