@@ -708,22 +708,49 @@ __device__ __forceinline__ void proj_fwd_item(const KArgs& p, const FwdFrags& F,
   next();
   PHF(5)
 #else
-  mlp_fwd<D, FL, BF>(p, F, x, h1, h2, po, row, bh, isK);
+  // d = 96 (java dims, 256 VGPRs): h1 leaves right after layer 1 has consumed it instead of being held to the
+  // item's end with h2 / po / hat (the held h1 spilled 18 VGPRs)
+#ifdef CSA_EXP_H1_LATE
+  constexpr bool H1E = false;
+#else
+  constexpr bool H1E = (D == 96);
+#endif
+  constexpr bool ABF = BF && (D == 64 || D == 96) && KT == 1;  // read back by k_proj_bwd_s<D, true>
+  constexpr int ABLK = (3 * D + 32 * KT) * 32;
+  auto act_blk = [&] { return p.Act + ((int64_t)bh * (p.NQB + p.NKB) + r) * ABLK; };
+  if constexpr (H1E) {
+    mlp_layer0<D, FL, BF>(p, F.W[0], F.b[0], x, h1, row, bh, isK);
+    mlp_layer<D, FL, BF>(F.W[1], F.b[1], h1, h2);
+#ifndef CSA_EXP_NO_ACT
+    if (p.Act) {
+      float* const blk = act_blk();
+      if (ABF && p.kp <= 16) store_act_lds_bf<D / 32>(blk, h1, scr);
+      else store_act_lds<D / 32>(blk, h1, scr);
+    }
+#endif
+    mlp_act<D>(p, h2, 1, row, bh, isK);
+    mlp_layer<D, FL, BF>(F.W[2], F.b[2], h2, po);
+  } else {
+    mlp_fwd<D, FL, BF>(p, F, x, h1, h2, po, row, bh, isK);
+  }
   cluster_hat<D, KT, FL, BF>(p, F.C, po, hat);
   if (isK) small_mm<KT, FL>(F.S, hat, t);
   next();
 #endif
 #ifndef CSA_EXP_NO_ACT
   if (p.Act) {  // save the activations for k_proj_bwd (item r of this (b,h): Q blocks, then K blocks)
+#ifdef CSA_PHASES_FWD
+    constexpr bool H1E = false, ABF = BF && (D == 64 || D == 96) && KT == 1;
     constexpr int ABLK = (3 * D + 32 * KT) * 32;
-    float* blk = p.Act + ((int64_t)bh * (p.NQB + p.NKB) + r) * ABLK;
-    constexpr bool ABF = BF && (D == 64 || D == 96) && KT == 1;  // read back by k_proj_bwd_s<D, true>
+    auto act_blk = [&] { return p.Act + ((int64_t)bh * (p.NQB + p.NKB) + r) * ABLK; };
+#endif
+    float* const blk = act_blk();
     if (ABF && p.kp <= 16) {
-      store_act_lds_bf<D / 32>(blk, h1, scr);
+      if (!H1E) store_act_lds_bf<D / 32>(blk, h1, scr);
       store_act_lds_bf<D / 32>(blk + 32 * D, h2, scr);
       store_act_lds_bf<D / 32>(blk + 64 * D, po, scr);
     } else {
-      store_act_lds<D / 32>(blk, h1, scr);
+      if (!H1E) store_act_lds<D / 32>(blk, h1, scr);
       store_act_lds<D / 32>(blk + 32 * D, h2, scr);
 #ifdef CSA_EXP_RECOMP_PO  // experiment: k_proj_bwd_s<64> recomputes po from h2
       if (!(D == 64 && KT == 1 && p.kp <= 16))
