@@ -1194,9 +1194,10 @@ __device__ __forceinline__ void bins_scatter16(float* bins, int LB, const float 
   }
 }
 
-// acc[t] (rows d = 16 t + 4 g + i, lanes = the bins' rows) += sum_r Lmat[r][d] bins[row][r] (dq_rel = G_c2p LK
-// or dk_rel = G_p2cT LQ). K-step s of lane group g is r = g Q4 + s (Q4 even, 4 Q4 >= L; rows >= L read 0); the
-// Lmat operand comes from L2 with a ring of RING groups of two K-steps in flight.
+// acc[t] (register i of lane group g: d = 16 g + 4 i + t, lanes = the bins' rows) += sum_r Lmat[r][d] bins[row][r]
+// (dq_rel = G_c2p LK or dk_rel = G_p2cT LQ): tile t's MFMA row m is d = 4 m + t, so lane x16's four A operands
+// of a K-step are one dwordx4, Lmat[r][4 x16 .. 4 x16 + 3]. K-step s of lane group g is r = g Q4 + s (Q4 even,
+// 4 Q4 >= L; rows >= L read 0); the Lmat operand comes from L2 with a ring of RING groups of two K-steps in flight.
 __device__ __forceinline__ void bins_times16(f32x4 (&acc)[4], const float* bins, int LB, int Q4,
                                              const float* __restrict__ Lmat, int L) {
   constexpr int D = 64, RING = 8;
@@ -1207,11 +1208,9 @@ __device__ __forceinline__ void bins_times16(f32x4 (&acc)[4], const float* bins,
     for (int e = 0; e < 2; ++e) {
       const int r = g * Q4 + 2 * s2 + e;
       const float* lr = Lmat + (int64_t)(r < L ? r : 0) * D;
+      const f32x4 lv = *reinterpret_cast<const f32x4*>(lr + 4 * x16);
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const float lv = lr[16 * t + x16];
-        v[e][t] = r < L ? lv : 0.f;
-      }
+      for (int t = 0; t < 4; ++t) v[e][t] = r < L ? lv[t] : 0.f;
     }
   };
   auto group = [&](int s2, const float (&v)[2][4]) {
@@ -1351,11 +1350,13 @@ __global__ __launch_bounds__(128, 2) void k_rel_bwd_qh(const RelArgs p) {
           dpacc[st] = mfma16(vv[s4 & 1][st][e], dO[4 * s4 + e], dpacc[st]);
         }
     }
-    float kT[4][8];  // A operands of dq: K[key 16 st + 4 g + i][d = 16 t + x16]
+    float kT[4][8];  // A operands of dq: K[key 16 st + 4 g + i][d = 4 x16 + t], one b128 read per key
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+    for (int e = 0; e < 8; ++e) {
+      const f32x4 kv = lds_f4(lds, img_elem(16 * (e >> 2) + 4 * g + (e & 3), 4 * x16, SW_BOTH));
 #pragma unroll
-      for (int e = 0; e < 8; ++e) kT[t][e] = lds_f1(lds, img_elem(16 * (e >> 2) + 4 * g + (e & 3), 16 * t + x16, SW_BOTH));
+      for (int t = 0; t < 4; ++t) kT[t][e] = kv[t];
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __syncthreads();  // both waves read tile kt out: refill
     if (kt + 1 < p.NKB) {
@@ -1389,9 +1390,9 @@ __global__ __launch_bounds__(128, 2) void k_rel_bwd_qh(const RelArgs p) {
 #endif
   bins_times16(dq, bins, p.LB16, p.Q4, p.lk + (int64_t)hd * p.L * D, p.L);
   if (iv) {
-    float* dst = p.dq + b * p.dq_sb + hd * p.dq_sh + (int64_t)i * p.dq_sn + 4 * g;
+    float* dst = p.dq + b * p.dq_sb + hd * p.dq_sh + (int64_t)i * p.dq_sn + 16 * g;  // d = 16 g + 4 r + t
 #pragma unroll
-    for (int t = 0; t < 4; ++t) *reinterpret_cast<f32x4*>(dst + 16 * t) = dq[t];
+    for (int r = 0; r < 4; ++r) *reinterpret_cast<f32x4*>(dst + 4 * r) = f32x4{dq[0][r], dq[1][r], dq[2][r], dq[3][r]};
     if (g == 0 && !p.qstat_pre) {
       f32x4 st;
       st[0] = rmax; st[1] = rinv; st[2] = delta; st[3] = 0.f;
@@ -1504,15 +1505,14 @@ __global__ __launch_bounds__(128, 2) void k_rel_bwd_kh(const RelArgs p) {
             __builtin_bit_cast(u32x4v_t, f32x4{gv[4 * st], gv[4 * st + 1], gv[4 * st + 2], gv[4 * st + 3]}), gr,
             4 * (yr * 32 + 4 * g + 16 * st), (qb * p.NKB + kbi) * 4096, 2);
     }
-    float xc[4][8], qc[4][8];  // A operands of dv / dk: X[query 16 st + 4 g + i][d = 16 t + x16]
+    float xc[4][8], qc[4][8];  // A operands of dv / dk: X[query 16 st + 4 g + i][d = 4 x16 + t], b128 per query
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+    for (int e = 0; e < 8; ++e) {
+      const int off = img_elem(16 * (e >> 2) + 4 * g + (e & 3), 4 * x16, SW_BOTH);
+      const f32x4 xv = lds_f4(lds, IMG + off), qv4 = lds_f4(lds, off);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int off = img_elem(16 * (e >> 2) + 4 * g + (e & 3), 16 * t + x16, SW_BOTH);
-        xc[t][e] = lds_f1(lds, IMG + off);
-        qc[t][e] = lds_f1(lds, off);
-      }
+      for (int t = 0; t < 4; ++t) { xc[t][e] = xv[t]; qc[t][e] = qv4[t]; }
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __syncthreads();
     if (qb + 1 < p.NQB) {
@@ -1540,12 +1540,12 @@ __global__ __launch_bounds__(128, 2) void k_rel_bwd_kh(const RelArgs p) {
 #endif
   bins_times16(dk, bins, p.LB16, p.Q4, p.lq + (int64_t)hd * p.L * D, p.L);
   if (jv) {
-    float* dkp = p.dk + b * p.dk_sb + hd * p.dk_sh + (int64_t)j * p.dk_sn + 4 * g;
-    float* dvp = p.dv + b * p.dv_sb + hd * p.dv_sh + (int64_t)j * p.dv_sn + 4 * g;
+    float* dkp = p.dk + b * p.dk_sb + hd * p.dk_sh + (int64_t)j * p.dk_sn + 16 * g;  // d = 16 g + 4 r + t
+    float* dvp = p.dv + b * p.dv_sb + hd * p.dv_sh + (int64_t)j * p.dv_sn + 16 * g;
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      *reinterpret_cast<f32x4*>(dkp + 16 * t) = dk[t];
-      *reinterpret_cast<f32x4*>(dvp + 16 * t) = dv[t];
+    for (int r = 0; r < 4; ++r) {
+      *reinterpret_cast<f32x4*>(dkp + 4 * r) = f32x4{dk[0][r], dk[1][r], dk[2][r], dk[3][r]};
+      *reinterpret_cast<f32x4*>(dvp + 4 * r) = f32x4{dv[0][r], dv[1][r], dv[2][r], dv[3][r]};
     }
   }
   bins_store16(p.gp2ct + ((int64_t)hd * p.B + b) * p.Lp * p.ldx, p.ldx, j, bins, p.LB16, p.Q4, p.Lp, jv);
@@ -1598,11 +1598,13 @@ __global__ __launch_bounds__(128, 2) void k_rel_bwd_qg(const RelArgs p) {
     uint32_t col[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) { gv[e] = gn[e]; col[e] = code8(cm, e) & 0xffu; }  // rel[x][y]: the c2p column
-    float kT[4][8];  // A operands of dq: K[key 16 st + 4 g + i][d = 16 t + x16]
+    float kT[4][8];  // A operands of dq: K[key 16 st + 4 g + i][d = 4 x16 + t], one b128 read per key
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+    for (int e = 0; e < 8; ++e) {
+      const f32x4 kv = lds_f4(lds, img_elem(16 * (e >> 2) + 4 * g + (e & 3), 4 * x16, SW_BOTH));
 #pragma unroll
-      for (int e = 0; e < 8; ++e) kT[t][e] = lds_f1(lds, img_elem(16 * (e >> 2) + 4 * g + (e & 3), 16 * t + x16, SW_BOTH));
+      for (int t = 0; t < 4; ++t) kT[t][e] = kv[t];
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __syncthreads();  // both waves read tile kt out: refill
     if (kt + 1 < p.NKB) {
@@ -1618,9 +1620,9 @@ __global__ __launch_bounds__(128, 2) void k_rel_bwd_qg(const RelArgs p) {
   }
   bins_times16(dq, bins, p.LB16, p.Q4, p.lk + (int64_t)hd * p.L * D, p.L);
   if (iv) {
-    float* dst = p.dq + b * p.dq_sb + hd * p.dq_sh + (int64_t)i * p.dq_sn + 4 * g;
+    float* dst = p.dq + b * p.dq_sb + hd * p.dq_sh + (int64_t)i * p.dq_sn + 16 * g;  // d = 16 g + 4 r + t
 #pragma unroll
-    for (int t = 0; t < 4; ++t) *reinterpret_cast<f32x4*>(dst + 16 * t) = dq[t];
+    for (int r = 0; r < 4; ++r) *reinterpret_cast<f32x4*>(dst + 4 * r) = f32x4{dq[0][r], dq[1][r], dq[2][r], dq[3][r]};
   }
   bins_store16(p.gc2p + ((int64_t)hd * p.B + b) * p.Lp * p.ldx, p.ldx, i, bins, p.LB16, p.Q4, p.Lp, iv);
 }
