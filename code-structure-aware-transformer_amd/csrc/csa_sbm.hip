@@ -1785,6 +1785,15 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 8) ? 4 : 2) void k_attn_bwd_
 // ------------------------------------------------------------------------------------
 // B1: per (b,h, key block), S orientation (queries = acc rows, keys = lanes): dK, dV, dT
 // ------------------------------------------------------------------------------------
+// SW_BOTH pair read for the d = 2m + t accumulator mapping (d = 64): columns 2c, 2c + 1 of row crow(r, h), one b64.
+// Address = 256 row + 16 ((c >> 1) ^ swz(row)) + 8 (c & 1); swz(crow(r, h)) = (12h) ^ ((r & 3) | 8 bit2(r)), so the
+// lane part (pair_base64) XORs with a per-register constant, as both_read's does.
+__device__ __forceinline__ int pair_base64(int c, int h) { return 1024 * h + 8 * (c & 1) + 16 * ((c >> 1) ^ (12 * h)); }
+__device__ __forceinline__ float2 pair_read(const float* lds, int base, int r, int off) {
+  const int kr = 16 * ((r & 3) | (8 * ((r >> 2) & 1)));
+  return *reinterpret_cast<const float2*>(reinterpret_cast<const char*>(lds) + off + 256 * crow(r, 0) + (base ^ kr));
+}
+
 template <int D, int KPH, bool DENSE, bool DROP, bool DG, bool BF>
 __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd_kv(const KArgs p) {
 #ifdef CSA_EXP_PRIO  // experiment: half of the waves (by dispatch slot parity) at priority 1
@@ -1796,6 +1805,11 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
   constexpr bool MB4 = !DENSE && KP == 16;  // dT on mfma4b (store_mb4)
   constexpr bool HO = bwd_handoff<BF>();    // ds / G tiles out for k_attn_bwd_qg (else k_attn_bwd_qr recomputes)
   constexpr bool W1 = HO && !DENSE && !DG;  // one-plane w tiles (W_NO_EDGE)
+#ifdef CSA_EXP_KV_SCALAR  // experiment: the 32t + m mapping with scalar column reads
+  constexpr bool PAIR = false;
+#else
+  constexpr bool PAIR = SWZ && !BF;  // dK / dV rows as d = 2m + t (b64 operand reads, pair_read)
+#endif
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const uint32_t L0 = lds_offset(lds), Ql = L0 + SH::KQ, Xl = L0 + SH::KX, Hl = L0 + SH::KH, Sl = L0 + SH::KS;
   const int lane = lane_id(), c = lane & 31, h = lane >> 5;
@@ -1980,6 +1994,17 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
           dv[t] = mfma_bf(pack8(xc), aw8, dv[t]);
           dk[t] = mfma_bf(pack8(qc), ds8, dk[t]);
         }
+      } else if constexpr (PAIR) {  // d = 2m + t: the two tiles' operands of a K-step are one b64 read
+        const int pb = pair_base64(c, h);
+#pragma unroll
+        for (int rr = 0; rr < 8; ++rr) {
+          const float2 xv = pair_read(lds, pb, 8 * half + rr, SH::KX), qv2 = pair_read(lds, pb, 8 * half + rr, SH::KQ);
+          dv[0] = mfma(xv.x, awv[rr], dv[0]);
+          dv[1] = mfma(xv.y, awv[rr], dv[1]);
+          dk[0] = mfma(qv2.x, dsv[rr], dk[0]);
+          dk[1] = mfma(qv2.y, dsv[rr], dk[1]);
+          if ((rr & 1) == 1) __builtin_amdgcn_sched_barrier(0);  // at most two K-steps of operands in flight
+        }
       } else {
 #pragma unroll
         for (int t = 0; t < DT; ++t)
@@ -2030,8 +2055,24 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
       }
     }
   }
-  store_rows<DT>(p.dK + b * p.dk_sb + hd * p.dk_sh + (int64_t)j * p.dk_sn, D, D, dk, jv);
-  store_rows<DT>(p.dV + b * p.dv_sb + hd * p.dv_sh + (int64_t)j * p.dv_sn, D, D, dv, jv);
+  if constexpr (PAIR) {  // d = 2 crow(r, h) + t: registers 4g .. 4g + 3 of both tiles are d = 16g + 8h .. + 7
+    if (jv) {
+      float* dkp = p.dK + b * p.dk_sb + hd * p.dk_sh + (int64_t)j * p.dk_sn + 8 * h;
+      float* dvp = p.dV + b * p.dv_sb + hd * p.dv_sh + (int64_t)j * p.dv_sn + 8 * h;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        *reinterpret_cast<f32x4*>(dkp + 16 * g) = f32x4{dk[0][4 * g], dk[1][4 * g], dk[0][4 * g + 1], dk[1][4 * g + 1]};
+        *reinterpret_cast<f32x4*>(dkp + 16 * g + 4) =
+            f32x4{dk[0][4 * g + 2], dk[1][4 * g + 2], dk[0][4 * g + 3], dk[1][4 * g + 3]};
+        *reinterpret_cast<f32x4*>(dvp + 16 * g) = f32x4{dv[0][4 * g], dv[1][4 * g], dv[0][4 * g + 1], dv[1][4 * g + 1]};
+        *reinterpret_cast<f32x4*>(dvp + 16 * g + 4) =
+            f32x4{dv[0][4 * g + 2], dv[1][4 * g + 2], dv[0][4 * g + 3], dv[1][4 * g + 3]};
+      }
+    }
+  } else {
+    store_rows<DT>(p.dK + b * p.dk_sb + hd * p.dk_sh + (int64_t)j * p.dk_sn, D, D, dk, jv);
+    store_rows<DT>(p.dV + b * p.dv_sb + hd * p.dv_sh + (int64_t)j * p.dv_sn, D, D, dv, jv);
+  }
   if constexpr (MB4) store_mb4(p.dT + ((int64_t)bh * p.M + kbi * 32) * p.kp, p.M - kbi * 32, p.kp, dtt[0]);
   else if constexpr (!DENSE) store_rows<KTA>(p.dT + ((int64_t)bh * p.M + j) * p.kp, p.kp, p.kp, dtt, jv);
 }
