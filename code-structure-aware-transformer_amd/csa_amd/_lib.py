@@ -12,9 +12,10 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CSA_HIP_LIB", os.path.join(_HERE, "lib", "libcsa_hip.so"))
 
-CSA_ABI_VERSION = 7
+CSA_ABI_VERSION = 8
 CSA_FLAG_DENSE = 1
 CSA_FLAG_FWD_ONLY = 2
+CSA_FLAG_BF16_WS = 4  # ABI v8: bf16-mode backward workspace (no fp32 tile handoff)
 CSA_SCHED_AUTO, CSA_SCHED_IN_ORDER, CSA_SCHED_CONCURRENT = 0, 1, 2
 SCHEDULES = {"auto": CSA_SCHED_AUTO, "in_order": CSA_SCHED_IN_ORDER, "concurrent": CSA_SCHED_CONCURRENT}
 CSA_DTYPE_F32, CSA_DTYPE_BF16 = 0, 1

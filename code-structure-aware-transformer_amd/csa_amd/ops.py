@@ -190,13 +190,14 @@ class SBMAttentionFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, Q, K, V, mask, cluster_w, w0, b0, w1, b1, w2, b2, uniforms, k, attn_p, proj_p, dense,
-                want_maps, bf16=False, schedule=0):
+                want_maps, bf16=False, schedule=0, fwd_only=False):
         shim()
         seed = _draw_seed()
         pw = [] if dense else [w0, w1, w2]
         pb = [] if dense else [b0, b1, b2]
-        # no input needs a gradient (eval / no_grad): the forward skips the activations only the backward reads
-        fwd_only = not any(ctx.needs_input_grad)
+        # fwd_only (decided by the caller before apply: grad mode is always off in here): no backward will run
+        # (eval under no_grad / inference_mode, or nothing requires grad), so the forward skips the activations
+        # only the backward reads
         X, sp, state = torch.ops.csa.sbm_fwd(Q, K, V, mask, None if dense else cluster_w, pw, pb, uniforms, k, seed, 0,
                                             attn_p, proj_p, dense, bf16, fwd_only)
         graph = attn = None
@@ -225,9 +226,15 @@ class SBMAttentionFunction(torch.autograd.Function):
         else:
             dQ, dK, dV = g[:3]
         if dense:
-            return (dQ, dK, dV) + (None,) * 16
+            return (dQ, dK, dV) + (None,) * 17
         dC, dw0, db0, dw1, db1, dw2, db2 = g[3:]
-        return dQ, dK, dV, None, dC, dw0, db0, dw1, db1, dw2, db2, None, None, None, None, None, None, None, None
+        return dQ, dK, dV, None, dC, dw0, db0, dw1, db1, dw2, db2, None, None, None, None, None, None, None, None, None
+
+
+def _fwd_only(*inputs):
+    """True when no backward can run through this call: grad mode off (no_grad / inference_mode) or no
+    input requiring grad. Evaluated before Function.apply, where grad mode is still the caller's."""
+    return not (torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in inputs))
 
 
 def sbm_attention(Q, K, V, mask, cluster_w, proj, k, uniforms=None, attn_p=0.0, proj_p=0.0, want_maps=True,
@@ -239,15 +246,17 @@ def sbm_attention(Q, K, V, mask, cluster_w, proj, k, uniforms=None, attn_p=0.0, 
     bf16: bf16-MFMA attention contractions (the maps, if requested, are still computed in fp32).
     schedule: the backward's "auto" | "in_order" | "concurrent" (CSA_SCHED_*; bitwise-identical results)."""
     w0, b0, w1, b1, w2, b2 = proj
+    fwd_only = _fwd_only(Q, K, V, cluster_w, w0, b0, w1, b1, w2, b2)
     return SBMAttentionFunction.apply(Q, K, V, mask, cluster_w, w0, b0, w1, b1, w2, b2, uniforms, int(k),
                                       float(attn_p), float(proj_p), False, bool(want_maps), bool(bf16),
-                                      schedule_code(schedule))
+                                      schedule_code(schedule), fwd_only)
 
 
 def dense_attention(Q, K, V, mask, attn_p=0.0, want_maps=True, bf16=False, schedule="auto"):
     """Fused FullAttention.forward (module/sbm_attn.py:77-87) -> (X, None, graph(unused), attn)."""
     return SBMAttentionFunction.apply(Q, K, V, mask, None, None, None, None, None, None, None, None, 0,
-                                      float(attn_p), 0.0, True, bool(want_maps), bool(bf16), schedule_code(schedule))
+                                      float(attn_p), 0.0, True, bool(want_maps), bool(bf16), schedule_code(schedule),
+                                      _fwd_only(Q, K, V))
 
 
 class _STEFunction(torch.autograd.Function):

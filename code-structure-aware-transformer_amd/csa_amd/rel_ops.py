@@ -72,7 +72,8 @@ def rel_attn(q, k, v, lq, lk, rel, mask, bf16=False, schedule="auto"):
 
     q,k,v (B,H,N,d) (strided views fine); lq,lk (1,H,L,d) or (H,L,d); rel/mask (B,H,N,N) (reference
     int64/bool layout) or (B,2,N,N) uint8 planes shared by head halves (compact CSE layout).
-    schedule: the backward's "auto" | "in_order" | "concurrent" (CSA_SCHED_*; bitwise-identical results)."""
+    schedule: the backward's "auto" | "in_order" | "concurrent" (CSA_SCHED_*; bitwise-identical results). Only
+    bf16 mode forks: the fp32 fused backward hands its key half's g tiles to the query half and runs in order."""
     H = q.shape[1]
     rel, mask, group = _planes(rel, mask, H)
     if lq.dim() == 4:  # (1,H,L,d): a view (select's backward would zero-fill a (1,H,L,d) gradient)

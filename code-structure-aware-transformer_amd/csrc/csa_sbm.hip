@@ -18,9 +18,12 @@
 //        k_reduce_slabs      fixed-order slab reduction
 //        k_cluster_grad      softmax_{k^2} backward -> dC
 // The N x N intermediates of the reference (expA, graph, dot, softmax, attn: ~11 fp32
-// (B,H,N,M) tensors) are never materialised: the sampled graph and the dropout keep-mask
-// are kept as 1 bit per edge for the backward, and the optional attn/graph maps are
-// produced by k_maps only when the caller asks for them.
+// (B,H,N,M) tensors) are never materialised in the forward: the sampled graph and the dropout
+// keep-mask are kept as 1 bit per edge for the backward, and the optional attn/graph maps are
+// produced by k_maps only when the caller asks for them. The fp32 backward hands one (with
+// clusters at most two) fp32 value per element from k_attn_bwd_kv to k_attn_bwd_qg through the
+// workspace (Layout::w_dsg, O(B*H*N*M)); bf16 mode recomputes instead and sizes it away
+// (CSA_FLAG_BF16_WS).
 #include "csa_common.hpp"
 #include "../../include/csa_hip.h"
 
@@ -157,7 +160,7 @@ Layout make_layout(int64_t B, int64_t H, int64_t N, int64_t M, int64_t D, int64_
   // ds and G (STE gradient) tiles handed from k_attn_bwd_kv to k_attn_bwd_qg: (b,h, query block, key block)
   // 32 x 32 fp32 tiles [key][query]; G only with clusters
   L.w_dsg_plane = B * H * L.NQB * L.NKB * 1024;
-  L.w_dsg = take(sizeof(float) * L.w_dsg_plane * (dense ? 1 : 2));
+  L.w_dsg = take(sizeof(float) * ((flags & CSA_FLAG_BF16_WS) ? 0 : L.w_dsg_plane * (dense ? 1 : 2)));
   // per query row (NQB * 32 rows per (b,h), padded rows included) the constants of k_attn_bwd_kv's elementwise
   // backward, written by k_attn_rowprep
   L.w_brow = take(sizeof(float) * B * H * L.NQB * 32 * 4);
@@ -3521,7 +3524,11 @@ csa_status csa_sbm_bwd(const csa_sbm_bwd_args* b, void* stream) {
     return fail(CSA_INVALID_ARG, "null parameter-gradient output");
   if (b->schedule > CSA_SCHED_CONCURRENT) return fail(CSA_INVALID_ARG, "schedule must be a CSA_SCHED_* value");
   if (a->flags & CSA_FLAG_FWD_ONLY) return fail(CSA_INVALID_ARG, "the forward ran with CSA_FLAG_FWD_ONLY: no backward state");
-  const Layout L = make_layout(a->B, a->H, a->N, a->M, a->d, a->k, a->flags);
+  if ((a->flags & CSA_FLAG_BF16_WS) && a->dtype != CSA_DTYPE_BF16)
+    return fail(CSA_INVALID_ARG, "CSA_FLAG_BF16_WS sizes the workspace of a CSA_DTYPE_BF16 call only");
+  // bf16 mode recomputes on the query side (bwd_handoff<true>() == false): no handoff tiles in its workspace
+  const Layout L = make_layout(a->B, a->H, a->N, a->M, a->d, a->k,
+                               a->flags | ((a->dtype == CSA_DTYPE_BF16 && !bwd_handoff<true>()) ? CSA_FLAG_BF16_WS : 0u));
   hipStream_t st = (hipStream_t)stream;
   const DeviceGuard guard(st);
   if (a->d == 64) {

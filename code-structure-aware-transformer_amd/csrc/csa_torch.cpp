@@ -227,7 +227,8 @@ std::vector<Tensor> sbm_bwd(const Tensor& Q, const Tensor& K, const Tensor& V, c
   b.dk_sb = dK.stride(0); b.dk_sh = dK.stride(1); b.dk_sn = dK.stride(2);
   b.dv_sb = dV.stride(0); b.dv_sh = dV.stride(1); b.dv_sn = dV.stride(2);
   Tensor ws, da, dsp, dg;
-  ws = at::empty({(int64_t)csa_sbm_bwd_workspace_bytes(B, H, N, M, d, k, flags)}, o.dtype(at::kByte));
+  ws = at::empty({(int64_t)csa_sbm_bwd_workspace_bytes(B, H, N, M, d, k, flags | (a.dtype == CSA_DTYPE_BF16 ? CSA_FLAG_BF16_WS : 0u))},
+                 o.dtype(at::kByte));
   b.workspace = ws.data_ptr();
   if (dattn) { da = f32c(*dattn); b.dattn = fp(da); }
   if (!dense) {

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define CSA_ABI_VERSION 7
+#define CSA_ABI_VERSION 8
 
 typedef enum csa_status {
   CSA_OK = 0,
@@ -58,6 +58,12 @@ typedef enum csa_status {
  * projection MLP's saved activations, which only the backward reads (csa_sbm_state_bytes shrinks, the forward
  * skips their stores); csa_sbm_bwd rejects such a state. */
 #define CSA_FLAG_FWD_ONLY 2u
+/* ABI v8: the call pair runs with dtype CSA_DTYPE_BF16. csa_sbm_bwd_workspace_bytes then omits the fp32 backward's
+ * ds / G tile handoff (bf16 mode recomputes S and dP on the query side instead), which is O(B*H*N*M) floats: with
+ * clusters two (B,H,NQB,NKB,32,32) fp32 planes (at B=16, H=8, N=M=1024: 1.07 GB), without (DENSE) one plane.
+ * csa_sbm_bwd lays a bf16 call's workspace out without the handoff whether or not the flag is set (a buffer sized
+ * without it is merely larger); the flag on an fp32 call is CSA_INVALID_ARG. csa_sbm_state_bytes ignores it. */
+#define CSA_FLAG_BF16_WS 4u
 
 /* ABI v5: schedule of an attention backward's two halves (csa_rel_attn_bwd_args .schedule). The key half
  * may run on a caller-owned side stream beside the query half, forked from and joined back into `stream`
@@ -201,7 +207,9 @@ typedef struct csa_rel_attn_bwd_args {
   void* workspace;
   /* ABI v3: element strides (b, h, row); a zero triple = contiguous; non-contiguous needs d = 64 */
   int64_t do_sb, do_sh, do_sn, dq_sb, dq_sh, dq_sn, dk_sb, dk_sh, dk_sn, dv_sb, dv_sh, dv_sn;
-  /* ABI v5: schedule and side lane as in csa_sbm_bwd_args; only the d_k = 64 fused path uses them */
+  /* ABI v5: schedule and side lane as in csa_sbm_bwd_args; only the d_k = 64 fused path uses them, and of it
+   * only bf16 mode (CSA_DTYPE_BF16): the fp32 fused backward hands the key half's g tiles to the query half
+   * (k_rel_bwd_kh -> k_rel_bwd_qg) and runs in order whatever the schedule */
   uint32_t schedule;
   void* side_stream; void* side_fork; void* side_join;
 } csa_rel_attn_bwd_args;

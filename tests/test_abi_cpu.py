@@ -56,6 +56,15 @@ def test_state_and_workspace_sizes_monotone():
     # the backward workspace holds the ds / G tiles (dense: ds only) and the per-row constants
     dense = _lib.CSA_FLAG_DENSE
     assert L.csa_sbm_bwd_workspace_bytes(4, 8, 150, 150, 64, 0, dense) >= 4 * 8 * 25 * 1024 * 4 + 4 * 8 * 160 * 16
+    # ABI v8: a bf16-mode backward recomputes on the query side: its workspace has no fp32 tile handoff (two
+    # (B,H,NQB,NKB,32,32) planes with clusters, one without); the state is unaffected
+    bf = _lib.CSA_FLAG_BF16_WS
+    for (n, k, fl, planes) in ((1024, 16, 0, 2), (150, 10, 0, 2), (150, 0, dense, 1)):
+        full = L.csa_sbm_bwd_workspace_bytes(2, 8, n, n, 64, k, fl)
+        slim = L.csa_sbm_bwd_workspace_bytes(2, 8, n, n, 64, k, fl | bf)
+        nb = (n + 31) // 32
+        assert full - slim == planes * 2 * 8 * nb * nb * 1024 * 4
+        assert L.csa_sbm_state_bytes(2, 8, n, n, 64, k, fl | bf) == L.csa_sbm_state_bytes(2, 8, n, n, 64, k, fl)
 
 
 def test_invalid_args_rejected_without_gpu():

@@ -84,21 +84,40 @@ def test_rel_attn_production_head_size_matches_reference(golden, layout):
         np.testing.assert_allclose(x.grad.cpu().numpy(), z[n], rtol=RTOL, atol=ATOL, err_msg=n)
 
 
-def _run_rel(q, k, v, lq, lk, rel, mask, dO, schedule="auto"):
+def _run_rel(q, k, v, lq, lk, rel, mask, dO, schedule="auto", bf16=False):
     from csa_amd import rel_ops
     t = [x.cuda().requires_grad_(True) for x in (q, k, v, lq, lk)]
-    o = rel_ops.rel_attn(*t, rel.cuda(), mask.cuda(), schedule=schedule)
+    o = rel_ops.rel_attn(*t, rel.cuda(), mask.cuda(), schedule=schedule, bf16=bf16)
     (o * dO.cuda()).sum().backward()
     torch.cuda.synchronize()
     return [o.detach().cpu()] + [x.grad.cpu() for x in t]
 
 
 @pytest.mark.skipif(not has_gpu(), reason="needs GPU")
+def test_rel_attn_bf16_concurrent_schedule_bit_identical():
+    """bf16 mode keeps the forking backward (k_rel_qstat + the key-side kernel on the caller's side stream beside
+    the query-side one): "concurrent" and "in_order" give bitwise-identical outputs and gradients."""
+    from csa_amd.data import synthetic_batch
+    B, H, N, dk, L = 64, 8, 150, 64, 150
+    sb = synthetic_batch(B, max_size=N, seed=6, min_nodes=60, max_nodes=N)
+    g = torch.Generator().manual_seed(10)
+    q, k, v, dO = (torch.randn(B, H, N, dk, generator=g) for _ in range(4))
+    lq, lk = (torch.randn(1, H, L, dk, generator=g) for _ in range(2))
+    rel = torch.from_numpy(np.stack([sb["L"], sb["T"]], 1).astype(np.uint8))
+    mask = torch.from_numpy(np.stack([sb["L_mask"], sb["T_mask"]], 1).astype(np.uint8))
+    r1 = _run_rel(q, k, v, lq, lk, rel, mask, dO, schedule="in_order", bf16=True)
+    r2 = _run_rel(q, k, v, lq, lk, rel, mask, dO, schedule="concurrent", bf16=True)
+    for a, b in zip(r1, r2):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.skipif(not has_gpu(), reason="needs GPU")
 def test_rel_attn_full_size_rows_match_oracle_and_deterministic():
     """The java train step's CSE shape (B=64 per GPU, H=8, N=L=150, d_k=64) in the compact layout:
-    two runs are bitwise identical (the first with the backward halves in order, the second with
-    the key-side kernel beside the query-side one on the caller's side stream: schedule "in_order" /
-    "concurrent"); out/dq/dk/dv of sampled batch rows match the fp64 oracle run on
+    two runs are bitwise identical (fp32 takes the g-tile handoff, which runs its key and query halves in order
+    whatever the schedule, so "in_order" vs "concurrent" here is a run-to-run determinism check; the forking
+    path is compared in test_rel_attn_bf16_concurrent_schedule_bit_identical); out/dq/dk/dv of sampled batch rows
+    match the fp64 oracle run on
     those rows alone (each row depends only on its AST); dlq/dlk (sums over the whole batch) match
     the fp64 oracle over all 64 rows."""
     from csa_amd.data import synthetic_batch

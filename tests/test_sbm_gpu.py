@@ -284,7 +284,8 @@ def _run_module(Q, K, V, mask, u, dX, dsp, params, k, training=False):
 
 @pytest.mark.skipif(not has_gpu(), reason="needs GPU")
 @pytest.mark.parametrize("shape", [(2, 2, 45, 64, 5), (2, 2, 200, 64, 64), (1, 2, 70, 64, 128), (1, 3, 150, 96, 20),
-                                   (1, 2, 33, 64, 32), (1, 1, 1024, 64, 16), (1, 1, 1024, 64, 128)])
+                                   (1, 2, 33, 64, 32), (1, 1, 1024, 64, 16), (1, 1, 1024, 64, 32),
+                                   (1, 1, 1024, 64, 64), (1, 1, 1024, 64, 128)])
 def test_sbm_shapes_vs_oracle(shape):
     """Shapes beyond the golden set (small k, k up to 128 = config-5 sweep, N > 150 up to the
     config-5 long-AST N = 1024) vs the pinned oracle."""
@@ -350,10 +351,13 @@ def test_sbm_full_size_rows_match_oracle_and_deterministic():
 
 @pytest.mark.skipif(not has_gpu(), reason="needs GPU")
 @pytest.mark.parametrize("shape", [(64, 8, 150, 64, 10), (8, 8, 150, 96, 10)])
-def test_concurrent_backward_schedule_bit_identical(shape):
-    """bwd_q beside (k_attn_gamma + bwd_kv) on the caller's side stream vs the in-order schedule
-    (CSA_SCHED_CONCURRENT / CSA_SCHED_IN_ORDER): gamma is recomputed in bwd_q's summation order, so every output and
-    gradient is bitwise identical -- train mode with dropout, padded keys, and an upstream dattn."""
+@pytest.mark.parametrize("with_dattn", [False, True])
+def test_concurrent_backward_schedule_bit_identical(shape, with_dattn):
+    """CSA_SCHED_CONCURRENT vs CSA_SCHED_IN_ORDER: the projection backward's key-block items (k_proj_bwd_s kind 1)
+    on the caller's side stream beside k_attn_bwd_qg, its query-block items (kind 2) after it, against both kinds
+    in ONE in-order launch (kind 3). Every workgroup gets the same items and slab either way, so every output and
+    gradient is bitwise identical -- train mode with dropout and padded keys; without an upstream dattn (the
+    training path: one-plane W_NO_EDGE handoff) and with one (the two-plane ds | G handoff)."""
     B, H, N, d, k = shape
     Q, K, V, mask, _, dX, dsp, params = _rand_case(B, H, N, d, k, seed=41 + d)
     cw = params["layer.weight"].cuda()
@@ -361,7 +365,7 @@ def test_concurrent_backward_schedule_bit_identical(shape):
     pb = [params[f"proj.{i}.bias"].cuda() for i in (0, 3, 6)]
     q, kk, v, mk = Q.cuda(), K.cuda(), V.cuda(), mask.cuda()
     gen = torch.Generator().manual_seed(3)
-    dattn = torch.randn(B, H, N, N, generator=gen).cuda()
+    dattn = torch.randn(B, H, N, N, generator=gen).cuda() if with_dattn else None
     seed, offset = 0x5EED, 9
     X, sp, state = torch.ops.csa.sbm_fwd(q, kk, v, mk, cw, pw, pb, None, k, seed, offset, 0.2, 0.1, False)
     outs = []
@@ -373,6 +377,29 @@ def test_concurrent_backward_schedule_bit_identical(shape):
     assert len(outs[0]) == len(outs[1]) > 0
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.skipif(not has_gpu(), reason="needs GPU")
+def test_forward_only_state_under_no_grad_gives_the_same_outputs():
+    """Under torch.no_grad() / inference_mode the module's parameters still require grad, but no backward can
+    run: the forward takes CSA_FLAG_FWD_ONLY (no saved MLP activations) and must return exactly the outputs of the
+    grad-enabled forward."""
+    from csa_amd import ops
+    B, H, N, d, k = 4, 8, 150, 64, 10
+    Q, K, V, mask, u, _, _, params = _rand_case(B, H, N, d, k, seed=19)
+    cw = params["layer.weight"].cuda().requires_grad_()
+    proj = []
+    for i in (0, 3, 6):
+        proj += [params[f"proj.{i}.weight"].cuda().requires_grad_(), params[f"proj.{i}.bias"].cuda().requires_grad_()]
+    q, kk, v, mk, uu = (t.cuda() for t in (Q, K, V, mask, u))
+    assert not ops._fwd_only(q, cw) and ops._fwd_only(q.detach())
+    ref = ops.sbm_attention(q, kk, v, mk, cw, proj, k, uniforms=uu)
+    for ctx in (torch.no_grad, torch.inference_mode):
+        with ctx():
+            assert ops._fwd_only(q, cw, *proj)
+            got = ops.sbm_attention(q, kk, v, mk, cw, proj, k, uniforms=uu)
+        for a, b in zip(ref, got):
+            assert torch.equal(a.detach(), b)
 
 
 @pytest.mark.skipif(not has_gpu(), reason="needs GPU")
