@@ -966,7 +966,7 @@ struct AttnFwdLds {
   static constexpr int T_BYTES = 32 * KP * 4;
   static constexpr int KOFF = 0, VOFF = KV_BYTES, TOFF = 2 * KV_BYTES, BOFF = TOFF + T_BYTES;
   // K image | V image | T image | key bias row (Mpad floats: 0 = valid key, -inf = padded / beyond M)
-  static size_t bytes(int Mpad) { return (size_t)BOFF + 4 * (size_t)Mpad; }
+  __host__ __device__ static size_t bytes(int Mpad) { return (size_t)BOFF + 4 * (size_t)Mpad; }
 };
 
 // Key bias row (0 for a valid unmasked key, -inf otherwise: sbm_attn.py:61 masked_fill) in two halves so the
@@ -997,24 +997,43 @@ __device__ __forceinline__ void key_bias_store(float* bias, const KArgs& p, int 
   }
 }
 
+// Key mask of batch b into registers without a value select (a select right after a load would make the
+// compiler wait for it there): clamped addresses, validity applied when the bias row is written.
+__device__ __forceinline__ KeyMask key_mask_load_raw(const KArgs& p, int b) {
+  KeyMask km;
+#pragma unroll
+  for (int u = 0; u < KB_UNROLL; ++u) km.v[u] = 0.f;
+  if (p.mask) {
+    const float* mk = p.mask + b * p.mask_sb;
+#pragma unroll
+    for (int u = 0; u < KB_UNROLL; ++u) km.v[u] = mk[imin(lane_id() + 64 * u, p.M - 1)];
+  }
+  return km;
+}
+
+#ifdef CSA_EXP_FWD_STAMPS  // experiment: per-phase s_memtime totals of k_attn_fwd, printed for sampled waves
+#define FST_DECL unsigned long long fst_t = 0, fst[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; FST_NOW(fst_t);
+#define FST_NOW(v) { __builtin_amdgcn_sched_barrier(0); asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) :: "memory"); __builtin_amdgcn_sched_barrier(0); }
+#define FST(i) { unsigned long long t_; FST_NOW(t_); fst[i] += t_ - fst_t; fst_t = t_; }
+#else
+#define FST_DECL
+#define FST(i)
+#endif
 // DROP: attention dropout on (keep <=> 16-bit uniform >= drop_thr). HAS_U: STE uniforms supplied by
 // the caller (bit-exact parity path, fp32 compare as torch.bernoulli); otherwise 16-bit Philox
 // uniforms u16 / 65536 (STE.py:13 draws u < p with p = clamp(expA, .01, .99)).
+// One (b, h, 32-query block) item of the forward on the wave's LDS images at lds (zero_images: first use of the
+// images; later items find rows past M holding earlier items' finite data, which their -inf key bias masks).
 template <int D, int KPH, bool DENSE, bool HAS_U, bool DROP, bool BF>
-__global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd(const KArgs p) {
-#ifdef CSA_EXP_PRIO  // experiment: half of the waves (by dispatch slot parity) at priority 1
-  if ((blockIdx.x >> 3) & 1) __builtin_amdgcn_s_setprio(1);
-#endif
+__device__ __forceinline__ void attn_fwd_item(const KArgs& p, float* __restrict__ lds, int bh, int qb, bool zero_images) {
+  FST_DECL
   using LY = AttnFwdLds<D, KPH>;
   constexpr int DT = D / 32, NS = D / 2, DP = LY::DP, KP = LY::KP;
   constexpr bool SWZ = LY::SWZ;
   constexpr int KPN = KP > 0 ? KP : 16;  // T image width (unused when DENSE)
-  extern __shared__ __attribute__((aligned(16))) float lds[];
   const uint32_t Kl = lds_offset(lds), Vl = Kl + LY::VOFF, Tl = Kl + LY::TOFF;
   const int lane = lane_id(), c = lane & 31, h = lane >> 5;
-  const BhBlock xb = xcd_block(p.NQB, p.B * p.H);
-  if (!xb.valid) return;
-  const int qb = xb.blk, bh = xb.bh, b = bh / p.H, hd = bh % p.H;
+  const int b = bh / p.H, hd = bh % p.H;
   const int i = qb * 32 + c;
   const bool iv = i < p.N;
   const int ic = imin(i, p.N - 1);
@@ -1023,8 +1042,10 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd
   const __amdgpu_buffer_rsrc_t kr = make_rsrc(p.K + b * p.k_sb + hd * p.k_sh, SWZ ? (p.M - 1) * kld + D * 4 : 0x7fffffff);
   const __amdgpu_buffer_rsrc_t vr = make_rsrc(p.V + b * p.v_sb + hd * p.v_sh, SWZ ? (p.M - 1) * vld + D * 4 : 0x7fffffff);
   const __amdgpu_buffer_rsrc_t tr = make_rsrc(DENSE ? p.K : p.T + (int64_t)bh * p.M * p.kp, p.M * p.kp * 4);
-  if constexpr (SWZ) lds_zero<(2 * LY::KV_BYTES + LY::T_BYTES) / 4>(lds);
-  else if constexpr (!DENSE) lds_zero<LY::T_BYTES / 4>(lds + LY::TOFF / 4);
+  if (zero_images) {
+    if constexpr (SWZ) lds_zero<(2 * LY::KV_BYTES + LY::T_BYTES) / 4>(lds);
+    else if constexpr (!DENSE) lds_zero<LY::T_BYTES / 4>(lds + LY::TOFF / 4);
+  }
   const DmaPat kpat = dma_pat(SW_ROW, kld), vpat = dma_pat(SW_COL, vld);
 #define CSA_ISSUE_FWD(row0)                                   \
   do {                                                        \
@@ -1037,18 +1058,19 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd
     }                                                         \
     if constexpr (!DENSE) dma_narrow(Tl, tr, (row0), KPN); \
   } while (0)
-  // prologue loads in need order (vmcnt retires in issue order): key mask, query operands, tile 0
-  const KeyMask km = key_mask_load(p, b);
-  float q[NS];
-  load_run<NS>(q, p.Q + b * p.q_sb + hd * p.q_sh + (int64_t)ic * p.q_sn + h * NS, iv);
-  float qh[KPH > 0 ? KPH : 1];
-  if constexpr (!DENSE) load_run<KPH>(qh, p.Qh + ((int64_t)bh * p.N + ic) * p.kp + h * KPH, iv);
-  // Philox STE compares u16 < 65536 p: E is computed 65536x scaled (qh scaled by a power of two, exact)
-  constexpr float ESC = HAS_U ? 1.f : 65536.f;
-  if constexpr (!DENSE && !HAS_U)
-#pragma unroll
-    for (int e = 0; e < KPH; ++e) qh[e] *= ESC;
+  // Prologue: nothing waits on a load before the first tile (s_memtime stamps, profiles/r05_stamps.txt: a prologue
+  // that scaled qh and selected the query rows right after their loads waited out one memory latency before
+  // issuing tile 0's DMA and another at the first tile, 19% of a wave's life). Issue order (vmcnt retires in
+  // issue order): the key mask, whose bias row is written as soon as it lands while the rest is in flight; tile 0's
+  // images; the query operands. Query rows past N read row N-1 (finite; their results are never stored).
+  const KeyMask km = key_mask_load_raw(p, b);
   CSA_ISSUE_FWD(0);
+  float q[NS];
+  load_run<NS>(q, p.Q + b * p.q_sb + hd * p.q_sh + (int64_t)ic * p.q_sn + h * NS, true);
+  float qh[KPH > 0 ? KPH : 1];
+  if constexpr (!DENSE) load_run<KPH>(qh, p.Qh + ((int64_t)bh * p.N + ic) * p.kp + h * KPH, true);
+  // Philox STE compares u16 < 65536 p: E is computed 65536x scaled (qh scaled by a power of two, exact, at tile 0)
+  constexpr float ESC = HAS_U ? 1.f : 65536.f;
   key_bias_store(lds + LY::BOFF / 4, p, b, km);
   const int kbase = SWZ ? row_base64(c, h) : 4 * (c * DP + NS * h);
   const int tbase = DENSE ? 0 : LY::TOFF + narrow_base<KPN>(c, (KPH / 4) * h);
@@ -1061,10 +1083,15 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd
 #pragma unroll
   for (int t = 0; t < DT; ++t) o[t] = zero16();
   uint32_t cntl = 0;
-
+  FST(0)
   for (int kt = 0; kt < p.NKB; ++kt) {
     const int j0 = kt * 32;
-    wait_vm_all();  // tile kt's K/V/T images have landed
+    wait_vm_all();  // tile kt's K/V/T images (at kt = 0 also the query operands) have landed
+    if constexpr (!DENSE && !HAS_U)
+      if (kt == 0)
+#pragma unroll
+        for (int e = 0; e < KPH; ++e) qh[e] *= ESC;
+    FST(1)
     // the tile's Philox words depend only on (query, tile, head): computed first, so their VALU work can
     // interleave with the S / expA MFMA chains below instead of waiting behind them
     u32x4 r_ste[2], r_drop[2];
@@ -1093,6 +1120,7 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd
       }
 #endif
     }
+    FST(2)
     // S^T = K Q^T : A operand = K rows from the image (row c, lin-perm chunks of half h)
     f32x16 sacc = zero16();
     if constexpr (BF) {
@@ -1110,6 +1138,7 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd
         for (int e = 0; e < 4; ++e) sacc = mfma(kv[e], q[4 * j + e], sacc);
       }
     }
+    FST(3)
     f32x16 eacc;
     if constexpr (!DENSE) {  // expA^T = T Qh^T (sbm_attn.py:55)
       eacc = zero16();
@@ -1120,6 +1149,7 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd
         for (int e = 0; e < 4; ++e) eacc = mfma(tv[e], qh[4 * j + e], eacc);
       }
     }
+    FST(4)
     // V^T operand values for this tile's PV: lane (d = 32t + c) reads V[key crow(r,h)][d]
     float vt[DT][16];
 #pragma unroll
@@ -1131,7 +1161,12 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd
     for (int g = 0; g < 4; ++g) bz[g] = lds_f4(lds, LY::BOFF + 4 * (j0 + 8 * g + 4 * h));
     // all of tile kt is in registers: start tile kt+1's DMA (overlaps the softmax and PV below)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    FST(5)
+#if defined(CSA_EXP_FWD_NO_LOOPDMA) || defined(CSA_EXP_FWD_MFMA_ONLY)  // experiment: tile 0's images reused (wrong)
+    if (false)
+#endif
     if (kt + 1 < p.NKB) CSA_ISSUE_FWD(j0 + 32);
+    FST(6)
     float s[16];
     float tmax = NEG_INF;
 #pragma unroll
@@ -1172,7 +1207,11 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd
       }
     }
     // bit-pack the sampled graph / dropout keep mask: word [qb][key] holds 32 query bits (lanes 0..31)
+#if defined(CSA_EXP_FWD_NO_PACK) || defined(CSA_EXP_FWD_NO_ELEM) || defined(CSA_EXP_FWD_MFMA_ONLY)
+    if constexpr (false) {  // experiment: no bit packing / bit stores (wrong backward)
+#else
     if constexpr (!DENSE || DROP) {
+#endif
       const uint32_t myA = DENSE ? 0u : pack_bits(av);
       const uint32_t myR = DROP ? pack_bits(keep) : 0u;
       const int64_t widx = ((int64_t)bh * p.NQB + qb) * p.Mpad + j0 + c;
@@ -1182,7 +1221,16 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd
       }
       if constexpr (DROP) if (h == 0) p.Rbits[widx] = myR;
     }
+    FST(7)
     // online softmax update (exp(-inf - m) = 0 covers masked keys; m_use keeps an all-masked prefix finite)
+    float w[16];
+#if defined(CSA_EXP_FWD_NO_ELEM) || defined(CSA_EXP_FWD_MFMA_ONLY)  // experiment: MFMA + DMA skeleton (wrong)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) w[r] = sacc[r] + eacc[r];
+    if (false) {
+#else
+    {
+#endif
     tmax = xhalf_max(tmax);
     const float m_new = fmaxf(m_run, tmax);
     const float m_use = (m_new == NEG_INF) ? 0.f : m_new;
@@ -1193,7 +1241,6 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd
     for (int t = 0; t < DT; ++t)
 #pragma unroll
       for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
-    float w[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const float e = __expf(s[r] - m_use);
@@ -1203,6 +1250,8 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd
       w[r] = keep[r] ? wa : 0.f;
     }
     m_run = m_new;
+    }
+    FST(8)
     // O^T += V^T W^T (keys beyond M carry w = 0)
     if constexpr (BF) {
       const bf16x8 w0 = pack8(&w[0]), w1 = pack8(&w[8]);
@@ -1217,6 +1266,7 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd
 #pragma unroll
         for (int r = 0; r < 16; ++r) o[t] = mfma(vt[t][r], w[r], o[t]);
     }
+    FST(9)
   }
   const float Z = xhalf_sum(zp), Zg = xhalf_sum(zgp);
   const float n = Zg / Z;
@@ -1243,6 +1293,289 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd
     }
   }
 #undef CSA_ISSUE_FWD
+  if constexpr (!DENSE) {
+    cntl = (h == 0) ? cntl : 0u;
+#pragma unroll
+    for (int o2 = 32; o2 >= 1; o2 >>= 1) cntl += __shfl_xor(cntl, o2, 64);
+    if (lane == 0 && cntl) atomicAdd(p.cnt + hd, (unsigned long long)cntl);
+  }
+#ifdef CSA_EXP_FWD_STAMPS
+  FST(10)
+  if (lane == 0 && blockIdx.x % 331 == 0)
+    printf("FST blk=%d pro %llu dmawait %llu rng %llu S %llu E %llu vtrd %llu dma %llu ste+pack %llu soft %llu pv %llu epi %llu\n",
+           (int)blockIdx.x, fst[0], fst[1], fst[2], fst[3], fst[4], fst[5], fst[6], fst[7], fst[8], fst[9], fst[10]);
+#endif
+}
+
+template <int D, int KPH, bool DENSE, bool HAS_U, bool DROP, bool BF>
+__global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd(const KArgs p) {
+#ifdef CSA_EXP_PRIO  // experiment: half of the waves (by dispatch slot parity) at priority 1
+  if ((blockIdx.x >> 3) & 1) __builtin_amdgcn_s_setprio(1);
+#endif
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const BhBlock xb = xcd_block(p.NQB, p.B * p.H);
+  if (!xb.valid) return;
+  attn_fwd_item<D, KPH, DENSE, HAS_U, DROP, BF>(p, lds, xb.bh, xb.blk, true);
+}
+
+// ------------------------------------------------------------------------------------
+// F3b: k_attn_fwd for d = 64 in fp32 (every python / dense config; the headline layer). Same tiles, images and
+// results as k_attn_fwd (up to fp32 rounding of the softmax); the per-tile schedule is built around what
+// s_memtime stamps of k_attn_fwd showed (profiles/r05_stamps.txt): per key tile a wave spent 2.8k cycles issuing
+// the next tile's 18 LDS-DMA pieces in one burst and ~3.7k in STE / packing / softmax VALU, against 4.6k of its
+// own MFMA time, so two waves per SIMD could not keep the matrix pipe busy. Here
+//   * the tile's Philox calls are spread over the S chain's 32 dependent MFMAs (sched_group_barrier: a few VALU
+//     per 64-cycle MFMA gap issue for free);
+//   * tile kt+1's K and T pieces are issued between the E chain's MFMAs (the S / E chains' K and T reads have
+//     returned), its V pieces between the PV MFMAs (the V^T operands are in registers), one piece per MFMA;
+//   * the V pieces are the youngest vector-memory operations at the next tile's top, so that wait is vmcnt(8)
+//     (K, T, the query operands and the bit stores) and the V image is waited for only right before its reads;
+//   * the key bias is the S chain's initial accumulator, q carries 1/sqrt(d) = 1/8 (exact), e = exp2(s log2e -
+//     m log2e) is one fma + exp, and the running max moves only when a row max grows by more than RESCALE_TH, so
+//     the o / Z rescale runs under a wave-uniform branch that is almost never taken after the first tile (e stays
+//     below exp(8));
+//   * the prologue waits on nothing: the key bias row is written at the first tile, after its wait.
+// ------------------------------------------------------------------------------------
+constexpr float RESCALE_TH = 8.f;
+
+template <int KPH, bool DENSE, bool HAS_U, bool DROP>
+__global__ __launch_bounds__(64, 2) void k_attn_fwd64(const KArgs p) {
+  constexpr int D = 64, DT = 2, NS = 32;
+  using LY = AttnFwdLds<D, KPH>;
+  constexpr int KPN = LY::KP > 0 ? LY::KP : 16, KPHA = KPH > 0 ? KPH : 1;
+  constexpr int TP = DENSE ? 0 : 2 * (KPN / 16);  // T image pieces (1 KiB each, dma_narrow)
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const uint32_t Kl = lds_offset(lds), Vl = Kl + LY::VOFF, Tl = Kl + LY::TOFF;
+  const int lane = lane_id(), c = lane & 31, h = lane >> 5;
+  const BhBlock xb = xcd_block(p.NQB, p.B * p.H);
+  if (!xb.valid) return;
+  const int qb = xb.blk, bh = xb.bh, b = bh / p.H, hd = bh % p.H;
+  const int i = qb * 32 + c;
+  const bool iv = i < p.N;
+  const int ic = imin(i, p.N - 1);
+  const int kld = (int)p.k_sn * 4, vld = (int)p.v_sn * 4;
+  // descriptors span exactly the M valid rows (rows >= M are never fetched; the images are zeroed once)
+  const __amdgpu_buffer_rsrc_t kr = make_rsrc(p.K + b * p.k_sb + hd * p.k_sh, (p.M - 1) * kld + D * 4);
+  const __amdgpu_buffer_rsrc_t vr = make_rsrc(p.V + b * p.v_sb + hd * p.v_sh, (p.M - 1) * vld + D * 4);
+  const __amdgpu_buffer_rsrc_t tr = make_rsrc(DENSE ? p.K : p.T + (int64_t)bh * p.M * p.kp, p.M * p.kp * 4);
+  lds_zero<(2 * LY::KV_BYTES + LY::T_BYTES) / 4>(lds);
+  const DmaPat kpat = dma_pat(SW_ROW, kld), vpat = dma_pat(SW_COL, vld);
+  // prologue, in issue order: key mask, tile 0's K and T images, the query operands (rows past N read row N-1:
+  // finite, never stored), tile 0's V image last (the youngest eight, as at every later tile top)
+  const KeyMask km = key_mask_load_raw(p, b);
+  dma64(Kl, kr, kpat, kld, 0);
+  if constexpr (!DENSE) dma_narrow(Tl, tr, 0, KPN);
+  float q[NS];
+  load_run<NS>(q, p.Q + b * p.q_sb + hd * p.q_sh + (int64_t)ic * p.q_sn + h * NS, true);
+  float qh[KPHA];
+  if constexpr (!DENSE) load_run<KPH>(qh, p.Qh + ((int64_t)bh * p.N + ic) * p.kp + h * KPH, true);
+  dma64(Vl, vr, vpat, vld, 0);
+  constexpr float ESC = HAS_U ? 1.f : 65536.f;  // Philox STE compares u16 < 65536 p (qh scaled, exact)
+  const int kbase = row_base64(c, h);
+  const int tbase = DENSE ? 0 : LY::TOFF + narrow_base<KPN>(c, (KPH / 4) * h);
+  int vb[DT];
+#pragma unroll
+  for (int t = 0; t < DT; ++t) vb[t] = LY::VOFF + col_base64(t, c, h);
+  const uint32_t qmask = (uint32_t)__ballot(iv);  // valid query bits of a packed word
+  float m_run = NEG_INF, zp = 0.f, zgp = 0.f;
+  f32x16 o[DT];
+#pragma unroll
+  for (int t = 0; t < DT; ++t) o[t] = zero16();
+  uint32_t cntl = 0;
+  for (int kt = 0; kt < p.NKB; ++kt) {
+    const int j0 = kt * 32;
+    const bool more = kt + 1 < p.NKB;
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // everything but tile kt's V image (the youngest 8)
+    if (kt == 0) {  // the bias row (0 / -inf, sbm_attn.py:61) and the scaled query operands
+      key_bias_store(lds + LY::BOFF / 4, p, b, km);
+#pragma unroll
+      for (int e = 0; e < NS; ++e) q[e] *= p.scale;
+      if constexpr (!DENSE && !HAS_U)
+#pragma unroll
+        for (int e = 0; e < KPH; ++e) qh[e] *= ESC;
+    }
+    // S^T = K (Q/8)^T on top of the key bias: registers 4g..4g+3 hold keys j0 + 8g + 4h + e
+    f32x16 sacc;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 bz = lds_f4(lds, LY::BOFF + 4 * (j0 + 8 * g + 4 * h));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) sacc[4 * g + e] = bz[e];
+    }
+    // the tile's Philox words (query, tile, head): their VALU is spread over the S chain's MFMA gaps
+    u32x4 r_ste[2], r_drop[2];
+    {
+      uint32_t sk0 = p.seed_lo, sk1 = p.seed_hi;  // opaque per tile: round keys are not held across the loop
+      asm volatile("" : "+s"(sk0), "+s"(sk1));
+#pragma unroll
+      for (int gp = 0; gp < 2; ++gp) {
+        if constexpr (!DENSE && !HAS_U)
+          r_ste[gp] = philox4x32(u32x4{(uint32_t)i, (uint32_t)(8 * kt + 4 * gp + h), (uint32_t)bh,
+                                       (RNG_STE << 28) ^ p.off}, sk0, sk1);
+        if constexpr (DROP)
+          r_drop[gp] = philox4x32(u32x4{(uint32_t)i, (uint32_t)(8 * kt + 4 * gp + h), (uint32_t)bh,
+                                        (RNG_ATTN_DROP << 28) ^ p.off}, sk0, sk1);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NS / 4; ++j) {
+      const f32x4 kv = lds_f4(lds, kbase ^ (16 * j));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) sacc = mfma(kv[e], q[4 * j + e], sacc);
+    }
+#pragma unroll
+    for (int m = 0; m < NS; ++m) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one S MFMA
+      __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);   // then up to six VALU (Philox)
+    }
+    // the Philox words are complete here (so they are computed among the S MFMAs, not sunk to their use)
+#pragma unroll
+    for (int gp = 0; gp < 2; ++gp) {
+      if constexpr (!DENSE && !HAS_U) asm volatile("" : "+v"(r_ste[gp].x), "+v"(r_ste[gp].y), "+v"(r_ste[gp].z), "+v"(r_ste[gp].w));
+      if constexpr (DROP) asm volatile("" : "+v"(r_drop[gp].x), "+v"(r_drop[gp].y), "+v"(r_drop[gp].z), "+v"(r_drop[gp].w));
+    }
+    // expA^T = T Qh^T (sbm_attn.py:55); tile kt+1's K and T pieces go out between its MFMAs
+    f32x4 tv[KPH > 0 ? KPH / 4 : 1];
+    if constexpr (!DENSE)
+#pragma unroll
+      for (int j = 0; j < KPH / 4; ++j) tv[j] = lds_f4(lds, tbase ^ (16 * j));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the K, T and bias reads have returned
+    f32x16 eacc = zero16();
+    if constexpr (!DENSE) {
+      static_assert(KPH == 8, "the E chain interleave assumes 8 MFMAs (kp = 16)");
+      if (more) {
+#pragma unroll
+        for (int m = 0; m < KPH; ++m) {
+          eacc = mfma(tv[m / 4][m % 4], qh[m], eacc);
+          dma64(Kl, kr, kpat, kld, j0 + 32, m, m + 1);
+        }
+        dma_narrow(Tl, tr, j0 + 32, KPN);
+#pragma unroll
+        for (int m = 0; m < KPH; ++m) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one E MFMA
+          __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // then one K piece
+        }
+      } else {
+#pragma unroll
+        for (int m = 0; m < KPH; ++m) eacc = mfma(tv[m / 4][m % 4], qh[m], eacc);
+      }
+    } else {
+      if (more) dma64(Kl, kr, kpat, kld, j0 + 32);
+    }
+    // V^T operand values for this tile's PV: lane (d = 32t + c) reads V[key crow(r,h)][d]
+    // tile kt's V image: older than tile kt+1's K and T pieces
+    if (more) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(8 + TP) : "memory");
+    else wait_vm_all();
+    float vt[DT][16];
+#pragma unroll
+    for (int t = 0; t < DT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) vt[t][r] = lds_f1(lds, vb[t] + 256 * crow(r, 0));
+    float tmax = NEG_INF;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, sacc[r]);
+    bool av[16], keep[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { av[r] = true; keep[r] = true; }
+    if constexpr (!DENSE) {
+      if constexpr (HAS_U) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int j = j0 + crow(r, h);
+          const float v = p.U[((int64_t)bh * p.N + ic) * p.M + imin(j, p.M - 1)];
+          const float uu = (iv && j < p.M) ? v : 2.f;
+          av[r] = uu < fminf(fmaxf(eacc[r], 0.01f), 0.99f);  // STE.py:11-13
+        }
+      } else {
+#pragma unroll
+        for (int gp = 0; gp < 2; ++gp)
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            av[8 * gp + e] = (float)u16_of(r_ste[gp], e) < __builtin_amdgcn_fmed3f(eacc[8 * gp + e], 0.01f * ESC, 0.99f * ESC);
+      }
+    }
+    if constexpr (DROP) {
+#pragma unroll
+      for (int gp = 0; gp < 2; ++gp)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) keep[8 * gp + e] = u16_of(r_drop[gp], e) >= p.drop_thr;
+    }
+    // bit-pack the sampled graph / dropout keep mask: word [qb][key] holds 32 query bits (lanes 0..31)
+    if constexpr (!DENSE || DROP) {
+      const uint32_t myA = DENSE ? 0u : pack_bits(av);
+      const uint32_t myR = DROP ? pack_bits(keep) : 0u;
+      const int64_t widx = ((int64_t)bh * p.NQB + qb) * p.Mpad + j0 + c;
+      if constexpr (!DENSE) {
+        if (h == 0) p.Abits[widx] = myA;
+        if (j0 + c < p.M) cntl += __popc(myA & qmask);  // sampled edges inside [0,N) x [0,M)
+      }
+      if constexpr (DROP) if (h == 0) p.Rbits[widx] = myR;
+    }
+    // online softmax: the reference max moves only when the row max grows by more than RESCALE_TH
+    tmax = xhalf_max(tmax);
+    const float m_tgt = (tmax > m_run + RESCALE_TH) ? tmax : m_run;
+    if (__builtin_amdgcn_ballot_w64(m_tgt != m_run) != 0) {
+      const float alpha = (m_tgt == m_run) ? 1.f : __builtin_amdgcn_exp2f((m_run - m_tgt) * LOG2E);
+      zp *= alpha;
+      zgp *= alpha;
+#pragma unroll
+      for (int t = 0; t < DT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
+      m_run = m_tgt;
+    }
+    const float nmL = -((m_run == NEG_INF) ? 0.f : m_run) * LOG2E;
+    float w[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float e = __builtin_amdgcn_exp2f(fmaf(sacc[r], LOG2E, nmL));
+      zp += e;
+      const float wa = av[r] ? e : 0.f;
+      zgp += wa;
+      w[r] = keep[r] ? wa : 0.f;
+    }
+    // O^T += V^T W^T (keys beyond M carry w = 0); tile kt+1's V pieces go out between the MFMAs (the vt reads have
+    // returned: this tile's V image is free)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (more) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+#pragma unroll
+        for (int t = 0; t < DT; ++t) o[t] = mfma(vt[t][r], w[r], o[t]);
+        if (r < 8) dma64(Vl, vr, vpat, vld, j0 + 32, r, r + 1);
+      }
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // two PV MFMAs
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // then one V piece
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+#pragma unroll
+        for (int t = 0; t < DT; ++t) o[t] = mfma(vt[t][r], w[r], o[t]);
+    }
+  }
+  const float Z = xhalf_sum(zp), Zg = xhalf_sum(zgp);
+  const float n = Zg / Z;
+  const float Dn = fmaxf(n, NORM_EPS);
+  const float dscale = DROP ? 1.f / (1.f - p.attn_p) : 1.f;  // dropout's 1/(1-p), applied once per row
+  const float inv = dscale / (Z * Dn);
+  if (iv) {
+#pragma unroll
+    for (int t = 0; t < DT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[t][r] *= inv;
+    store_rows<DT>(p.X + b * p.x_sb + hd * p.x_sh + (int64_t)i * p.x_sn, D, D, o, true);
+    if (h == 0) {
+      f32x4 st;
+      st[0] = m_run + logf(Z);   // lse: P = exp(s - lse)
+      st[1] = 1.f / Dn;          // 1 / max(n, eps)
+      st[2] = (n >= NORM_EPS) ? 1.f : 0.f;
+      st[3] = 0.f;               // gamma, filled by the backward
+      *reinterpret_cast<f32x4*>(p.stats + ((int64_t)bh * p.N + i) * 4) = st;
+    }
+  }
   if constexpr (!DENSE) {
     cntl = (h == 0) ? cntl : 0u;
 #pragma unroll
@@ -1802,6 +2135,7 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
 #ifdef CSA_EXP_PRIO  // experiment: half of the waves (by dispatch slot parity) at priority 1
   if ((blockIdx.x >> 3) & 1) __builtin_amdgcn_s_setprio(1);
 #endif
+  FST_DECL
   using SH = AttnBwdShape<D, KPH>;
   constexpr int DT = D / 32, NS = D / 2, DP = SH::DP, KP = SH::KP, KPN = SH::KPN, KTA = SH::KTA;
   constexpr bool SWZ = SH::SWZ;
@@ -1843,23 +2177,26 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
   const int64_t wcol = (int64_t)bh * p.NQB * p.Mpad + j;
   uint32_t wAn = DENSE ? 0xffffffffu : p.Abits[wcol];
   uint32_t wRn = DROP ? p.Rbits[wcol] : 0xffffffffu;
+  // Nothing waits on these loads before the first tile (the prologue used to select on the key rows and the mask
+  // value right after loading them: a memory latency exposed per wave, profiles/r05_stamps.txt). A key past M reads
+  // row M-1 (finite); its A bits, P (kbias = -inf) and stored rows are masked.
   const float* mk = p.mask ? p.mask + b * p.mask_sb : nullptr;
   const float mval = mk ? mk[jc] : 0.f;
-  const float kbias = (jv && mval == 0.f) ? 0.f : NEG_INF;  // this lane's key (sbm_attn.py:61)
+  const float dspv = (!DENSE && p.dsp) ? p.dsp[hd] : 0.f;
   const uint32_t kvm = jv ? 0xffffffffu : 0u;  // a key past M counts as not sampled: its G is stored as 0
   // this lane's row (key j) of the ds / G tiles handed to k_attn_bwd_qg, tile (qb, kbi) at + qb * NKB * 1024
   float* dsw = p.dsg + ((int64_t)bh * p.NQB * p.NKB + kbi) * 1024 + c * 32 + 4 * h;
   float kr[NS], vr[NS];
-  load_run<NS>(kr, p.K + b * p.k_sb + hd * p.k_sh + (int64_t)jc * p.k_sn + h * NS, jv);
-  load_run<NS>(vr, p.V + b * p.v_sb + hd * p.v_sh + (int64_t)jc * p.v_sn + h * NS, jv);
+  load_run<NS>(kr, p.K + b * p.k_sb + hd * p.k_sh + (int64_t)jc * p.k_sn + h * NS, true);
+  load_run<NS>(vr, p.V + b * p.v_sb + hd * p.v_sh + (int64_t)jc * p.v_sn + h * NS, true);
   const float dscale = DROP ? 1.f / (1.f - p.attn_p) : 1.f;
-  const float csp = (!DENSE && p.dsp) ? p.dsp[hd] / ((float)p.B * (float)p.N * (float)p.M) : 0.f;
   const float c1 = p.scale * LOG2E;
   f32x16 dv[DT], dk[DT], dtt[KTA];
 #pragma unroll
   for (int t = 0; t < DT; ++t) { dv[t] = zero16(); dk[t] = zero16(); }
 #pragma unroll
   for (int t = 0; t < KTA; ++t) dtt[t] = zero16();
+  FST(0)
   for (int qb = 0; qb < p.NQB; ++qb) {
     int ln = threadIdx.x;  // opaque per iteration: keeps the per-row LDS addresses out of the prologue
     asm volatile("" : "+v"(ln));
@@ -1867,6 +2204,11 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
     const int i0 = qb * 32;
     const bool more = qb + 1 < p.NQB;
     wait_vm_all();  // query block qb's Q / dX / Qh / row-constant images and bit words have landed
+    float mvl = mval, dsl = dspv;  // opaque per tile: their uses stay behind the wait above
+    asm volatile("" : "+v"(mvl), "+v"(dsl));
+    const float kbias = (jv && mvl == 0.f) ? 0.f : NEG_INF;  // this lane's key (sbm_attn.py:61)
+    const float csp = dsl / ((float)p.B * (float)p.N * (float)p.M);
+    FST(1)
     // W1: does a row of this query block have rho != 0 (its query side then needs P as well)?
     const bool rho_any = W1 && __builtin_amdgcn_ballot_w64(lds_f1(lds, SH::KS + 16 * c + 12) != 0.f) != 0;
     // sampled / keep bits shifted so that register r's query is bit crow(r, 0); queries past N and keys past M
@@ -1903,6 +2245,7 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
         for (int e = 0; e < 4; ++e) dpacc = mfma(xv[e], vr[4 * s4 + e], dpacc);
       }
     }
+    FST(2)
     // column read of element (query crow(r,h), d = 32t + c) of the Q / dX image at byte offset off
     int cb[DT];
 #pragma unroll
@@ -1949,7 +2292,13 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
         awv[rr] = (a && kp) ? P * rec[1] : 0.f;  // dropout(attn) weight for dV
 #ifndef CSA_EXP_NO_DSG_STORE
         if constexpr (W1) {  // stored as soon as four are ready (fewer live registers); non-temporal, see below
+#if defined(CSA_EXP_KV_NOST1)  // experiment: no stores of the second half's w (wrong results)
+          if ((rr & 3) == 3 && half == 0)
+#elif defined(CSA_EXP_KV_NOST0)  // experiment: no stores of the first half's w (wrong results)
+          if ((rr & 3) == 3 && half == 1)
+#else
           if ((rr & 3) == 3)
+#endif
             __builtin_nontemporal_store((f32x4{wv[0], wv[1], wv[2], wv[3]}), reinterpret_cast<f32x4*>(wst + 2 * (rr & 4)));
         }
 #endif
@@ -1986,6 +2335,7 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
 #undef CSA_ST4
       }
 #endif
+      FST(3 + 2 * half)
       // dV^T += dX^T attw ; dK^T += Q^T ds ; dT^T += Qh^T G  (queries beyond N carry zeros)
       if constexpr (BF) {
         const bf16x8 aw8 = pack8(awv), ds8 = pack8(dsv);
@@ -2032,6 +2382,7 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
             dtt[at] = mfma((KP >= 32 || c < KP) ? v : 0.f, gv[rr], dtt[at]);
           }
       }
+      FST(4 + 2 * half)
 #ifdef CSA_EXP_NO_LOOP_DMA  // experiment: timing without the in-loop refills (wrong results)
       if (false) {
 #else
@@ -2057,6 +2408,7 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
         }
       }
     }
+    FST(7)
   }
   if constexpr (PAIR) {  // d = 2 crow(r, h) + t: registers 4g .. 4g + 3 of both tiles are d = 16g + 8h .. + 7
     if (jv) {
@@ -2078,6 +2430,12 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
   }
   if constexpr (MB4) store_mb4(p.dT + ((int64_t)bh * p.M + kbi * 32) * p.kp, p.M - kbi * 32, p.kp, dtt[0]);
   else if constexpr (!DENSE) store_rows<KTA>(p.dT + ((int64_t)bh * p.M + j) * p.kp, p.kp, p.kp, dtt, jv);
+#ifdef CSA_EXP_FWD_STAMPS
+  FST(8)
+  if (lane == 0 && blockIdx.x % 331 == 0)
+    printf("KST blk=%d pro %llu wait %llu S+dP %llu el0 %llu mm0 %llu el1 %llu mm1 %llu refill %llu epi %llu\n",
+           (int)blockIdx.x, fst[0], fst[1], fst[2], fst[3], fst[4], fst[5], fst[6], fst[7], fst[8]);
+#endif
 }
 
 // ------------------------------------------------------------------------------------
@@ -3197,8 +3555,40 @@ csa_status validate_fwd(const csa_sbm_fwd_args* a) {
   return CSA_OK;
 }
 
+// d = 64 fp32 with kp <= 16 clusters: k_attn_fwd64 (q carries the exact 1/8 scale). Opt-in experiment: same box,
+// 1.3-3% slower than k_attn_fwd (profiles/r05_ab_fwd.txt), so the shipped forward is k_attn_fwd.
+template <int D, int KPH, bool BF>
+bool fwd64(const KArgs& p) {
+#ifndef CSA_EXP_FWD64
+  return false;
+#endif
+  return D == 64 && !BF && KPH <= 8 && p.scale == 0.125f;
+}
+
 template <int D, int KPH, bool DENSE, bool BF>
 void launch_attn_fwd(const KArgs& p, int BH, const Layout& L, bool has_u, bool drop, hipStream_t st) {
+  if constexpr (D == 64 && !BF && KPH <= 8) {
+    if (fwd64<D, KPH, BF>(p)) {
+      const size_t lb = AttnFwdLds<D, KPH>::bytes((int)L.Mpad);
+      const dim3 grid(xcd_grid((int)L.NQB, BH));
+#define CSA_F64_KERNEL k_attn_fwd64
+#define CSA_F64_LAUNCH(HU, DR)                                                                  \
+  do {                                                                                          \
+    if (lb > 64 * 1024) set_dyn_lds((const void*)CSA_F64_KERNEL<KPH, DENSE, HU, DR>, (int)lb);  \
+    hipLaunchKernelGGL((CSA_F64_KERNEL<KPH, DENSE, HU, DR>), grid, dim3(64), lb, st, p);        \
+  } while (0)
+      if (!DENSE && has_u) {
+        if (drop) CSA_F64_LAUNCH(!DENSE, true);
+        else CSA_F64_LAUNCH(!DENSE, false);
+      } else {
+        if (drop) CSA_F64_LAUNCH(false, true);
+        else CSA_F64_LAUNCH(false, false);
+      }
+#undef CSA_F64_LAUNCH
+#undef CSA_F64_KERNEL
+      return;
+    }
+  }
   const size_t lds_bytes = AttnFwdLds<D, KPH>::bytes((int)L.Mpad);
   const dim3 grid(xcd_grid((int)L.NQB, BH));
   if (lds_bytes > 64 * 1024) {
