@@ -8,8 +8,9 @@ in HBM. The upstream gradients are X's (dX ~ N(0,1)) and sparsity's (sw/32 per h
 what the reference's train step feeds the layer (script/train.py:109).
 
 Multi-GPU (torchrun, one process per GPU): each rank processes its own 256 ASTs (weak scaling)
-and the layer's parameter gradients are all-reduced by DDP over RCCL, the one exchange of
-script/train.py:83,109. value = ASTs processed by all ranks / max-over-ranks wall time.
+and the layer's parameter gradients are all-reduced over RCCL (csa_amd.train's bucketed data-parallel
+reducer, DDP semantics), the one exchange of script/train.py:83,109. value = ASTs processed by all
+ranks / max-over-ranks wall time.
 
 Printed JSON line (rank 0): contract fields + "roofline" for the dominant kernel (HIP events
 recorded around that kernel's launch on its stream, every timed step; the dominant kernel and the
@@ -318,15 +319,17 @@ def gpu_config1(dev, reps=10, B=32, N=150):
             "peak_note": "torch.cuda.max_memory_allocated over each leg's timed passes (parameters and grads included)"}
 
 
-def train_step_bench(world, rank, dev, steps, warmup, config="java", per_gpu_batch=64, nbatches=3, force_ddp=False):
-    """script/train.py:_update (config/java.py dims) under DDP/RCCL; returns samples/s over all ranks.
-    force_ddp: wrap in DDP even at world size 1 (needs an initialised process group)."""
+def train_step_bench(world, rank, dev, steps, warmup, config="java", per_gpu_batch=64, nbatches=3, force_ddp=False,
+                     impl="bucketed"):
+    """script/train.py:_update (config/java.py dims), data parallel over RCCL; returns samples/s over all ranks.
+    force_ddp: wrap even at world size 1 (needs an initialised process group). impl: wrap_ddp's reducer
+    ("bucketed" = csa_amd.train.BucketedDataParallel, "torch" = DistributedDataParallel)."""
     from csa_amd.data import synthetic_batch
     from csa_amd.model import CONFIGS, CSATrans, batch_to_device, label_smoothing_loss
     from csa_amd.train import AdamW, make_train_step, wrap_ddp
     torch.manual_seed(2021 + rank)  # set_seed(seed + rank), script/train.py:158
     model = CSATrans(**CONFIGS[config]).to(dev)
-    ddp = wrap_ddp(model, dev, force=force_ddp)
+    ddp = wrap_ddp(model, dev, force=force_ddp, impl=impl)
     opt = AdamW(model.parameters(), lr=1e-4, correct_bias=False)
     scaler = torch.amp.GradScaler("cuda")
     step = make_train_step(ddp, opt, label_smoothing_loss, sw=1e-2, scaler=scaler)
@@ -339,15 +342,16 @@ def train_step_bench(world, rank, dev, steps, warmup, config="java", per_gpu_bat
     mean_loss = float(torch.stack(losses).mean())
     nparam = sum(p.numel() for p in model.parameters())
     wrapped = world > 1 or force_ddp
-    return {"config": f"config/{config}.py CSATrans summary train step" + (" (DDP over RCCL)" if wrapped else
-                                                                           " (one GPU, no DDP wrapper)"),
+    reducer = "BucketedDataParallel" if impl == "bucketed" else "torch DDP"
+    return {"config": f"config/{config}.py CSATrans summary train step" + (f" ({reducer} over RCCL)" if wrapped else
+                                                                           " (one GPU, no data-parallel wrapper)"),
             "per_gpu_batch": per_gpu_batch,
             "global_batch": per_gpu_batch * world, "steps": steps, "warmup": warmup,
             "ms_per_step": round(el * 1000 / steps, 3), "samples_per_s": round(world * per_gpu_batch * steps / el, 1),
             "params": nparam, "mean_loss": round(mean_loss, 4), "n_ranks": world,
-            "exchange": ("DDP gradient all-reduce over RCCL (64 MB buckets)" if world > 1 else
-                         "DDP over a world-size-1 RCCL group (reducer + bucket copies, no peer)" if force_ddp else
-                         "none (1 GPU, unwrapped)")}
+            "exchange": (f"{reducer} gradient all-reduce over RCCL (64 MB buckets)" if world > 1 else
+                         f"{reducer} over a world-size-1 RCCL group (hooks + bucket packing, no peer)" if force_ddp
+                         else "none (1 GPU, unwrapped)")}
 
 
 def launch_ranks(nproc):
@@ -410,10 +414,12 @@ def timed_region(world, dev, steps, step):
 
 def launcher_selftest(args, world, rank, dev):
     """--device cpu: exercises the launcher, the process group and the max-over-ranks timing on host
-    CPUs (gloo) with a DDP-wrapped Linear; no kernel of this repo runs, so the line says so."""
+    CPUs (gloo) with a Linear under the bucketed data-parallel reducer; no kernel of this repo runs, so the
+    line says so."""
+    from csa_amd.train import BucketedDataParallel
     torch.manual_seed(rank)
     lin = torch.nn.Linear(64, 64)
-    model = torch.nn.parallel.DistributedDataParallel(lin) if world > 1 else lin
+    model = BucketedDataParallel(lin) if world > 1 else lin
     x = torch.randn(32, 64)
 
     def step(i):
@@ -423,7 +429,7 @@ def launcher_selftest(args, world, rank, dev):
     for i in range(args.warmup):
         step(i)
     el = timed_region(world, dev, args.steps, step)
-    return {"metric": "launcher self-test (DDP Linear on CPU/gloo; not the hot path)", "value": round(world * 32 *
+    return {"metric": "launcher self-test (data-parallel Linear on CPU/gloo; not the hot path)", "value": round(world * 32 *
             args.steps / el, 1), "unit": "samples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(el * 1000 / args.steps, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f32", "data": "synthetic",
@@ -445,6 +451,7 @@ def main():
     ap.add_argument("--precision", choices=("fp32", "bf16"), default="fp32",
                     help="operand precision of the attention contractions (fp32 = the reference's)")
     ap.add_argument("--no-bf16-leg", action="store_true", help="skip the bf16-mode side measurement")
+    ap.add_argument("--no-padded-leg", action="store_true", help="skip the padded-mask (n_b ~ U[50,150]) leg")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cpu-config1", action="store_true", help="skip the config-1 CPU CSATrans protocol")
@@ -485,8 +492,8 @@ def main():
     mod.train(not args.eval)
     model = mod
     if world > 1 and not args.dense:  # FullAttention has no parameters: no gradient exchange exists
-        mod.bwd_schedule = "in_order"  # as csa_amd.train.wrap_ddp: no side stream beside RCCL
-        model = torch.nn.parallel.DistributedDataParallel(mod, device_ids=[local])
+        from csa_amd.train import wrap_ddp
+        model = wrap_ddp(mod, dev)  # bucketed reducer; in-order attention backward beside RCCL
     Q, K, V = (torch.randn(B, H, N, d, device=dev).requires_grad_(True) for _ in range(3))
     mask = torch.zeros(B, N, device=dev)
     dX = torch.randn(B, H, N, d, device=dev)
@@ -591,7 +598,10 @@ def main():
         ach = flops[dom] * B / (dom_ms * 1e-3) / 1e12
         roofline = {"bound": "mfma", "kernel": kernel_of[dom], "achieved": round(ach, 2),
                     "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / PEAK_F32_MFMA_TFLOPS, 4),
-                    "traffic": None, "avg_launch_ms": round(dom_ms, 4)}
+                    "traffic": None, "avg_launch_ms": round(dom_ms, 4),
+                    "frac_basis": "live: HIP events on the kernel's stream around each of its launches in the timed "
+                                  "steps (event timestamps include the launch's dispatch edge; frac_rocprof, when "
+                                  "present, uses the committed rocprofv3 kernel-trace average)"}
     headline = (B, N, d, k, args.precision, args.dense, args.eval) == (256, 150, 64, 10, "fp32", False, False)
     table = pmc_table() if headline else None
     if roofline and table:
@@ -616,7 +626,7 @@ def main():
                    "head_dim": d, "clusters": 0 if args.dense else k, "mode": "eval" if args.eval else "train",
                    "parallelism": f"dp{world}",
                    "exchange": "none (FullAttention has no parameters)" if args.dense else
-                   ("DDP gradient all-reduce over RCCL" if world > 1 else "none (1 GPU)")},
+                   ("bucketed gradient all-reduce over RCCL" if world > 1 else "none (1 GPU)")},
         "roofline": roofline,
         "step_tflops": round(total_flops / (ms_per_step * 1e-3) / 1e12, 2),
         "step_frac_of_f32_mfma_peak": round(total_flops / (ms_per_step * 1e-3) / 1e12 / PEAK_F32_MFMA_TFLOPS, 4),
@@ -651,6 +661,21 @@ def main():
             "frac_at_bf16_io": round(vb * IDEAL_BYTES_PER_AST_BF16IO / 1e9 / PEAK_HBM_GBS, 4),
             "note": "ideal fused bytes per AST x ASTs/s against 8 TB/s (SURVEY 8(d) config 2); frac with the "
                     "fp32 I/O the mode takes and returns, frac_at_bf16_io with 2.05 MB/AST bf16 I/O"}
+    if not args.dense and N == 150 and not args.no_padded_leg:
+        # config 2's real batches are padded: n_b ~ U[50, 150] nodes per AST, the rest key-masked (same layer, B)
+        progress("padded-mask leg")
+        gpad = torch.Generator().manual_seed(4321 + rank)
+        nb = torch.randint(50, N + 1, (B,), generator=gpad)
+        mask.copy_((torch.arange(N)[None, :] >= nb[:, None]).float())
+        for _ in range(args.warmup):
+            step()
+        el_pad = timed_region(world, dev, args.steps, lambda i: step())
+        mask.zero_()
+        out["padded_mask"] = {"value": round(world * B * args.steps / el_pad, 1), "unit": "ASTs/s",
+                              "ms_per_step": round(el_pad * 1000.0 / args.steps, 4),
+                              "mean_nodes": round(float(nb.float().mean()), 2),
+                              "note": "config 2 padded batches: n_b ~ U[50,150] real nodes per AST (seeded), key mask "
+                                      "1 on the padding; every kernel still runs the full 150-node tiles"}
     if not args.no_train:
         progress("train-step leg (config/java.py, 64 ASTs per GPU)")
         from csa_amd.train import GEMM_TABLE, use_tuned_gemms
@@ -659,7 +684,8 @@ def main():
         out["train"]["gemms"] = (f"TunableOp table {os.path.basename(GEMM_TABLE)} ({ntuned} shapes)" if ntuned
                                  else "hipBLASLt default heuristic")
         if world == 1:
-            # the same step wrapped in DDP over a world-size-1 RCCL group: the reducer's own cost on record
+            # the same step under the data-parallel wrapper over a world-size-1 RCCL group: the reducer's own
+            # cost on record (BucketedDataParallel, and torch DDP beside it for comparison)
             import socket
             with socket.socket() as s_:
                 s_.bind(("127.0.0.1", 0))
@@ -668,6 +694,8 @@ def main():
             try:
                 out["train_ddp_world1"] = train_step_bench(1, rank, dev, args.train_steps, args.train_warmup,
                                                            force_ddp=True)
+                out["train_torch_ddp_world1"] = train_step_bench(1, rank, dev, args.train_steps, args.train_warmup,
+                                                                 force_ddp=True, impl="torch")
             finally:
                 dist.destroy_process_group()
             progress("config-1 protocol on the GPU")

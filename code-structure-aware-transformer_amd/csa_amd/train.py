@@ -4,12 +4,13 @@
              loss = LabelSmoothing(y_pred, y); GradScaler.scale(loss + sw*sparsity).backward()
              scaler.step(AdamW); scaler.update()
 
-Multi-GPU: one process per GPU (torchrun), DistributedDataParallel over the "nccl" backend (= RCCL
-on ROCm, xGMI between the GPUs of a node) as idist.auto_model does (script/train.py:83,331); each
-rank draws its own batches (DistributedSampler semantics: per-rank shard) and seeds with
-seed + rank (script/train.py:158). DDP averages gradients, so the global step equals the mean of
-the per-rank losses, exactly the reference's semantics (LabelSmoothing divides by per-rank
-ntokens, utils/label_smooth.py:27,40).
+Multi-GPU: one process per GPU (torchrun), data parallel over the "nccl" backend (= RCCL on ROCm,
+xGMI between the GPUs of a node) as idist.auto_model's DistributedDataParallel does
+(script/train.py:83,331), with this repo's bucketed reducer (BucketedDataParallel: one pack launch
+per 64 MB bucket instead of DDP's per-parameter copies); each rank draws its own batches
+(DistributedSampler semantics: per-rank shard) and seeds with seed + rank (script/train.py:158).
+Gradients are averaged, so the global step equals the mean of the per-rank losses, exactly the
+reference's semantics (LabelSmoothing divides by per-rank ntokens, utils/label_smooth.py:27,40).
 
 The optimizer is the reference's HF-style AdamW (script/optimizer.py:49-106) with
 correct_bias=False (script/train.py:80). On GPU every parameter is updated by ONE launch of the
@@ -219,14 +220,178 @@ def set_bwd_schedule(model, schedule):
     return n
 
 
-def wrap_ddp(model, device, force=False, bucket_cap_mb=64):
-    """DistributedDataParallel over the initialised process group (idist.auto_model, script/train.py:83),
-    gradient_as_bucket_view, 64 MB buckets. Without a process group of more than one rank the model is
-    returned unwrapped, unless `force` (DDP over a world-size-1 group: the reducer's own cost, tests).
+def _world1_no_comm_hook(state, bucket):
+    """Diagnostic DDP comm hook (tools/ddp_variants.py): a world-size-1 group's all-reduce is the identity, so the
+    bucket is returned as it is (no division by 1, no RCCL call). Only ever registered at world size 1."""
+    fut = torch.futures.Future()
+    fut.set_result(bucket.buffer())
+    return fut
+
+
+class BucketedDataParallel(torch.nn.Module):
+    """Data-parallel gradient averaging over the initialised process group, the semantics of
+    idist.auto_model's DistributedDataParallel (script/train.py:83): identical initial parameters on
+    every rank (rank 0's, broadcast once), and after each backward every parameter gradient is the mean
+    of the per-rank gradients. `.module` is the wrapped model, as in DDP (state_dict keys "module.*",
+    GreedyGenerator's `model.module`).
+
+    The reducer is built for this model's gradient traffic instead of DDP's per-parameter one. DDP copies
+    every parameter gradient into its bucket with its own kernel (283 tensors in config/java.py: 283
+    copy launches per step, 1.7 ms at world size 1, tools/ddp_variants.py). Here each bucket of
+    parameters (~`bucket_cap_mb`, in gradient arrival order) is packed by ONE torch.cat into its slice
+    of a persistent flat fp32 gradient buffer the moment its last gradient has been accumulated
+    (post-accumulate-grad hooks), its all-reduce is issued right away on RCCL's stream (overlapping the
+    rest of the backward), and every `p.grad` becomes a view of the flat buffer, so the optimizer's
+    gradient pointers stay fixed from step to step. One autograd-engine callback at the end of the
+    backward packs any bucket left incomplete (parameters without a gradient contribute zeros, as in
+    DDP's find_unused_parameters), waits for the all-reduces and averages.
+
+    Averaging: RCCL's AVG reduction (a pre-multiply by 1/world, DDP's `div_(world)` then SUM), gloo:
+    SUM then one division per bucket. For power-of-two world sizes both are exact scalings, so the
+    result is bit-identical to DDP's. Buffers (the positional-encoding table) are broadcast once at
+    construction; the model has no buffer that changes in training. `no_sync()` skips the reduction
+    (local gradient accumulation); the next synchronised backward reduces the accumulated gradients.
+    The first backward records the order in which gradients arrive; the buckets are then re-laid in
+    that order (DDP's bucket rebuild), so later steps start all-reducing as early as possible."""
+
+    def __init__(self, module, bucket_cap_mb=64, process_group=None):
+        super().__init__()
+        self.module = module
+        self.group = process_group
+        self.world = dist.get_world_size(process_group)
+        params = [p for p in module.parameters() if p.requires_grad]
+        if not params:
+            raise ValueError("BucketedDataParallel: the module has no trainable parameters")
+        if len({(p.dtype, p.device) for p in params}) != 1:
+            raise ValueError("BucketedDataParallel: all parameters must share one dtype and device")
+        self._params = params
+        self._cap = max(1, int(bucket_cap_mb * 2 ** 20 // params[0].element_size()))
+        with torch.no_grad():  # DDP's _sync_module_states: rank 0's parameters and buffers everywhere
+            if self.world > 1:
+                for t in params + list(module.buffers()):
+                    dist.broadcast(t.data, 0, group=process_group)
+        self._op = (dist.ReduceOp.AVG if dist.get_backend(process_group) == "nccl" else dist.ReduceOp.SUM)
+        self._layout(list(reversed(range(len(params)))))  # DDP's initial guess: reverse registration order
+        self._arrival, self._rebuilt = [], False
+        self._sync, self._queued = True, False
+        self._hooks = [p.register_post_accumulate_grad_hook(self._make_hook(i)) for i, p in enumerate(params)]
+
+    def _layout(self, order):
+        """Buckets of consecutive parameters in `order` (~cap elements each) and one flat buffer."""
+        p0 = self._params[0]
+        self._bucket_of = [0] * len(self._params)
+        self._buckets, cur, size = [], [], 0
+        for i in order:
+            n = self._params[i].numel()
+            if cur and size + n > self._cap:
+                self._buckets.append(cur)
+                cur, size = [], 0
+            cur.append(i)
+            size += n
+        self._buckets.append(cur)
+        self._spans, self._views, off = [], [None] * len(self._params), 0
+        total = sum(p.numel() for p in self._params)
+        self.flat = torch.zeros(total, dtype=p0.dtype, device=p0.device)
+        for b, idx in enumerate(self._buckets):
+            lo = off
+            for i in idx:
+                p = self._params[i]
+                self._bucket_of[i] = b
+                self._views[i] = self.flat[off:off + p.numel()].view_as(p)
+                off += p.numel()
+            self._spans.append((lo, off))
+        self._pending = [len(idx) for idx in self._buckets]
+        self._works = []
+
+    def _make_hook(self, i):
+        def hook(p):
+            if not self._sync:
+                return
+            if not self._queued:  # first gradient of this backward: finish at its end
+                torch.autograd.Variable._execution_engine.queue_callback(self._finish)
+                self._queued = True
+            if not self._rebuilt:
+                self._arrival.append(i)
+            b = self._bucket_of[i]
+            self._pending[b] -= 1
+            if self._pending[b] == 0 and self._rebuilt:
+                self._reduce(b)
+        return hook
+
+    @torch.no_grad()
+    def _reduce(self, b):
+        lo, hi = self._spans[b]
+        dst = self.flat[lo:hi]
+        grads = []
+        for i in self._buckets[b]:
+            g = self._params[i].grad
+            grads.append(torch.zeros_like(self._params[i]) if g is None else g)
+        aliased = [g.data_ptr() == self._views[i].data_ptr() for g, i in zip(grads, self._buckets[b])]
+        if not any(aliased):
+            torch.cat([g.reshape(-1) for g in grads], out=dst)
+        else:  # gradients accumulated in place into the flat views (no_sync / set_to_none=False)
+            for g, i, a in zip(grads, self._buckets[b], aliased):
+                if not a:
+                    self._views[i].copy_(g)
+        for i in self._buckets[b]:
+            self._params[i].grad = self._views[i]
+        if self.world > 1:
+            self._works.append((b, dist.all_reduce(dst, op=self._op, group=self.group, async_op=True)))
+
+    @torch.no_grad()
+    def _finish(self):
+        self._queued = False
+        if not self._rebuilt:  # first step: adopt the observed arrival order, then reduce everything
+            seen = set(self._arrival)
+            order = self._arrival + [i for i in reversed(range(len(self._params))) if i not in seen]
+            self._layout(order)
+            self._rebuilt = True
+            self._arrival = []
+            for b in range(len(self._buckets)):
+                self._reduce(b)
+        else:
+            for b in range(len(self._buckets)):
+                if self._pending[b] > 0:
+                    self._reduce(b)
+        for b, w in self._works:
+            w.wait()
+            if self._op == dist.ReduceOp.SUM:
+                lo, hi = self._spans[b]
+                self.flat[lo:hi].div_(self.world)
+        self._works = []
+        self._pending = [len(idx) for idx in self._buckets]
+
+    def forward(self, *args, **kwargs):
+        return self.module(*args, **kwargs)
+
+    def no_sync(self):
+        """Context manager: backwards inside it accumulate local gradients without reducing them."""
+        import contextlib
+
+        @contextlib.contextmanager
+        def ctx():
+            old, self._sync = self._sync, False
+            try:
+                yield
+            finally:
+                self._sync = old
+        return ctx()
+
+
+def wrap_ddp(model, device, force=False, bucket_cap_mb=64, impl="bucketed", broadcast_buffers=True,
+             static_graph=False, comm_hook=None):
+    """Data parallelism over the initialised process group (idist.auto_model, script/train.py:83).
+    Without a process group of more than one rank the model is returned unwrapped, unless `force`
+    (the wrapper over a world-size-1 group: the reducer's own cost, tests).
+
+    impl "bucketed" (default): BucketedDataParallel, 64 MB buckets, one pack launch per bucket.
+    impl "torch": torch DistributedDataParallel (gradient_as_bucket_view; broadcast_buffers, static_graph
+    and the world-size-1 diagnostic comm_hook "world1_none" apply to it only), kept for A/B runs
+    (tools/ddp_variants.py).
 
     The modules' packed parameters (Attention W_q/W_k/W_v, the CSE q/k/v linears) are packed at
-    construction and after every device move, so DDP's buckets and hooks see the final storages.
-    DDP's all-reduces overlap the backward on RCCL's stream; with 4 hardware queues per process
+    construction and after every device move, so the reducer's buckets and hooks see the final storages.
+    The all-reduces overlap the backward on RCCL's stream; with 4 hardware queues per process
     (GPU_MAX_HW_QUEUES) an attention backward's side stream could share a queue with it and wait behind
     an in-flight all-reduce, so multi-rank GPU training keeps each attention backward on one stream
     (bwd_schedule "in_order", per module: no process-global switch)."""
@@ -234,9 +399,18 @@ def wrap_ddp(model, device, force=False, bucket_cap_mb=64):
     if world > 1 or (force and dist.is_initialized()):
         if device.type == "cuda" and world > 1:
             set_bwd_schedule(model, "in_order")
-        return torch.nn.parallel.DistributedDataParallel(
+        if impl == "bucketed":
+            return BucketedDataParallel(model, bucket_cap_mb=bucket_cap_mb)
+        if impl != "torch":
+            raise ValueError(f"wrap_ddp: unknown impl {impl!r}")
+        ddp = torch.nn.parallel.DistributedDataParallel(
             model, device_ids=[device.index] if device.type == "cuda" else None,
-            gradient_as_bucket_view=True, bucket_cap_mb=bucket_cap_mb)
+            gradient_as_bucket_view=True, bucket_cap_mb=bucket_cap_mb, broadcast_buffers=bool(broadcast_buffers),
+            static_graph=bool(static_graph))
+        if comm_hook == "world1_none":
+            assert world == 1, "the no-communication hook is a world-size-1 diagnostic"
+            ddp.register_comm_hook(None, _world1_no_comm_hook)
+        return ddp
     return model
 
 

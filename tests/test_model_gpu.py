@@ -206,19 +206,20 @@ def test_csatrans_python_dims_match_reference(golden):
 
 @pytest.mark.gpu
 @pytest.mark.skipif(not has_gpu(), reason="needs GPU")
-def test_csatrans_java_ddp_train_step_matches_reference(golden):
-    """script/train.py:73-86,103-116 as the reference runs it: the java CSATrans wrapped in
-    DistributedDataParallel (gradient_as_bucket_view, 64 MB buckets; forced at world size 1 over an
-    in-process RCCL group), make_train_step with GradScaler and the fused AdamW (eval mode, as the
-    fixture). Packed QKV parameters, bucket-view gradients and the optimizer step must reproduce the
-    reference golden exactly as the unwrapped model does."""
+@pytest.mark.parametrize("impl", ["bucketed", "torch"])
+def test_csatrans_java_ddp_train_step_matches_reference(golden, impl):
+    """script/train.py:73-86,103-116 as the reference runs it: the java CSATrans wrapped for data parallelism
+    (the bucketed reducer, and torch DistributedDataParallel with gradient_as_bucket_view; 64 MB buckets;
+    forced at world size 1 over an in-process RCCL group), make_train_step with GradScaler and the fused
+    AdamW (eval mode, as the fixture). Packed QKV parameters, flat-buffer gradients and the optimizer step
+    must reproduce the reference golden exactly as the unwrapped model does."""
     import socket
 
     import torch.distributed as dist
 
     import golden_inputs as gi
     from csa_amd.model import label_smoothing_loss
-    from csa_amd.train import AdamW, make_train_step, wrap_ddp
+    from csa_amd.train import AdamW, BucketedDataParallel, make_train_step, wrap_ddp
     z = golden("csatrans_java")
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -229,8 +230,8 @@ def test_csatrans_java_ddp_train_step_matches_reference(golden):
     try:
         m, (x, y) = _java_model_and_batch(dev)
         m = m.cuda()
-        ddp = wrap_ddp(m, dev, force=True)
-        assert isinstance(ddp, torch.nn.parallel.DistributedDataParallel)
+        ddp = wrap_ddp(m, dev, force=True, impl=impl)
+        assert isinstance(ddp, BucketedDataParallel if impl == "bucketed" else torch.nn.parallel.DistributedDataParallel)
         opt = AdamW(m.parameters(), lr=1e-4, correct_bias=False)
 
         def step_fn(x, y, scaler):
@@ -240,6 +241,11 @@ def test_csatrans_java_ddp_train_step_matches_reference(golden):
         # the packing survived DDP and the step: W_q/W_k/W_v still share one storage
         a = m.SBM.transformer_0.mha
         assert len({w.untyped_storage().data_ptr() for w in (a.W_q.weight, a.W_k.weight, a.W_v.weight)}) == 1
+        if impl == "bucketed":  # every gradient is a view of the one flat buffer, step after step
+            for _ in range(2):
+                step_fn(x, y, torch.amp.GradScaler("cuda"))
+                assert all(p.grad.untyped_storage().data_ptr() == ddp.flat.untyped_storage().data_ptr()
+                           for p in m.parameters())
     finally:
         dist.destroy_process_group()
 

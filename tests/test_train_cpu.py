@@ -85,26 +85,42 @@ def _packed_storage(model):
     return len({w.untyped_storage().data_ptr() for w in ws}) == 1
 
 
-def _worker(rank, world, port, q):
+def _batch(rank, i):
+    g = torch.Generator().manual_seed(100 + 10 * i + rank)  # per-rank shard (set_seed(seed + rank))
+    return torch.randn(4, 3, 6, generator=g), torch.randint(1, 5, (4, 3), generator=g)
+
+
+def _worker(rank, world, port, q, cases, steps):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     from csa_amd.model import label_smoothing_loss
-    from csa_amd.train import AdamW, init_distributed, make_train_step, wrap_ddp
+    from csa_amd.train import AdamW, BucketedDataParallel, init_distributed, make_train_step, wrap_ddp
     r, w, _, dev = init_distributed()
-    torch.manual_seed(0)
-    model = Tiny()
-    assert _packed_storage(model)
-    ddp = wrap_ddp(model, dev)
-    assert isinstance(ddp, torch.nn.parallel.DistributedDataParallel)
-    opt = AdamW(model.parameters(), lr=1e-3, correct_bias=False)
-    g = torch.Generator().manual_seed(100 + rank)  # per-rank shard (set_seed(seed + rank))
-    x = torch.randn(4, 3, 6, generator=g)
-    y = torch.randint(1, 5, (4, 3), generator=g)
-    step = make_train_step(ddp, opt, label_smoothing_loss, sw=1e-2)
-    step(x, y)
-    assert _packed_storage(model)  # DDP and the optimizer kept the packed storages
-    q.put((rank, [p.grad.numpy().copy() for p in model.parameters()],
-           [p.detach().numpy().copy() for p in model.parameters()]))
+    out = {}
+    for impl, cap_mb in cases:
+        torch.manual_seed(0 if rank == 0 else 1 + rank)  # different replicas: the wrapper broadcasts rank 0's
+        model = Tiny()
+        assert _packed_storage(model)
+        ddp = wrap_ddp(model, dev, impl=impl, bucket_cap_mb=cap_mb)
+        assert isinstance(ddp, BucketedDataParallel if impl == "bucketed" else torch.nn.parallel.DistributedDataParallel)
+        opt = AdamW(model.parameters(), lr=1e-3, correct_bias=False)
+        step = make_train_step(ddp, opt, label_smoothing_loss, sw=1e-2)
+        grads, weights = [], []
+        for i in range(steps):
+            step(*_batch(rank, i))
+            assert _packed_storage(model)  # the reducer and the optimizer kept the packed storages
+            grads.append([p.grad.numpy().copy() for p in model.parameters()])
+            weights.append([p.detach().numpy().copy() for p in model.parameters()])
+        # local accumulation under no_sync, then one synchronised backward over the accumulated gradients
+        opt.zero_grad(set_to_none=True)
+        with ddp.no_sync():
+            o, sp, *_ = ddp(_batch(rank, 7)[0])
+            (label_smoothing_loss(o, _batch(rank, 7)[1]) + 1e-2 * sp).backward()
+        o, sp, *_ = ddp(_batch(rank, 8)[0])
+        (label_smoothing_loss(o, _batch(rank, 8)[1]) + 1e-2 * sp).backward()
+        grads.append([p.grad.numpy().copy() for p in model.parameters()])
+        out[(impl, cap_mb)] = (grads, weights)
+    q.put((rank, out))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -118,37 +134,50 @@ def _free_port():
 
 
 def test_ddp_two_ranks_average_gradients():
-    """2-rank gloo DDP step == mean of the per-rank single-process gradients (DDP semantics), through the
-    packed QKV path (parameters packed before DDP is built, one GEMM forward, three gradient views of one
-    GEMM backward landing in gradient_as_bucket_view buckets) against plain unpacked per-rank GEMMs."""
+    """2-rank gloo data-parallel steps through the packed QKV path (parameters packed before the wrapper is
+    built, one GEMM forward, three gradient views of one GEMM backward): the bucketed reducer (one bucket, and
+    a tiny bucket cap giving one bucket per few parameters) and torch DDP. Step 1 == the mean of the per-rank
+    single-process gradients against plain unpacked per-rank GEMMs (DDP semantics) from rank 0's initial
+    weights (the wrapper's broadcast); every step's gradients and weights, and a no_sync accumulation
+    followed by a synchronised backward, are bit-identical between the bucketed reducer and DDP."""
     from csa_amd.model import label_smoothing_loss
+    cases = [("torch", 64), ("bucketed", 64), ("bucketed", 1e-4)]
+    steps = 3
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, cases, steps)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict((r, (g, w)) for r, g, w in [q.get(timeout=120) for _ in range(2)])
+    res = dict(q.get(timeout=180) for _ in range(2))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    # single-process per-rank gradients
+    # single-process per-rank gradients of step 1 from rank 0's initial weights
     ref = []
     for rank in range(2):
         torch.manual_seed(0)
         m = Tiny(packed=False)  # same initial values, plain per-layer GEMMs
-        g = torch.Generator().manual_seed(100 + rank)
-        x = torch.randn(4, 3, 6, generator=g)
-        y = torch.randint(1, 5, (4, 3), generator=g)
+        x, y = _batch(rank, 0)
         out, sp, *_ = m(x)
         (label_smoothing_loss(out, y) + 1e-2 * sp).backward()
         ref.append([p.grad.clone() for p in m.parameters()])
     mean = [(a + b) / 2 for a, b in zip(*ref)]
-    for rank in range(2):
-        for gd, gm in zip(res[rank][0], mean):
-            np.testing.assert_allclose(gd, gm.numpy(), rtol=1e-5, atol=1e-6)
-    for wa, wb in zip(res[0][1], res[1][1]):  # replicas stay identical after the step
-        np.testing.assert_array_equal(wa, wb)
+    for case in cases:
+        for rank in range(2):
+            for gd, gm in zip(res[rank][case][0][0], mean):
+                np.testing.assert_allclose(gd, gm.numpy(), rtol=1e-5, atol=1e-6)
+            for s in range(steps):  # replicas stay identical after every step
+                for wa, wb in zip(res[0][case][1][s], res[1][case][1][s]):
+                    np.testing.assert_array_equal(wa, wb)
+    for case in cases[1:]:
+        for rank in range(2):
+            for ga, gb in zip(res[rank][case][0], res[rank][cases[0]][0]):  # steps + the no_sync round
+                for x, y in zip(ga, gb):
+                    np.testing.assert_array_equal(x, y)
+            for wa, wb in zip(res[rank][case][1], res[rank][cases[0]][1]):
+                for x, y in zip(wa, wb):
+                    np.testing.assert_array_equal(x, y)
 
 
 def _reference_label_smoothing(x, target, padding_idx, smoothing):

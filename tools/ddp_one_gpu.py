@@ -5,7 +5,7 @@ Launch (no GPU call happens before the process group exists):
 
 Both ranks run on cuda:0 over the gloo backend (RCCL refuses two ranks on one GPU). Each rank builds the
 config/java.py CSATrans with the same deterministic weights, wraps it with csa_amd.train.wrap_ddp (world 2:
-DistributedDataParallel, gradient_as_bucket_view, 64 MB buckets, the packed QKV parameters, the in-order
+the bucketed reducer, or torch DDP with CSA_DDP_IMPL=torch; 64 MB buckets, the packed QKV parameters, the in-order
 attention backward) and runs one eval-mode step (script/train.py:103-116: label-smoothing loss +
 sw * sparsity, backward) on its own batch. It then runs the same step on an unwrapped copy of the model on the
 same batch and the same Philox seeds, all-gathers those per-rank gradients and checks that DDP's averaged
@@ -51,8 +51,8 @@ def main():
         return float(loss.detach())
 
     t0 = time.time()
-    ddp = wrap_ddp(build(), dev)
-    assert isinstance(ddp, torch.nn.parallel.DistributedDataParallel)
+    impl = os.environ.get("CSA_DDP_IMPL", "bucketed")
+    ddp = wrap_ddp(build(), dev, impl=impl)
     loss_ddp = step(ddp)
     g_ddp = {k: p.grad.detach().clone() for k, p in ddp.module.named_parameters() if p.grad is not None}
 
@@ -72,7 +72,7 @@ def main():
     losses = [None] * world
     dist.all_gather_object(losses, (loss_ddp, loss_ref))
     if rank == 0:
-        print(json.dumps({"test": "DDP (gloo, 2 ranks on cuda:0) gradient == mean of per-rank gradients",
+        print(json.dumps({"test": "DDP (gloo, 2 ranks on cuda:0) gradient == mean of per-rank gradients", "impl": impl,
                           "model": "config/java.py CSATrans (HIP kernels), eval mode", "per_rank_batch": B,
                           "world": world, "tensors": len(g_ref), "tensors_off": int(nbad),
                           "worst_rel_diff": worst, "per_rank_loss_ddp_vs_plain": losses,
