@@ -349,7 +349,8 @@ def train_step_bench(world, rank, dev, steps, warmup, config="java", per_gpu_bat
             "global_batch": per_gpu_batch * world, "steps": steps, "warmup": warmup,
             "ms_per_step": round(el * 1000 / steps, 3), "samples_per_s": round(world * per_gpu_batch * steps / el, 1),
             "params": nparam, "mean_loss": round(mean_loss, 4), "n_ranks": world,
-            "exchange": (f"{reducer} gradient all-reduce over RCCL (64 MB buckets)" if world > 1 else
+            "exchange": (f"{reducer} gradient all-reduce over RCCL ({16 if impl == 'bucketed' else 64} MB buckets)"
+                         if world > 1 else
                          f"{reducer} over a world-size-1 RCCL group (hooks + bucket packing, no peer)" if force_ddp
                          else "none (1 GPU, unwrapped)")}
 

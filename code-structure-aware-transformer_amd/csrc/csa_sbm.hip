@@ -250,6 +250,14 @@ __device__ __forceinline__ void frag_chain(const float* __restrict__ frag, int n
     for (int t = 0; t < NTO; ++t)
 #pragma unroll
       for (int e = 0; e < 4; ++e) out[t] = mfma(wq[s4 % (LA + 1)][t][e], bval(4 * s4 + e), out[t]);
+#ifndef CSA_EXP_FL_SINK
+    if constexpr (FL) {
+      // LDS fragments: the scheduler otherwise sinks the lookahead reads to the group's last MFMA (register
+      // pressure heuristics), so the next group starts on lgkmcnt(0); pin them ahead of the group's MFMAs
+      if (s4 + LA < S4N) __builtin_amdgcn_sched_group_barrier(0x100, NTO, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 4 * NTO, 0);
+    }
+#endif
     fence_sched();
   }
 }

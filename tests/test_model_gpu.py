@@ -209,7 +209,7 @@ def test_csatrans_python_dims_match_reference(golden):
 @pytest.mark.parametrize("impl", ["bucketed", "torch"])
 def test_csatrans_java_ddp_train_step_matches_reference(golden, impl):
     """script/train.py:73-86,103-116 as the reference runs it: the java CSATrans wrapped for data parallelism
-    (the bucketed reducer, and torch DistributedDataParallel with gradient_as_bucket_view; 64 MB buckets;
+    (the bucketed reducer with 16 MB buckets, and torch DistributedDataParallel with gradient_as_bucket_view, 64 MB;
     forced at world size 1 over an in-process RCCL group), make_train_step with GradScaler and the fused
     AdamW (eval mode, as the fixture). Packed QKV parameters, flat-buffer gradients and the optimizer step
     must reproduce the reference golden exactly as the unwrapped model does."""

@@ -5,7 +5,7 @@ Launch (no GPU call happens before the process group exists):
 
 Both ranks run on cuda:0 over the gloo backend (RCCL refuses two ranks on one GPU). Each rank builds the
 config/java.py CSATrans with the same deterministic weights, wraps it with csa_amd.train.wrap_ddp (world 2:
-the bucketed reducer, or torch DDP with CSA_DDP_IMPL=torch; 64 MB buckets, the packed QKV parameters, the in-order
+the bucketed reducer (16 MB buckets), or torch DDP with CSA_DDP_IMPL=torch (64 MB); the packed QKV parameters, the in-order
 attention backward) and runs one eval-mode step (script/train.py:103-116: label-smoothing loss +
 sw * sparsity, backward) on its own batch. It then runs the same step on an unwrapped copy of the model on the
 same batch and the same Philox seeds, all-gathers those per-rank gradients and checks that DDP's averaged
