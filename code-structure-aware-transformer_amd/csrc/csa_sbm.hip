@@ -205,8 +205,12 @@ __device__ __forceinline__ f32x4 frag4_lds(const float* __restrict__ f, int it, 
 // BF16: the same chain on v_mfma_f32_32x32x16_bf16 (CSA_DTYPE_BF16's projection contractions): one
 // instruction takes two consecutive K-groups (8 K-steps, csa_common.hpp pack8), both operands rounded to
 // bf16 (RNE) as they are packed; accumulation stays fp32. S4N must be even.
-template <int NTO, int S4N, int LA = 1, bool FL = false, bool BF16 = false, typename BV>
-__device__ __forceinline__ void frag_chain(const float* __restrict__ frag, int nsteps, f32x16 (&out)[NTO], BV bval) {
+// side(g) runs inside K-group g's scheduling region (g = 0 .. groups - 1; a compile-time constant once the loop is
+// unrolled): independent work (activation stores, ActStager) that the scheduler interleaves with the group's MFMAs.
+struct NoSide { __device__ __forceinline__ void operator()(int) const {} };
+template <int NTO, int S4N, int LA = 1, bool FL = false, bool BF16 = false, typename BV, typename SIDE = NoSide>
+__device__ __forceinline__ void frag_chain(const float* __restrict__ frag, int nsteps, f32x16 (&out)[NTO], BV bval,
+                                           SIDE side = SIDE()) {
   static_assert(LA == 1 || LA == 2, "lookahead of one or two K-groups");
   auto ld = [&](int t, int s4) { return FL ? frag4_lds(frag, t, nsteps, s4) : frag4(frag, t, nsteps, s4); };
   if constexpr (BF16) {
@@ -230,6 +234,7 @@ __device__ __forceinline__ void frag_chain(const float* __restrict__ frag, int n
       const bf16x8 b8 = pack8(bv);
 #pragma unroll
       for (int t = 0; t < NTO; ++t) out[t] = mfma_bf(pack8(wq[s8 & 1][t][0], wq[s8 & 1][t][1]), b8, out[t]);
+      side(s8);
       fence_sched();
     }
     return;
@@ -258,6 +263,7 @@ __device__ __forceinline__ void frag_chain(const float* __restrict__ frag, int n
       __builtin_amdgcn_sched_group_barrier(0x008, 4 * NTO, 0);
     }
 #endif
+    side(s4);
     fence_sched();
   }
 }
@@ -419,6 +425,9 @@ __device__ __forceinline__ uint32_t u16_of(const u32x4& r, int e) {
 // mask keyed by (row, feature, layer, Q/K), so the backward regenerates it bit-identically.
 template <int D>
 __device__ __forceinline__ void mlp_act(const KArgs& p, f32x16 (&a)[D / 32], int layer, int row, int bh, int isK) {
+#ifdef CSA_EXP_PF_MFMA_ONLY  // experiment: the projection forward's MFMA chains alone (wrong results)
+  return;
+#endif
   constexpr int DT = D / 32;
   const int h = lane_id() >> 5;
   const bool drop = p.proj_p > 0.f;
@@ -489,43 +498,37 @@ __device__ __forceinline__ void mlp_layer0(const KArgs& p, const float* W0, cons
 }
 
 // out = W_l in + b_l  (acc-perm input), l = 1, 2
-template <int D, bool FL, bool BF = false>
+template <int D, bool FL, bool BF = false, typename SIDE = NoSide>
 __device__ __forceinline__ void mlp_layer(const float* Wl, const float* bl, const f32x16 (&in)[D / 32],
-                                          f32x16 (&out)[D / 32]) {
+                                          f32x16 (&out)[D / 32], SIDE side = SIDE()) {
   constexpr int DT = D / 32, NS = D / 2;
   float ba[DT];
   bias_operand<D>(bl, ba);
 #pragma unroll
   for (int ot = 0; ot < DT; ++ot) out[ot] = zero16();
-  frag_chain<DT, NS / 4, FL ? FL_LA : MLP_LA, FL, BF>(Wl, NS, out, [&](int s) { return in[s / 16][s % 16]; });
+  frag_chain<DT, NS / 4, FL ? FL_LA : MLP_LA, FL, BF>(Wl, NS, out, [&](int s) { return in[s / 16][s % 16]; }, side);
   add_bias<D>(ba, out);
 }
 
-// BF: CSA_DTYPE_BF16 (the three d x d layers on bf16 MFMA; biases, dropout and ReLU in fp32)
-template <int D, bool FL, bool BF = false>
-__device__ __forceinline__ void mlp_fwd(const KArgs& p, const FwdFrags& F, const float (&x)[D / 2], f32x16 (&h1)[D / 32],
-                                        f32x16 (&h2)[D / 32], f32x16 (&po)[D / 32], int row, int bh, int isK) {
-  mlp_layer0<D, FL, BF>(p, F.W[0], F.b[0], x, h1, row, bh, isK);
-  mlp_layer<D, FL, BF>(F.W[1], F.b[1], h1, h2);
-  mlp_act<D>(p, h2, 1, row, bh, isK);
-  mlp_layer<D, FL, BF>(F.W[2], F.b[2], h2, po);
-}
-
 // hat^T = sigmoid(C_h p^T), rows (clusters) >= k zeroed. Cf: the head's cluster fragments.
-template <int D, int KT, bool FL, bool BF = false>
-__device__ __forceinline__ void cluster_hat(const KArgs& p, const float* Cf, const f32x16 (&po)[D / 32], f32x16 (&hat)[KT]) {
+template <int D, int KT, bool FL, bool BF = false, typename SIDE = NoSide>
+__device__ __forceinline__ void cluster_hat(const KArgs& p, const float* Cf, const f32x16 (&po)[D / 32], f32x16 (&hat)[KT],
+                                            SIDE side = SIDE()) {
   constexpr int NS = D / 2;
   const int h = lane_id() >> 5;
 #pragma unroll
   for (int kt = 0; kt < KT; ++kt) hat[kt] = zero16();
-  frag_chain<KT, NS / 4, 1, FL, BF>(Cf, NS, hat, [&](int s) { return po[s / 16][s % 16]; });
+  frag_chain<KT, NS / 4, 1, FL, BF>(Cf, NS, hat, [&](int s) { return po[s / 16][s % 16]; }, side);
 #pragma unroll
   for (int kt = 0; kt < KT; ++kt) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int a = 32 * kt + crow(r, h);
       // sigmoid via hardware exp / divide (a few ulp; branch-free): sbm_attn.py:47,53
+#ifndef CSA_EXP_PF_MFMA_ONLY
       hat[kt][r] = (a < p.k) ? __fdividef(1.f, 1.f + __expf(-hat[kt][r])) : 0.f;
+#endif
+      (void)a;
     }
   }
 }
@@ -628,6 +631,75 @@ __device__ __forceinline__ void store_act_lds_bf(float* __restrict__ blk, const 
   }
 }
 
+#ifdef CSA_EXP_ACT_AUX  // experiment: other cache policies for the staged activation stores
+constexpr int CSA_AUX_NT = CSA_EXP_ACT_AUX;
+#else
+constexpr int CSA_AUX_NT = 2;  // buffer instruction cache policy: non-temporal (as __builtin_nontemporal_store)
+#endif
+// store_act_lds / store_act_lds_bf split into three stages per tile, so that the stores ride along an MFMA chain
+// as its side work (frag_chain's side(g)) instead of running as a phase of their own after the item's products
+// (round 5: the store phase was 25% of a k_proj_fwd_l wave's time, s_memtime stamps). Stage W: the tile's 16
+// scattered ds_write_b32 into the scratch; R: its nf / 8 ds_read_b128 back; S: the non-temporal global stores.
+// Chain group 2t runs S(t - 1) then W(t), group 2t + 1 runs R(t), group 2 NT runs S(NT - 1), so a chain of
+// >= 2 NT + 1 K-groups carries NT tiles. A wave's LDS operations complete in order, so W(t) may follow R(t - 1)
+// into the same scratch without a wait. Same bytes in the same places as store_act_lds(_bf).
+// The global stores go through a buffer resource over the item's activation block (num_records 0 when the call
+// saves no activations: the hardware drops them), so no branch splits the chain's scheduling regions; `off` is
+// the slice's byte offset in the block.
+template <int NT, int NF = 32 * NT, bool BFS = false>
+struct ActStager {
+  __amdgpu_buffer_rsrc_t rs;
+  int off;
+  float* scr;
+  const f32x16* a;
+  f32x4 v[4];
+  __device__ __forceinline__ static constexpr int nf(int t) { return NF - 32 * t < 32 ? NF - 32 * t : 32; }
+  __device__ __forceinline__ void W(int t) {
+    const int c = lane_id() & 31, h = lane_id() >> 5;
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      if (crow(r, 0) < nf(t)) scr[act_off(crow(r, h), c)] = a[t][r];
+  }
+  __device__ __forceinline__ void R(int t) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (k < nf(t) / 8) v[k] = *reinterpret_cast<const f32x4*>(scr + 4 * (lane + 64 * k));
+  }
+  __device__ __forceinline__ void S(int t) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (k >= nf(t) / 8) continue;
+      if constexpr (BFS) {
+        bf16x4 b;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) b[e] = (__bf16)v[k][e];
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2v, b), rs, 8 * lane,
+                                              off + 8 * (256 * t + 64 * k), CSA_AUX_NT);
+      } else {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, v[k]), rs, 16 * lane,
+                                               off + 4 * (1024 * t + 256 * k), CSA_AUX_NT);
+      }
+    }
+  }
+  // the side work of chain group g
+  __device__ __forceinline__ void operator()(int g) {
+    if ((g & 1) == 0) {
+      if (g >= 2 && g / 2 - 1 < NT) S(g / 2 - 1);
+      if (g / 2 < NT) W(g / 2);
+    } else if (g / 2 < NT) {
+      R(g / 2);
+    }
+  }
+  // stages a chain of `groups` K-groups did not reach (none when groups >= 2 NT + 1)
+  __device__ __forceinline__ void finish(int groups) {
+#pragma unroll
+    for (int g = 0; g <= 2 * NT; ++g)
+      if (g >= groups) (*this)(g);
+  }
+};
+
 // The bf16 slice of store_act_lds_bf, DMA'd into the upper half of a wave's R-float LDS region, widened in
 // place to the fp32 slice over the whole region (element order, hence the act_off layout, unchanged).
 // Elements [0, R/2) first: their fp32 lands below the bf16 data. Then [R/2, R): every read of the phase
@@ -705,68 +777,67 @@ __device__ __forceinline__ void proj_fwd_item(const KArgs& p, const FwdFrags& F,
   unsigned long long* ph = g_phf[threadIdx.x >> 6];
   unsigned long long tq = __builtin_amdgcn_s_memtime();
 #define PHF(i) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if ((blockIdx.x | blockIdx.y) == 0) ph[i] += t_ - tq; tq = t_; }
+#else
+#define PHF(i)
+#endif
+  constexpr bool ABF = BF && (D == 64 || D == 96) && KT == 1;  // read back by k_proj_bwd_s<D, true>
+  constexpr int ABLK = (3 * D + 32 * KT) * 32;
+  // fp32 activations: h1 | h2 | po leave as the side work of the chain that consumes them (layer 1, layer 2, the
+  // cluster product: ActStager), their stores interleaved with that chain's MFMAs instead of a store phase after
+  // the item's products; hat and the Qh / Kh / T rows at the end
+#if defined(CSA_EXP_STORE_PHASE) || defined(CSA_EXP_NO_ACT) || defined(CSA_EXP_RECOMP_PO)
+  constexpr bool STAGED = false;
+#else
+  constexpr bool STAGED = !BF;
+#endif
+  // unstaged d = 96 (java dims, 256 VGPRs): h1 leaves right after layer 1 has consumed it instead of being held to
+  // the item's end with h2 / po / hat (the held h1 spilled 18 VGPRs)
+#ifdef CSA_EXP_H1_LATE
+  constexpr bool H1E = false;
+#else
+  constexpr bool H1E = !STAGED && D == 96;
+#endif
+  float* const blk = p.Act ? p.Act + ((int64_t)bh * (p.NQB + p.NKB) + r) * ABLK : nullptr;
+  const bool on = blk != nullptr;
+  const __amdgpu_buffer_rsrc_t ars = make_rsrc(blk, on ? ABLK * 4 : 0);
+  struct Side {
+    ActStager<D / 32> st;
+    __device__ __forceinline__ void operator()(int g) { if constexpr (STAGED) st(g); }
+  };
   mlp_layer0<D, FL, BF>(p, F.W[0], F.b[0], x, h1, row, bh, isK);
   PHF(0)
-  mlp_layer<D, FL, BF>(F.W[1], F.b[1], h1, h2);
+  mlp_layer<D, FL, BF>(F.W[1], F.b[1], h1, h2, Side{{ars, 0, scr, h1, {}}});
+#ifndef CSA_EXP_NO_ACT
+  if (H1E && on) {
+    if (ABF && p.kp <= 16) store_act_lds_bf<D / 32>(blk, h1, scr);
+    else store_act_lds<D / 32>(blk, h1, scr);
+  }
+#endif
   PHF(1)
   mlp_act<D>(p, h2, 1, row, bh, isK);
   PHF(2)
-  mlp_layer<D, FL, BF>(F.W[2], F.b[2], h2, po);
+  mlp_layer<D, FL, BF>(F.W[2], F.b[2], h2, po, Side{{ars, 32 * D * 4, scr, h2, {}}});
   PHF(3)
-  cluster_hat<D, KT, FL, BF>(p, F.C, po, hat);
+  cluster_hat<D, KT, FL, BF>(p, F.C, po, hat, Side{{ars, 64 * D * 4, scr, po, {}}});
   PHF(4)
   if (isK) small_mm<KT, FL>(F.S, hat, t);
   next();
   PHF(5)
-#else
-  // d = 96 (java dims, 256 VGPRs): h1 leaves right after layer 1 has consumed it instead of being held to the
-  // item's end with h2 / po / hat (the held h1 spilled 18 VGPRs)
-#ifdef CSA_EXP_H1_LATE
-  constexpr bool H1E = false;
-#else
-  constexpr bool H1E = (D == 96);
-#endif
-  constexpr bool ABF = BF && (D == 64 || D == 96) && KT == 1;  // read back by k_proj_bwd_s<D, true>
-  constexpr int ABLK = (3 * D + 32 * KT) * 32;
-  auto act_blk = [&] { return p.Act + ((int64_t)bh * (p.NQB + p.NKB) + r) * ABLK; };
-  if constexpr (H1E) {
-    mlp_layer0<D, FL, BF>(p, F.W[0], F.b[0], x, h1, row, bh, isK);
-    mlp_layer<D, FL, BF>(F.W[1], F.b[1], h1, h2);
 #ifndef CSA_EXP_NO_ACT
-    if (p.Act) {
-      float* const blk = act_blk();
-      if (ABF && p.kp <= 16) store_act_lds_bf<D / 32>(blk, h1, scr);
-      else store_act_lds<D / 32>(blk, h1, scr);
-    }
-#endif
-    mlp_act<D>(p, h2, 1, row, bh, isK);
-    mlp_layer<D, FL, BF>(F.W[2], F.b[2], h2, po);
-  } else {
-    mlp_fwd<D, FL, BF>(p, F, x, h1, h2, po, row, bh, isK);
-  }
-  cluster_hat<D, KT, FL, BF>(p, F.C, po, hat);
-  if (isK) small_mm<KT, FL>(F.S, hat, t);
-  next();
-#endif
-#ifndef CSA_EXP_NO_ACT
-  if (p.Act) {  // save the activations for k_proj_bwd (item r of this (b,h): Q blocks, then K blocks)
-#ifdef CSA_PHASES_FWD
-    constexpr bool H1E = false, ABF = BF && (D == 64 || D == 96) && KT == 1;
-    constexpr int ABLK = (3 * D + 32 * KT) * 32;
-    auto act_blk = [&] { return p.Act + ((int64_t)bh * (p.NQB + p.NKB) + r) * ABLK; };
-#endif
-    float* const blk = act_blk();
-    if (ABF && p.kp <= 16) {
-      if (!H1E) store_act_lds_bf<D / 32>(blk, h1, scr);
-      store_act_lds_bf<D / 32>(blk + 32 * D, h2, scr);
-      store_act_lds_bf<D / 32>(blk + 64 * D, po, scr);
-    } else {
-      if (!H1E) store_act_lds<D / 32>(blk, h1, scr);
-      store_act_lds<D / 32>(blk + 32 * D, h2, scr);
+  if (on) {  // save the activations for k_proj_bwd (item r of this (b,h): Q blocks, then K blocks)
+    if constexpr (!STAGED) {
+      if (ABF && p.kp <= 16) {
+        if (!H1E) store_act_lds_bf<D / 32>(blk, h1, scr);
+        store_act_lds_bf<D / 32>(blk + 32 * D, h2, scr);
+        store_act_lds_bf<D / 32>(blk + 64 * D, po, scr);
+      } else {
+        if (!H1E) store_act_lds<D / 32>(blk, h1, scr);
+        store_act_lds<D / 32>(blk + 32 * D, h2, scr);
 #ifdef CSA_EXP_RECOMP_PO  // experiment: k_proj_bwd_s<64> recomputes po from h2
-      if (!(D == 64 && KT == 1 && p.kp <= 16))
+        if (!(D == 64 && KT == 1 && p.kp <= 16))
 #endif
-      store_act_lds<D / 32>(blk + 64 * D, po, scr);
+        store_act_lds<D / 32>(blk + 64 * D, po, scr);
+      }
     }
     bool hat16 = false;
     if constexpr (KT == 1) {
@@ -778,16 +849,17 @@ __device__ __forceinline__ void proj_fwd_item(const KArgs& p, const FwdFrags& F,
     if (!hat16) store_act_lds<KT>(blk + 96 * D, hat, scr);
   }
 #endif
+#ifdef CSA_EXP_PF_MFMA_ONLY
+  if (row == -1)
+#endif
   if (!isK) {
     store_rows<KT>(p.Qh + ((int64_t)bh * p.N + row) * p.kp, p.kp, p.kp, hat, rv);
   } else {
     store_rows<KT>(p.Kh + ((int64_t)bh * p.M + row) * p.kp, p.kp, p.kp, hat, rv);
     store_rows<KT>(p.T + ((int64_t)bh * p.M + row) * p.kp, p.kp, p.kp, t, rv);
   }
-#ifdef CSA_PHASES_FWD
   PHF(6)
 #undef PHF
-#endif
   (void)lane; (void)h;
 }
 
@@ -857,7 +929,9 @@ __global__ __launch_bounds__((64 * ProjFwdLds<D, KT>::NW)) void k_proj_fwd_l(con
   for (int it = i_lo + w; it < i_hi; it += LY::NW) {
     const int nx = it + LY::NW;
     auto nextf = [&] {
+#ifndef CSA_EXP_PF_MFMA_ONLY
       if (nx < i_hi) load_item_x<D>(p, nx / per_b, hd, nx % per_b, x);
+#endif
     };
     proj_fwd_item<D, KT, true, decltype(nextf), BF>(p, F, it / per_b, hd, it % per_b, x, scr, nextf);
   }

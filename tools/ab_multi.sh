@@ -3,7 +3,7 @@
 # ms/step + per-stage kernel times of each run. usage: BENCH_ARGS="..." bash tools/ab_multi.sh R lib...
 set -o pipefail
 R=$1; shift
-ARGS=${BENCH_ARGS:-"--steps 20 --warmup 3 --no-cpu-baseline --no-train --no-bf16-leg --no-cpu-config1"}
+ARGS=${BENCH_ARGS:-"--steps 20 --warmup 3 --no-cpu-baseline --no-train --no-bf16-leg --no-padded-leg --no-cpu-config1"}
 for i in $(seq 1 "$R"); do
   for L in "$@"; do
     out=$(CSA_HIP_LIB=$L timeout -k 10 120 python bench.py $ARGS) || exit $?
