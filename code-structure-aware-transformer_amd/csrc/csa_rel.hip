@@ -477,10 +477,59 @@ __global__ __launch_bounds__(64) void k_rel_scatter(const RelArgs p, float* __re
 // (asymmetric) mask stays exact. Entries outside [0,N)^2 hold 0x0100.
 __host__ __device__ constexpr int tile_pos(int j) { return 16 * ((j >> 2) & 1) + (j & 3) + 4 * (j >> 3); }
 
-// One 32 x 32 tile of one plane per workgroup; a thread codes 4 consecutive columns of one row, which
+// One 32-row block of one plane per workgroup (round 5; was one 32 x 32 tile per workgroup, 5x the workgroups
+// for the same bytes: 11.6 us at B = 64, latency-bound). The block's rel / mask rows are one contiguous byte
+// range of the (.., N, N) plane, staged into LDS (dword loads when it is 4-byte aligned, as at N = 150); a
+// thread then codes 4 consecutive columns of one row in every column tile, which tile_pos keeps contiguous
+// (positions 16 (k & 1) + 4 (k >> 1) + 0..3 for column group k): RM takes one 8-B store per thread and tile, and
+// so does RT, whose row y of this block reads the staged column y.
+// Dynamic LDS: rel_prep_lds_bytes(N) = two staged 32 x N byte blocks (64 KB at N = 1024).
+inline size_t rel_prep_lds_bytes(int64_t N) { return 2 * (size_t)((32 * N + 15) / 16 * 16); }
+__global__ __launch_bounds__(256) void k_rel_prep(const RelArgs p, uint16_t* __restrict__ RM, uint16_t* __restrict__ RT) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t srel[];
+  uint8_t* const smask = srel + (32 * p.N + 15) / 16 * 16;
+  const int NT = p.NP / 32, at = (int)blockIdx.x;
+  const int bp = blockIdx.y, b = bp / p.P_, pl = bp % p.P_;
+  const int hd = p.group > 0 ? (pl == 0 ? 0 : p.group) : pl;  // a head that reads plane pl
+  const int a0 = at * 32, nrow = imin(32, p.N - a0);
+  const uint8_t* rp = p.rel + plane_off(p, b, hd, p.rel_sb, p.rel_sh) + (int64_t)a0 * p.N;
+  const uint8_t* mp = p.mask + plane_off(p, b, hd, p.mask_sb, p.mask_sh) + (int64_t)a0 * p.N;
+  const int nbytes = nrow * p.N, t = (int)threadIdx.x;
+  if ((((uintptr_t)rp | (uintptr_t)mp | (uintptr_t)nbytes) & 3) == 0) {
+    for (int e = t; e < nbytes / 4; e += 256) {
+      reinterpret_cast<uint32_t*>(srel)[e] = reinterpret_cast<const uint32_t*>(rp)[e];
+      reinterpret_cast<uint32_t*>(smask)[e] = reinterpret_cast<const uint32_t*>(mp)[e];
+    }
+  } else {
+    for (int e = t; e < nbytes; e += 256) { srel[e] = rp[e]; smask[e] = mp[e]; }
+  }
+  __syncthreads();
+  uint16_t* rm = RM + (size_t)bp * p.NP * p.NP;
+  uint16_t* rt = RT + (size_t)bp * p.NP * p.NP;
+  const int rl = t >> 3, k = t & 7, pos = 16 * (k & 1) + 4 * (k >> 1);
+  const int a = a0 + rl;
+  auto code = [&](int row, int col) -> uint32_t {  // staged (row, col) of this block; 0x0100 outside [0,N)^2
+    if (row >= nrow || col >= p.N) return 0x0100u;
+    int r = srel[row * p.N + col];
+    r = r < p.L ? r : p.L - 1;  // memory safety; the reference requires rel < L
+    return (uint32_t)r | (smask[row * p.N + col] ? 0x100u : 0u);
+  };
+  for (int bt = 0; bt < NT; ++bt) {
+    const int c0 = bt * 32 + 4 * k;
+    // RM row a, columns c0 .. c0 + 3: rel[a][c] | mask[a][c] << 8
+    *reinterpret_cast<uint2*>(rm + (size_t)a * p.NP + bt * 32 + pos) =
+        uint2{code(rl, c0) | (code(rl, c0 + 1) << 16), code(rl, c0 + 2) | (code(rl, c0 + 3) << 16)};
+    // RT row y = bt * 32 + rl, columns a0 + 4 k .. + 3: rel[x][y] of the staged rows x
+    const int y = bt * 32 + rl, x0 = 4 * k;
+    *reinterpret_cast<uint2*>(rt + (size_t)y * p.NP + a0 + pos) =
+        uint2{code(x0, y) | (code(x0 + 1, y) << 16), code(x0 + 2, y) | (code(x0 + 3, y) << 16)};
+  }
+}
+
+// k_rel_prep for N > 1024 (its staged rows would exceed 64 KB of LDS): one 32 x 32 tile of one plane per workgroup; a thread codes 4 consecutive columns of one row, which
 // tile_pos keeps contiguous (positions 16 (k & 1) + 4 (k >> 1) + 0..3 for column group k), so RM and RT
 // take one 8-B store per thread (RT through the LDS transpose).
-__global__ __launch_bounds__(256) void k_rel_prep(const RelArgs p, uint16_t* __restrict__ RM, uint16_t* __restrict__ RT) {
+__global__ __launch_bounds__(256) void k_rel_prep_t(const RelArgs p, uint16_t* __restrict__ RM, uint16_t* __restrict__ RT) {
   __shared__ uint16_t tile[32][36];  // [row a][column b] of the tile's codes (36: 8-B aligned rows)
   const int NT = p.NP / 32, at = (int)blockIdx.x / NT, bt = (int)blockIdx.x % NT;
   const int bp = blockIdx.y, b = bp / p.P_, pl = bp % p.P_;
@@ -2006,8 +2055,14 @@ csa_status csa_rel_attn_fwd(const csa_rel_attn_args* a, void* stream) {
     hipLaunchKernelGGL(k_rel_logits<64>, dim3(xcd_grid(2 * (int)((p.NQB + 1) / 2), (int)(a->B * a->H))), dim3(64),
                        32 * 64 * 4, st, p, (float*)p.c2p, (float*)p.p2ct);
     const int NT = (int)(R.NP / 32);
-    hipLaunchKernelGGL(k_rel_prep, dim3((unsigned)(NT * NT), (unsigned)(a->B * p.P_)), dim3(256), 0, st, p,
-                       (uint16_t*)p.RM, (uint16_t*)p.RT);
+    if (rel_prep_lds_bytes(a->N) <= 65536) {
+      set_dyn_lds((const void*)k_rel_prep, (int)rel_prep_lds_bytes(a->N));
+      hipLaunchKernelGGL(k_rel_prep, dim3((unsigned)NT, (unsigned)(a->B * p.P_)), dim3(256), rel_prep_lds_bytes(a->N),
+                         st, p, (uint16_t*)p.RM, (uint16_t*)p.RT);
+    } else {
+      hipLaunchKernelGGL(k_rel_prep_t, dim3((unsigned)(NT * NT), (unsigned)(a->B * p.P_)), dim3(256), 0, st, p,
+                         (uint16_t*)p.RM, (uint16_t*)p.RT);
+    }
     if (p.bf16) hipLaunchKernelGGL((k_rel_fwd_f<64, true>), grid, dim3(64), 2 * 32 * 64 * 4, st, p);
     else hipLaunchKernelGGL((k_rel_fwd_f<64, false>), grid, dim3(64), 2 * 32 * 64 * 4, st, p);
     return rcheck("csa_rel_attn_fwd");

@@ -146,3 +146,30 @@ def test_rel_attn_full_size_rows_match_oracle_and_deterministic():
         ref = t[i - 1].grad.numpy()
         np.testing.assert_allclose(r1[i].numpy(), ref, rtol=RTOL, atol=ATOL * max(1.0, np.abs(ref).max() / 100),
                                    err_msg=n)
+
+
+@pytest.mark.skipif(not has_gpu(), reason="needs GPU")
+def test_rel_attn_long_ast_tile_prep_matches_oracle():
+    """N = 1040 > 1024: the relation planes are prepared one 32 x 32 tile per workgroup (k_rel_prep_t; at
+    N <= 1024 k_rel_prep stages whole 32-row blocks in LDS, covered by every other test here: dword staging at
+    N = 150, byte staging at N = 37 and 23). Random relation codes and masks in the compact (B,2,N,N) layout;
+    outputs and gradients vs the fp64 oracle."""
+    from oracle import cse_ref
+    B, H, N, dk, L = 1, 8, 1040, 64, 150
+    g = torch.Generator().manual_seed(21)
+    Lr, Tr = (torch.randint(0, L, (B, N, N), generator=g, dtype=torch.int64) for _ in range(2))
+    Lm, Tm = ((torch.rand(B, N, N, generator=g) < 0.3) for _ in range(2))
+    q, k, v, dO = (torch.randn(B, H, N, dk, generator=g) for _ in range(4))
+    lq, lk = (torch.randn(1, H, L, dk, generator=g) for _ in range(2))
+    rel = torch.stack([Lr, Tr], 1).to(torch.uint8)
+    mask = torch.stack([Lm, Tm], 1).to(torch.uint8)
+    r = _run_rel(q, k, v, lq, lk, rel, mask, dO)
+    refrel, refmask = cse_ref.build_rel_mask(Lr, Tr, Lm, Tm)
+    t = [x.double().requires_grad_(True) for x in (q, k, v, lq, lk)]
+    o = cse_ref.rel_attn(*t, refrel, refmask)
+    (o * dO.double()).sum().backward()
+    np.testing.assert_allclose(r[0].numpy(), o.detach().numpy(), rtol=RTOL, atol=ATOL)
+    for i, n in ((1, "dq"), (2, "dk"), (3, "dv"), (4, "dlq"), (5, "dlk")):
+        ref = t[i - 1].grad.numpy()
+        np.testing.assert_allclose(r[i].numpy(), ref, rtol=RTOL, atol=ATOL * max(1.0, np.abs(ref).max() / 100),
+                                   err_msg=n)
