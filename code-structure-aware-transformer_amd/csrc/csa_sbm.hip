@@ -457,6 +457,17 @@ __device__ __forceinline__ void mlp_act(const KArgs& p, f32x16 (&a)[D / 32], int
     }
 }
 
+// fp32, k <= 16, d = 64 / 96 (k_proj_bwd_s): the cluster-weight gradient is formed from h2 instead of po,
+//   dC_h = sum dZ^T po = (sum dZ^T h2) W2^T + (sum dZ^T 1) b2^T     (po = h2 W2^T + b2, proj.6)
+// so the forward does not save po (a third of the activation bytes: 168 MB written and read per B = 256 step) and
+// k_cluster_grad applies W2 / b2 once per head. A reassociation of the same sums (fp32 rounding only).
+#if defined(CSA_EXP_SAVE_PO) || defined(CSA_EXP_RECOMP_PO)
+constexpr bool H2C_ON = false;
+#else
+constexpr bool H2C_ON = true;
+#endif
+__host__ __device__ constexpr bool h2c_path(int D, int KT, bool BF) { return H2C_ON && !BF && (D == 64 || D == 96) && KT == 1; }
+
 constexpr int MLP_LA = 2;  // forward MLP chains: fragments two K-groups ahead
 #ifdef CSA_EXP_FL2
 constexpr int FL_LA = 2;   // LDS fragment chains: lookahead (experiment)
@@ -818,7 +829,9 @@ __device__ __forceinline__ void proj_fwd_item(const KArgs& p, const FwdFrags& F,
   PHF(2)
   mlp_layer<D, FL, BF>(F.W[2], F.b[2], h2, po, Side{{ars, 32 * D * 4, scr, h2, {}}});
   PHF(3)
-  cluster_hat<D, KT, FL, BF>(p, F.C, po, hat, Side{{ars, 64 * D * 4, scr, po, {}}});
+  // po is not saved when k_proj_bwd_s forms dC from h2 (h2c_path): its stores go to a null range
+  const __amdgpu_buffer_rsrc_t ars_po = make_rsrc(blk, (on && !(h2c_path(D, KT, BF) && p.kp <= 16)) ? ABLK * 4 : 0);
+  cluster_hat<D, KT, FL, BF>(p, F.C, po, hat, Side{{ars_po, 64 * D * 4, scr, po, {}}});
   PHF(4)
   if (isK) small_mm<KT, FL>(F.S, hat, t);
   next();
@@ -2932,7 +2945,7 @@ struct ProjBwdSmallShape {
   static constexpr int NSL = D == 64 ? 1 : 3;               // dW tile slots per wave per stage
   static constexpr int HATF = 16 * 32;                       // hat block: 16 features x 32 rows
   static constexpr int GINF = 32 * 16;                       // dT / dQh rows of the item: 32 rows x 16
-  static constexpr int PARTF = 256 + 16 * D + 3 * D;         // end-of-kernel wave partial: dS | dC | db
+  static constexpr int PARTF = 256 + 16 * D + 3 * D + 16;    // end-of-kernel wave partial: dS | dC | db | sum dZ
   // d = 96 (one workgroup per CU anyway): weight fragments in LDS. WF holds the d x d layer of the next
   // chain product (W2, W1, W0 in turn, DMA'd a stage ahead); CF / SF the head's cluster fragments
   // (K-groups 0, 1 only: k <= 16), loaded once.
@@ -3078,7 +3091,8 @@ __global__ __launch_bounds__(256, ProjBwdSmallShape<D>::LCS ? 1 : 2) void k_proj
   for (int l = 0; l < 3; ++l)
 #pragma unroll
     for (int j = 0; j < NSL; ++j) acc[l][j] = zero16();
-  f32x4 accS = {0.f, 0.f, 0.f, 0.f}, accC[D / 16];
+  constexpr bool H2C = h2c_path(D, 1, BF);  // dC from h2 (see h2c_path); this kernel runs for k <= 16 only
+  f32x4 accS = {0.f, 0.f, 0.f, 0.f}, accC[D / 16], accZ = accS;
 #pragma unroll
   for (int t = 0; t < D / 16; ++t) accC[t] = accS;
   float dbp[3][2] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};  // db0 | db1 | db2 partials (own_rowsum)
@@ -3146,7 +3160,8 @@ __global__ __launch_bounds__(256, ProjBwdSmallShape<D>::LCS ? 1 : 2) void k_proj
     dma_block16<D * 128>(INl, ar, (D == 64 ? 32 : 64) * D * 4);  // experiment: h2 (po is recomputed from it)
 #else
     if constexpr (BF) dma_block16<D * 64>(INl + 2 * REG, ar, 64 * D * 4);  // bf16 po -> upper half (widened below)
-    else dma_block16<D * 128>(INl, ar, 64 * D * 4);  // po -> own IN region (free since B6), lands under dS / dZ / dp
+    else if constexpr (H2C) dma_block16<D * 128>(INl, ar, 32 * D * 4);  // h2 -> own IN region (free since B6): the dC
+    else dma_block16<D * 128>(INl, ar, 64 * D * 4);  // product below, then layer 2's stage (po -> IN otherwise)
 #endif
     f32x16 gin[1];
     float dTt[8];
@@ -3205,11 +3220,13 @@ __global__ __launch_bounds__(256, ProjBwdSmallShape<D>::LCS ? 1 : 2) void k_proj
     }
 #endif
     // ---- dC_h += dZ^T po, private 16x16x4: A = dZ[row 4s + g4][cluster c16], B = po[row 4s + g4][16t + c16]
+    //      (H2C: dZ^T h2, and accZ[e] = sum over rows of dZ[.][cluster 4 g4 + e], B = 1)
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
       const float a = DSw[(4 * s + g4) * 16 + c16];
 #pragma unroll
       for (int t = 0; t < D / 16; ++t) accC[t] = mfma16(a, INw[act_off(16 * t + c16, 4 * s + g4)], accC[t]);
+      if constexpr (H2C) accZ = mfma16(a, 1.f, accZ);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     PHASE(1);
@@ -3217,7 +3234,7 @@ __global__ __launch_bounds__(256, ProjBwdSmallShape<D>::LCS ? 1 : 2) void k_proj
     stage_ds<DT>(DSw, dcur, D, ln);
     if constexpr (LW) __syncthreads();  // B0: every wave's quarter of the W2 fragments landed
     if constexpr (BF) dma_block16<D * 64>(INl + 2 * REG, ar, 32 * D * 4);  // bf16 h2 -> upper half
-    else dma_block16<D * 128>(INl, ar, 32 * D * 4);  // h2
+    else if constexpr (!H2C) dma_block16<D * 128>(INl, ar, 32 * D * 4);  // h2 (H2C: in IN since the group top)
     f32x16 dh[DT];
     mm_acc_f<DT, DT, 4 * DT, 16 * DT, LW, BF>(LW ? WFs : p.WfT[2], dcur, dh);
     wait_vm_all();
@@ -3343,6 +3360,7 @@ __global__ __launch_bounds__(256, ProjBwdSmallShape<D>::LCS ? 1 : 2) void k_proj
     part[(4 * g4 + e) * 16 + c16] = accS[e];
 #pragma unroll
     for (int t = 0; t < D / 16; ++t) part[256 + (4 * g4 + e) * D + 16 * t + c16] = accC[t][e];
+    if (H2C && c16 == 0) part[256 + 19 * D + 4 * g4 + e] = accZ[e];
   }
 #pragma unroll
   for (int l = 0; l < 3; ++l)
@@ -3397,6 +3415,9 @@ __global__ __launch_bounds__(256, ProjBwdSmallShape<D>::LCS ? 1 : 2) void k_proj
       if (a < 16) {
 #pragma unroll
         for (int ww = 0; ww < 4; ++ww) v += lds[ww * Sh::PARTF + 256 + a * D + f];
+      } else if (H2C && a == 16 && f < 16) {  // H2C: row 16 holds sum dZ per cluster f (k_cluster_grad)
+#pragma unroll
+        for (int ww = 0; ww < 4; ++ww) v += lds[ww * Sh::PARTF + 256 + 19 * D + f];
       }
       sC[e] = v;
     } else {
@@ -3480,9 +3501,13 @@ __global__ __launch_bounds__(64 * RS_WAVES) void k_reduce_slabs(const KArgs p, i
 // One workgroup per (cluster row a, head): the k coefficients dD(a,b) + dD(b,a) go to LDS once and
 // the D outputs of row a are k-term fmaf chains over coalesced rows of C (b ascending; the <S, dS>
 // reduction is a fixed-order tree), so the result is deterministic.
+// h2c (h2c_path): dC_ws rows 0..15 hold sum dZ^T h2 and row 16 sum dZ per cluster; the po product is formed here,
+// once per head: sum_f dZ^T h2[a][f] W2[t][f] + sumdZ[a] b2[t] (fixed order)
 __global__ __launch_bounds__(128) void k_cluster_grad(const float* __restrict__ S, const float* __restrict__ dS_ws,
                                                       const float* __restrict__ dC_ws, const float* __restrict__ C,
-                                                      float* __restrict__ dC, int k, int D, int KP32) {
+                                                      float* __restrict__ dC, int k, int D, int KP32,
+                                                      const float* __restrict__ W2, const float* __restrict__ b2,
+                                                      int h2c) {
   const int a = blockIdx.x, hd = blockIdx.y, tid = threadIdx.x;
   __shared__ float red[128];
   __shared__ float coef[128];
@@ -3504,8 +3529,16 @@ __global__ __launch_bounds__(128) void k_cluster_grad(const float* __restrict__ 
     coef[tid] = Sh[a * KP32 + tid] * (dSh[a * KP32 + tid] - dot) + Sh[tid * KP32 + a] * (dSh[tid * KP32 + a] - dot);
   __syncthreads();
   const float* Ch = C + (size_t)hd * k * D;
+  const float* Ah = dC_ws + (size_t)hd * KP32 * D;
   for (int t = tid; t < D; t += 128) {
-    float s = dC_ws[((size_t)hd * KP32 + a) * D + t];
+    float s;
+    if (h2c) {
+      s = 0.f;
+      for (int f = 0; f < D; ++f) s = fmaf(Ah[a * D + f], W2[(size_t)t * D + f], s);
+      s = fmaf(Ah[16 * D + a], b2[t], s);
+    } else {
+      s = Ah[a * D + t];
+    }
     for (int b = 0; b < k; ++b) s = fmaf(coef[b], Ch[b * D + t], s);
     dC[((size_t)hd * k + a) * D + t] = s;
   }
@@ -3829,6 +3862,9 @@ void launch_proj_bwd_s(KArgs p, int kind, int G, int goff, int gk, int Gtot, int
   }
 }
 
+template <int D, int KPH>
+constexpr bool SPLIT_H2C() { return (D == 64 || D == 96) && KPH == 8 && h2c_path(D, 1, false); }
+
 template <int D, int KPH, int KT>
 csa_status launch_bwd(const csa_sbm_bwd_args* b, const Layout& L, hipStream_t st) {
   const csa_sbm_fwd_args* a = b->fwd;
@@ -3900,8 +3936,10 @@ csa_status launch_bwd(const csa_sbm_bwd_args* b, const Layout& L, hipStream_t st
     hipLaunchKernelGGL(k_reduce_slabs, dim3((unsigned)((total + 63) / 64)), dim3(64 * RS_WAVES), 0, st, p, D, KP32,
                        b->dproj_w[0], b->dproj_w[1], b->dproj_w[2], b->dproj_b[0], b->dproj_b[1], b->dproj_b[2],
                        dS_ws, dC_ws);
+    const int h2c = (SPLIT_H2C<D, KPH>() && !p.bf16) ? 1 : 0;  // k_proj_bwd_s formed dC from h2
     hipLaunchKernelGGL(k_cluster_grad, dim3((unsigned)a->k, (unsigned)a->H), dim3(128), 0, st, p.S, (const float*)dS_ws,
-                       (const float*)dC_ws, a->cluster_w, b->dcluster_w, (int)a->k, D, KP32);
+                       (const float*)dC_ws, a->cluster_w, b->dcluster_w, (int)a->k, D, KP32, a->proj_w[2],
+                       a->proj_b[2], h2c);
   } else {
     launch_attn_bwd<D, 0, true>(p, BH, L, a->attn_dropout > 0.f, pf, st, [] {});
   }
