@@ -854,8 +854,10 @@ __device__ __forceinline__ void proj_fwd_item(const KArgs& p, const FwdFrags& F,
     }
     bool hat16 = false;
     if constexpr (KT == 1) {
-      if ((D == 64 || D == 96) && p.kp <= 16) {  // clusters >= 16 are zero, never read back (k_proj_bwd_s)
-        store_act_lds<1, 16>(blk + 96 * D, hat, scr);
+      if ((D == 64 || D == 96) && p.kp <= 16) {  // k_proj_bwd_s reads hat from the Qh / Kh rows stored below
+#ifdef CSA_EXP_HAT_ACT
+        store_act_lds<1, 16>(blk + 96 * D, hat, scr);  // clusters >= 16 are zero, never read back
+#endif
         hat16 = true;
       }
     }
@@ -3115,7 +3117,25 @@ __global__ __launch_bounds__(256, ProjBwdSmallShape<D>::LCS ? 1 : 2) void k_proj
   // per-item operands DMA'd into LDS one group ahead (register-free, so they are issued early):
   // the hat block and the item's 32 dT / dQh rows, read at the top of the group both in the acc
   // orientation (lane = row) and as the 16x16x4 A operand (lane (c16, g4), step s: dT[row 4s + g4][c16]).
-  auto prefetch_hat = [&](const Item& it) { dma_block16<2048>(HATl, act_rsrc(it), 96 * D * 4); };
+  // the item's hat block: its rows of Qh / Kh as k_proj_fwd_l stored them for the attention kernels ([row][16],
+  // rows past the item's last row not fetched), so the forward saves no second copy in the activation block
+  // (HAT_ACT: the activation block's feature-major copy, the round-4 form)
+#ifdef CSA_EXP_HAT_ACT
+  constexpr bool HQK = false;
+#else
+  constexpr bool HQK = true;
+#endif
+  auto prefetch_hat = [&](const Item& it) {
+    if constexpr (HQK) {
+      const int bh = it.b * p.H + hd, row0 = it.rb * 32;
+      const float* src = it.isK ? p.Kh + ((int64_t)bh * p.M + row0) * p.kp : p.Qh + ((int64_t)bh * p.N + row0) * p.kp;
+      dma_block16<2048>(HATl, make_rsrc(src, imin(32, it.nrows - row0) * p.kp * 4), 0);
+    } else {
+      dma_block16<2048>(HATl, act_rsrc(it), 96 * D * 4);
+    }
+  };
+  // element (row, cluster f < 16) of the wave's hat block
+  auto hat_at = [&](int row, int f) { return HQK ? HATw[row * 16 + f] : HATw[act_off(f, row)]; };
   auto prefetch = [&](const Item& it) {
     const int bh = it.b * p.H + hd, row0 = it.rb * 32;
     const float* src = it.isK ? p.dT + ((int64_t)bh * p.M + row0) * p.kp : p.dQh + ((int64_t)bh * p.N + row0) * p.kp;
@@ -3131,6 +3151,11 @@ __global__ __launch_bounds__(256, ProjBwdSmallShape<D>::LCS ? 1 : 2) void k_proj
     else if (w == 3) dma_block16<2048>(lds_offset(lds) + 4 * Sh::SF, make_rsrc(SfT, 4 * 32 * 32), 0);
     wait_vm_all();
     __syncthreads();
+  }
+  if constexpr (HQK) {  // rows past an item's last row are never fetched: they only ever hold finite data
+#pragma unroll
+    for (int e = 0; e < Sh::HATF / 64; ++e) HATw[lane + 64 * e] = 0.f;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
   prefetch_hat(item_of(0));
   prefetch(item_of(0));
@@ -3181,12 +3206,18 @@ __global__ __launch_bounds__(256, ProjBwdSmallShape<D>::LCS ? 1 : 2) void k_proj
     // ---- dS_h += dT^T Kh (K items), private 16x16x4: B = Kh[row 4s + g4][cluster c16] from the hat block
     if (it.isK) {
 #pragma unroll
-      for (int s = 0; s < 8; ++s) accS = mfma16(dTt[s], HATw[act_off(c16, 4 * s + g4)], accS);
+      for (int s = 0; s < 8; ++s) accS = mfma16(dTt[s], hat_at(4 * s + g4, c16), accS);
     }
     // ---- hat (acc orientation, clusters >= 16 are zero) and dZ = (S^T dT | dQh) * hat (1 - hat)
     f32x16 hat;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) hat[r] = r < 8 ? HATw[act_off(crow(r, h), c)] : 0.f;
+    for (int r = 0; r < 16; ++r) hat[r] = r < 8 ? hat_at(c, crow(r, h)) : 0.f;
+    if constexpr (HQK) {  // registers 0-3 / 4-7 are clusters 4h .. 4h+3 / 8+4h .. of row c: two b128 reads
+      const f32x4 h0 = *reinterpret_cast<const f32x4*>(HATw + c * 16 + 4 * h);
+      const f32x4 h1 = *reinterpret_cast<const f32x4*>(HATw + c * 16 + 8 + 4 * h);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { hat[e] = h0[e]; hat[4 + e] = h1[e]; }
+    }
     f32x16 dz[1];
     if (it.isK) {
       mm_acc_f<1, 1, 2, LCS ? 8 : 16, LCS>(LCS ? SFs : SfT, gin, dz);  // dKh^T = S^T dT^T (clusters < 16)
@@ -3511,6 +3542,18 @@ __global__ __launch_bounds__(128) void k_cluster_grad(const float* __restrict__ 
   const int a = blockIdx.x, hd = blockIdx.y, tid = threadIdx.x;
   __shared__ float red[128];
   __shared__ float coef[128];
+  __shared__ float arow[256];  // h2c: row a of sum dZ^T h2 (D <= 256)
+  if (h2c)
+    for (int f = tid; f < D; f += 128) arow[f] = dC_ws[((size_t)hd * KP32 + a) * D + f];
+  // h2c: this thread's row t = tid of W2, loaded before the softmax backward so its latency overlaps it
+  const bool w4 = h2c && ((uintptr_t)W2 & 15) == 0 && (D & 3) == 0 && D <= 128;
+  f32x4 wv[32];
+  if (w4 && tid < D) {
+    const f32x4* wr = reinterpret_cast<const f32x4*>(W2 + (size_t)tid * D);
+#pragma unroll
+    for (int j = 0; j < 32; ++j)
+      if (4 * j < D) wv[j] = wr[j];
+  }
   const float* Sh = S + (size_t)hd * KP32 * KP32;
   const float* dSh = dS_ws + (size_t)hd * KP32 * KP32;
   float acc = 0.f;
@@ -3532,9 +3575,17 @@ __global__ __launch_bounds__(128) void k_cluster_grad(const float* __restrict__ 
   const float* Ah = dC_ws + (size_t)hd * KP32 * D;
   for (int t = tid; t < D; t += 128) {
     float s;
-    if (h2c) {
+    if (h2c) {  // row t of W2 (w4: preloaded in 16-B pieces, t = tid); f ascending (fixed order)
       s = 0.f;
-      for (int f = 0; f < D; ++f) s = fmaf(Ah[a * D + f], W2[(size_t)t * D + f], s);
+      if (w4) {
+#pragma unroll
+        for (int j = 0; j < 32; ++j)
+          if (4 * j < D)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) s = fmaf(arow[4 * j + e], wv[j][e], s);
+      } else {
+        for (int f = 0; f < D; ++f) s = fmaf(arow[f], W2[(size_t)t * D + f], s);
+      }
       s = fmaf(Ah[16 * D + a], b2[t], s);
     } else {
       s = Ah[a * D + t];
