@@ -829,9 +829,13 @@ __device__ __forceinline__ void proj_fwd_item(const KArgs& p, const FwdFrags& F,
   PHF(2)
   mlp_layer<D, FL, BF>(F.W[2], F.b[2], h2, po, Side{{ars, 32 * D * 4, scr, h2, {}}});
   PHF(3)
-  // po is not saved when k_proj_bwd_s forms dC from h2 (h2c_path): its stores go to a null range
-  const __amdgpu_buffer_rsrc_t ars_po = make_rsrc(blk, (on && !(h2c_path(D, KT, BF) && p.kp <= 16)) ? ABLK * 4 : 0);
-  cluster_hat<D, KT, FL, BF>(p, F.C, po, hat, Side{{ars_po, 64 * D * 4, scr, po, {}}});
+  // po is not saved when k_proj_bwd_s forms dC from h2 (h2c_path): its stager is skipped (wave-uniform branch)
+  struct SideIf {
+    ActStager<D / 32> st;
+    bool run;
+    __device__ __forceinline__ void operator()(int g) { if constexpr (STAGED) { if (run) st(g); } }
+  };
+  cluster_hat<D, KT, FL, BF>(p, F.C, po, hat, SideIf{{ars, 64 * D * 4, scr, po, {}}, !(h2c_path(D, KT, BF) && p.kp <= 16)});
   PHF(4)
   if (isK) small_mm<KT, FL>(F.S, hat, t);
   next();
