@@ -375,6 +375,11 @@ class BucketedDataParallel(torch.nn.Module):
         return [(b, hi - lo, len(self._buckets[b])) for b, (lo, hi) in enumerate(self._spans)]
 
     def forward(self, *args, **kwargs):
+        if self._queued or self._works:  # a previous backward ended early (it raised): start this one clean
+            for _, w in self._works:
+                w.wait()
+            self._works, self._queued = [], False
+            self._pending = [len(idx) for idx in self._buckets]
         out = self.module(*args, **kwargs)
         self._mark("forward", -1)
         return out
