@@ -467,11 +467,21 @@ def main():
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus))
+    # stdout carries exactly one line, the JSON result: RCCL prints a version banner on fd 1 when a communicator
+    # comes up (the world-size-1 train legs), so fd 1 is kept for the result and everything else written to it
+    # goes to stderr
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
+
+    def emit(obj):
+        os.write(json_fd, (json.dumps(obj) + "\n").encode())
+
     world, rank, local, dev = init_ranks(args)
     if args.device == "cpu":
         out = launcher_selftest(args, world, rank, dev)
         if rank == 0:
-            print(json.dumps(out), flush=True)
+            emit(out)
         if world > 1:
             dist.destroy_process_group()
         return
@@ -715,7 +725,7 @@ def main():
             progress("config-1 protocol on host cores (oracle CSATrans)")
             out["cpu_config1"] = cpu_config1()
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        emit(out)
     if world > 1:
         dist.destroy_process_group()
 
