@@ -1224,7 +1224,10 @@ __device__ __forceinline__ int img_elem(int row, int col, const int sw) { return
 // 16-row bins (16 rows x LB floats, LB / 2 odd: the 16 rows of a b64 read hit distinct bank pairs) += g at
 // column rel; the four lane groups share the rows, so they add in four exec-masked passes, lanes of a pass
 // own distinct rows and a row's additions happen in a fixed order -> deterministic. An element whose g is
-// zero in every lane of the pass (masked relations: most of the matrix) skips its add.
+// zero in every lane of the pass (masked relations: most of the matrix) skips its add. The passes need no
+// wait between them: one wave's LDS instructions execute in issue order, and the empty asm keeps the compiler
+// from merging or reordering them (round 5: 8 of 9 same-box rounds faster, java layer -1.3 us,
+// profiles/r05_ab_cse_passwait.txt; CSA_EXP_PASSWAIT restores the lgkmcnt(0) per pass).
 __device__ __forceinline__ void bins_scatter16(float* bins, int LB, const float (&gv)[8], const uint32_t (&col)[8]) {
   const int x16 = lane_id() & 15, g = lane_id() >> 4;
   float* row = bins + x16 * LB;
@@ -1235,10 +1238,10 @@ __device__ __forceinline__ void bins_scatter16(float* bins, int LB, const float 
       for (int e = 0; e < 8; ++e)
         if (gv[e] != 0.f) atomicAdd(row + col[e], gv[e]);
     }
-#ifdef CSA_EXP_NOPASSWAIT
-    asm volatile("" ::: "memory");  // keeps the passes apart (the compiler would merge them into one)
+#ifdef CSA_EXP_PASSWAIT
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // experiment (the round-4 form): lgkmcnt(0) between the passes
 #else
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this pass's adds land before the next pass's
+    asm volatile("" ::: "memory");  // keeps the passes apart (the compiler would merge them into one)
 #endif
   }
 }
