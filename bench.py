@@ -320,7 +320,7 @@ def gpu_config1(dev, reps=10, B=32, N=150):
 
 
 def train_step_bench(world, rank, dev, steps, warmup, config="java", per_gpu_batch=64, nbatches=3, force_ddp=False,
-                     impl="bucketed"):
+                     impl="torch"):
     """script/train.py:_update (config/java.py dims), data parallel over RCCL; returns samples/s over all ranks.
     force_ddp: wrap even at world size 1 (needs an initialised process group). impl: wrap_ddp's reducer
     ("bucketed" = csa_amd.train.BucketedDataParallel, "torch" = DistributedDataParallel)."""
@@ -457,6 +457,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cpu-config1", action="store_true", help="skip the config-1 CPU CSATrans protocol")
     ap.add_argument("--no-train", action="store_true", help="skip the full train-step measurement")
+    ap.add_argument("--reducer", choices=("torch", "bucketed"), default="torch",
+                    help="multi-GPU gradient reducer (csa_amd.train.wrap_ddp impl; bucketed is unverified over RCCL "
+                         "with more than one rank)")
     ap.add_argument("--default-gemms", action="store_true",
                     help="train legs on hipBLASLt's default GEMM heuristic instead of the tuned table")
     ap.add_argument("--train-steps", type=int, default=50)
@@ -504,7 +507,7 @@ def main():
     model = mod
     if world > 1 and not args.dense:  # FullAttention has no parameters: no gradient exchange exists
         from csa_amd.train import wrap_ddp
-        model = wrap_ddp(mod, dev)  # bucketed reducer; in-order attention backward beside RCCL
+        model = wrap_ddp(mod, dev, impl=args.reducer)  # in-order attention backward beside RCCL
     Q, K, V = (torch.randn(B, H, N, d, device=dev).requires_grad_(True) for _ in range(3))
     mask = torch.zeros(B, N, device=dev)
     dX = torch.randn(B, H, N, d, device=dev)
@@ -637,7 +640,7 @@ def main():
                    "head_dim": d, "clusters": 0 if args.dense else k, "mode": "eval" if args.eval else "train",
                    "parallelism": f"dp{world}",
                    "exchange": "none (FullAttention has no parameters)" if args.dense else
-                   ("bucketed gradient all-reduce over RCCL" if world > 1 else "none (1 GPU)")},
+                   (f"gradient all-reduce over RCCL ({args.reducer} reducer)" if world > 1 else "none (1 GPU)")},
         "roofline": roofline,
         "step_tflops": round(total_flops / (ms_per_step * 1e-3) / 1e12, 2),
         "step_frac_of_f32_mfma_peak": round(total_flops / (ms_per_step * 1e-3) / 1e12 / PEAK_F32_MFMA_TFLOPS, 4),
@@ -691,7 +694,7 @@ def main():
         progress("train-step leg (config/java.py, 64 ASTs per GPU)")
         from csa_amd.train import GEMM_TABLE, use_tuned_gemms
         ntuned = use_tuned_gemms(not args.default_gemms)
-        out["train"] = train_step_bench(world, rank, dev, args.train_steps, args.train_warmup)
+        out["train"] = train_step_bench(world, rank, dev, args.train_steps, args.train_warmup, impl=args.reducer)
         out["train"]["gemms"] = (f"TunableOp table {os.path.basename(GEMM_TABLE)} ({ntuned} shapes)" if ntuned
                                  else "hipBLASLt default heuristic")
         if world == 1:
@@ -704,7 +707,7 @@ def main():
             dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=dev)
             try:
                 out["train_ddp_world1"] = train_step_bench(1, rank, dev, args.train_steps, args.train_warmup,
-                                                           force_ddp=True)
+                                                           force_ddp=True, impl="bucketed")
                 out["train_torch_ddp_world1"] = train_step_bench(1, rank, dev, args.train_steps, args.train_warmup,
                                                                  force_ddp=True, impl="torch")
             finally:

@@ -252,7 +252,16 @@ class BucketedDataParallel(torch.nn.Module):
     construction; the model has no buffer that changes in training. `no_sync()` skips the reduction
     (local gradient accumulation); the next synchronised backward reduces the accumulated gradients.
     The first backward records the order in which gradients arrive; the buckets are then re-laid in
-    that order (DDP's bucket rebuild), so later steps start all-reducing as early as possible."""
+    that order (DDP's bucket rebuild), so later steps start all-reducing as early as possible. Every rank
+    adopts RANK 0's arrival order (broadcast, as DDP's sync_bucket_indices), and bucket all-reduces are
+    issued strictly in bucket-index order (a complete bucket waits until every lower-index bucket has been
+    issued, DDP's next_bucket_), so the collectives of all ranks pair up bucket for bucket even when the
+    ranks see different gradient arrival orders or different unused parameters.
+
+    Multi-GPU status: the world > 1 all-reduce path is exercised by the 2-rank gloo tests
+    (tests/test_train_cpu.py, including ranks with different unused parameters) and on one GPU by
+    tools/ddp_one_gpu.py (gloo); it has not been run over RCCL with more than one rank, so wrap_ddp keeps
+    torch DDP as the multi-GPU default and this reducer is opt-in there (impl="bucketed")."""
 
     def __init__(self, module, bucket_cap_mb=16, process_group=None):
         super().__init__()
@@ -274,6 +283,7 @@ class BucketedDataParallel(torch.nn.Module):
         self._layout(list(reversed(range(len(params)))))  # DDP's initial guess: reverse registration order
         self._arrival, self._rebuilt = [], False
         self._sync, self._queued = True, False
+        self._next = 0  # lowest bucket index whose all-reduce has not been issued in this backward
         self.timeline = None  # list -> (tag, bucket, cuda Event) per forward end / bucket pack / finish (tools/)
         self._hooks = [p.register_post_accumulate_grad_hook(self._make_hook(i)) for i, p in enumerate(params)]
 
@@ -303,6 +313,7 @@ class BucketedDataParallel(torch.nn.Module):
             self._spans.append((lo, off))
         self._pending = [len(idx) for idx in self._buckets]
         self._works = []
+        self._next = 0
 
     def _make_hook(self, i):
         def hook(p):
@@ -315,8 +326,10 @@ class BucketedDataParallel(torch.nn.Module):
                 self._arrival.append(i)
             b = self._bucket_of[i]
             self._pending[b] -= 1
-            if self._pending[b] == 0 and self._rebuilt:
-                self._reduce(b)
+            if self._rebuilt:  # issue every complete bucket whose lower-index buckets are all issued
+                while self._next < len(self._buckets) and self._pending[self._next] == 0:
+                    self._reduce(self._next)
+                    self._next += 1
         return hook
 
     @torch.no_grad()
@@ -343,18 +356,20 @@ class BucketedDataParallel(torch.nn.Module):
     @torch.no_grad()
     def _finish(self):
         self._queued = False
-        if not self._rebuilt:  # first step: adopt the observed arrival order, then reduce everything
+        if not self._rebuilt:  # first step: adopt rank 0's observed arrival order, then reduce everything
             seen = set(self._arrival)
             order = self._arrival + [i for i in reversed(range(len(self._params))) if i not in seen]
+            if self.world > 1:  # every rank lays its buckets out in rank 0's order (DDP's sync_bucket_indices)
+                dev = self.flat.device if dist.get_backend(self.group) == "nccl" else torch.device("cpu")
+                t = torch.tensor(order, dtype=torch.int64, device=dev)
+                dist.broadcast(t, 0, group=self.group)
+                order = t.tolist()
             self._layout(order)
             self._rebuilt = True
             self._arrival = []
-            for b in range(len(self._buckets)):
-                self._reduce(b)
-        else:
-            for b in range(len(self._buckets)):
-                if self._pending[b] > 0:
-                    self._reduce(b)
+        # the buckets not issued yet, in index order (incomplete ones: parameters without a gradient add zeros)
+        for b in range(self._next, len(self._buckets)):
+            self._reduce(b)
         for b, w in self._works:
             w.wait()
             if self._op == dist.ReduceOp.SUM:
@@ -362,6 +377,7 @@ class BucketedDataParallel(torch.nn.Module):
                 self.flat[lo:hi].div_(self.world)
         self._works = []
         self._pending = [len(idx) for idx in self._buckets]
+        self._next = 0
         self._mark("finish", -1)
 
     def _mark(self, tag, b):
@@ -378,8 +394,10 @@ class BucketedDataParallel(torch.nn.Module):
         if self._queued or self._works:  # a previous backward ended early (it raised): start this one clean
             for _, w in self._works:
                 w.wait()
-            self._works, self._queued = [], False
+            self._works, self._queued, self._next = [], False, 0
             self._pending = [len(idx) for idx in self._buckets]
+            if not self._rebuilt:  # the arrival record of the failed first backward is incomplete
+                self._arrival = []
         out = self.module(*args, **kwargs)
         self._mark("forward", -1)
         return out
@@ -398,18 +416,20 @@ class BucketedDataParallel(torch.nn.Module):
         return ctx()
 
 
-def wrap_ddp(model, device, force=False, bucket_cap_mb=None, impl="bucketed", broadcast_buffers=True,
+def wrap_ddp(model, device, force=False, bucket_cap_mb=None, impl="torch", broadcast_buffers=True,
              static_graph=False, comm_hook=None):
     """Data parallelism over the initialised process group (idist.auto_model, script/train.py:83).
     Without a process group of more than one rank the model is returned unwrapped, unless `force`
     (the wrapper over a world-size-1 group: the reducer's own cost, tests).
 
-    impl "bucketed" (default): BucketedDataParallel, 16 MB buckets (bucket_cap_mb=None), one pack launch per
-    bucket. 16 MB: the java step's bucket-ready timeline (tools/ddp_timeline.py) leaves 0.2 ms of a
-    projected 8-rank all-reduce exposed at 300 GB/s bus bandwidth, against 0.4 ms with 64 MB buckets.
-    impl "torch": torch DistributedDataParallel, 64 MB buckets (gradient_as_bucket_view; broadcast_buffers, static_graph
-    and the world-size-1 diagnostic comm_hook "world1_none" apply to it only), kept for A/B runs
-    (tools/ddp_variants.py).
+    impl "torch" (default): torch DistributedDataParallel, 64 MB buckets (gradient_as_bucket_view; broadcast_buffers,
+    static_graph and the world-size-1 diagnostic comm_hook "world1_none" apply to it only). The default for
+    multi-GPU runs: its RCCL path is the one known to work with more than one rank.
+    impl "bucketed": BucketedDataParallel, 16 MB buckets (bucket_cap_mb=None), one pack launch per bucket
+    (+0.7% on the java step at world size 1 against torch DDP's +7-9%). 16 MB: the java step's bucket-ready
+    timeline (tools/ddp_timeline.py) leaves 0.2 ms of a projected 8-rank all-reduce exposed at
+    300 GB/s bus bandwidth, against 0.4 ms with 64 MB buckets. Verified at world size 2 over gloo and over a
+    world-size-1 RCCL group; unverified over RCCL with more than one rank (opt-in there).
 
     The modules' packed parameters (Attention W_q/W_k/W_v, the CSE q/k/v linears) are packed at
     construction and after every device move, so the reducer's buckets and hooks see the final storages.

@@ -180,6 +180,125 @@ def test_ddp_two_ranks_average_gradients():
                     np.testing.assert_array_equal(x, y)
 
 
+class Branchy(torch.nn.Module):
+    """Two branches a / b plus a shared trunk; forward(x, use) runs the branches named in `use` in that order, so
+    ranks can leave different parameters unused and see different gradient arrival orders."""
+
+    def __init__(self):
+        super().__init__()
+        self.trunk = torch.nn.Linear(6, 6)
+        self.a1, self.a2 = torch.nn.Linear(6, 6), torch.nn.Linear(6, 6)
+        self.b1, self.b2 = torch.nn.Linear(6, 6), torch.nn.Linear(6, 6)
+        self.head = torch.nn.Linear(6, 3)
+
+    def forward(self, x, use):
+        h = torch.tanh(self.trunk(x))
+        for br in use:
+            h = h + torch.tanh(getattr(self, br + "2")(torch.tanh(getattr(self, br + "1")(h))))
+        return self.head(h)
+
+
+def _branchy_use(rank, i):
+    # rank 0 leaves branch b unused on even steps, rank 1 leaves branch a unused; the order of the branches
+    # (hence the gradient arrival order) also differs between the ranks
+    if rank == 0:
+        return ("a",) if i % 2 == 0 else ("a", "b")
+    return ("b",) if i % 2 == 0 else ("b", "a")
+
+
+def _worker_unused(rank, world, port, q, steps):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from csa_amd.train import BucketedDataParallel, init_distributed
+    init_distributed()
+    torch.manual_seed(0)
+    model = Branchy()
+    ddp = BucketedDataParallel(model, bucket_cap_mb=40 * 4 / 2 ** 20)  # ~40 floats per bucket: many buckets
+    grads = []
+    for i in range(steps):
+        for p in model.parameters():
+            p.grad = None
+        g = torch.Generator().manual_seed(50 + 7 * i + rank)
+        x, y = torch.randn(5, 6, generator=g), torch.randn(5, 3, generator=g)
+        ((ddp(x, _branchy_use(rank, i)) - y) ** 2).sum().backward()
+        grads.append([p.grad.numpy().copy() for p in model.parameters()])
+    # a backward that raises part-way through (before the reducer has finished its first layout on a fresh
+    # wrapper), then normal steps on the same wrapper
+    torch.manual_seed(0)
+    m2 = Branchy()
+    d2 = BucketedDataParallel(m2, bucket_cap_mb=40 * 4 / 2 ** 20)
+    g = torch.Generator().manual_seed(99)
+    x, y = torch.randn(5, 6, generator=g), torch.randn(5, 3, generator=g)
+    out = d2(x, ("a", "b"))
+
+    def boom(grad):
+        raise RuntimeError("injected")
+    h = torch.tanh(m2.trunk(x))
+    raised = False
+    try:
+        out.register_hook(lambda g_: g_)  # the head's gradients arrive, then the trunk path raises
+        h2 = d2.module.a1.weight * 1.0
+        h2.register_hook(boom)
+        (((out - y) ** 2).sum() + h2.sum()).backward()
+    except RuntimeError as e:
+        raised = "injected" in str(e)
+    after = []
+    for i in range(2):
+        for p in m2.parameters():
+            p.grad = None
+        g = torch.Generator().manual_seed(50 + 7 * i + rank)
+        x, y = torch.randn(5, 6, generator=g), torch.randn(5, 3, generator=g)
+        ((d2(x, _branchy_use(rank, i)) - y) ** 2).sum().backward()
+        after.append([p.grad.numpy().copy() for p in m2.parameters()])
+    q.put((rank, grads, raised, after))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bucketed_reducer_ranks_with_different_unused_parameters():
+    """2-rank gloo: the ranks leave DIFFERENT parameters unused and see different gradient arrival orders, over
+    many small buckets. Every rank adopts rank 0's bucket layout and issues the bucket all-reduces in index order,
+    so each gradient is the mean of the per-rank gradients (an unused parameter contributes zero, DDP's
+    find_unused_parameters); a wrapper whose first backward raised part-way reduces correctly afterwards."""
+    steps = 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_unused, args=(r, 2, port, q, steps)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        rank, grads, raised, after = q.get(timeout=180)
+        res[rank] = (grads, raised, after)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+
+    def ref_grads(i):
+        per_rank = []
+        for rank in range(2):
+            torch.manual_seed(0)
+            m = Branchy()
+            g = torch.Generator().manual_seed(50 + 7 * i + rank)
+            x, y = torch.randn(5, 6, generator=g), torch.randn(5, 3, generator=g)
+            ((m(x, _branchy_use(rank, i)) - y) ** 2).sum().backward()
+            per_rank.append([torch.zeros_like(p) if p.grad is None else p.grad for p in m.parameters()])
+        return [(a + b) / 2 for a, b in zip(*per_rank)]
+
+    for i in range(steps):
+        # the weights never change (no optimizer), so every step's reference starts from the same parameters
+        ref = ref_grads(i)
+        for rank in range(2):
+            for got, want in zip(res[rank][0][i], ref):
+                np.testing.assert_allclose(got, want.numpy(), rtol=1e-6, atol=1e-7)
+    for rank in range(2):
+        assert res[rank][1], "the injected error did not propagate"
+        for i in range(2):
+            for got, want in zip(res[rank][2][i], ref_grads(i)):
+                np.testing.assert_allclose(got, want.numpy(), rtol=1e-6, atol=1e-7)
+
+
 def _reference_label_smoothing(x, target, padding_idx, smoothing):
     """utils/label_smooth.py:24-40 restated (materialised true_dist + KLDiv(sum) / ntokens)."""
     x = x.contiguous().view(-1, x.size(-1))
