@@ -131,9 +131,6 @@ constexpr int PHILOX_ROUNDS = 7;
 
 __device__ __forceinline__ u32x4 philox4x32(u32x4 ctr, uint32_t k0, uint32_t k1) {
   const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
-#ifdef CSA_EXP_NO_PHILOX
-  return u32x4{ctr.x * M0 ^ k0, ctr.y * M1 ^ k1, ctr.z ^ ctr.w, ctr.x ^ ctr.y};
-#endif
 #pragma unroll
   for (int i = 0; i < PHILOX_ROUNDS; ++i) {
     // one v_mad_u64_u32 per 32x32->64 product (measured 20% cheaper than mul_hi + mul_lo)
@@ -223,11 +220,7 @@ __device__ __forceinline__ void dma_block16(uint32_t lds_off, __amdgpu_buffer_rs
   const int voff = lane_id() * 16;
 #pragma unroll
   for (int i = 0; i < NBYTES / 1024; ++i)
-#ifdef CSA_EXP_ACT_NT
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(src, lds_at(lds_off + 1024 * i), 16, voff, src_byte_off + 1024 * i, 0, 2);
-#else
     __builtin_amdgcn_raw_ptr_buffer_load_lds(src, lds_at(lds_off + 1024 * i), 16, voff, src_byte_off + 1024 * i, 0, 0);
-#endif
 }
 
 // ---------------------------------------------------------------------------------------

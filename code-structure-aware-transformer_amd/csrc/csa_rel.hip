@@ -206,7 +206,7 @@ struct RelArgs {
   float* gt;  // fp32 16-row path: softmax-input gradient tiles k_rel_bwd_kh -> k_rel_bwd_qg ([key][query] 32 x 32)
   const float *lq, *lk;
   int qstat_pre;  // qstat written by k_rel_qstat (concurrent backward): k_rel_bwd_qf leaves it alone
-  int LB16, Q4;   // 16-row bins (k_rel_bwd_qh / kh): row stride and the per-lane-group K range
+  int LB16, Q4;   // 16-row bins (k_rel_bwd_kh / qg): row stride and the per-lane-group K range
 };
 
 __device__ __forceinline__ int64_t plane_off(const RelArgs& p, int b, int hd, int64_t sb, int64_t sh) {
@@ -1007,14 +1007,10 @@ __global__ __launch_bounds__(64, 1) void k_rel_bwd_qf(const RelArgs p) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) dq[t] = mfma(kT[t][r], gv[r], dq[t]);
     }
-#ifndef CSA_EXP_NOSCATTER
     bins_scatter(bins, p.LB, gv, col);
-#endif
   }
   __syncthreads();
-#ifndef CSA_EXP_NOBT
   bins_times<DT>(dq, bins, p.LB, p.KB2, p.lk + (int64_t)hd * p.L * D, p.L, D);
-#endif
   if (iv) {
     store_rows_f<DT>(p.dq + b * p.dq_sb + hd * p.dq_sh + (int64_t)i * p.dq_sn, dq);
     if (h == 0 && !p.qstat_pre) {
@@ -1029,7 +1025,7 @@ __global__ __launch_bounds__(64, 1) void k_rel_bwd_qf(const RelArgs p) {
 // Per-query (row max, 1/row sum, delta = rowsum(dO * O), 0) into qstat for the key-side kernel when it runs
 // beside the query-side one on a second stream (csa_rel_attn_bwd). PARTS lanes per row, each a run of
 // 64 / PARTS elements in the query-side kernel's order (sequential fma, then the parts added pairwise:
-// PARTS = 2 for k_rel_bwd_qf, 4 for k_rel_bwd_qh): the same delta bit for bit. HBM-bound (2 x 256 B per row).
+// PARTS = 2 for k_rel_bwd_qf; 4 for the 16-row kernels: (q0 + q1) + (q2 + q3) over 16-element runs). HBM-bound (2 x 256 B per row).
 template <int PARTS>
 __global__ __launch_bounds__(256) void k_rel_qstat(const RelArgs p) {
   constexpr int NS = 64 / PARTS;
@@ -1178,14 +1174,10 @@ __global__ __launch_bounds__(64, 1) void k_rel_bwd_kf(const RelArgs p) {
       dma_block16<4096>(Rl, rbr, ((qb + 1) * p.NKB + kbi) * 4096);
       cm = load_codes(rmrow, qb + 1);
     }
-#ifndef CSA_EXP_NOSCATTER
     bins_scatter(bins, p.LB, gv, col);
-#endif
   }
   __syncthreads();
-#ifndef CSA_EXP_NOBT
   bins_times<DT>(dk, bins, p.LB, p.KB2, p.lq + (int64_t)hd * p.L * D, p.L, D);
-#endif
   if (jv) {
     store_rows_f<DT>(p.dk + b * p.dk_sb + hd * p.dk_sh + (int64_t)j * p.dk_sn, dk);
     store_rows_f<DT>(p.dv + b * p.dv_sb + hd * p.dv_sh + (int64_t)j * p.dv_sn, dv);
@@ -1194,7 +1186,7 @@ __global__ __launch_bounds__(64, 1) void k_rel_bwd_kf(const RelArgs p) {
 }
 
 // ------------------------------------------------------------------------------------
-// fp32 backward with 16-row waves (k_rel_bwd_qh / k_rel_bwd_kh). The 32-row kernels above hold 40 KB of
+// fp32 backward with 16-row waves (k_rel_bwd_kh, then k_rel_bwd_qg from its g tiles). The 32-row kernels above hold 40 KB of
 // LDS per wave (K/V images 16 KB, bias tile 4 KB, bins 20 KB): one wave per SIMD, latency-bound. Here a
 // workgroup of two waves covers the same 32-row block: the two waves share the tile images and the bias
 // tile (each DMAs half of them), and each owns 16 rows and a 16-row bins table (~10 KB), so the workgroup
@@ -1227,7 +1219,7 @@ __device__ __forceinline__ int img_elem(int row, int col, const int sw) { return
 // zero in every lane of the pass (masked relations: most of the matrix) skips its add. The passes need no
 // wait between them: one wave's LDS instructions execute in issue order, and the empty asm keeps the compiler
 // from merging or reordering them (round 5: 8 of 9 same-box rounds faster, java layer -1.3 us,
-// profiles/r05_ab_cse_passwait.txt; CSA_EXP_PASSWAIT restores the lgkmcnt(0) per pass).
+// profiles/r05_ab_cse_passwait.txt).
 __device__ __forceinline__ void bins_scatter16(float* bins, int LB, const float (&gv)[8], const uint32_t (&col)[8]) {
   const int x16 = lane_id() & 15, g = lane_id() >> 4;
   float* row = bins + x16 * LB;
@@ -1238,11 +1230,7 @@ __device__ __forceinline__ void bins_scatter16(float* bins, int LB, const float 
       for (int e = 0; e < 8; ++e)
         if (gv[e] != 0.f) atomicAdd(row + col[e], gv[e]);
     }
-#ifdef CSA_EXP_PASSWAIT
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // experiment (the round-4 form): lgkmcnt(0) between the passes
-#else
     asm volatile("" ::: "memory");  // keeps the passes apart (the compiler would merge them into one)
-#endif
   }
 }
 
@@ -1305,155 +1293,6 @@ __host__ __device__ constexpr int rel16_bins_off(bool key_side) { return 2 * 32 
 
 typedef uint32_t u32x4v_t __attribute__((ext_vector_type(4)));
 
-// Query side, 16-row waves: workgroup = (b,h, 32-query block), wave w = queries 16 w .. 16 w + 15.
-// Same algebra and outputs as k_rel_bwd_qf.
-__global__ __launch_bounds__(128, 2) void k_rel_bwd_qh(const RelArgs p) {
-  constexpr int D = 64, IMG = 32 * D * 4;
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  const uint32_t Kl = lds_offset(lds), Vl = Kl + IMG, Rl = Kl + 2 * IMG;
-  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const int lane = lane_id(), x16 = lane & 15, g = lane >> 4;
-  float* bins = lds + rel16_bins_off(false) / 4 + w * 16 * p.LB16;
-  const BhBlock xb = xcd_block(p.NQB, p.B * p.H);
-  if (!xb.valid) return;  // whole workgroup
-  const int qb = xb.blk, bh = xb.bh, b = bh / p.H, hd = bh % p.H;
-  const int xr = 16 * w + x16, i = qb * 32 + xr;
-  const bool iv = i < p.N;
-  const int ic = imin(i, p.N - 1);
-  const int kld = (int)p.k_sn * 4, vld = (int)p.v_sn * 4;
-  const __amdgpu_buffer_rsrc_t kr = make_rsrc(p.k + b * p.k_sb + hd * p.k_sh, (p.N - 1) * kld + D * 4);
-  const __amdgpu_buffer_rsrc_t vr = make_rsrc(p.v + b * p.v_sb + hd * p.v_sh, (p.N - 1) * vld + D * 4);
-  const __amdgpu_buffer_rsrc_t rbr = make_rsrc(p.RB + ((int64_t)bh * p.NQB + qb) * p.NKB * 1024, p.NKB * 4096);
-  // rows past N are never fetched: the images hold zeros there (zeroed before any DMA can land)
-  for (int e = (int)threadIdx.x; e < 2 * IMG / 16; e += 128) reinterpret_cast<f32x4*>(lds)[e] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int e = lane; e < 16 * p.LB16; e += 64) bins[e] = 0.f;
-  __syncthreads();
-  const DmaPat kpat = dma_pat(SW_BOTH, kld), vpat = dma_pat(SW_ROW, vld);
-  const uint16_t* rmrow = prep_row(p, p.RM, b, hd, ic);
-  Codes8 cm = load_codes8(rmrow, 0);
-  float q[16], dO[16];
-  load_run<16>(q, p.q + b * p.q_sb + hd * p.q_sh + (int64_t)ic * p.q_sn + 16 * g, iv);
-  load_run<16>(dO, p.dout + b * p.do_sb + hd * p.do_sh + (int64_t)ic * p.do_sn + 16 * g, iv);
-  // wave w fetches rows 16 w .. 16 w + 15 of each image and half of the bias tile
-  dma64(Kl, kr, kpat, kld, 0, 4 * w, 4 * w + 4);
-  dma64(Vl, vr, vpat, vld, 0, 4 * w, 4 * w + 4);
-  dma_block16<2048>(Rl + 2048 * w, rbr, 2048 * w);
-  float dp = 0.f;
-  {
-    float o[16];
-    load_run<16>(o, p.out + b * p.o_sb + hd * p.o_sh + (int64_t)ic * p.o_sn + 16 * g, iv);
-#pragma unroll
-    for (int s = 0; s < 16; ++s) dp = fmaf(dO[s], o[s], dp);
-  }
-  const float dp2 = dp + __shfl_xor(dp, 16, 64);
-  const float delta = dp2 + __shfl_xor(dp2, 32, 64);  // (q0 + q1) + (q2 + q3): k_rel_qstat<4>'s order
-  const float rmax = p.stats[((int64_t)bh * p.N + ic) * 2];
-  const float rinv = p.stats[((int64_t)bh * p.N + ic) * 2 + 1];
-  f32x4 dq[4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t) dq[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // CSA_EXP_DEFER (experiment): the bins scatter of tile kt at the top of iteration kt + 1, after the wait for
-  // tile kt + 1's DMA (the compiler orders every LDS access behind the LDS-DMAs in flight, so the scatter
-  // right after the refill waits for it); measured slower (DESIGN.md §3 CSE A/B)
-  float gsv[8];
-  uint32_t csv[8];
-  for (int kt = 0; kt < p.NKB; ++kt) {
-    const int j0 = kt * 32;
-    wait_vm_all();
-    __syncthreads();  // both waves' pieces of tile kt landed
-#ifdef CSA_EXP_DEFER
-    if (kt > 0) bins_scatter16(bins, p.LB16, gsv, csv);
-#endif
-    float gl[8];
-    uint32_t col[8];
-#pragma unroll
-    for (int st = 0; st < 2; ++st) {
-      const f32x4 v = lds_f4(lds, 2 * IMG + 4 * rb_off(xr, pbase16(g) + 8 * st));
-#pragma unroll
-      for (int e = 0; e < 4; ++e) gl[4 * st + e] = v[e];
-    }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) col[e] = code8(cm, e) & 0xffu;  // rel[x][y]: the c2p gather's column
-    // the four chains (S^T, dP^T of both key halves) interleaved: a 16x16x4 result feeds its own chain
-    // after 40 cycles, its issue slot is 32, so one chain alone would run at 80% of the pipe rate
-    f32x4 sacc[2], dpacc[2];
-#pragma unroll
-    for (int st = 0; st < 2; ++st) { sacc[st] = f32x4{0.f, 0.f, 0.f, 0.f}; dpacc[st] = sacc[st]; }
-    f32x4 kv[2][2], vv[2][2];  // operand groups, one K-group of reads ahead of the MFMAs
-    auto rd = [&](int s4, f32x4 (&kd)[2], f32x4 (&vd)[2]) {
-#pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        kd[st] = lds_f4(lds, img_elem(16 * st + x16, 16 * g + 4 * s4, SW_BOTH));
-        vd[st] = lds_f4(lds, IMG + img_elem(16 * st + x16, 16 * g + 4 * s4, SW_ROW));
-      }
-    };
-    rd(0, kv[0], vv[0]);
-#pragma unroll
-    for (int s4 = 0; s4 < 4; ++s4) {
-      if (s4 + 1 < 4) rd(s4 + 1, kv[(s4 + 1) & 1], vv[(s4 + 1) & 1]);
-#ifndef CSA_EXP_NOSB
-      __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead of this group's MFMAs
-#endif
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-#pragma unroll
-        for (int st = 0; st < 2; ++st) {
-          sacc[st] = mfma16(kv[s4 & 1][st][e], q[4 * s4 + e], sacc[st]);
-          dpacc[st] = mfma16(vv[s4 & 1][st][e], dO[4 * s4 + e], dpacc[st]);
-        }
-    }
-    float kT[4][8];  // A operands of dq: K[key 16 st + 4 g + i][d = 4 x16 + t], one b128 read per key
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const f32x4 kv = lds_f4(lds, img_elem(16 * (e >> 2) + 4 * g + (e & 3), 4 * x16, SW_BOTH));
-#pragma unroll
-      for (int t = 0; t < 4; ++t) kT[t][e] = kv[t];
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __syncthreads();  // both waves read tile kt out: refill
-    if (kt + 1 < p.NKB) {
-      dma64(Kl, kr, kpat, kld, j0 + 32, 4 * w, 4 * w + 4);
-      dma64(Vl, vr, vpat, vld, j0 + 32, 4 * w, 4 * w + 4);
-      dma_block16<2048>(Rl + 2048 * w, rbr, (kt + 1) * 4096 + 2048 * w);
-      cm = load_codes8(rmrow, kt + 1);
-    }
-    float gv[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float sa = sacc[e >> 2][e & 3], dpa = dpacc[e >> 2][e & 3];
-      const bool inside = iv && (j0 + 16 * (e >> 2) + 4 * g + (e & 3) < p.N);
-      const bool msk = gl[e] == NEG_INF;
-      const float s = msk ? -1e9f : (sa + gl[e]) * p.inv_scale;
-      const float P = inside ? __expf(s - rmax) * rinv : 0.f;
-      gv[e] = (inside && !msk) ? P * (dpa - delta) * p.inv_scale : 0.f;
-    }
-#pragma unroll
-    for (int e = 0; e < 8; ++e)
-#pragma unroll
-      for (int t = 0; t < 4; ++t) dq[t] = mfma16(kT[t][e], gv[e], dq[t]);
-#ifndef CSA_EXP_DEFER
-    bins_scatter16(bins, p.LB16, gv, col);
-  }
-#else
-#pragma unroll
-    for (int e = 0; e < 8; ++e) { gsv[e] = gv[e]; csv[e] = col[e]; }
-  }
-  bins_scatter16(bins, p.LB16, gsv, csv);
-#endif
-  bins_times16(dq, bins, p.LB16, p.Q4, p.lk + (int64_t)hd * p.L * D, p.L);
-  if (iv) {
-    float* dst = p.dq + b * p.dq_sb + hd * p.dq_sh + (int64_t)i * p.dq_sn + 16 * g;  // d = 16 g + 4 r + t
-#pragma unroll
-    for (int r = 0; r < 4; ++r) *reinterpret_cast<f32x4*>(dst + 4 * r) = f32x4{dq[0][r], dq[1][r], dq[2][r], dq[3][r]};
-    if (g == 0 && !p.qstat_pre) {
-      f32x4 st;
-      st[0] = rmax; st[1] = rinv; st[2] = delta; st[3] = 0.f;
-      *reinterpret_cast<f32x4*>(p.qstat + ((int64_t)bh * p.N + i) * 4) = st;
-    }
-  }
-  bins_store16(p.gc2p + ((int64_t)hd * p.B + b) * p.Lp * p.ldx, p.ldx, i, bins, p.LB16, p.Q4, p.Lp, iv);
-}
-
 // Key side, 16-row waves: workgroup = (b,h, 32-key block), wave w = keys 16 w .. 16 w + 15. Same algebra and
 // outputs as k_rel_bwd_kf.
 __global__ __launch_bounds__(128, 2) void k_rel_bwd_kh(const RelArgs p) {
@@ -1492,15 +1331,12 @@ __global__ __launch_bounds__(128, 2) void k_rel_bwd_kh(const RelArgs p) {
   f32x4 dv[4], dk[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) { dv[t] = f32x4{0.f, 0.f, 0.f, 0.f}; dk[t] = dv[t]; }
-  float gsv[8];  // deferred bins scatter (see k_rel_bwd_qh)
+  float gsv[8];  // deferred bins scatter
   uint32_t csv[8];
   for (int qb = 0; qb < p.NQB; ++qb) {
     const int i0 = qb * 32;
     wait_vm_all();
     __syncthreads();
-#ifdef CSA_EXP_DEFER
-    if (qb > 0) bins_scatter16(bins, p.LB16, gsv, csv);
-#endif
     float gl[8], rm[8], ri[8], dl[8];
     uint32_t col[8];
 #pragma unroll
@@ -1511,7 +1347,9 @@ __global__ __launch_bounds__(128, 2) void k_rel_bwd_kh(const RelArgs p) {
       rm[e] = st[0]; ri[e] = st[1]; dl[e] = st[2];
       col[e] = code8(cm, e) & 0xffu;  // rel[y][x]: the p2c gather's column
     }
-    f32x4 sacc[2], dpacc[2];  // four interleaved chains (see k_rel_bwd_qh)
+    // four interleaved chains (S, dP of both query halves): a 16x16x4 result feeds its own chain after 40 cycles,
+    // its issue slot is 32, so one chain alone would run at 80% of the pipe rate
+    f32x4 sacc[2], dpacc[2];
 #pragma unroll
     for (int st = 0; st < 2; ++st) { sacc[st] = f32x4{0.f, 0.f, 0.f, 0.f}; dpacc[st] = sacc[st]; }
     f32x4 qv[2][2], xv[2][2];
@@ -1526,9 +1364,7 @@ __global__ __launch_bounds__(128, 2) void k_rel_bwd_kh(const RelArgs p) {
 #pragma unroll
     for (int s4 = 0; s4 < 4; ++s4) {
       if (s4 + 1 < 4) rd(s4 + 1, qv[(s4 + 1) & 1], xv[(s4 + 1) & 1]);
-#ifndef CSA_EXP_NOSB
       __builtin_amdgcn_sched_barrier(0);
-#endif
 #pragma unroll
       for (int e = 0; e < 4; ++e)
 #pragma unroll
@@ -1581,15 +1417,8 @@ __global__ __launch_bounds__(128, 2) void k_rel_bwd_kh(const RelArgs p) {
         dv[t] = mfma16(xc[t][e], Pv[e], dv[t]);
         dk[t] = mfma16(qc[t][e], gv[e], dk[t]);
       }
-#ifndef CSA_EXP_DEFER
     bins_scatter16(bins, p.LB16, gv, col);
   }
-#else
-#pragma unroll
-    for (int e = 0; e < 8; ++e) { gsv[e] = gv[e]; csv[e] = col[e]; }
-  }
-  bins_scatter16(bins, p.LB16, gsv, csv);
-#endif
   bins_times16(dk, bins, p.LB16, p.Q4, p.lq + (int64_t)hd * p.L * D, p.L);
   if (jv) {
     float* dkp = p.dk + b * p.dk_sb + hd * p.dk_sh + (int64_t)j * p.dk_sn + 16 * g;  // d = 16 g + 4 r + t
@@ -1607,7 +1436,7 @@ __global__ __launch_bounds__(128, 2) void k_rel_bwd_kh(const RelArgs p) {
 // queries 16 w .. 16 w + 15. k_rel_bwd_kh stored the softmax-input gradient g = P (dP - delta) / sqrt(3 d)
 // of every element as [key][query] tiles, so this kernel neither recomputes the scores (no V image, no bias
 // tile, no exp) nor dP: dq = g K (16x16x4 MFMA, K image by LDS-DMA) and the c2p gather backward
-// (G_c2p bins, then dq += G_c2p LK), with k_rel_bwd_qh's operand layouts and summation orders.
+// (G_c2p bins, then dq += G_c2p LK) in the 16-row operand layouts above.
 __global__ __launch_bounds__(128, 2) void k_rel_bwd_qg(const RelArgs p) {
   constexpr int D = 64, IMG = 32 * D * 4;
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -1740,25 +1569,6 @@ __global__ __launch_bounds__(512) void k_rel_lgrad(const LgradArgs g) {
 #pragma unroll
   for (int t = 0; t < 2; ++t) vb[t] = col_base64(t, c, h);
   f32x16 acc[2] = {zero16(), zero16()};
-#ifdef CSA_EXP_LGRAD_G1  // experiment: the G runs one chunk ahead only (the round-3 form)
-  f32x4 a4[4], an[4];
-  if (c0 < c1) { issue_x(c0, 0); issue_g(c0, a4); }
-  for (int ch = c0; ch < c1; ++ch) {
-    const int cur = (ch - c0) & 1, n0 = (ch % cpb) * 32;
-    wait_vm_all();     // this wave's pieces of chunk ch and its G runs have landed
-    __syncthreads();   // every wave's pieces landed; every wave read out image cur ^ 1 (chunk ch - 1)
-    if (ch + 1 < c1) { issue_x(ch + 1, cur ^ 1); issue_g(ch + 1, an); }
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float a = (n0 + crow(r, h) < N) ? a4[r >> 2][r & 3] : 0.f;
-        acc[t] = mfma(a, lds_f1(lds, IMG * cur + vb[t] + 256 * crow(r, 0)), acc[t]);
-      }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) a4[q] = an[q];
-  }
-#else
   // The G runs (the kernel's HBM stream: 100 MB at B = 64) are loaded two chunks ahead into a ring of three
   // register buffers (the loop unrolled by three, so no buffer is copied while its loads are in flight), the
   // X images one chunk ahead. Issue order per chunk: X pieces of chunk ch + 1, then the G runs of ch + 2
@@ -1798,7 +1608,6 @@ __global__ __launch_bounds__(512) void k_rel_lgrad(const LgradArgs g) {
     if (ch + 2 >= c1) break;
     step(ch + 2, B2, B1);
   }
-#endif
   float* out = g.part[which] + ((int64_t)sp * g.H + hd) * g.L * D;
 #pragma unroll
   for (int t = 0; t < 2; ++t)
@@ -1955,24 +1764,10 @@ size_t bins_lds_bytes(const RelArgs& p) { return sizeof(float) * 32 * (size_t)p.
 size_t bins16_lds_bytes(const RelArgs& p) { return sizeof(float) * 2 * 16 * (size_t)p.LB16; }
 
 // fp32 backward on the 16-row kernels (two waves per SIMD); bf16 mode keeps the 32-row kernels.
-// CSA_EXP_REL32: experiment build that keeps the 32-row fp32 kernels (DESIGN.md §3 CSE A/B).
 inline bool rel_use16(const RelArgs& p) {
-#ifdef CSA_EXP_REL32
-  return false;
-#else
   return !p.bf16;
-#endif
 }
 
-// fp32 16-row backward: the key side hands its g tiles to k_rel_bwd_qg (no score / dP recompute on the query
-// side). CSA_EXP_REL_RECOMP: experiment build with the round-3 recomputing query kernel (DESIGN.md §3 CSE A/B).
-inline bool rel_handoff() {
-#ifdef CSA_EXP_REL_RECOMP
-  return false;
-#else
-  return true;
-#endif
-}
 
 // relation logits: C2P[b,h] = Q LK_h^T (N x L), P2CT[b,h] = K LQ_h^T (N x L)
 void rel_logits(const csa_rel_attn_args* a, const RelLayout& R, hipStream_t st) {
@@ -2129,11 +1924,8 @@ csa_status csa_rel_attn_bwd(const csa_rel_attn_bwd_args* b, void* stream) {
                         bwd_concurrent(b->schedule, b->side_stream, stream_device(st), (int64_t)p.NQB * B * H, 1);
     const SideLane lane{(hipStream_t)b->side_stream, (hipEvent_t)b->side_fork, (hipEvent_t)b->side_join};
     const SideLane* side = concur ? &lane : nullptr;
-    auto launch_q = [&](hipStream_t s_) {
-      if (w16) {
-        set_dyn_lds((const void*)k_rel_bwd_qh, (int)lq_bytes);
-        hipLaunchKernelGGL(k_rel_bwd_qh, gq, blk, lq_bytes, s_, p);
-      } else if (p.bf16) {
+    auto launch_q = [&](hipStream_t s_) {  // (bf16 mode: the fp32 path runs k_rel_bwd_qg below)
+      if (p.bf16) {
         hipLaunchKernelGGL((k_rel_bwd_qf<64, true>), gq, blk, lq_bytes, s_, p);
       } else {
         hipLaunchKernelGGL((k_rel_bwd_qf<64, false>), gq, blk, lq_bytes, s_, p);
@@ -2149,7 +1941,9 @@ csa_status csa_rel_attn_bwd(const csa_rel_attn_bwd_args* b, void* stream) {
         hipLaunchKernelGGL((k_rel_bwd_kf<64, false>), gk, blk, lk_bytes, s_, p);
       }
     };
-    if (w16 && rel_handoff()) {  // fp32: row statistics, key side (g tiles out), query side from the tiles
+    // fp32: row statistics, key side (g tiles out), then the query side from the key side's g tiles (no score / dP
+    // recompute on the query side; the round-3 recomputing query kernel measured slower, DESIGN.md §3 CSE A/B)
+    if (w16) {
       p.qstat_pre = 1;
       p.gt = (float*)((char*)ws + R.gt);
       const int64_t threads = 4LL * B * H * N;

@@ -1,7 +1,7 @@
 // SBM attention (module/sbm_attn.py:11-87 + module/STE.py) as gfx950 HIP kernels.
 //
-// CSA_EXP_* macros select throw-away experiment builds (tools/build_variant.py);
-// the shipped library is built without them.
+// The throw-away experiment variants of earlier rounds live in git history (round-5
+// tree, commit 0b877e5), not in these sources.
 // Pipeline (one forward + one backward = 10 launches, all stream-ordered, no host sync):
 //   fwd: k_prep              S_h = softmax_{k^2}(C_h C_h^T) (sbm_attn.py:37-39) and the weights ->
 //                            MFMA-operand-major fragments (L2-resident), one launch
@@ -184,13 +184,7 @@ __device__ __forceinline__ void fence_sched() { __builtin_amdgcn_sched_barrier(0
 __device__ __forceinline__ f32x4 frag4(const float* __restrict__ f, int it, int nsteps, int s4) {
   const __amdgpu_buffer_rsrc_t r =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(f), (short)0, 0x7fffffff, 0x00020000);
-#ifdef CSA_EXP_FRAG_L1
-  const int soff = 0 * (it + s4 + nsteps);
-#elif defined(CSA_EXP_FRAG_SPREAD)
-  const int soff = (it * (nsteps >> 2) + s4) * 1024 + (int)((blockIdx.x + blockIdx.y) & 15) * 69632;
-#else
   const int soff = (it * (nsteps >> 2) + s4) * 1024;
-#endif
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, lane_id() * 16, soff, 0));
 }
 
@@ -255,14 +249,12 @@ __device__ __forceinline__ void frag_chain(const float* __restrict__ frag, int n
     for (int t = 0; t < NTO; ++t)
 #pragma unroll
       for (int e = 0; e < 4; ++e) out[t] = mfma(wq[s4 % (LA + 1)][t][e], bval(4 * s4 + e), out[t]);
-#ifndef CSA_EXP_FL_SINK
     if constexpr (FL) {
       // LDS fragments: the scheduler otherwise sinks the lookahead reads to the group's last MFMA (register
       // pressure heuristics), so the next group starts on lgkmcnt(0); pin them ahead of the group's MFMAs
       if (s4 + LA < S4N) __builtin_amdgcn_sched_group_barrier(0x100, NTO, 0);
       __builtin_amdgcn_sched_group_barrier(0x008, 4 * NTO, 0);
     }
-#endif
     side(s4);
     fence_sched();
   }
@@ -425,9 +417,6 @@ __device__ __forceinline__ uint32_t u16_of(const u32x4& r, int e) {
 // mask keyed by (row, feature, layer, Q/K), so the backward regenerates it bit-identically.
 template <int D>
 __device__ __forceinline__ void mlp_act(const KArgs& p, f32x16 (&a)[D / 32], int layer, int row, int bh, int isK) {
-#ifdef CSA_EXP_PF_MFMA_ONLY  // experiment: the projection forward's MFMA chains alone (wrong results)
-  return;
-#endif
   constexpr int DT = D / 32;
   const int h = lane_id() >> 5;
   const bool drop = p.proj_p > 0.f;
@@ -441,13 +430,6 @@ __device__ __forceinline__ void mlp_act(const KArgs& p, f32x16 (&a)[D / 32], int
       if (drop)
         u = philox4x32(u32x4{(uint32_t)row, (uint32_t)(4 * ot + 2 * gp + h) | (layer << 16) | (isK << 20),
                              (uint32_t)bh, (RNG_PROJ_DROP << 28) ^ p.off}, p.seed_lo, p.seed_hi);
-#ifdef CSA_EXP_RNG24_COST  // experiment: the half extra Philox call per 8 uniforms of 24-bit draws
-      if (drop && gp == 0) {
-        const u32x4 x = philox4x32(u32x4{(uint32_t)row, (uint32_t)(4 * ot + h) | (layer << 16) | (isK << 20),
-                                         (uint32_t)bh, 0x50000000u ^ p.off}, p.seed_lo, p.seed_hi);
-        u.x ^= ((x.x ^ x.y ^ x.z ^ x.w) == 0x9e3779b9u) ? 1u : 0u;
-      }
-#endif
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         float v = a[ot][8 * gp + e];
@@ -461,19 +443,11 @@ __device__ __forceinline__ void mlp_act(const KArgs& p, f32x16 (&a)[D / 32], int
 //   dC_h = sum dZ^T po = (sum dZ^T h2) W2^T + (sum dZ^T 1) b2^T     (po = h2 W2^T + b2, proj.6)
 // so the forward does not save po (a third of the activation bytes: 168 MB written and read per B = 256 step) and
 // k_cluster_grad applies W2 / b2 once per head. A reassociation of the same sums (fp32 rounding only).
-#if defined(CSA_EXP_SAVE_PO) || defined(CSA_EXP_RECOMP_PO)
-constexpr bool H2C_ON = false;
-#else
 constexpr bool H2C_ON = true;
-#endif
 __host__ __device__ constexpr bool h2c_path(int D, int KT, bool BF) { return H2C_ON && !BF && (D == 64 || D == 96) && KT == 1; }
 
 constexpr int MLP_LA = 2;  // forward MLP chains: fragments two K-groups ahead
-#ifdef CSA_EXP_FL2
-constexpr int FL_LA = 2;   // LDS fragment chains: lookahead (experiment)
-#else
 constexpr int FL_LA = 1;   // LDS fragment chains: one K-group ahead covers the LDS latency
-#endif
 
 // Linear bias as one more MFMA K-step after the weight chain (x W^T + b, summed last like addmm):
 // A = b[32 ot + c] on every lane (raw load issued before the chain, no select on it), B = 1 on the
@@ -536,9 +510,7 @@ __device__ __forceinline__ void cluster_hat(const KArgs& p, const float* Cf, con
     for (int r = 0; r < 16; ++r) {
       const int a = 32 * kt + crow(r, h);
       // sigmoid via hardware exp / divide (a few ulp; branch-free): sbm_attn.py:47,53
-#ifndef CSA_EXP_PF_MFMA_ONLY
       hat[kt][r] = (a < p.k) ? __fdividef(1.f, 1.f + __expf(-hat[kt][r])) : 0.f;
-#endif
       (void)a;
     }
   }
@@ -642,11 +614,7 @@ __device__ __forceinline__ void store_act_lds_bf(float* __restrict__ blk, const 
   }
 }
 
-#ifdef CSA_EXP_ACT_AUX  // experiment: other cache policies for the staged activation stores
-constexpr int CSA_AUX_NT = CSA_EXP_ACT_AUX;
-#else
 constexpr int CSA_AUX_NT = 2;  // buffer instruction cache policy: non-temporal (as __builtin_nontemporal_store)
-#endif
 // store_act_lds / store_act_lds_bf split into three stages per tile, so that the stores ride along an MFMA chain
 // as its side work (frag_chain's side(g)) instead of running as a phase of their own after the item's products
 // (round 5: the store phase was 25% of a k_proj_fwd_l wave's time, s_memtime stamps). Stage W: the tile's 16
@@ -768,9 +736,6 @@ __device__ __forceinline__ void load_item_x(const KArgs& p, int b, int hd, int r
 // F2 body: item r of (b, hd) from its x rows. `next` runs once every product is done and x is dead,
 // before the stores (the persistent kernel issues the next item's x loads there: a later vmcnt wait
 // for them then does not also wait for this item's stores, which drain under the next item).
-#ifdef CSA_PHASES_FWD
-__device__ unsigned long long g_phf[16][8];
-#endif
 template <int D, int KT, bool FL, typename NEXT, bool BF = false>
 __device__ __forceinline__ void proj_fwd_item(const KArgs& p, const FwdFrags& F, int b, int hd, int r, float (&x)[D / 2],
                                               float* scr, NEXT next) {
@@ -784,30 +749,16 @@ __device__ __forceinline__ void proj_fwd_item(const KArgs& p, const FwdFrags& F,
   f32x16 h1[D / 32], h2[D / 32], po[D / 32], hat[KT], t[KT];
 #pragma unroll
   for (int i = 0; i < D / 2; ++i) x[i] = rv ? x[i] : 0.f;
-#ifdef CSA_PHASES_FWD  // dev instrumentation: issue-to-issue cycles by phase (s_memtime), see k_proj_fwd_l
-  unsigned long long* ph = g_phf[threadIdx.x >> 6];
-  unsigned long long tq = __builtin_amdgcn_s_memtime();
-#define PHF(i) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if ((blockIdx.x | blockIdx.y) == 0) ph[i] += t_ - tq; tq = t_; }
-#else
 #define PHF(i)
-#endif
   constexpr bool ABF = BF && (D == 64 || D == 96) && KT == 1;  // read back by k_proj_bwd_s<D, true>
   constexpr int ABLK = (3 * D + 32 * KT) * 32;
   // fp32 activations: h1 | h2 | po leave as the side work of the chain that consumes them (layer 1, layer 2, the
   // cluster product: ActStager), their stores interleaved with that chain's MFMAs instead of a store phase after
   // the item's products; hat and the Qh / Kh / T rows at the end
-#if defined(CSA_EXP_STORE_PHASE) || defined(CSA_EXP_NO_ACT) || defined(CSA_EXP_RECOMP_PO)
-  constexpr bool STAGED = false;
-#else
   constexpr bool STAGED = !BF;
-#endif
   // unstaged d = 96 (java dims, 256 VGPRs): h1 leaves right after layer 1 has consumed it instead of being held to
   // the item's end with h2 / po / hat (the held h1 spilled 18 VGPRs)
-#ifdef CSA_EXP_H1_LATE
-  constexpr bool H1E = false;
-#else
   constexpr bool H1E = !STAGED && D == 96;
-#endif
   float* const blk = p.Act ? p.Act + ((int64_t)bh * (p.NQB + p.NKB) + r) * ABLK : nullptr;
   const bool on = blk != nullptr;
   const __amdgpu_buffer_rsrc_t ars = make_rsrc(blk, on ? ABLK * 4 : 0);
@@ -818,12 +769,10 @@ __device__ __forceinline__ void proj_fwd_item(const KArgs& p, const FwdFrags& F,
   mlp_layer0<D, FL, BF>(p, F.W[0], F.b[0], x, h1, row, bh, isK);
   PHF(0)
   mlp_layer<D, FL, BF>(F.W[1], F.b[1], h1, h2, Side{{ars, 0, scr, h1, {}}});
-#ifndef CSA_EXP_NO_ACT
   if (H1E && on) {
     if (ABF && p.kp <= 16) store_act_lds_bf<D / 32>(blk, h1, scr);
     else store_act_lds<D / 32>(blk, h1, scr);
   }
-#endif
   PHF(1)
   mlp_act<D>(p, h2, 1, row, bh, isK);
   PHF(2)
@@ -840,7 +789,6 @@ __device__ __forceinline__ void proj_fwd_item(const KArgs& p, const FwdFrags& F,
   if (isK) small_mm<KT, FL>(F.S, hat, t);
   next();
   PHF(5)
-#ifndef CSA_EXP_NO_ACT
   if (on) {  // save the activations for k_proj_bwd (item r of this (b,h): Q blocks, then K blocks)
     if constexpr (!STAGED) {
       if (ABF && p.kp <= 16) {
@@ -850,27 +798,17 @@ __device__ __forceinline__ void proj_fwd_item(const KArgs& p, const FwdFrags& F,
       } else {
         if (!H1E) store_act_lds<D / 32>(blk, h1, scr);
         store_act_lds<D / 32>(blk + 32 * D, h2, scr);
-#ifdef CSA_EXP_RECOMP_PO  // experiment: k_proj_bwd_s<64> recomputes po from h2
-        if (!(D == 64 && KT == 1 && p.kp <= 16))
-#endif
         store_act_lds<D / 32>(blk + 64 * D, po, scr);
       }
     }
     bool hat16 = false;
     if constexpr (KT == 1) {
       if ((D == 64 || D == 96) && p.kp <= 16) {  // k_proj_bwd_s reads hat from the Qh / Kh rows stored below
-#ifdef CSA_EXP_HAT_ACT
-        store_act_lds<1, 16>(blk + 96 * D, hat, scr);  // clusters >= 16 are zero, never read back
-#endif
         hat16 = true;
       }
     }
     if (!hat16) store_act_lds<KT>(blk + 96 * D, hat, scr);
   }
-#endif
-#ifdef CSA_EXP_PF_MFMA_ONLY
-  if (row == -1)
-#endif
   if (!isK) {
     store_rows<KT>(p.Qh + ((int64_t)bh * p.N + row) * p.kp, p.kp, p.kp, hat, rv);
   } else {
@@ -905,11 +843,7 @@ __global__ __launch_bounds__(64) void k_proj_fwd(const KArgs p) {
 template <int D, int KT>
 struct ProjFwdLds {
   static constexpr int WB = D * D * 4, CB = 32 * KT * D * 4, SB = 1024 * KT * KT * 4;  // bytes
-#ifdef CSA_EXP_PF6
-  static constexpr int NW = D == 64 ? 12 : 8;  // d = 64: one workgroup of 12 waves per CU (3 per SIMD)
-#else
   static constexpr int NW = D == 64 ? 4 : 8;  // d = 64: two workgroups per CU; d = 96: one of 8 waves
-#endif
   static constexpr int PIECES = (3 * WB + CB + SB) / 1024;
   static constexpr size_t FBYTES = 3 * WB + CB + SB;
   static constexpr size_t BBYTES = (3 * D * 4 + 15) / 16 * 16;  // the three biases
@@ -948,19 +882,10 @@ __global__ __launch_bounds__((64 * ProjFwdLds<D, KT>::NW)) void k_proj_fwd_l(con
   for (int it = i_lo + w; it < i_hi; it += LY::NW) {
     const int nx = it + LY::NW;
     auto nextf = [&] {
-#ifndef CSA_EXP_PF_MFMA_ONLY
       if (nx < i_hi) load_item_x<D>(p, nx / per_b, hd, nx % per_b, x);
-#endif
     };
     proj_fwd_item<D, KT, true, decltype(nextf), BF>(p, F, it / per_b, hd, it % per_b, x, scr, nextf);
   }
-#ifdef CSA_PHASES_FWD
-  if (blockIdx.x == 0 && blockIdx.y == 0 && lane_id() == 0) {
-    const unsigned long long* q = g_phf[w];
-    printf("PHF d=%d w=%d layer0+act %llu layer1 %llu act1 %llu layer2 %llu hat %llu T+next %llu stores %llu\n", D, w,
-           q[0], q[1], q[2], q[3], q[4], q[5], q[6]);
-  }
-#endif
 }
 
 // fp32: k_attn_bwd_kv runs the elementwise backward once per element and hands the ds / G tiles to
@@ -978,13 +903,7 @@ constexpr uint32_t W_NO_EDGE = 0x7f800001u;
 
 template <bool BF>
 constexpr bool bwd_handoff() {
-#ifdef CSA_EXP_RECOMP  // experiment: the recompute pipeline for fp32 too
-  return false;
-#elif defined(CSA_EXP_BF_HANDOFF)  // experiment: the (one-plane) handoff in bf16 mode too
-  return true;
-#else
   return !BF;
-#endif
 }
 
 // ------------------------------------------------------------------------------------
@@ -1112,14 +1031,6 @@ __device__ __forceinline__ KeyMask key_mask_load_raw(const KArgs& p, int b) {
   return km;
 }
 
-#ifdef CSA_EXP_FWD_STAMPS  // experiment: per-phase s_memtime totals of k_attn_fwd, printed for sampled waves
-#define FST_DECL unsigned long long fst_t = 0, fst[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; FST_NOW(fst_t);
-#define FST_NOW(v) { __builtin_amdgcn_sched_barrier(0); asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) :: "memory"); __builtin_amdgcn_sched_barrier(0); }
-#define FST(i) { unsigned long long t_; FST_NOW(t_); fst[i] += t_ - fst_t; fst_t = t_; }
-#else
-#define FST_DECL
-#define FST(i)
-#endif
 // DROP: attention dropout on (keep <=> 16-bit uniform >= drop_thr). HAS_U: STE uniforms supplied by
 // the caller (bit-exact parity path, fp32 compare as torch.bernoulli); otherwise 16-bit Philox
 // uniforms u16 / 65536 (STE.py:13 draws u < p with p = clamp(expA, .01, .99)).
@@ -1127,7 +1038,6 @@ __device__ __forceinline__ KeyMask key_mask_load_raw(const KArgs& p, int b) {
 // images; later items find rows past M holding earlier items' finite data, which their -inf key bias masks).
 template <int D, int KPH, bool DENSE, bool HAS_U, bool DROP, bool BF>
 __device__ __forceinline__ void attn_fwd_item(const KArgs& p, float* __restrict__ lds, int bh, int qb, bool zero_images) {
-  FST_DECL
   using LY = AttnFwdLds<D, KPH>;
   constexpr int DT = D / 32, NS = D / 2, DP = LY::DP, KP = LY::KP;
   constexpr bool SWZ = LY::SWZ;
@@ -1184,7 +1094,6 @@ __device__ __forceinline__ void attn_fwd_item(const KArgs& p, float* __restrict_
 #pragma unroll
   for (int t = 0; t < DT; ++t) o[t] = zero16();
   uint32_t cntl = 0;
-  FST(0)
   for (int kt = 0; kt < p.NKB; ++kt) {
     const int j0 = kt * 32;
     wait_vm_all();  // tile kt's K/V/T images (at kt = 0 also the query operands) have landed
@@ -1192,17 +1101,12 @@ __device__ __forceinline__ void attn_fwd_item(const KArgs& p, float* __restrict_
       if (kt == 0)
 #pragma unroll
         for (int e = 0; e < KPH; ++e) qh[e] *= ESC;
-    FST(1)
     // the tile's Philox words depend only on (query, tile, head): computed first, so their VALU work can
     // interleave with the S / expA MFMA chains below instead of waiting behind them
     u32x4 r_ste[2], r_drop[2];
     {
       uint32_t sk0 = p.seed_lo, sk1 = p.seed_hi;  // opaque per tile: round keys are not held across the loop
       asm volatile("" : "+s"(sk0), "+s"(sk1));
-#ifdef CSA_EXP_FWD_NO_RNG  // experiment: timing without the tile's Philox calls (wrong masks)
-      r_ste[0] = r_ste[1] = r_drop[0] = r_drop[1] = u32x4{(uint32_t)i * 2654435761u, sk0 ^ (uint32_t)kt, sk1, (uint32_t)bh};
-      if (false)
-#endif
 #pragma unroll
       for (int gp = 0; gp < 2; ++gp) {
         if constexpr (!DENSE && !HAS_U)
@@ -1212,16 +1116,7 @@ __device__ __forceinline__ void attn_fwd_item(const KArgs& p, float* __restrict_
           r_drop[gp] = philox4x32(u32x4{(uint32_t)i, (uint32_t)(8 * kt + 4 * gp + h), (uint32_t)bh,
                                         (RNG_ATTN_DROP << 28) ^ p.off}, sk0, sk1);
       }
-#ifdef CSA_EXP_RNG24_COST  // experiment: the two extra Philox calls per tile that 24-bit uniforms would need
-      {
-        const u32x4 x1 = philox4x32(u32x4{(uint32_t)i, (uint32_t)(8 * kt + h), (uint32_t)bh, 0x70000000u ^ p.off}, sk0, sk1);
-        const u32x4 x2 = philox4x32(u32x4{(uint32_t)i, (uint32_t)(8 * kt + 4 + h), (uint32_t)bh, 0x60000000u ^ p.off}, sk0, sk1);
-        const uint32_t z = x1.x ^ x1.y ^ x1.z ^ x1.w ^ x2.x ^ x2.y ^ x2.z ^ x2.w;
-        r_drop[0].x ^= (z == 0x9e3779b9u) ? 1u : 0u;  // never changes a result in practice; keeps the calls live
-      }
-#endif
     }
-    FST(2)
     // S^T = K Q^T : A operand = K rows from the image (row c, lin-perm chunks of half h)
     f32x16 sacc = zero16();
     if constexpr (BF) {
@@ -1239,7 +1134,6 @@ __device__ __forceinline__ void attn_fwd_item(const KArgs& p, float* __restrict_
         for (int e = 0; e < 4; ++e) sacc = mfma(kv[e], q[4 * j + e], sacc);
       }
     }
-    FST(3)
     f32x16 eacc;
     if constexpr (!DENSE) {  // expA^T = T Qh^T (sbm_attn.py:55)
       eacc = zero16();
@@ -1250,7 +1144,6 @@ __device__ __forceinline__ void attn_fwd_item(const KArgs& p, float* __restrict_
         for (int e = 0; e < 4; ++e) eacc = mfma(tv[e], qh[4 * j + e], eacc);
       }
     }
-    FST(4)
     // V^T operand values for this tile's PV: lane (d = 32t + c) reads V[key crow(r,h)][d]
     float vt[DT][16];
 #pragma unroll
@@ -1262,12 +1155,7 @@ __device__ __forceinline__ void attn_fwd_item(const KArgs& p, float* __restrict_
     for (int g = 0; g < 4; ++g) bz[g] = lds_f4(lds, LY::BOFF + 4 * (j0 + 8 * g + 4 * h));
     // all of tile kt is in registers: start tile kt+1's DMA (overlaps the softmax and PV below)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    FST(5)
-#if defined(CSA_EXP_FWD_NO_LOOPDMA) || defined(CSA_EXP_FWD_MFMA_ONLY)  // experiment: tile 0's images reused (wrong)
-    if (false)
-#endif
     if (kt + 1 < p.NKB) CSA_ISSUE_FWD(j0 + 32);
-    FST(6)
     float s[16];
     float tmax = NEG_INF;
 #pragma unroll
@@ -1308,11 +1196,7 @@ __device__ __forceinline__ void attn_fwd_item(const KArgs& p, float* __restrict_
       }
     }
     // bit-pack the sampled graph / dropout keep mask: word [qb][key] holds 32 query bits (lanes 0..31)
-#if defined(CSA_EXP_FWD_NO_PACK) || defined(CSA_EXP_FWD_NO_ELEM) || defined(CSA_EXP_FWD_MFMA_ONLY)
-    if constexpr (false) {  // experiment: no bit packing / bit stores (wrong backward)
-#else
     if constexpr (!DENSE || DROP) {
-#endif
       const uint32_t myA = DENSE ? 0u : pack_bits(av);
       const uint32_t myR = DROP ? pack_bits(keep) : 0u;
       const int64_t widx = ((int64_t)bh * p.NQB + qb) * p.Mpad + j0 + c;
@@ -1322,16 +1206,9 @@ __device__ __forceinline__ void attn_fwd_item(const KArgs& p, float* __restrict_
       }
       if constexpr (DROP) if (h == 0) p.Rbits[widx] = myR;
     }
-    FST(7)
     // online softmax update (exp(-inf - m) = 0 covers masked keys; m_use keeps an all-masked prefix finite)
     float w[16];
-#if defined(CSA_EXP_FWD_NO_ELEM) || defined(CSA_EXP_FWD_MFMA_ONLY)  // experiment: MFMA + DMA skeleton (wrong)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) w[r] = sacc[r] + eacc[r];
-    if (false) {
-#else
     {
-#endif
     tmax = xhalf_max(tmax);
     const float m_new = fmaxf(m_run, tmax);
     const float m_use = (m_new == NEG_INF) ? 0.f : m_new;
@@ -1352,7 +1229,6 @@ __device__ __forceinline__ void attn_fwd_item(const KArgs& p, float* __restrict_
     }
     m_run = m_new;
     }
-    FST(8)
     // O^T += V^T W^T (keys beyond M carry w = 0)
     if constexpr (BF) {
       const bf16x8 w0 = pack8(&w[0]), w1 = pack8(&w[8]);
@@ -1367,7 +1243,6 @@ __device__ __forceinline__ void attn_fwd_item(const KArgs& p, float* __restrict_
 #pragma unroll
         for (int r = 0; r < 16; ++r) o[t] = mfma(vt[t][r], w[r], o[t]);
     }
-    FST(9)
   }
   const float Z = xhalf_sum(zp), Zg = xhalf_sum(zgp);
   const float n = Zg / Z;
@@ -1400,289 +1275,14 @@ __device__ __forceinline__ void attn_fwd_item(const KArgs& p, float* __restrict_
     for (int o2 = 32; o2 >= 1; o2 >>= 1) cntl += __shfl_xor(cntl, o2, 64);
     if (lane == 0 && cntl) atomicAdd(p.cnt + hd, (unsigned long long)cntl);
   }
-#ifdef CSA_EXP_FWD_STAMPS
-  FST(10)
-  if (lane == 0 && blockIdx.x % 331 == 0)
-    printf("FST blk=%d pro %llu dmawait %llu rng %llu S %llu E %llu vtrd %llu dma %llu ste+pack %llu soft %llu pv %llu epi %llu\n",
-           (int)blockIdx.x, fst[0], fst[1], fst[2], fst[3], fst[4], fst[5], fst[6], fst[7], fst[8], fst[9], fst[10]);
-#endif
 }
 
 template <int D, int KPH, bool DENSE, bool HAS_U, bool DROP, bool BF>
 __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd(const KArgs p) {
-#ifdef CSA_EXP_PRIO  // experiment: half of the waves (by dispatch slot parity) at priority 1
-  if ((blockIdx.x >> 3) & 1) __builtin_amdgcn_s_setprio(1);
-#endif
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const BhBlock xb = xcd_block(p.NQB, p.B * p.H);
   if (!xb.valid) return;
   attn_fwd_item<D, KPH, DENSE, HAS_U, DROP, BF>(p, lds, xb.bh, xb.blk, true);
-}
-
-// ------------------------------------------------------------------------------------
-// F3b: k_attn_fwd for d = 64 in fp32 (every python / dense config; the headline layer). Same tiles, images and
-// results as k_attn_fwd (up to fp32 rounding of the softmax); the per-tile schedule is built around what
-// s_memtime stamps of k_attn_fwd showed (profiles/r05_stamps.txt): per key tile a wave spent 2.8k cycles issuing
-// the next tile's 18 LDS-DMA pieces in one burst and ~3.7k in STE / packing / softmax VALU, against 4.6k of its
-// own MFMA time, so two waves per SIMD could not keep the matrix pipe busy. Here
-//   * the tile's Philox calls are spread over the S chain's 32 dependent MFMAs (sched_group_barrier: a few VALU
-//     per 64-cycle MFMA gap issue for free);
-//   * tile kt+1's K and T pieces are issued between the E chain's MFMAs (the S / E chains' K and T reads have
-//     returned), its V pieces between the PV MFMAs (the V^T operands are in registers), one piece per MFMA;
-//   * the V pieces are the youngest vector-memory operations at the next tile's top, so that wait is vmcnt(8)
-//     (K, T, the query operands and the bit stores) and the V image is waited for only right before its reads;
-//   * the key bias is the S chain's initial accumulator, q carries 1/sqrt(d) = 1/8 (exact), e = exp2(s log2e -
-//     m log2e) is one fma + exp, and the running max moves only when a row max grows by more than RESCALE_TH, so
-//     the o / Z rescale runs under a wave-uniform branch that is almost never taken after the first tile (e stays
-//     below exp(8));
-//   * the prologue waits on nothing: the key bias row is written at the first tile, after its wait.
-// ------------------------------------------------------------------------------------
-constexpr float RESCALE_TH = 8.f;
-
-template <int KPH, bool DENSE, bool HAS_U, bool DROP>
-__global__ __launch_bounds__(64, 2) void k_attn_fwd64(const KArgs p) {
-  constexpr int D = 64, DT = 2, NS = 32;
-  using LY = AttnFwdLds<D, KPH>;
-  constexpr int KPN = LY::KP > 0 ? LY::KP : 16, KPHA = KPH > 0 ? KPH : 1;
-  constexpr int TP = DENSE ? 0 : 2 * (KPN / 16);  // T image pieces (1 KiB each, dma_narrow)
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  const uint32_t Kl = lds_offset(lds), Vl = Kl + LY::VOFF, Tl = Kl + LY::TOFF;
-  const int lane = lane_id(), c = lane & 31, h = lane >> 5;
-  const BhBlock xb = xcd_block(p.NQB, p.B * p.H);
-  if (!xb.valid) return;
-  const int qb = xb.blk, bh = xb.bh, b = bh / p.H, hd = bh % p.H;
-  const int i = qb * 32 + c;
-  const bool iv = i < p.N;
-  const int ic = imin(i, p.N - 1);
-  const int kld = (int)p.k_sn * 4, vld = (int)p.v_sn * 4;
-  // descriptors span exactly the M valid rows (rows >= M are never fetched; the images are zeroed once)
-  const __amdgpu_buffer_rsrc_t kr = make_rsrc(p.K + b * p.k_sb + hd * p.k_sh, (p.M - 1) * kld + D * 4);
-  const __amdgpu_buffer_rsrc_t vr = make_rsrc(p.V + b * p.v_sb + hd * p.v_sh, (p.M - 1) * vld + D * 4);
-  const __amdgpu_buffer_rsrc_t tr = make_rsrc(DENSE ? p.K : p.T + (int64_t)bh * p.M * p.kp, p.M * p.kp * 4);
-  lds_zero<(2 * LY::KV_BYTES + LY::T_BYTES) / 4>(lds);
-  const DmaPat kpat = dma_pat(SW_ROW, kld), vpat = dma_pat(SW_COL, vld);
-  // prologue, in issue order: key mask, tile 0's K and T images, the query operands (rows past N read row N-1:
-  // finite, never stored), tile 0's V image last (the youngest eight, as at every later tile top)
-  const KeyMask km = key_mask_load_raw(p, b);
-  dma64(Kl, kr, kpat, kld, 0);
-  if constexpr (!DENSE) dma_narrow(Tl, tr, 0, KPN);
-  float q[NS];
-  load_run<NS>(q, p.Q + b * p.q_sb + hd * p.q_sh + (int64_t)ic * p.q_sn + h * NS, true);
-  float qh[KPHA];
-  if constexpr (!DENSE) load_run<KPH>(qh, p.Qh + ((int64_t)bh * p.N + ic) * p.kp + h * KPH, true);
-  dma64(Vl, vr, vpat, vld, 0);
-  constexpr float ESC = HAS_U ? 1.f : 65536.f;  // Philox STE compares u16 < 65536 p (qh scaled, exact)
-  const int kbase = row_base64(c, h);
-  const int tbase = DENSE ? 0 : LY::TOFF + narrow_base<KPN>(c, (KPH / 4) * h);
-  int vb[DT];
-#pragma unroll
-  for (int t = 0; t < DT; ++t) vb[t] = LY::VOFF + col_base64(t, c, h);
-  const uint32_t qmask = (uint32_t)__ballot(iv);  // valid query bits of a packed word
-  float m_run = NEG_INF, zp = 0.f, zgp = 0.f;
-  f32x16 o[DT];
-#pragma unroll
-  for (int t = 0; t < DT; ++t) o[t] = zero16();
-  uint32_t cntl = 0;
-  for (int kt = 0; kt < p.NKB; ++kt) {
-    const int j0 = kt * 32;
-    const bool more = kt + 1 < p.NKB;
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // everything but tile kt's V image (the youngest 8)
-    if (kt == 0) {  // the bias row (0 / -inf, sbm_attn.py:61) and the scaled query operands
-      key_bias_store(lds + LY::BOFF / 4, p, b, km);
-#pragma unroll
-      for (int e = 0; e < NS; ++e) q[e] *= p.scale;
-      if constexpr (!DENSE && !HAS_U)
-#pragma unroll
-        for (int e = 0; e < KPH; ++e) qh[e] *= ESC;
-    }
-    // S^T = K (Q/8)^T on top of the key bias: registers 4g..4g+3 hold keys j0 + 8g + 4h + e
-    f32x16 sacc;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const f32x4 bz = lds_f4(lds, LY::BOFF + 4 * (j0 + 8 * g + 4 * h));
-#pragma unroll
-      for (int e = 0; e < 4; ++e) sacc[4 * g + e] = bz[e];
-    }
-    // the tile's Philox words (query, tile, head): their VALU is spread over the S chain's MFMA gaps
-    u32x4 r_ste[2], r_drop[2];
-    {
-      uint32_t sk0 = p.seed_lo, sk1 = p.seed_hi;  // opaque per tile: round keys are not held across the loop
-      asm volatile("" : "+s"(sk0), "+s"(sk1));
-#pragma unroll
-      for (int gp = 0; gp < 2; ++gp) {
-        if constexpr (!DENSE && !HAS_U)
-          r_ste[gp] = philox4x32(u32x4{(uint32_t)i, (uint32_t)(8 * kt + 4 * gp + h), (uint32_t)bh,
-                                       (RNG_STE << 28) ^ p.off}, sk0, sk1);
-        if constexpr (DROP)
-          r_drop[gp] = philox4x32(u32x4{(uint32_t)i, (uint32_t)(8 * kt + 4 * gp + h), (uint32_t)bh,
-                                        (RNG_ATTN_DROP << 28) ^ p.off}, sk0, sk1);
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < NS / 4; ++j) {
-      const f32x4 kv = lds_f4(lds, kbase ^ (16 * j));
-#pragma unroll
-      for (int e = 0; e < 4; ++e) sacc = mfma(kv[e], q[4 * j + e], sacc);
-    }
-#pragma unroll
-    for (int m = 0; m < NS; ++m) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one S MFMA
-      __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);   // then up to six VALU (Philox)
-    }
-    // the Philox words are complete here (so they are computed among the S MFMAs, not sunk to their use)
-#pragma unroll
-    for (int gp = 0; gp < 2; ++gp) {
-      if constexpr (!DENSE && !HAS_U) asm volatile("" : "+v"(r_ste[gp].x), "+v"(r_ste[gp].y), "+v"(r_ste[gp].z), "+v"(r_ste[gp].w));
-      if constexpr (DROP) asm volatile("" : "+v"(r_drop[gp].x), "+v"(r_drop[gp].y), "+v"(r_drop[gp].z), "+v"(r_drop[gp].w));
-    }
-    // expA^T = T Qh^T (sbm_attn.py:55); tile kt+1's K and T pieces go out between its MFMAs
-    f32x4 tv[KPH > 0 ? KPH / 4 : 1];
-    if constexpr (!DENSE)
-#pragma unroll
-      for (int j = 0; j < KPH / 4; ++j) tv[j] = lds_f4(lds, tbase ^ (16 * j));
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the K, T and bias reads have returned
-    f32x16 eacc = zero16();
-    if constexpr (!DENSE) {
-      static_assert(KPH == 8, "the E chain interleave assumes 8 MFMAs (kp = 16)");
-      if (more) {
-#pragma unroll
-        for (int m = 0; m < KPH; ++m) {
-          eacc = mfma(tv[m / 4][m % 4], qh[m], eacc);
-          dma64(Kl, kr, kpat, kld, j0 + 32, m, m + 1);
-        }
-        dma_narrow(Tl, tr, j0 + 32, KPN);
-#pragma unroll
-        for (int m = 0; m < KPH; ++m) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one E MFMA
-          __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // then one K piece
-        }
-      } else {
-#pragma unroll
-        for (int m = 0; m < KPH; ++m) eacc = mfma(tv[m / 4][m % 4], qh[m], eacc);
-      }
-    } else {
-      if (more) dma64(Kl, kr, kpat, kld, j0 + 32);
-    }
-    // V^T operand values for this tile's PV: lane (d = 32t + c) reads V[key crow(r,h)][d]
-    // tile kt's V image: older than tile kt+1's K and T pieces
-    if (more) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(8 + TP) : "memory");
-    else wait_vm_all();
-    float vt[DT][16];
-#pragma unroll
-    for (int t = 0; t < DT; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) vt[t][r] = lds_f1(lds, vb[t] + 256 * crow(r, 0));
-    float tmax = NEG_INF;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, sacc[r]);
-    bool av[16], keep[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) { av[r] = true; keep[r] = true; }
-    if constexpr (!DENSE) {
-      if constexpr (HAS_U) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int j = j0 + crow(r, h);
-          const float v = p.U[((int64_t)bh * p.N + ic) * p.M + imin(j, p.M - 1)];
-          const float uu = (iv && j < p.M) ? v : 2.f;
-          av[r] = uu < fminf(fmaxf(eacc[r], 0.01f), 0.99f);  // STE.py:11-13
-        }
-      } else {
-#pragma unroll
-        for (int gp = 0; gp < 2; ++gp)
-#pragma unroll
-          for (int e = 0; e < 8; ++e)
-            av[8 * gp + e] = (float)u16_of(r_ste[gp], e) < __builtin_amdgcn_fmed3f(eacc[8 * gp + e], 0.01f * ESC, 0.99f * ESC);
-      }
-    }
-    if constexpr (DROP) {
-#pragma unroll
-      for (int gp = 0; gp < 2; ++gp)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) keep[8 * gp + e] = u16_of(r_drop[gp], e) >= p.drop_thr;
-    }
-    // bit-pack the sampled graph / dropout keep mask: word [qb][key] holds 32 query bits (lanes 0..31)
-    if constexpr (!DENSE || DROP) {
-      const uint32_t myA = DENSE ? 0u : pack_bits(av);
-      const uint32_t myR = DROP ? pack_bits(keep) : 0u;
-      const int64_t widx = ((int64_t)bh * p.NQB + qb) * p.Mpad + j0 + c;
-      if constexpr (!DENSE) {
-        if (h == 0) p.Abits[widx] = myA;
-        if (j0 + c < p.M) cntl += __popc(myA & qmask);  // sampled edges inside [0,N) x [0,M)
-      }
-      if constexpr (DROP) if (h == 0) p.Rbits[widx] = myR;
-    }
-    // online softmax: the reference max moves only when the row max grows by more than RESCALE_TH
-    tmax = xhalf_max(tmax);
-    const float m_tgt = (tmax > m_run + RESCALE_TH) ? tmax : m_run;
-    if (__builtin_amdgcn_ballot_w64(m_tgt != m_run) != 0) {
-      const float alpha = (m_tgt == m_run) ? 1.f : __builtin_amdgcn_exp2f((m_run - m_tgt) * LOG2E);
-      zp *= alpha;
-      zgp *= alpha;
-#pragma unroll
-      for (int t = 0; t < DT; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
-      m_run = m_tgt;
-    }
-    const float nmL = -((m_run == NEG_INF) ? 0.f : m_run) * LOG2E;
-    float w[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float e = __builtin_amdgcn_exp2f(fmaf(sacc[r], LOG2E, nmL));
-      zp += e;
-      const float wa = av[r] ? e : 0.f;
-      zgp += wa;
-      w[r] = keep[r] ? wa : 0.f;
-    }
-    // O^T += V^T W^T (keys beyond M carry w = 0); tile kt+1's V pieces go out between the MFMAs (the vt reads have
-    // returned: this tile's V image is free)
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (more) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-#pragma unroll
-        for (int t = 0; t < DT; ++t) o[t] = mfma(vt[t][r], w[r], o[t]);
-        if (r < 8) dma64(Vl, vr, vpat, vld, j0 + 32, r, r + 1);
-      }
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // two PV MFMAs
-        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // then one V piece
-      }
-    } else {
-#pragma unroll
-      for (int r = 0; r < 16; ++r)
-#pragma unroll
-        for (int t = 0; t < DT; ++t) o[t] = mfma(vt[t][r], w[r], o[t]);
-    }
-  }
-  const float Z = xhalf_sum(zp), Zg = xhalf_sum(zgp);
-  const float n = Zg / Z;
-  const float Dn = fmaxf(n, NORM_EPS);
-  const float dscale = DROP ? 1.f / (1.f - p.attn_p) : 1.f;  // dropout's 1/(1-p), applied once per row
-  const float inv = dscale / (Z * Dn);
-  if (iv) {
-#pragma unroll
-    for (int t = 0; t < DT; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) o[t][r] *= inv;
-    store_rows<DT>(p.X + b * p.x_sb + hd * p.x_sh + (int64_t)i * p.x_sn, D, D, o, true);
-    if (h == 0) {
-      f32x4 st;
-      st[0] = m_run + logf(Z);   // lse: P = exp(s - lse)
-      st[1] = 1.f / Dn;          // 1 / max(n, eps)
-      st[2] = (n >= NORM_EPS) ? 1.f : 0.f;
-      st[3] = 0.f;               // gamma, filled by the backward
-      *reinterpret_cast<f32x4*>(p.stats + ((int64_t)bh * p.N + i) * 4) = st;
-    }
-  }
-  if constexpr (!DENSE) {
-    cntl = (h == 0) ? cntl : 0u;
-#pragma unroll
-    for (int o2 = 32; o2 >= 1; o2 >>= 1) cntl += __shfl_xor(cntl, o2, 64);
-    if (lane == 0 && cntl) atomicAdd(p.cnt + hd, (unsigned long long)cntl);
-  }
 }
 
 __global__ void k_sparsity_finish(const unsigned long long* __restrict__ cnt, float* __restrict__ sp, int H, float bnm) {
@@ -2233,21 +1833,13 @@ __device__ __forceinline__ float2 pair_read(const float* lds, int base, int r, i
 
 template <int D, int KPH, bool DENSE, bool DROP, bool DG, bool BF>
 __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd_kv(const KArgs p) {
-#ifdef CSA_EXP_PRIO  // experiment: half of the waves (by dispatch slot parity) at priority 1
-  if ((blockIdx.x >> 3) & 1) __builtin_amdgcn_s_setprio(1);
-#endif
-  FST_DECL
   using SH = AttnBwdShape<D, KPH>;
   constexpr int DT = D / 32, NS = D / 2, DP = SH::DP, KP = SH::KP, KPN = SH::KPN, KTA = SH::KTA;
   constexpr bool SWZ = SH::SWZ;
   constexpr bool MB4 = !DENSE && KP == 16;  // dT on mfma4b (store_mb4)
   constexpr bool HO = bwd_handoff<BF>();    // ds / G tiles out for k_attn_bwd_qg (else k_attn_bwd_qr recomputes)
   constexpr bool W1 = HO && !DENSE && !DG;  // one-plane w tiles (W_NO_EDGE)
-#ifdef CSA_EXP_KV_SCALAR  // experiment: the 32t + m mapping with scalar column reads
-  constexpr bool PAIR = false;
-#else
   constexpr bool PAIR = SWZ && !BF;  // dK / dV rows as d = 2m + t (b64 operand reads, pair_read)
-#endif
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const uint32_t L0 = lds_offset(lds), Ql = L0 + SH::KQ, Xl = L0 + SH::KX, Hl = L0 + SH::KH, Sl = L0 + SH::KS;
   const int lane = lane_id(), c = lane & 31, h = lane >> 5;
@@ -2297,7 +1889,6 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
   for (int t = 0; t < DT; ++t) { dv[t] = zero16(); dk[t] = zero16(); }
 #pragma unroll
   for (int t = 0; t < KTA; ++t) dtt[t] = zero16();
-  FST(0)
   for (int qb = 0; qb < p.NQB; ++qb) {
     int ln = threadIdx.x;  // opaque per iteration: keeps the per-row LDS addresses out of the prologue
     asm volatile("" : "+v"(ln));
@@ -2309,7 +1900,6 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
     asm volatile("" : "+v"(mvl), "+v"(dsl));
     const float kbias = (jv && mvl == 0.f) ? 0.f : NEG_INF;  // this lane's key (sbm_attn.py:61)
     const float csp = dsl / ((float)p.B * (float)p.N * (float)p.M);
-    FST(1)
     // W1: does a row of this query block have rho != 0 (its query side then needs P as well)?
     const bool rho_any = W1 && __builtin_amdgcn_ballot_w64(lds_f1(lds, SH::KS + 16 * c + 12) != 0.f) != 0;
     // sampled / keep bits shifted so that register r's query is bit crow(r, 0); queries past N and keys past M
@@ -2346,7 +1936,6 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
         for (int e = 0; e < 4; ++e) dpacc = mfma(xv[e], vr[4 * s4 + e], dpacc);
       }
     }
-    FST(2)
     // column read of element (query crow(r,h), d = 32t + c) of the Q / dX image at byte offset off
     int cb[DT];
 #pragma unroll
@@ -2391,25 +1980,11 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
           gv[rr] = a ? __builtin_amdgcn_fmed3f(fmaf(dM, P, cg), -1.f, 1.f) : 0.f;  // STE.py:19 hardtanh(A * grad)
         }
         awv[rr] = (a && kp) ? P * rec[1] : 0.f;  // dropout(attn) weight for dV
-#ifndef CSA_EXP_NO_DSG_STORE
         if constexpr (W1) {  // stored as soon as four are ready (fewer live registers); non-temporal, see below
-#if defined(CSA_EXP_KV_NOST1)  // experiment: no stores of the second half's w (wrong results)
-          if ((rr & 3) == 3 && half == 0)
-#elif defined(CSA_EXP_KV_NOST0)  // experiment: no stores of the first half's w (wrong results)
-          if ((rr & 3) == 3 && half == 1)
-#else
           if ((rr & 3) == 3)
-#endif
             __builtin_nontemporal_store((f32x4{wv[0], wv[1], wv[2], wv[3]}), reinterpret_cast<f32x4*>(wst + 2 * (rr & 4)));
         }
-#endif
-#ifdef CSA_EXP_NO_ELEM  // experiment: timing without the elementwise algebra (wrong results)
-        dsv[rr] = sacc[r] * dpacc[r];
-        gv[rr] = dpacc[r];
-        awv[rr] = sacc[r];
-#endif
       }
-#ifndef CSA_EXP_NO_DSG_STORE  // experiment: timing without the ds / G stores (wrong results)
       if constexpr (HO) {  // queries 16 half + 4 h + (0..3) and + 8: two f32x4 per tile, for ds and for G
         float* const w = wst;
         // non-temporal: the tiles are read once, by the next kernel (same-box A/B: k_attn_bwd_qg 157 -> 134 us)
@@ -2435,8 +2010,6 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
         }
 #undef CSA_ST4
       }
-#endif
-      FST(3 + 2 * half)
       // dV^T += dX^T attw ; dK^T += Q^T ds ; dT^T += Qh^T G  (queries beyond N carry zeros)
       if constexpr (BF) {
         const bf16x8 aw8 = pack8(awv), ds8 = pack8(dsv);
@@ -2483,12 +2056,7 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
             dtt[at] = mfma((KP >= 32 || c < KP) ? v : 0.f, gv[rr], dtt[at]);
           }
       }
-      FST(4 + 2 * half)
-#ifdef CSA_EXP_NO_LOOP_DMA  // experiment: timing without the in-loop refills (wrong results)
-      if (false) {
-#else
       if (more) {
-#endif
         // the whole refill after the second half: no mid-tile wait on the first half's reads, so the second
         // half's elementwise can be scheduled among the first half's MFMAs (a per-half rolling refill measured
         // 4 us slower, profiles/r04_ab_kv_refill.txt)
@@ -2509,7 +2077,6 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
         }
       }
     }
-    FST(7)
   }
   if constexpr (PAIR) {  // d = 2 crow(r, h) + t: registers 4g .. 4g + 3 of both tiles are d = 16g + 8h .. + 7
     if (jv) {
@@ -2531,12 +2098,6 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
   }
   if constexpr (MB4) store_mb4(p.dT + ((int64_t)bh * p.M + kbi * 32) * p.kp, p.M - kbi * 32, p.kp, dtt[0]);
   else if constexpr (!DENSE) store_rows<KTA>(p.dT + ((int64_t)bh * p.M + j) * p.kp, p.kp, p.kp, dtt, jv);
-#ifdef CSA_EXP_FWD_STAMPS
-  FST(8)
-  if (lane == 0 && blockIdx.x % 331 == 0)
-    printf("KST blk=%d pro %llu wait %llu S+dP %llu el0 %llu mm0 %llu el1 %llu mm1 %llu refill %llu epi %llu\n",
-           (int)blockIdx.x, fst[0], fst[1], fst[2], fst[3], fst[4], fst[5], fst[6], fst[7], fst[8]);
-#endif
 }
 
 // ------------------------------------------------------------------------------------
@@ -3124,11 +2685,7 @@ __global__ __launch_bounds__(256, ProjBwdSmallShape<D>::LCS ? 1 : 2) void k_proj
   // the item's hat block: its rows of Qh / Kh as k_proj_fwd_l stored them for the attention kernels ([row][16],
   // rows past the item's last row not fetched), so the forward saves no second copy in the activation block
   // (HAT_ACT: the activation block's feature-major copy, the round-4 form)
-#ifdef CSA_EXP_HAT_ACT
-  constexpr bool HQK = false;
-#else
   constexpr bool HQK = true;
-#endif
   auto prefetch_hat = [&](const Item& it) {
     if constexpr (HQK) {
       const int bh = it.b * p.H + hd, row0 = it.rb * 32;
@@ -3164,12 +2721,7 @@ __global__ __launch_bounds__(256, ProjBwdSmallShape<D>::LCS ? 1 : 2) void k_proj
   prefetch_hat(item_of(0));
   prefetch(item_of(0));
   if constexpr (LW) load_wf(2);
-#ifdef CSA_PHASES  // dev instrumentation: per-wave cycles by phase of workgroup (0, 0), printed at exit
-  unsigned long long ph_t = __builtin_amdgcn_s_memtime(), ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#define PHASE(i) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); ph[i] += t_ - ph_t; ph_t = t_; }
-#else
 #define PHASE(i)
-#endif
 
   for (int grp = 0; grp * 4 < n_items; ++grp) {
     int tid = threadIdx.x;  // opaque: per-lane addresses are recomputed in the loop, not hoisted
@@ -3185,13 +2737,9 @@ __global__ __launch_bounds__(256, ProjBwdSmallShape<D>::LCS ? 1 : 2) void k_proj
     if constexpr (LW) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D * D / 1024) : "memory");
     else wait_vm_all();
     PHASE(0);
-#ifdef CSA_EXP_RECOMP_PO
-    dma_block16<D * 128>(INl, ar, (D == 64 ? 32 : 64) * D * 4);  // experiment: h2 (po is recomputed from it)
-#else
     if constexpr (BF) dma_block16<D * 64>(INl + 2 * REG, ar, 64 * D * 4);  // bf16 po -> upper half (widened below)
     else if constexpr (H2C) dma_block16<D * 128>(INl, ar, 32 * D * 4);  // h2 -> own IN region (free since B6): the dC
     else dma_block16<D * 128>(INl, ar, 64 * D * 4);  // product below, then layer 2's stage (po -> IN otherwise)
-#endif
     f32x16 gin[1];
     float dTt[8];
 #pragma unroll
@@ -3242,18 +2790,7 @@ __global__ __launch_bounds__(256, ProjBwdSmallShape<D>::LCS ? 1 : 2) void k_proj
     f32x16 dcur[DT];
     mm_acc_f<DT, 1, 2, LCS ? 8 : 16, LCS, BF>(LCS ? CFs : CfT, dz, dcur);
     wait_vm_all();  // po (LW: and the W2 fragments)
-#ifndef CSA_EXP_RECOMP_PO
     if constexpr (BF) widen_act_bf<REG>(INw, ln);
-#endif
-#ifdef CSA_EXP_RECOMP_PO
-    if constexpr (D == 64) {  // po = W2 h2 + b2: the forward's own chain (L2 fragments), bit-identical
-      f32x16 h2v[DT], pov[DT];
-      read_act<DT>(h2v, INw, ln);
-      mlp_layer<D, false, BF>(p.Wf[2], p.pb[2], h2v, pov);
-      stage_ds<DT>(INw, pov, D, ln);  // same wave: its LDS reads above complete before these writes
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    }
-#endif
     // ---- dC_h += dZ^T po, private 16x16x4: A = dZ[row 4s + g4][cluster c16], B = po[row 4s + g4][16t + c16]
     //      (H2C: dZ^T h2, and accZ[e] = sum over rows of dZ[.][cluster 4 g4 + e], B = 1)
 #pragma unroll
@@ -3382,11 +2919,6 @@ __global__ __launch_bounds__(256, ProjBwdSmallShape<D>::LCS ? 1 : 2) void k_proj
       if (more) load_wf(2);                   // waits for them with the W2 fragments still in flight)
     }
   }
-#ifdef CSA_PHASES
-  if (blockIdx.x == 0 && blockIdx.y == 0 && lane == 0)
-    printf("PHASES d=%d w=%d prefetch %llu preB1 %llu chainW2 %llu barrier %llu outer %llu chainW1 %llu stageX %llu dx %llu\n",
-           D, w, ph[0], ph[1], ph[7], ph[2], ph[3], ph[4], ph[5], ph[6]);
-#endif
 #undef PHASE
   // ---- slab, written once: dW tiles, bias sums and dS / dC, wave partials combined in a fixed order
   float* part = lds + w * Sh::PARTF;  // [dS 16 x 16 | dC 16 x D | db0 | db1 | db2] of this wave
@@ -3725,40 +3257,8 @@ csa_status validate_fwd(const csa_sbm_fwd_args* a) {
   return CSA_OK;
 }
 
-// d = 64 fp32 with kp <= 16 clusters: k_attn_fwd64 (q carries the exact 1/8 scale). Opt-in experiment: same box,
-// 1.3-3% slower than k_attn_fwd (profiles/r05_ab_fwd.txt), so the shipped forward is k_attn_fwd.
-template <int D, int KPH, bool BF>
-bool fwd64(const KArgs& p) {
-#ifndef CSA_EXP_FWD64
-  return false;
-#endif
-  return D == 64 && !BF && KPH <= 8 && p.scale == 0.125f;
-}
-
 template <int D, int KPH, bool DENSE, bool BF>
 void launch_attn_fwd(const KArgs& p, int BH, const Layout& L, bool has_u, bool drop, hipStream_t st) {
-  if constexpr (D == 64 && !BF && KPH <= 8) {
-    if (fwd64<D, KPH, BF>(p)) {
-      const size_t lb = AttnFwdLds<D, KPH>::bytes((int)L.Mpad);
-      const dim3 grid(xcd_grid((int)L.NQB, BH));
-#define CSA_F64_KERNEL k_attn_fwd64
-#define CSA_F64_LAUNCH(HU, DR)                                                                  \
-  do {                                                                                          \
-    if (lb > 64 * 1024) set_dyn_lds((const void*)CSA_F64_KERNEL<KPH, DENSE, HU, DR>, (int)lb);  \
-    hipLaunchKernelGGL((CSA_F64_KERNEL<KPH, DENSE, HU, DR>), grid, dim3(64), lb, st, p);        \
-  } while (0)
-      if (!DENSE && has_u) {
-        if (drop) CSA_F64_LAUNCH(!DENSE, true);
-        else CSA_F64_LAUNCH(!DENSE, false);
-      } else {
-        if (drop) CSA_F64_LAUNCH(false, true);
-        else CSA_F64_LAUNCH(false, false);
-      }
-#undef CSA_F64_LAUNCH
-#undef CSA_F64_KERNEL
-      return;
-    }
-  }
   const size_t lds_bytes = AttnFwdLds<D, KPH>::bytes((int)L.Mpad);
   const dim3 grid(xcd_grid((int)L.NQB, BH));
   if (lds_bytes > 64 * 1024) {
