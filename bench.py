@@ -437,6 +437,258 @@ def launcher_selftest(args, world, rank, dev):
             "config": {"workload": "launcher self-test", "parallelism": f"dp{world}"}}
 
 
+def stage_profilers():
+    """(HipEvents, make_profs(n, stages, slots, fwd_stages), stage_times(profs, stages, slots, fwd_stages))."""
+    from csa_amd._lib import CsaProf
+    ev = HipEvents()
+
+    def make_profs(n, stages, slots, fwd_stages):
+        out = []
+        for _ in range(n):
+            pf, pb = CsaProf(), CsaProf()
+            for name in stages:
+                s_ = slots[name]
+                tgt = pf if name in fwd_stages else pb
+                tgt.start[s_], tgt.stop[s_] = ev.create().value, ev.create().value
+            out.append((pf, pb))
+        return out
+
+    def stage_times(profs, stages, slots, fwd_stages):
+        res = {}
+        for name in stages:
+            s_ = slots[name]
+            vals = []
+            for pf, pb in profs:
+                tgt = pf if name in fwd_stages else pb
+                if tgt.start[s_] and tgt.stop[s_]:
+                    vals.append(ev.elapsed_ms(ctypes.c_void_p(tgt.start[s_]), ctypes.c_void_p(tgt.stop[s_])))
+            vals = [v for v in vals if v == v and v > 0]
+            if vals:
+                res[name] = sum(vals) / len(vals)
+        return res
+    return ev, make_profs, stage_times
+
+
+def measure_layer(world, rank, dev, steps, warmup, B, N, d, k, dense, precision, eval_, reducer="torch"):
+    """One SBMAttention (or FullAttention) fwd+bwd step on synthetic inputs resident in HBM: an untimed pass with
+    HIP events around every stage (per-stage kernel times, the dominant stage), then the timed region with events
+    only around the dominant kernel's launch (its live average launch duration). Returns the pieces of the line."""
+    from csa_amd import ops
+    from csa_amd._lib import STAGES, KERNEL_OF_STAGE
+    from csa_amd.module.sbm_attn import FullAttention, SBMAttention
+    H = 8
+    torch.manual_seed(1234 + rank)
+    cfg = {"attention_dropout": 0.2, "head_dim": d, "num_head": H, "num_clusters": [k], "return_maps": False,
+           "attn_precision": precision}
+    mod = (FullAttention(cfg, 0) if dense else SBMAttention(cfg, 0)).to(dev)
+    for p in mod.parameters():
+        if p.dim() > 1:
+            torch.nn.init.xavier_uniform_(p)
+    if not dense:
+        torch.nn.init.orthogonal_(mod.layer.weight)
+    mod.train(not eval_)
+    model = mod
+    if world > 1 and not dense:  # FullAttention has no parameters: no gradient exchange exists
+        from csa_amd.train import wrap_ddp
+        model = wrap_ddp(mod, dev, impl=reducer)  # in-order attention backward beside RCCL
+    Q, K, V = (torch.randn(B, H, N, d, device=dev).requires_grad_(True) for _ in range(3))
+    mask = torch.zeros(B, N, device=dev)
+    dX = torch.randn(B, H, N, d, device=dev)
+    dsp = torch.full((H,), 3.125e-4, device=dev)
+
+    def step(i=0):
+        for t in (Q, K, V):
+            t.grad = None
+        for p in mod.parameters():
+            p.grad = None
+        X, sp, _, _ = model(Q, K, V, mask)
+        if sp is None:
+            torch.autograd.backward([X], [dX])
+        else:
+            torch.autograd.backward([X, sp], [dX, dsp])
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    ev, make_profs_, stage_times_ = stage_profilers()
+    fwd_stages = ("prep", "proj_fwd", "attn_fwd")
+    make_profs = lambda n, stages: make_profs_(n, stages, STAGES, fwd_stages)  # noqa: E731
+    stage_times = lambda profs, stages: stage_times_(profs, stages, STAGES, fwd_stages)  # noqa: E731
+
+    # 1) untimed profiling pass: HIP events around every stage -> per-stage kernel times (diagnostic)
+    nprof = max(3, min(steps, 10))
+    profs = make_profs(nprof, list(STAGES))
+    for i in range(nprof):
+        ops.set_stage_profiler(*profs[i])
+        step()
+    ops.set_stage_profiler(None, None)
+    torch.cuda.synchronize()
+    stage_ms = stage_times(profs, list(STAGES))
+    flops = stage_flops_per_ast(H, N, N, d, 0 if dense else k)
+    if dense:
+        flops = {"attn_fwd": H * 4 * N * N * d, "attn_bwd_q": H * 2 * N * N * d, "attn_bwd_kv": H * 6 * N * N * d}
+    if "proj_bwd_k" in stage_ms:  # concurrent schedule: the projection backward's key / query items split
+        flops["proj_bwd_k"] = H * (N * (12 * d * d + 4 * k * d) + N * 4 * k * k)
+        flops["proj_bwd"] = H * N * (12 * d * d + 4 * k * d)
+    timed = {s_: v for s_, v in stage_ms.items() if s_ in flops}
+    # side-stream backward: a stage window that overlaps another backward stage's window is not one kernel's
+    # launch alone on the device, so it cannot be the roofline kernel
+    pb0 = profs[-1][1]
+    win = {}
+    base = None
+    for name in ("attn_rowprep", "attn_bwd_kv", "attn_bwd_q", "proj_bwd_k", "proj_bwd", "reduce"):
+        s_ = STAGES[name]
+        if pb0.start[s_] and pb0.stop[s_]:
+            if base is None:
+                base = pb0.start[s_]
+            win[name] = (ev.elapsed_ms(ctypes.c_void_p(base), ctypes.c_void_p(pb0.start[s_])),
+                         ev.elapsed_ms(ctypes.c_void_p(base), ctypes.c_void_p(pb0.stop[s_])))
+    over = {a for a in win for b_ in win if a != b_ and win[a][0] < win[b_][1] - 1e-4 and win[b_][0] < win[a][1] - 1e-4}
+    cand = {s_: v for s_, v in timed.items() if s_ not in over}
+    dom = max(cand, key=cand.get) if cand else None
+    kernel_of = dict(KERNEL_OF_STAGE)
+    if not dense and d in (64, 96) and k <= 16:
+        kernel_of["proj_bwd"] = kernel_of["proj_bwd_k"] = "k_proj_bwd_s"  # the k <= 16 projection-backward variant
+
+    # 2) timed region: events only around the dominant kernel (its live average launch duration)
+    profs = make_profs(steps, [dom] if dom else [])
+
+    def timed_step(i):
+        ops.set_stage_profiler(*profs[i])
+        step()
+
+    elapsed = timed_region(world, dev, steps, timed_step)
+    ops.set_stage_profiler(None, None)
+    dom_ms = stage_times(profs, [dom]).get(dom) if dom else None
+    ev.destroy()
+    roofline = None
+    if dom and dom_ms:
+        ach = flops[dom] * B / (dom_ms * 1e-3) / 1e12
+        roofline = {"bound": "mfma", "kernel": kernel_of[dom], "achieved": round(ach, 2),
+                    "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / PEAK_F32_MFMA_TFLOPS, 4),
+                    "traffic": None, "avg_launch_ms": round(dom_ms, 4),
+                    "frac_basis": "live: HIP events on the kernel's stream around each of its launches in the timed "
+                                  "steps (event timestamps include the launch's dispatch edge; frac_rocprof, when "
+                                  "present, uses the committed rocprofv3 kernel-trace average)"}
+    return {"mod": mod, "step": step, "mask": mask, "stage_ms": stage_ms, "flops": flops, "timed": timed,
+            "over": over, "overlapped": bool(over), "dom": dom, "dom_ms": dom_ms, "kernel_of": kernel_of,
+            "elapsed": elapsed, "roofline": roofline}
+
+
+def rocprof_frac(table, leg, kernel, flops_per_launch):
+    """frac_rocprof of a side leg's dominant kernel from the shipped rocprof table (tools/pmc_traffic.py legs)."""
+    if not table:
+        return {}
+    t = (table.get("legs", {}).get(leg, {}) or {}).get(kernel)
+    if not t or not t.get("rocprof_avg_ns"):
+        return {}
+    ach = flops_per_launch / (t["rocprof_avg_ns"] * 1e-9) / 1e12
+    return {"frac_rocprof": round(ach / PEAK_F32_MFMA_TFLOPS, 4), "rocprof_avg_launch_ms": round(t["rocprof_avg_ns"] * 1e-6, 4),
+            "pmc_table_matches_library": table.get("csa_source_hash") == _loaded_hash()}
+
+
+def _loaded_hash():
+    from csa_amd._lib import loaded_source_hash
+    return loaded_source_hash()
+
+
+def side_layer_leg(dev, steps, warmup, B, N, d, k, dense, table, leg):
+    """A BASELINE config beside the headline (config 4 dense FullAttention, config 5 long ASTs): the same
+    measurement as the headline (measure_layer) on one GPU; its own line fields, never `value`."""
+    L = measure_layer(1, 0, dev, steps, warmup, B, N, d, k, dense, "fp32", False)
+    ms = L["elapsed"] * 1000.0 / steps
+    total = sum(L["flops"].values()) * B
+    out = {"value": round(B * steps / L["elapsed"], 1), "unit": "ASTs/s", "ms_per_step": round(ms, 4),
+           "batch": B, "seq_len": N, "head_dim": d, "clusters": 0 if dense else k, "steps": steps,
+           "step_tflops": round(total / (ms * 1e-3) / 1e12, 2),
+           "step_frac_of_f32_mfma_peak": round(total / (ms * 1e-3) / 1e12 / PEAK_F32_MFMA_TFLOPS, 4),
+           "stage_ms": {s_: round(v, 4) for s_, v in L["stage_ms"].items()}}
+    if L["roofline"]:
+        r = dict(L["roofline"])
+        r.pop("frac_basis", None)
+        r.update(rocprof_frac(table, leg, r["kernel"], L["flops"][L["dom"]] * B))
+        out["roofline"] = r
+    del L
+    torch.cuda.empty_cache()
+    return out
+
+
+CSE_FLOPS_PER_AST = 3 * 8 * 8 * 150 * 150 * 64  # SURVEY 8(d): 3 * H * 8 N^2 d_k (fwd + bwd) = 276.5 MFLOP
+
+
+def cse_leg(dev, steps, warmup, table, B=64):
+    """north_star's second kernel: the CSE relation attention (module/disentangled_attn.py:44-65) alone at the java
+    train step's shape (B = 64 ASTs per GPU, H = 8, N = L = 150, d_k = 64, synthetic AST relation planes), fwd+bwd
+    with fresh input gradients each step (the train step's zero_grad(set_to_none=True)). HIP events around every
+    CSE stage in an untimed pass (ABI v9 CSA_REL_STAGE_*), then the timed steps with events around the dominant
+    kernel only."""
+    import numpy as np
+    from csa_amd import ops, rel_ops
+    from csa_amd._lib import REL_STAGES, REL_KERNEL_OF_STAGE
+    from csa_amd.data import synthetic_batch
+    H, N, d, Lr = 8, 150, 64, 150
+    sb = synthetic_batch(B, N, seed=3)
+    rel = torch.from_numpy(np.stack([sb["L"], sb["T"]], 1)).to(dev)
+    msk = torch.from_numpy(np.stack([sb["L_mask"], sb["T_mask"]], 1).astype(np.uint8)).to(dev)
+    g = torch.Generator(device=dev).manual_seed(77)
+    q, k, v, dO = (torch.randn(B, H, N, d, device=dev, generator=g) for _ in range(4))
+    lq, lk = (torch.randn(H, Lr, d, device=dev, generator=g) for _ in range(2))
+    for t in (q, k, v, lq, lk):
+        t.requires_grad_(True)
+
+    def step(i=0):
+        for t in (q, k, v, lq, lk):
+            t.grad = None
+        rel_ops.rel_attn(q, k, v, lq, lk, rel, msk).backward(dO)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    ev, make_profs_, stage_times_ = stage_profilers()
+    fwd_stages = ("logits", "fwd")
+    stages = list(REL_STAGES)
+    profs = make_profs_(max(3, min(steps, 10)), stages, REL_STAGES, fwd_stages)
+    for pr in profs:
+        ops.set_rel_profiler(*pr)
+        step()
+    ops.set_rel_profiler(None, None)
+    torch.cuda.synchronize()
+    stage_ms = stage_times_(profs, stages, REL_STAGES, fwd_stages)
+    # algorithmic FLOP per stage and AST (SURVEY 8(d): 12 products of 2 H N^2 d = 276.5 MFLOP with L = N), split as
+    # the kernels compute them: logits c2p = Q LK^T, p2c = K LQ^T; forward Q K^T, P V; key side dP = dO V^T,
+    # dv = P^T dO, dk = g^T Q + G_p2c^T LQ (S recomputed, not counted); query side dq = g K + G_c2p LK; lgrad
+    # dlk = G_c2p^T Q, dlq = G_p2c^T K
+    u, ul = 2 * H * N * N * d, 2 * H * N * Lr * d
+    flops = {"logits": 2 * ul, "fwd": 2 * u, "bwd_k": 3 * u + ul, "bwd_q": u + ul, "lgrad": 2 * ul}
+    dom = max((s_ for s_ in stage_ms if s_ in flops), key=stage_ms.get)
+    profs = make_profs_(steps, [dom], REL_STAGES, fwd_stages)
+
+    def timed_step(i):
+        ops.set_rel_profiler(*profs[i])
+        step()
+
+    el = timed_region(1, dev, steps, timed_step)
+    ops.set_rel_profiler(None, None)
+    dom_ms = stage_times_(profs, [dom], REL_STAGES, fwd_stages).get(dom)
+    ev.destroy()
+    ms = el * 1000.0 / steps
+    out = {"value": round(B * steps / el, 1), "unit": "ASTs/s", "ms_per_layer": round(ms, 4), "batch": B,
+           "seq_len": N, "heads": H, "d_k": d, "steps": steps,
+           "workload": "CSE DisentangledAttn.rel_attn fwd+bwd (config/java.py pegen_dim 512 / 8 heads), synthetic "
+                       "AST relation planes",
+           "layer_tflops": round(CSE_FLOPS_PER_AST * B / (ms * 1e-3) / 1e12, 2),
+           "layer_frac_of_f32_mfma_peak": round(CSE_FLOPS_PER_AST * B / (ms * 1e-3) / 1e12 / PEAK_F32_MFMA_TFLOPS, 4),
+           "stage_ms": {s_: round(v, 4) for s_, v in stage_ms.items()}}
+    if dom_ms:
+        ach = flops[dom] * B / (dom_ms * 1e-3) / 1e12
+        r = {"bound": "mfma", "kernel": REL_KERNEL_OF_STAGE[dom], "achieved": round(ach, 2),
+             "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / PEAK_F32_MFMA_TFLOPS, 4),
+             "avg_launch_ms": round(dom_ms, 4), "flops_per_ast": flops[dom]}
+        r.update(rocprof_frac(table, "cse", r["kernel"], flops[dom] * B))
+        out["roofline"] = r
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -457,6 +709,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cpu-config1", action="store_true", help="skip the config-1 CPU CSATrans protocol")
     ap.add_argument("--no-train", action="store_true", help="skip the full train-step measurement")
+    ap.add_argument("--no-side-legs", action="store_true",
+                    help="skip the CSE (java), dense (config 4) and long-AST (config 5) legs")
     ap.add_argument("--reducer", choices=("torch", "bucketed"), default="torch",
                     help="multi-GPU gradient reducer (csa_amd.train.wrap_ddp impl; bucketed is unverified over RCCL "
                          "with more than one rank)")
@@ -489,133 +743,18 @@ def main():
             dist.destroy_process_group()
         return
 
-    from csa_amd import ops
-    from csa_amd._lib import STAGES, CsaProf, KERNEL_OF_STAGE, loaded_source_hash
-    from csa_amd.module.sbm_attn import FullAttention, SBMAttention
+    from csa_amd._lib import loaded_source_hash
 
     B, H, N, d, k = args.batch, 8, args.seq_len, args.head_dim, args.clusters
-    torch.manual_seed(1234 + rank)
-    cfg = {"attention_dropout": 0.2, "head_dim": d, "num_head": H, "num_clusters": [k], "return_maps": False,
-           "attn_precision": args.precision}
-    mod = (FullAttention(cfg, 0) if args.dense else SBMAttention(cfg, 0)).to(dev)
-    for p in mod.parameters():
-        if p.dim() > 1:
-            torch.nn.init.xavier_uniform_(p)
-    if not args.dense:
-        torch.nn.init.orthogonal_(mod.layer.weight)
-    mod.train(not args.eval)
-    model = mod
-    if world > 1 and not args.dense:  # FullAttention has no parameters: no gradient exchange exists
-        from csa_amd.train import wrap_ddp
-        model = wrap_ddp(mod, dev, impl=args.reducer)  # in-order attention backward beside RCCL
-    Q, K, V = (torch.randn(B, H, N, d, device=dev).requires_grad_(True) for _ in range(3))
-    mask = torch.zeros(B, N, device=dev)
-    dX = torch.randn(B, H, N, d, device=dev)
-    dsp = torch.full((H,), 3.125e-4, device=dev)
-
-    def step(i=0):
-        for t in (Q, K, V):
-            t.grad = None
-        for p in mod.parameters():
-            p.grad = None
-        X, sp, _, _ = model(Q, K, V, mask)
-        if sp is None:
-            torch.autograd.backward([X], [dX])
-        else:
-            torch.autograd.backward([X, sp], [dX, dsp])
-
     progress(f"SBM layer B={B} N={N} d={d} k={k}: warm-up")
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-
-    ev = HipEvents()
-    fwd_stages = ("prep", "proj_fwd", "attn_fwd")
-
-    def make_profs(n, stages):
-        out = []
-        for _ in range(n):
-            pf, pb = CsaProf(), CsaProf()
-            for name in stages:
-                s = STAGES[name]
-                tgt = pf if name in fwd_stages else pb
-                tgt.start[s], tgt.stop[s] = ev.create().value, ev.create().value
-            out.append((pf, pb))
-        return out
-
-    def stage_times(profs, stages):
-        res = {}
-        for name in stages:
-            s = STAGES[name]
-            vals = []
-            for pf, pb in profs:
-                tgt = pf if name in fwd_stages else pb
-                if tgt.start[s] and tgt.stop[s]:
-                    vals.append(ev.elapsed_ms(ctypes.c_void_p(tgt.start[s]), ctypes.c_void_p(tgt.stop[s])))
-            vals = [v for v in vals if v == v and v > 0]
-            if vals:
-                res[name] = sum(vals) / len(vals)
-        return res
-
-    # 1) untimed profiling pass: HIP events around every stage -> per-stage kernel times (diagnostic)
-    nprof = max(3, min(args.steps, 10))
-    profs = make_profs(nprof, list(STAGES))
-    for i in range(nprof):
-        ops.set_stage_profiler(*profs[i])
-        step()
-    ops.set_stage_profiler(None, None)
-    torch.cuda.synchronize()
-    stage_ms = stage_times(profs, list(STAGES))
-    flops = stage_flops_per_ast(H, N, N, d, 0 if args.dense else k)
-    if args.dense:
-        flops = {"attn_fwd": H * 4 * N * N * d, "attn_bwd_q": H * 2 * N * N * d, "attn_bwd_kv": H * 6 * N * N * d}
-    if "proj_bwd_k" in stage_ms:  # concurrent schedule: the projection backward's key / query items split
-        flops["proj_bwd_k"] = H * (N * (12 * d * d + 4 * k * d) + N * 4 * k * k)
-        flops["proj_bwd"] = H * N * (12 * d * d + 4 * k * d)
-    timed = {s: v for s, v in stage_ms.items() if s in flops}
-    # side-stream backward: a stage window that overlaps another backward stage's window is not one kernel's
-    # launch alone on the device, so it cannot be the roofline kernel
-    pb0 = profs[-1][1]
-    win = {}
-    base = None
-    for name in ("attn_rowprep", "attn_bwd_kv", "attn_bwd_q", "proj_bwd_k", "proj_bwd", "reduce"):
-        s_ = STAGES[name]
-        if pb0.start[s_] and pb0.stop[s_]:
-            if base is None:
-                base = pb0.start[s_]
-            win[name] = (ev.elapsed_ms(ctypes.c_void_p(base), ctypes.c_void_p(pb0.start[s_])),
-                         ev.elapsed_ms(ctypes.c_void_p(base), ctypes.c_void_p(pb0.stop[s_])))
-    over = {a for a in win for b_ in win if a != b_ and win[a][0] < win[b_][1] - 1e-4 and win[b_][0] < win[a][1] - 1e-4}
-    overlapped = bool(over)
-    cand = {s: v for s, v in timed.items() if s not in over}
-    dom = max(cand, key=cand.get) if cand else None
-    kernel_of = dict(KERNEL_OF_STAGE)
-    if not args.dense and d in (64, 96) and k <= 16:
-        kernel_of["proj_bwd"] = kernel_of["proj_bwd_k"] = "k_proj_bwd_s"  # the k <= 16 projection-backward variant
-
-    # 2) timed region: events only around the dominant kernel (its live average launch duration)
-    profs = make_profs(args.steps, [dom] if dom else [])
-
-    def timed_step(i):
-        ops.set_stage_profiler(*profs[i])
-        step()
-
-    elapsed = timed_region(world, dev, args.steps, timed_step)
-    ops.set_stage_profiler(None, None)
-    dom_ms = stage_times(profs, [dom]).get(dom) if dom else None
-    ev.destroy()
-
+    L = measure_layer(world, rank, dev, args.steps, args.warmup, B, N, d, k, args.dense, args.precision, args.eval,
+                      reducer=args.reducer)
+    mod, step, mask = L["mod"], L["step"], L["mask"]
+    stage_ms, flops, timed, over, overlapped = L["stage_ms"], L["flops"], L["timed"], L["over"], L["overlapped"]
+    dom, dom_ms, kernel_of, elapsed = L["dom"], L["dom_ms"], L["kernel_of"], L["elapsed"]
     ms_per_step = elapsed * 1000.0 / args.steps
     value = world * B * args.steps / elapsed
-    roofline = None
-    if dom and dom_ms:
-        ach = flops[dom] * B / (dom_ms * 1e-3) / 1e12
-        roofline = {"bound": "mfma", "kernel": kernel_of[dom], "achieved": round(ach, 2),
-                    "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / PEAK_F32_MFMA_TFLOPS, 4),
-                    "traffic": None, "avg_launch_ms": round(dom_ms, 4),
-                    "frac_basis": "live: HIP events on the kernel's stream around each of its launches in the timed "
-                                  "steps (event timestamps include the launch's dispatch edge; frac_rocprof, when "
-                                  "present, uses the committed rocprofv3 kernel-trace average)"}
+    roofline = L["roofline"]
     headline = (B, N, d, k, args.precision, args.dense, args.eval) == (256, 150, 64, 10, "fp32", False, False)
     table = pmc_table() if headline else None
     if roofline and table:
@@ -690,6 +829,18 @@ def main():
                               "mean_nodes": round(float(nb.float().mean()), 2),
                               "note": "config 2 padded batches: n_b ~ U[50,150] real nodes per AST (seeded), key mask "
                                       "1 on the padding; every kernel still runs the full 150-node tiles"}
+    if world == 1 and headline and not args.no_side_legs:
+        # BASELINE's other kernel configurations beside the headline, each with its dominant kernel's live roofline
+        progress("CSE leg (java relation attention, B=64)")
+        out["cse"] = cse_leg(dev, args.steps, args.warmup, table)
+        progress("dense leg (config 4: FullAttention, B=256)")
+        out["dense"] = side_layer_leg(dev, args.steps, args.warmup, 256, 150, 64, 0, True, table, "dense")
+        out["dense"]["workload"] = "config 4: FullAttention fwd+bwd (config/python_full_att.py), train mode"
+        out["long_ast"] = {"workload": "config 5: SBM fwd+bwd at N = 1024 (B = 16), k sweep, train mode"}
+        for kk in (16, 32, 64, 128):
+            progress(f"long-AST leg (config 5: N=1024, k={kk}, B=16)")
+            out["long_ast"][f"k{kk}"] = side_layer_leg(dev, max(5, args.steps // 2), max(2, args.warmup // 2), 16,
+                                                       1024, 64, kk, False, table, f"long_k{kk}")
     if not args.no_train:
         progress("train-step leg (config/java.py, 64 ASTs per GPU)")
         from csa_amd.train import GEMM_TABLE, use_tuned_gemms

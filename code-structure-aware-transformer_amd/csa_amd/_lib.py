@@ -12,7 +12,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CSA_HIP_LIB", os.path.join(_HERE, "lib", "libcsa_hip.so"))
 
-CSA_ABI_VERSION = 8
+CSA_ABI_VERSION = 9
 CSA_FLAG_DENSE = 1
 CSA_FLAG_FWD_ONLY = 2
 CSA_FLAG_BF16_WS = 4  # ABI v8: bf16-mode backward workspace (no fp32 tile handoff)
@@ -27,6 +27,10 @@ i64, u64, u32, f32, vp = ctypes.c_int64, ctypes.c_uint64, ctypes.c_uint32, ctype
 CSA_STAGE_COUNT = 9
 STAGES = {"prep": 0, "proj_fwd": 1, "attn_fwd": 2, "attn_bwd_q": 3, "attn_bwd_kv": 4, "proj_bwd": 5, "reduce": 6,
           "proj_bwd_k": 7, "attn_rowprep": 8}
+# ABI v9: CSE relation-attention stages (csa_rel_attn_args.prof / csa_rel_attn_bwd_args.prof) and their kernels
+REL_STAGES = {"logits": 0, "fwd": 1, "qstat": 2, "bwd_k": 3, "bwd_q": 4, "lgrad": 5}
+REL_KERNEL_OF_STAGE = {"logits": "k_rel_logits", "fwd": "k_rel_fwd_f", "qstat": "k_rel_qstat", "bwd_k": "k_rel_bwd_kh",
+                       "bwd_q": "k_rel_bwd_qg", "lgrad": "k_rel_lgrad"}
 KERNEL_OF_STAGE = {"proj_fwd": "k_proj_fwd", "attn_fwd": "k_attn_fwd", "attn_bwd_q": "k_attn_bwd_qg",
                    "attn_bwd_kv": "k_attn_bwd_kv", "proj_bwd": "k_proj_bwd", "proj_bwd_k": "k_proj_bwd",
                    "attn_rowprep": "k_attn_rowprep"}
@@ -93,6 +97,7 @@ class RelAttnArgs(ctypes.Structure):
         ("out", vp), ("row_stats", vp),
         ("state", vp),
         ("o_sb", i64), ("o_sh", i64), ("o_sn", i64),  # ABI v3: 0,0,0 = contiguous
+        ("prof", ctypes.POINTER(CsaProf)),  # ABI v9
     ]
 
 
@@ -106,6 +111,7 @@ class RelAttnBwdArgs(ctypes.Structure):
         ("do_sb", i64), ("do_sh", i64), ("do_sn", i64), ("dq_sb", i64), ("dq_sh", i64), ("dq_sn", i64),
         ("dk_sb", i64), ("dk_sh", i64), ("dk_sn", i64), ("dv_sb", i64), ("dv_sh", i64), ("dv_sn", i64),
         ("schedule", u32), ("side_stream", vp), ("side_fork", vp), ("side_join", vp),  # ABI v5
+        ("prof", ctypes.POINTER(CsaProf)),  # ABI v9
     ]
 
 

@@ -61,6 +61,8 @@ def shim():
         S = ctypes.CDLL(SHIM_PATH)
         S.csa_torch_set_stage_profiler.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         S.csa_torch_set_stage_profiler.restype = None
+        S.csa_torch_set_rel_profiler.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        S.csa_torch_set_rel_profiler.restype = None
         _SHIM = S
     return _SHIM
 
@@ -70,7 +72,7 @@ if os.path.exists(_lib.LIB_PATH) and os.path.exists(SHIM_PATH):
 
 
 # Optional per-stage event profiling (bench.py): csa_prof structs owned by the caller (kept alive here).
-_PROF = {"fwd": None, "bwd": None}
+_PROF = {"fwd": None, "bwd": None, "rel_fwd": None, "rel_bwd": None}
 
 
 def set_stage_profiler(fwd_prof=None, bwd_prof=None):
@@ -78,6 +80,13 @@ def set_stage_profiler(fwd_prof=None, bwd_prof=None):
     _PROF["fwd"], _PROF["bwd"] = fwd_prof, bwd_prof
     shim().csa_torch_set_stage_profiler(None if fwd_prof is None else ctypes.addressof(fwd_prof),
                                         None if bwd_prof is None else ctypes.addressof(bwd_prof))
+
+
+def set_rel_profiler(fwd_prof=None, bwd_prof=None):
+    """The same for the CSE relation attention's stages (ABI v9, _lib.REL_STAGES slots)."""
+    _PROF["rel_fwd"], _PROF["rel_bwd"] = fwd_prof, bwd_prof
+    shim().csa_torch_set_rel_profiler(None if fwd_prof is None else ctypes.addressof(fwd_prof),
+                                      None if bwd_prof is None else ctypes.addressof(bwd_prof))
 
 
 def _stream(device):

@@ -1786,6 +1786,17 @@ void rel_logits(const csa_rel_attn_args* a, const RelLayout& R, hipStream_t st) 
   }
 }
 
+// ABI v9 stage timing: records the caller's events around one CSE stage (no-op when prof is NULL)
+struct RelStage {
+  const csa_prof* pf; int s; hipStream_t st;
+  RelStage(const csa_prof* pf_, int s_, hipStream_t st_) : pf(pf_), s(s_), st(st_) {
+    if (pf && pf->start[s]) (void)hipEventRecord((hipEvent_t)pf->start[s], st);
+  }
+  ~RelStage() {
+    if (pf && pf->stop[s]) (void)hipEventRecord((hipEvent_t)pf->stop[s], st);
+  }
+};
+
 void rel_param_grads(const csa_rel_attn_args* a, const csa_rel_attn_bwd_args* b, const RelLayout& R, float* gc2p,
                      float* gp2ct, hipStream_t st) {
   void* ws = b->workspace;
@@ -1793,6 +1804,7 @@ void rel_param_grads(const csa_rel_attn_args* a, const csa_rel_attn_bwd_args* b,
   const int64_t Lp = R.Lp;
   // dlk_h = sum_b G_c2p^T Q ; dlq_h = sum_b G_p2cT^T K    (C(m=r, n=dd) = sum_b sum_x G(x,r) X(x,dd))
   if (R.fused) {
+    const RelStage sg(b->prof, CSA_REL_STAGE_LGRAD, st);
     float* part = (float*)((char*)ws + R.part);
     const int64_t n = (int64_t)H * L * D;
     LgradArgs g;
@@ -1850,6 +1862,8 @@ csa_status csa_rel_attn_fwd(const csa_rel_attn_args* a, void* stream) {
   RelArgs p = make_rel(a, R);
   const dim3 grid(xcd_grid(p.NQB, (int)(a->B * a->H)));
   if (R.fused) {
+    {
+    const RelStage sg(a->prof, CSA_REL_STAGE_LOGITS, st);
     hipLaunchKernelGGL(k_rel_logits<64>, dim3(xcd_grid(2 * (int)((p.NQB + 1) / 2), (int)(a->B * a->H))), dim3(64),
                        32 * 64 * 4, st, p, (float*)p.c2p, (float*)p.p2ct);
     const int NT = (int)(R.NP / 32);
@@ -1861,6 +1875,8 @@ csa_status csa_rel_attn_fwd(const csa_rel_attn_args* a, void* stream) {
       hipLaunchKernelGGL(k_rel_prep_t, dim3((unsigned)(NT * NT), (unsigned)(a->B * p.P_)), dim3(256), 0, st, p,
                          (uint16_t*)p.RM, (uint16_t*)p.RT);
     }
+    }
+    const RelStage sg(a->prof, CSA_REL_STAGE_FWD, st);
     if (p.bf16) hipLaunchKernelGGL((k_rel_fwd_f<64, true>), grid, dim3(64), 2 * 32 * 64 * 4, st, p);
     else hipLaunchKernelGGL((k_rel_fwd_f<64, false>), grid, dim3(64), 2 * 32 * 64 * 4, st, p);
     return rcheck("csa_rel_attn_fwd");
@@ -1947,10 +1963,17 @@ csa_status csa_rel_attn_bwd(const csa_rel_attn_bwd_args* b, void* stream) {
       p.qstat_pre = 1;
       p.gt = (float*)((char*)ws + R.gt);
       const int64_t threads = 4LL * B * H * N;
-      hipLaunchKernelGGL(k_rel_qstat<4>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, p);
-      launch_k(st);
+      {
+        const RelStage sg(b->prof, CSA_REL_STAGE_QSTAT, st);
+        hipLaunchKernelGGL(k_rel_qstat<4>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, p);
+      }
+      {
+        const RelStage sg(b->prof, CSA_REL_STAGE_BWD_K, st);
+        launch_k(st);
+      }
       const size_t lg_bytes = rel16_bins_off(false) + bins16_lds_bytes(p);
       set_dyn_lds((const void*)k_rel_bwd_qg, (int)lg_bytes);
+      const RelStage sg(b->prof, CSA_REL_STAGE_BWD_Q, st);
       hipLaunchKernelGGL(k_rel_bwd_qg, gq, blk, lg_bytes, st, p);
     } else if (side) {  // fork: row statistics + key side on the side stream, query side here, join before the lgrad
       if (!side->fork(st)) return rfail_hip("csa_rel_attn_bwd: side-stream fork");

@@ -29,6 +29,8 @@ using c10::optional;
 // per-stage profiling records (bench.py): caller-owned csa_prof structs, installed from Python
 const csa_prof* g_prof_fwd = nullptr;
 const csa_prof* g_prof_bwd = nullptr;
+const csa_prof* g_prof_rel_fwd = nullptr;  // ABI v9: CSE relation attention (CSA_REL_STAGE_*)
+const csa_prof* g_prof_rel_bwd = nullptr;
 
 void check(csa_status s, const char* what) {
   TORCH_CHECK(s == CSA_OK, what, " failed: ", csa_status_str(s), ": ", csa_last_error_str());
@@ -292,6 +294,7 @@ csa_rel_attn_args rel_args(const Tensor& q, const Tensor& k, const Tensor& v, co
   a.mask = mask.data_ptr<uint8_t>(); a.mask_sb = mask.stride(0); a.mask_sh = mask.stride(1);
   a.rel_head_group = group;
   a.dtype = bf16 ? CSA_DTYPE_BF16 : CSA_DTYPE_F32;
+  a.prof = g_prof_rel_fwd;
   return a;
 }
 
@@ -348,6 +351,8 @@ std::vector<Tensor> rel_attn_bwd(const Tensor& q_, const Tensor& k_, const Tenso
     b.dv_sb = dv.stride(0); b.dv_sh = dv.stride(1); b.dv_sn = dv.stride(2);
   }
   b.dlq = fpw(dlq); b.dlk = fpw(dlk); b.workspace = ws.data_ptr();
+  b.prof = g_prof_rel_bwd;
+  a.prof = nullptr;  // the forward's stages are not re-run by the backward
   {
     const std::unique_lock<std::mutex> lane_lock = set_side_lane(b, q, schedule);
     check(csa_rel_attn_bwd(&b, cur_stream(q)), "csa_rel_attn_bwd");
@@ -363,6 +368,11 @@ extern "C" {
 void csa_torch_set_stage_profiler(const csa_prof* fwd, const csa_prof* bwd) {
   g_prof_fwd = fwd;
   g_prof_bwd = bwd;
+}
+// the same for the CSE relation attention (ABI v9 CSA_REL_STAGE_* slots)
+void csa_torch_set_rel_profiler(const csa_prof* fwd, const csa_prof* bwd) {
+  g_prof_rel_fwd = fwd;
+  g_prof_rel_bwd = bwd;
 }
 }
 

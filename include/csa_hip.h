@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define CSA_ABI_VERSION 8
+#define CSA_ABI_VERSION 9
 
 typedef enum csa_status {
   CSA_OK = 0,
@@ -107,6 +107,16 @@ typedef struct csa_prof {
   void* start[CSA_STAGE_COUNT];
   void* stop[CSA_STAGE_COUNT];
 } csa_prof;
+/* ABI v9: the same profiling struct (slots 0..5) around the CSE relation attention's stages (d_k = 64 fused path):
+ * csa_rel_attn_args.prof / csa_rel_attn_bwd_args.prof */
+enum {
+  CSA_REL_STAGE_LOGITS = 0, /* k_rel_logits + k_rel_prep (relation logits, code planes) */
+  CSA_REL_STAGE_FWD = 1,    /* k_rel_fwd_f */
+  CSA_REL_STAGE_QSTAT = 2,  /* k_rel_qstat (row statistics for the key side) */
+  CSA_REL_STAGE_BWD_K = 3,  /* k_rel_bwd_kh (fp32) / k_rel_bwd_kf (bf16) */
+  CSA_REL_STAGE_BWD_Q = 4,  /* k_rel_bwd_qg (fp32) / k_rel_bwd_qf (bf16) */
+  CSA_REL_STAGE_LGRAD = 5   /* k_rel_lgrad + k_sum_splits2 (dlq, dlk) */
+};
 
 typedef struct csa_sbm_fwd_args {
   int64_t B, H, N, M, d, k; /* batch, heads, queries, keys, head_dim, clusters (k ignored if DENSE) */
@@ -197,6 +207,7 @@ typedef struct csa_rel_attn_args {
   /* ABI v3: element strides (b, h, row) of out; zero triple = (B,H,N,d) contiguous. Non-contiguous
    * layouts need d = 64 (the fused path); 16-byte aligned, strides multiple of 4 elements. */
   int64_t o_sb, o_sh, o_sn;
+  const csa_prof* prof; /* ABI v9: optional stage timing (CSA_REL_STAGE_*; NULL = off) */
 } csa_rel_attn_args;
 
 typedef struct csa_rel_attn_bwd_args {
@@ -212,6 +223,7 @@ typedef struct csa_rel_attn_bwd_args {
    * (k_rel_bwd_kh -> k_rel_bwd_qg) and runs in order whatever the schedule */
   uint32_t schedule;
   void* side_stream; void* side_fork; void* side_join;
+  const csa_prof* prof; /* ABI v9: optional stage timing (CSA_REL_STAGE_*; NULL = off) */
 } csa_rel_attn_bwd_args;
 
 size_t csa_rel_attn_state_bytes(int64_t B, int64_t H, int64_t N, int64_t L, int64_t d);

@@ -32,6 +32,8 @@ def main():
     ap.add_argument("stats")
     ap.add_argument("--cmd", default="python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-train --no-bf16-leg")
     ap.add_argument("--source-hash", default="")
+    ap.add_argument("--leg", action="append", default=[],
+                    help="NAME=kernel_stats.csv of a side-leg run (bench.py's cse / dense / long_k* roofline legs)")
     a = ap.parse_args()
     fetch, write = load(a.fetch), load(a.write)
     dur = {}
@@ -48,8 +50,16 @@ def main():
         w = write.get(n, {}).get("WRITE_SIZE", 0.0)
         kernels[b] = {"bytes": int(round((2.0 * f + w) * 1024)), "fetch_bytes_corrected": int(round(2.0 * f * 1024)),
                       "write_bytes": int(round(w * 1024)), "rocprof_avg_ns": dur.get(b)}
+    legs = {}
+    for spec in a.leg:
+        name, path = spec.split("=", 1)
+        legs[name] = {}
+        for r in csv.DictReader(open(path)):
+            n = base(r["Name"])
+            if n.startswith("k_"):
+                legs[name].setdefault(n, {"rocprof_avg_ns": float(r["AverageNs"]), "calls": int(r["Calls"])})
     out = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) + --kernel-trace --stats",
-           "command": a.cmd, "csa_source_hash": a.source_hash, "kernels": kernels}
+           "command": a.cmd, "csa_source_hash": a.source_hash, "kernels": kernels, "legs": legs}
     json.dump(out, sys.stdout, indent=1, sort_keys=True)
     print()
 
