@@ -28,6 +28,7 @@
 #include "../../include/csa_hip.h"
 
 #include <algorithm>
+#include <type_traits>
 #include <mutex>
 #include <stdint.h>
 #include <math.h>
@@ -87,7 +88,7 @@ typedef float f2 __attribute__((ext_vector_type(2)));  // register pairs for pac
 // ------------------------------------------------------------------------------------
 struct Layout {
   int64_t B, H, N, M, D, k, kp, KT, NQB, NKB, Mpad;
-  size_t S, Qh, Kh, T, stats, Abits, Rbits, cnt, Wf[3], WfT[3], Cf, CfT, Sf, SfT, Act, total;
+  size_t S, Qh, Kh, T, stats, Abits, Rbits, cnt, tdead, Wf[3], WfT[3], Cf, CfT, Sf, SfT, Act, total;
   // bwd workspace
   size_t w_dQh, w_dT, w_slab, w_dS, w_dC, w_gx, w_dsg, w_brow, w_total;
   int64_t G, slab_floats, w_dsg_plane;
@@ -131,6 +132,7 @@ Layout make_layout(int64_t B, int64_t H, int64_t N, int64_t M, int64_t D, int64_
   L.Abits = take(sizeof(uint32_t) * B * H * L.NQB * L.Mpad);
   L.Rbits = take(sizeof(uint32_t) * B * H * L.NQB * L.Mpad);
   L.cnt = take(sizeof(unsigned long long) * H);
+  L.tdead = take(sizeof(unsigned long long) * B);  // per AST: key tiles whose every key is masked (bit kt)
   for (int l = 0; l < 3; ++l) L.Wf[l] = take(sizeof(float) * (dense ? 0 : D * D));
   for (int l = 0; l < 3; ++l) L.WfT[l] = take(sizeof(float) * (dense ? 0 : D * D));
   L.Cf = take(sizeof(float) * H * KP32 * D);
@@ -385,6 +387,7 @@ struct KArgs {
   float *Qh, *Kh, *T, *stats, *Act;  // Act NULL for CSA_FLAG_FWD_ONLY (no activation blocks saved)
   uint32_t *Abits, *Rbits;
   unsigned long long* cnt;
+  unsigned long long* tdead;  // per AST: fully masked key tiles (k_attn_fwd; bit 0 never set), NKB <= 64
   const float* U;
   uint32_t seed_lo, seed_hi, off;
   float attn_p, proj_p, scale;
@@ -969,14 +972,6 @@ __device__ __forceinline__ uint32_t writelane_batch(uint32_t dst, const unsigned
 #undef CSA_WL_OPS
   return dst;
 }
-__device__ __forceinline__ uint32_t pack_bits(const bool (&v)[16]) {
-  unsigned long long b[16];
-#pragma unroll
-  for (int r = 0; r < 16; ++r) b[r] = __ballot(v[r]);
-  uint32_t w = 0;
-  w = writelane_batch<0>(w, b);
-  return writelane_batch<8>(w, b);
-}
 
 template <int D, int KPH>
 struct AttnFwdLds {
@@ -1089,54 +1084,45 @@ __device__ __forceinline__ void attn_fwd_item(const KArgs& p, float* __restrict_
 #pragma unroll
   for (int t = 0; t < DT; ++t) vb[t] = LY::VOFF + (SWZ ? col_base64(t, c, h) : 4 * (32 * t + c) + 16 * DP * h);
   const uint32_t qmask = (uint32_t)__ballot(iv);  // valid query bits of a packed word
+  // Loop-invariant scalars the tile loop uses, pinned in VGPRs (the opaque asm): the SGPR file is full in the
+  // dropout variant, and left to the compiler they spill to VGPR lanes and are re-read (v_readlane) every tile.
+  typedef __attribute__((address_space(1))) uint32_t gu32;  // global (not flat) stores
+  gu32* abp = (gu32*)(p.Abits + ((int64_t)bh * p.NQB + qb) * p.Mpad + c);  // this lane's packed-word columns
+  gu32* rbp = (gu32*)(p.Rbits + ((int64_t)bh * p.NQB + qb) * p.Mpad + c);
+  uint32_t ctr_bh = (uint32_t)bh, ctr_ste = (RNG_STE << 28) ^ p.off, ctr_drop = (RNG_ATTN_DROP << 28) ^ p.off;
+  uint32_t drop_thr = p.drop_thr;
+  float scale = p.scale, e_lo = 0.01f * ESC, e_hi = 0.99f * ESC;
+  asm volatile("" : "+v"(abp), "+v"(rbp), "+v"(ctr_bh), "+v"(ctr_ste), "+v"(ctr_drop), "+v"(drop_thr));
+  asm volatile("" : "+v"(scale), "+v"(e_lo), "+v"(e_hi));
   float m_run = NEG_INF, zp = 0.f, zgp = 0.f;
   f32x16 o[DT];
 #pragma unroll
   for (int t = 0; t < DT; ++t) o[t] = zero16();
   uint32_t cntl = 0;
-  for (int kt = 0; kt < p.NKB; ++kt) {
-    const int j0 = kt * 32;
-    wait_vm_all();  // tile kt's K/V/T images (at kt = 0 also the query operands) have landed
-    if constexpr (!DENSE && !HAS_U)
-      if (kt == 0)
+  // Key tiles whose every key is masked (padded ASTs, sbm_attn.py:61) contribute exactly nothing to the softmax sums
+  // and to X (their P is 0), so after the live tiles (ascending, the softmax order of a full pass) they run a light
+  // body: expA, sampling and the bit words only (the graph counts padded positions, sbm_attn.py:64, and the backward's
+  // STE term reads them), no K / V images, no S or PV products. Tile 0, whose images the prologue loads, is always
+  // processed as live. More than 64 key tiles: every tile live.
+  uint64_t rem_live = 0, rem_dead = 0, dead = 0;
+  const bool tmask = p.NKB <= 64;
+  int kt = 0;
+  // Philox words of tile kt (they depend only on (query, tile, head))
+  auto philox_tile = [&](int kt_, u32x4 (&r_ste)[2], u32x4 (&r_drop)[2]) {
+    uint32_t sk0 = p.seed_lo, sk1 = p.seed_hi;  // opaque per tile: round keys are not held across the loop
+    asm volatile("" : "+s"(sk0), "+s"(sk1));
 #pragma unroll
-        for (int e = 0; e < KPH; ++e) qh[e] *= ESC;
-    // the tile's Philox words depend only on (query, tile, head): computed first, so their VALU work can
-    // interleave with the S / expA MFMA chains below instead of waiting behind them
-    u32x4 r_ste[2], r_drop[2];
-    {
-      uint32_t sk0 = p.seed_lo, sk1 = p.seed_hi;  // opaque per tile: round keys are not held across the loop
-      asm volatile("" : "+s"(sk0), "+s"(sk1));
-#pragma unroll
-      for (int gp = 0; gp < 2; ++gp) {
-        if constexpr (!DENSE && !HAS_U)
-          r_ste[gp] = philox4x32(u32x4{(uint32_t)i, (uint32_t)(8 * kt + 4 * gp + h), (uint32_t)bh,
-                                       (RNG_STE << 28) ^ p.off}, sk0, sk1);
-        if constexpr (DROP)
-          r_drop[gp] = philox4x32(u32x4{(uint32_t)i, (uint32_t)(8 * kt + 4 * gp + h), (uint32_t)bh,
-                                        (RNG_ATTN_DROP << 28) ^ p.off}, sk0, sk1);
-      }
+    for (int gp = 0; gp < 2; ++gp) {
+      if constexpr (!DENSE && !HAS_U)
+        r_ste[gp] = philox4x32(u32x4{(uint32_t)i, (uint32_t)(8 * kt_ + 4 * gp + h), ctr_bh, ctr_ste}, sk0, sk1);
+      if constexpr (DROP)
+        r_drop[gp] = philox4x32(u32x4{(uint32_t)i, (uint32_t)(8 * kt_ + 4 * gp + h), ctr_bh, ctr_drop}, sk0, sk1);
     }
-    // S^T = K Q^T : A operand = K rows from the image (row c, lin-perm chunks of half h)
-    f32x16 sacc = zero16();
-    if constexpr (BF) {
-#pragma unroll
-      for (int j2 = 0; j2 < NS / 8; ++j2) {
-        const f32x4 k0 = lds_f4(lds, SWZ ? (kbase ^ (32 * j2)) : kbase + 32 * j2);
-        const f32x4 k1 = lds_f4(lds, SWZ ? (kbase ^ (32 * j2 + 16)) : kbase + 32 * j2 + 16);
-        sacc = mfma_bf(pack8(k0, k1), pack8(&q[8 * j2]), sacc);
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < NS / 4; ++j) {
-        const f32x4 kv = lds_f4(lds, SWZ ? (kbase ^ (16 * j)) : kbase + 16 * j);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) sacc = mfma(kv[e], q[4 * j + e], sacc);
-      }
-    }
-    f32x16 eacc;
-    if constexpr (!DENSE) {  // expA^T = T Qh^T (sbm_attn.py:55)
-      eacc = zero16();
+  };
+  // expA^T = T Qh^T (sbm_attn.py:55) of the tile in the T image
+  auto echain = [&]() {
+    f32x16 eacc = zero16();
+    if constexpr (!DENSE) {
 #pragma unroll
       for (int j = 0; j < KPH / 4; ++j) {
         const f32x4 tv = lds_f4(lds, tbase ^ (16 * j));
@@ -1144,104 +1130,199 @@ __device__ __forceinline__ void attn_fwd_item(const KArgs& p, float* __restrict_
         for (int e = 0; e < 4; ++e) eacc = mfma(tv[e], qh[4 * j + e], eacc);
       }
     }
-    // V^T operand values for this tile's PV: lane (d = 32t + c) reads V[key crow(r,h)][d]
-    float vt[DT][16];
+    return eacc;
+  };
+  // The sampled graph and the dropout keep mask of one group of eight registers: each compare's lane mask is consumed
+  // right away, by the bit packing (ballot -> v_writelane into the key's lane) and by the 0 / 1 multipliers the
+  // softmax applies later (ma: sampled, mak: sampled and kept), so at most 8 masks (16 SGPRs) are live. Independent
+  // of S: a live tile runs it between the S chain's MFMAs.
+  uint32_t myA = 0u, myR = 0u;
+  auto sample_group = [&](int gp, int j0_, const f32x16& eacc, const u32x4 (&r_ste)[2], const u32x4 (&r_drop)[2],
+                          float (&ma)[16], float (&mak)[16]) {
+    unsigned long long bA[16], bR[16];
 #pragma unroll
-    for (int t = 0; t < DT; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) vt[t][r] = lds_f1(lds, vb[t] + (SWZ ? 256 * crow(r, 0) : 4 * DP * crow(r, 0)));
-    f32x4 bz[4];  // key bias of registers 4g..4g+3 (keys j0 + 8g + 4h + e)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) bz[g] = lds_f4(lds, LY::BOFF + 4 * (j0 + 8 * g + 4 * h));
-    // all of tile kt is in registers: start tile kt+1's DMA (overlaps the softmax and PV below)
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (kt + 1 < p.NKB) CSA_ISSUE_FWD(j0 + 32);
-    float s[16];
-    float tmax = NEG_INF;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      s[r] = fmaf(sacc[r], p.scale, bz[r >> 2][r & 3]);
-      tmax = fmaxf(tmax, s[r]);
-    }
-    bool av[16], keep[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) { av[r] = true; keep[r] = true; }
-    if constexpr (!DENSE) {
-      if constexpr (HAS_U) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int j = j0 + crow(r, h);
+    for (int e = 0; e < 8; ++e) {
+      const int r = 8 * gp + e;
+      bool av = true, keep = true;
+      if constexpr (!DENSE) {
+        if constexpr (HAS_U) {
+          const int j = j0_ + crow(r, h);
           const float v = p.U[((int64_t)bh * p.N + ic) * p.M + imin(j, p.M - 1)];
           const float uu = (iv && j < p.M) ? v : 2.f;
-          av[r] = uu < fminf(fmaxf(eacc[r], 0.01f), 0.99f);  // STE.py:11-13
+          av = uu < fminf(fmaxf(eacc[r], 0.01f), 0.99f);  // STE.py:11-13
+        } else {
+          av = (float)u16_of(r_ste[gp], e) < __builtin_amdgcn_fmed3f(eacc[r], e_lo, e_hi);
         }
-      } else {
+      }
+      if constexpr (DROP) keep = u16_of(r_drop[gp], e) >= drop_thr;
+      ma[r] = av ? 1.f : 0.f;
+      mak[r] = (av && keep) ? 1.f : 0.f;
+      bA[r] = __ballot(av);
+      bR[r] = __ballot(keep);
+    }
+    // bit-pack: word [qb][key] holds 32 query bits (lanes 0..31); this group's 8 ballots into their key lanes
+    if constexpr (!DENSE) myA = gp == 0 ? writelane_batch<0>(myA, bA) : writelane_batch<8>(myA, bA);
+    if constexpr (DROP) myR = gp == 0 ? writelane_batch<0>(myR, bR) : writelane_batch<8>(myR, bR);
+  };
+  // the tile's bit words out, its sampled edges counted
+  auto store_bits = [&](int j0_) {
+    if constexpr (!DENSE) {
+      if (h == 0) abp[j0_] = myA;
+      if (j0_ + c < p.M) cntl += __popc(myA & qmask);  // sampled edges inside [0,N) x [0,M)
+    }
+    if constexpr (DROP) if (h == 0) rbp[j0_] = myR;
+  };
+  // the tile after the current one in processing order (-1: none), taken off the remaining sets
+  auto pop_next = [&](int kt_) {
+    if (!tmask) return kt_ + 1 < p.NKB ? kt_ + 1 : -1;
+    if (rem_live) {
+      const int nx = __builtin_ctzll(rem_live);
+      rem_live &= rem_live - 1;
+      return nx;
+    }
+    if (rem_dead) {
+      const int nx = __builtin_ctzll(rem_dead);
+      rem_dead &= rem_dead - 1;
+      return nx;
+    }
+    return -1;
+  };
+  auto is_live = [&](int kt_) { return !tmask || !((dead >> kt_) & 1ull); };
+  for (int idx = 0; idx < p.NKB; ++idx) {
+    wait_vm_all();  // tile kt's K/V/T images (at idx = 0 also the query operands) have landed
+    if (idx == 0) {
+      if constexpr (!DENSE && !HAS_U)
 #pragma unroll
-        for (int gp = 0; gp < 2; ++gp) {
-          const u32x4 rr = r_ste[gp];
+        for (int e = 0; e < KPH; ++e) qh[e] *= ESC;
+      if (tmask) {  // dead tiles from the key bias row (written before the loop)
+        for (int u = 0; 2 * u < p.NKB; ++u) {
+          const int jj = imin(64 * u + lane, p.NKB * 32 - 1);  // (a missing odd tile reads the last key)
+          const uint64_t bl = __builtin_amdgcn_ballot_w64(lds_f1(lds, LY::BOFF + 4 * jj) == NEG_INF);
+          if ((uint32_t)bl == 0xffffffffu) dead |= 1ull << (2 * u);
+          if ((uint32_t)(bl >> 32) == 0xffffffffu && 2 * u + 1 < p.NKB) dead |= 1ull << (2 * u + 1);
+        }
+        const uint64_t all = p.NKB == 64 ? ~0ull : (1ull << p.NKB) - 1;
+        dead &= ~1ull;  // tile 0 runs as live (its images are loaded)
+        rem_live = all & ~dead & ~1ull;
+        rem_dead = dead;
+        if (hd == 0 && qb == 0 && lane == 0) p.tdead[b] = dead;  // for the backward's query side
+      }
+    }
+    const int j0 = kt * 32;
+    u32x4 r_ste[2], r_drop[2];
+    float w[16];
+    myA = myR = 0u;
+    if (is_live(kt)) {
+      // Region 1: the tile's Philox words, expA and the first third of S; region 2: more of S beside the sampling of
+      // registers 0-7; region 3: the rest of S beside registers 8-15 (scheduling barriers between them: each region's
+      // VALU issues in the shadow of its own MFMAs, and at most one group's masks are live)
+      philox_tile(kt, r_ste, r_drop);
+      const f32x16 eacc = echain();
+      f32x16 sacc = zero16();
+      auto s_chain = [&](int j_lo, int j_hi) {  // S^T = K Q^T K-groups [j_lo, j_hi): A = K rows from the image
+        if constexpr (BF) {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const int r = 8 * gp + e;
-            av[r] = (float)u16_of(rr, e) < __builtin_amdgcn_fmed3f(eacc[r], 0.01f * ESC, 0.99f * ESC);
+          for (int j2 = 0; j2 < NS / 8; ++j2) {
+            if (2 * j2 < j_lo || 2 * j2 >= j_hi) continue;  // (one bf16 step = K-groups 2 j2, 2 j2 + 1)
+            const f32x4 k0 = lds_f4(lds, SWZ ? (kbase ^ (32 * j2)) : kbase + 32 * j2);
+            const f32x4 k1 = lds_f4(lds, SWZ ? (kbase ^ (32 * j2 + 16)) : kbase + 32 * j2 + 16);
+            sacc = mfma_bf(pack8(k0, k1), pack8(&q[8 * j2]), sacc);
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < NS / 4; ++j) {
+            if (j < j_lo || j >= j_hi) continue;
+            const f32x4 kv = lds_f4(lds, SWZ ? (kbase ^ (16 * j)) : kbase + 16 * j);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) sacc = mfma(kv[e], q[4 * j + e], sacc);
           }
         }
-      }
-    }
-    if constexpr (DROP) {
-#pragma unroll
-      for (int gp = 0; gp < 2; ++gp) {
-        const u32x4 rr = r_drop[gp];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) keep[8 * gp + e] = u16_of(rr, e) >= p.drop_thr;
-      }
-    }
-    // bit-pack the sampled graph / dropout keep mask: word [qb][key] holds 32 query bits (lanes 0..31)
-    if constexpr (!DENSE || DROP) {
-      const uint32_t myA = DENSE ? 0u : pack_bits(av);
-      const uint32_t myR = DROP ? pack_bits(keep) : 0u;
-      const int64_t widx = ((int64_t)bh * p.NQB + qb) * p.Mpad + j0 + c;
-      if constexpr (!DENSE) {
-        if (h == 0) p.Abits[widx] = myA;
-        if (j0 + c < p.M) cntl += __popc(myA & qmask);  // sampled edges inside [0,N) x [0,M)
-      }
-      if constexpr (DROP) if (h == 0) p.Rbits[widx] = myR;
-    }
-    // online softmax update (exp(-inf - m) = 0 covers masked keys; m_use keeps an all-masked prefix finite)
-    float w[16];
-    {
-    tmax = xhalf_max(tmax);
-    const float m_new = fmaxf(m_run, tmax);
-    const float m_use = (m_new == NEG_INF) ? 0.f : m_new;
-    const float alpha = __expf(m_run - m_use);
-    zp *= alpha;
-    zgp *= alpha;
-#pragma unroll
-    for (int t = 0; t < DT; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float e = __expf(s[r] - m_use);
-      zp += e;
-      const float wa = av[r] ? e : 0.f;
-      zgp += wa;
-      w[r] = keep[r] ? wa : 0.f;
-    }
-    m_run = m_new;
-    }
-    // O^T += V^T W^T (keys beyond M carry w = 0)
-    if constexpr (BF) {
-      const bf16x8 w0 = pack8(&w[0]), w1 = pack8(&w[8]);
-#pragma unroll
-      for (int t = 0; t < DT; ++t) {
-        o[t] = mfma_bf(pack8(&vt[t][0]), w0, o[t]);
-        o[t] = mfma_bf(pack8(&vt[t][8]), w1, o[t]);
-      }
-    } else {
+      };
+      constexpr int J1 = (NS / 4) * 3 / 8, J2 = (NS / 4) * 11 / 16;  // d = 64: K-groups 0-2 | 3-4 | 5-7
+      float ma[16], mak[16];
+      s_chain(0, J1);
+      __builtin_amdgcn_sched_barrier(0);
+      s_chain(J1, J2);
+      sample_group(0, j0, eacc, r_ste, r_drop, ma, mak);
+      __builtin_amdgcn_sched_barrier(0);
+      s_chain(J2, NS / 4);
+      sample_group(1, j0, eacc, r_ste, r_drop, ma, mak);
+      __builtin_amdgcn_sched_barrier(0);
+      store_bits(j0);
+      // V^T operand values for this tile's PV: lane (d = 32t + c) reads V[key crow(r,h)][d]
+      float vt[DT][16];
 #pragma unroll
       for (int t = 0; t < DT; ++t)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) o[t] = mfma(vt[t][r], w[r], o[t]);
+        for (int r = 0; r < 16; ++r) vt[t][r] = lds_f1(lds, vb[t] + (SWZ ? 256 * crow(r, 0) : 4 * DP * crow(r, 0)));
+      f32x4 bz[4];  // key bias of registers 4g..4g+3 (keys j0 + 8g + 4h + e)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) bz[g] = lds_f4(lds, LY::BOFF + 4 * (j0 + 8 * g + 4 * h));
+      // all of tile kt is in registers: start the next tile's DMA (overlaps the softmax and PV below)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      const int nx = pop_next(kt);
+      if (nx >= 0) {
+        if (is_live(nx)) CSA_ISSUE_FWD(nx * 32);
+        else if constexpr (!DENSE) dma_narrow(Tl, tr, nx * 32, KPN);
+      }
+      float s[16];
+      float tmax = NEG_INF;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        s[r] = fmaf(sacc[r], scale, bz[r >> 2][r & 3]);
+        tmax = fmaxf(tmax, s[r]);
+      }
+      // online softmax update (exp(-inf - m) = 0 covers masked keys; m_use keeps an all-masked prefix finite). Z and
+      // Zg are summed in register order; ex * {0, 1} is the select ex or 0 bit for bit.
+      tmax = xhalf_max(tmax);
+      const float m_new = fmaxf(m_run, tmax);
+      const float m_use = (m_new == NEG_INF) ? 0.f : m_new;
+      const float alpha = __expf(m_run - m_use);
+      zp *= alpha;
+      zgp *= alpha;
+#pragma unroll
+      for (int t = 0; t < DT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
+      float ex[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        ex[r] = __expf(s[r] - m_use);
+        zp += ex[r];
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        zgp += ex[r] * ma[r];
+        w[r] = ex[r] * mak[r];
+      }
+      m_run = m_new;
+      // O^T += V^T W^T (keys beyond M carry w = 0)
+      if constexpr (BF) {
+        const bf16x8 w0 = pack8(&w[0]), w1 = pack8(&w[8]);
+#pragma unroll
+        for (int t = 0; t < DT; ++t) {
+          o[t] = mfma_bf(pack8(&vt[t][0]), w0, o[t]);
+          o[t] = mfma_bf(pack8(&vt[t][8]), w1, o[t]);
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < DT; ++t)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) o[t] = mfma(vt[t][r], w[r], o[t]);
+      }
+      kt = nx;
+    } else {  // every key of the tile masked: P = 0, so no softmax / PV work; sampling and bit words only
+      philox_tile(kt, r_ste, r_drop);
+      const f32x16 eacc = echain();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      const int nx = pop_next(kt);  // (a dead tile: the ones after it are dead too)
+      if constexpr (!DENSE)
+        if (nx >= 0) dma_narrow(Tl, tr, nx * 32, KPN);
+      float ma[16], mak[16];
+      sample_group(0, j0, eacc, r_ste, r_drop, ma, mak);
+      sample_group(1, j0, eacc, r_ste, r_drop, ma, mak);
+      store_bits(j0);
+      kt = nx;
     }
   }
   const float Z = xhalf_sum(zp), Zg = xhalf_sum(zgp);
@@ -1740,6 +1821,9 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 8) ? 4 : 2) void k_attn_bwd_
   // W1: this lane's rho (k_attn_rowprep) and the STE term; ds is summed unscaled and dQ scaled at the end
   const float rho = W1 ? p.brow[(((int64_t)bh * p.NQB + qb) * 32 + c) * 4 + 3] : 0.f;
   const float csp = (W1 && p.dsp) ? p.dsp[hd] / ((float)p.B * (float)p.N * (float)p.M) : 0.f;
+  // key tiles whose every key is masked (the forward's record): their ds is 0 (P = 0), so no dQ products and no K
+  // image; the T image and the tile (its A bits carry the STE term into dQh) still stream in
+  const uint64_t tdead = (p.mask && p.NKB <= 64) ? p.tdead[b] : 0ull;
   CSA_ISSUE_BQ(0);
   load_tile(0);
   f32x16 dq[DT], dqh[KTA];
@@ -1747,64 +1831,138 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 8) ? 4 : 2) void k_attn_bwd_
   for (int t = 0; t < DT; ++t) dq[t] = zero16();
 #pragma unroll
   for (int t = 0; t < KTA; ++t) dqh[t] = zero16();
-  for (int kt = 0; kt < p.NKB; ++kt) {
-    int ln = threadIdx.x;  // opaque per iteration: keeps the per-row LDS addresses out of the prologue
-    asm volatile("" : "+v"(ln));
-    const int c = ln & 31, h = (ln >> 5) & 1;
-    const bool more = kt + 1 < p.NKB;
-    wait_vm_all();  // tile kt's K / T images and ds / G values have landed
-    if constexpr (W1) {  // k_attn_bwd_kv's expressions (W_NO_EDGE)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const bool a = __float_as_uint(dsv[r]) != W_NO_EDGE;
-        const float w = a ? dsv[r] : 0.f;
-        gv[r] = a ? __builtin_amdgcn_fmed3f(w + csp, -1.f, 1.f) : 0.f;
-        dsv[r] = w;
-      }
-      if (rho != 0.f) {  // rare: a degenerate row (n < eps) also takes -rho P from the second plane
-#pragma unroll
-        for (int r = 0; r < 16; ++r) dsv[r] = fmaf(-rho, tb[p.gplane + kt * 1024 + 32 * crow(r, h)], dsv[r]);
-      }
-    }
-    // dQ^T += K^T ds^T (lane d holds K[key crow(r,h)][d], read from the SW_COL / padded image per K-step)
-#pragma unroll
-    for (int t = 0; t < DT; ++t) {
-      const int cb = SH::GK + (SWZ ? col_base64(t, c, h) : 4 * (32 * t + c) + 16 * DP * h);
-      float kT[16];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) kT[r] = lds_f1(lds, cb + (SWZ ? 256 * crow(r, 0) : 4 * DP * crow(r, 0)));
-      if constexpr (BF) {
-        dq[t] = mfma_bf(pack8(&kT[0]), pack8(&dsv[0]), dq[t]);
-        dq[t] = mfma_bf(pack8(&kT[8]), pack8(&dsv[8]), dq[t]);
-      } else {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) dq[t] = mfma(kT[r], dsv[r], dq[t]);
-      }
-    }
-    // dQh^T += T^T G^T
-    if constexpr (MB4) {  // lane (c, h): T[key crow(r,h)][cluster c & 15]
-      float tT[16];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) tT[r] = lds_f1(lds, SH::GT + narrow_elem(crow(r, h), c & 15, KPN));
-#pragma unroll
-      for (int r = 0; r < 16; ++r) dqh[0] = mfma4b(tT[r], gv[r], dqh[0]);
-    } else if constexpr (!DENSE) {
-#pragma unroll
-      for (int at = 0; at < KTA; ++at) {
-        float tT[16];
-#pragma unroll
+  // the tile loop twice: without dead tiles (every unpadded batch: tdead is 0) the compiler folds the skips away and
+  // the body stays one scheduling region
+  if (tdead) {
+    for (int kt = 0; kt < p.NKB; ++kt) {
+      int ln = threadIdx.x;  // opaque per iteration: keeps the per-row LDS addresses out of the prologue
+      asm volatile("" : "+v"(ln));
+      const int c = ln & 31, h = (ln >> 5) & 1;
+      const bool more = kt + 1 < p.NKB;
+      wait_vm_all();  // tile kt's K / T images and ds / G values have landed
+      if constexpr (W1) {  // k_attn_bwd_kv's expressions (W_NO_EDGE)
+  #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float v = lds_f1(lds, SH::GT + narrow_elem(crow(r, h), imin(32 * at + c, KP - 1), KPN));
-          tT[r] = (KP >= 32 || c < KP) ? v : 0.f;
+          const bool a = __float_as_uint(dsv[r]) != W_NO_EDGE;
+          const float w = a ? dsv[r] : 0.f;
+          gv[r] = a ? __builtin_amdgcn_fmed3f(w + csp, -1.f, 1.f) : 0.f;
+          dsv[r] = w;
         }
-#pragma unroll
-        for (int r = 0; r < 16; ++r) dqh[at] = mfma(tT[r], gv[r], dqh[at]);
+        if (rho != 0.f) {  // rare: a degenerate row (n < eps) also takes -rho P from the second plane
+  #pragma unroll
+          for (int r = 0; r < 16; ++r) dsv[r] = fmaf(-rho, tb[p.gplane + kt * 1024 + 32 * crow(r, h)], dsv[r]);
+        }
+      }
+      // dQ^T += K^T ds^T (lane d holds K[key crow(r,h)][d], read from the SW_COL / padded image per K-step)
+  #pragma unroll
+      for (int t = 0; t < (((tdead >> kt) & 1ull) ? 0 : DT); ++t) {
+        const int cb = SH::GK + (SWZ ? col_base64(t, c, h) : 4 * (32 * t + c) + 16 * DP * h);
+        float kT[16];
+  #pragma unroll
+        for (int r = 0; r < 16; ++r) kT[r] = lds_f1(lds, cb + (SWZ ? 256 * crow(r, 0) : 4 * DP * crow(r, 0)));
+        if constexpr (BF) {
+          dq[t] = mfma_bf(pack8(&kT[0]), pack8(&dsv[0]), dq[t]);
+          dq[t] = mfma_bf(pack8(&kT[8]), pack8(&dsv[8]), dq[t]);
+        } else {
+  #pragma unroll
+          for (int r = 0; r < 16; ++r) dq[t] = mfma(kT[r], dsv[r], dq[t]);
+        }
+      }
+      // dQh^T += T^T G^T
+      if constexpr (MB4) {  // lane (c, h): T[key crow(r,h)][cluster c & 15]
+        float tT[16];
+  #pragma unroll
+        for (int r = 0; r < 16; ++r) tT[r] = lds_f1(lds, SH::GT + narrow_elem(crow(r, h), c & 15, KPN));
+  #pragma unroll
+        for (int r = 0; r < 16; ++r) dqh[0] = mfma4b(tT[r], gv[r], dqh[0]);
+      } else if constexpr (!DENSE) {
+  #pragma unroll
+        for (int at = 0; at < KTA; ++at) {
+          float tT[16];
+  #pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float v = lds_f1(lds, SH::GT + narrow_elem(crow(r, h), imin(32 * at + c, KP - 1), KPN));
+            tT[r] = (KP >= 32 || c < KP) ? v : 0.f;
+          }
+  #pragma unroll
+          for (int r = 0; r < 16; ++r) dqh[at] = mfma(tT[r], gv[r], dqh[at]);
+        }
+      }
+      if (more) {  // images read out and ds / G consumed by the MFMAs above: tile kt+1 streams in
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if ((tdead >> (kt + 1)) & 1ull) {
+          if constexpr (!DENSE) dma_narrow(Tl, tr, kt * 32 + 32, KPN);
+        } else {
+          CSA_ISSUE_BQ(kt * 32 + 32);
+        }
+        load_tile(kt + 1);
       }
     }
-    if (more) {  // images read out and ds / G consumed by the MFMAs above: tile kt+1 streams in
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      CSA_ISSUE_BQ(kt * 32 + 32);
-      load_tile(kt + 1);
+  } else {
+    const uint64_t tdead = 0;
+    for (int kt = 0; kt < p.NKB; ++kt) {
+      int ln = threadIdx.x;  // opaque per iteration: keeps the per-row LDS addresses out of the prologue
+      asm volatile("" : "+v"(ln));
+      const int c = ln & 31, h = (ln >> 5) & 1;
+      const bool more = kt + 1 < p.NKB;
+      wait_vm_all();  // tile kt's K / T images and ds / G values have landed
+      if constexpr (W1) {  // k_attn_bwd_kv's expressions (W_NO_EDGE)
+  #pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const bool a = __float_as_uint(dsv[r]) != W_NO_EDGE;
+          const float w = a ? dsv[r] : 0.f;
+          gv[r] = a ? __builtin_amdgcn_fmed3f(w + csp, -1.f, 1.f) : 0.f;
+          dsv[r] = w;
+        }
+        if (rho != 0.f) {  // rare: a degenerate row (n < eps) also takes -rho P from the second plane
+  #pragma unroll
+          for (int r = 0; r < 16; ++r) dsv[r] = fmaf(-rho, tb[p.gplane + kt * 1024 + 32 * crow(r, h)], dsv[r]);
+        }
+      }
+      // dQ^T += K^T ds^T (lane d holds K[key crow(r,h)][d], read from the SW_COL / padded image per K-step)
+  #pragma unroll
+      for (int t = 0; t < (((tdead >> kt) & 1ull) ? 0 : DT); ++t) {
+        const int cb = SH::GK + (SWZ ? col_base64(t, c, h) : 4 * (32 * t + c) + 16 * DP * h);
+        float kT[16];
+  #pragma unroll
+        for (int r = 0; r < 16; ++r) kT[r] = lds_f1(lds, cb + (SWZ ? 256 * crow(r, 0) : 4 * DP * crow(r, 0)));
+        if constexpr (BF) {
+          dq[t] = mfma_bf(pack8(&kT[0]), pack8(&dsv[0]), dq[t]);
+          dq[t] = mfma_bf(pack8(&kT[8]), pack8(&dsv[8]), dq[t]);
+        } else {
+  #pragma unroll
+          for (int r = 0; r < 16; ++r) dq[t] = mfma(kT[r], dsv[r], dq[t]);
+        }
+      }
+      // dQh^T += T^T G^T
+      if constexpr (MB4) {  // lane (c, h): T[key crow(r,h)][cluster c & 15]
+        float tT[16];
+  #pragma unroll
+        for (int r = 0; r < 16; ++r) tT[r] = lds_f1(lds, SH::GT + narrow_elem(crow(r, h), c & 15, KPN));
+  #pragma unroll
+        for (int r = 0; r < 16; ++r) dqh[0] = mfma4b(tT[r], gv[r], dqh[0]);
+      } else if constexpr (!DENSE) {
+  #pragma unroll
+        for (int at = 0; at < KTA; ++at) {
+          float tT[16];
+  #pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float v = lds_f1(lds, SH::GT + narrow_elem(crow(r, h), imin(32 * at + c, KP - 1), KPN));
+            tT[r] = (KP >= 32 || c < KP) ? v : 0.f;
+          }
+  #pragma unroll
+          for (int r = 0; r < 16; ++r) dqh[at] = mfma(tT[r], gv[r], dqh[at]);
+        }
+      }
+      if (more) {  // images read out and ds / G consumed by the MFMAs above: tile kt+1 streams in
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if ((tdead >> (kt + 1)) & 1ull) {
+          if constexpr (!DENSE) dma_narrow(Tl, tr, kt * 32 + 32, KPN);
+        } else {
+          CSA_ISSUE_BQ(kt * 32 + 32);
+        }
+        load_tile(kt + 1);
+      }
     }
   }
 #undef CSA_ISSUE_BQ
@@ -1840,6 +1998,11 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
   constexpr bool HO = bwd_handoff<BF>();    // ds / G tiles out for k_attn_bwd_qg (else k_attn_bwd_qr recomputes)
   constexpr bool W1 = HO && !DENSE && !DG;  // one-plane w tiles (W_NO_EDGE)
   constexpr bool PAIR = SWZ && !BF;  // dK / dV rows as d = 2m + t (b64 operand reads, pair_read)
+  // FG (every variant without map gradients): the row constants are formed here from the forward's row statistics
+  // and gamma = rowsum(dX * X), computed per query block from the dX image and the lane's X row; the key block 0
+  // waves store them for the query-side kernel. With map gradients (DG) gamma also takes k_attn_gx's term and
+  // k_attn_rowprep forms them before this kernel.
+  constexpr bool FG = !DG;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const uint32_t L0 = lds_offset(lds), Ql = L0 + SH::KQ, Xl = L0 + SH::KX, Hl = L0 + SH::KH, Sl = L0 + SH::KS;
   const int lane = lane_id(), c = lane & 31, h = lane >> 5;
@@ -1853,7 +2016,20 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
   const __amdgpu_buffer_rsrc_t qr_ = make_rsrc(p.Q + b * p.q_sb + hd * p.q_sh, SWZ ? (p.N - 1) * qld + D * 4 : 0x7fffffff);
   const __amdgpu_buffer_rsrc_t xr_ = make_rsrc(p.dX + b * p.dx_sb + hd * p.dx_sh, SWZ ? (p.N - 1) * xld + D * 4 : 0x7fffffff);
   const __amdgpu_buffer_rsrc_t hr_ = make_rsrc(DENSE ? p.dX : p.Qh + (int64_t)bh * p.N * p.kp, p.N * p.kp * 4);
-  const __amdgpu_buffer_rsrc_t sr_ = make_rsrc(p.brow + (int64_t)bh * p.NQB * 128, p.NQB * 512);
+  // row-constant image source: the forward's (lse, 1 / max(n, eps), [n >= eps], 0) rows (FG; rows >= N out of range)
+  // or k_attn_rowprep's (c0, u, v, rho) records
+  const __amdgpu_buffer_rsrc_t sr_ = FG ? make_rsrc(p.stats + (int64_t)bh * p.N * 4, p.N * 16)
+                                        : make_rsrc(p.brow + (int64_t)bh * p.NQB * 128, p.NQB * 512);
+  // FG: this lane's half of X row (query i0 + c, clamped): NS floats at columns NS h .., one f32x4 per dP K-group
+  const float* xrow = p.X + b * p.x_sb + hd * p.x_sh + NS * h;
+  f32x4 xv4[NS / 4];
+  auto load_x = [&](int i0) {
+    if constexpr (FG) {
+      const float* xp = xrow + (int64_t)imin(i0 + (lane & 31), p.N - 1) * p.x_sn;
+#pragma unroll
+      for (int s4 = 0; s4 < NS / 4; ++s4) xv4[s4] = *reinterpret_cast<const f32x4*>(xp + 4 * s4);
+    }
+  };
   // rows past N are never fetched: zero the images once so they only ever hold finite data
   if constexpr (SWZ) lds_zero<(int)(SH::KV_BYTES / 4)>(lds);
   else lds_zero<(SH::NIMG + 512) / 4>(lds + SH::KH / 4);
@@ -1889,7 +2065,81 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
   for (int t = 0; t < DT; ++t) { dv[t] = zero16(); dk[t] = zero16(); }
 #pragma unroll
   for (int t = 0; t < KTA; ++t) dtt[t] = zero16();
-  for (int qb = 0; qb < p.NQB; ++qb) {
+  // A key block whose every key is masked (padded ASTs, sbm_attn.py:61): P = 0 on all its elements, so dK = dV = 0
+  // and its only gradient is the STE term G = A ? hardtanh(csp (+ dgraph)) : 0 (STE.py:17-19), into dT here and, via
+  // its w tiles (w = 0 on every edge), into the query side's dQh. Key block 0 always runs the full loop (with FG it
+  // forms the row constants the query side reads).
+  bool dead = false;
+  if (mk && kbi > 0) {
+    wait_vm_all();
+    dead = __builtin_amdgcn_ballot_w64(jv && mval == 0.f) == 0;
+  }
+  if (dead) {
+    for (int qb = 0; qb < p.NQB; ++qb) {
+      const int i0 = qb * 32;
+      wait_vm_all();  // query block qb's Qh image and bit words have landed
+      const float csp = dspv / ((float)p.B * (float)p.N * (float)p.M);
+      const uint32_t qvm = p.N - i0 >= 32 ? 0xffffffffu : (1u << (p.N - i0)) - 1u;
+      const uint32_t wAs = (wAn & qvm & kvm) >> (4 * h);
+      if (qb + 1 < p.NQB) {
+        if constexpr (!DENSE) wAn = p.Abits[wcol + (int64_t)(qb + 1) * p.Mpad];
+      }
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        float gv[8], wv[8];
+#pragma unroll
+        for (int rr = 0; rr < 8; ++rr) {
+          const int r = 8 * half + rr;
+          const bool a = !DENSE && ((wAs >> crow(r, 0)) & 1u);
+          float cg = csp;
+          if constexpr (DG) {
+            const int ii = i0 + crow(r, h);
+            const int64_t me = ((int64_t)bh * p.N + imin(ii, p.N - 1)) * p.M + jc;
+            if (p.dgraph) cg += ldz(p.dgraph, me, INT64_MAX, (ii < p.N) && jv);
+          }
+          gv[rr] = a ? __builtin_amdgcn_fmed3f(0.f + cg, -1.f, 1.f) : 0.f;  // w = dM P = 0
+          wv[rr] = __uint_as_float(a ? 0u : W_NO_EDGE);
+        }
+        if constexpr (HO) {
+          float* const w = dsw + (int64_t)qb * p.NKB * 1024 + 16 * half;
+          const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+          if constexpr (W1) {  // w tiles, and P = 0 in the second plane (read for rows with rho != 0)
+            __builtin_nontemporal_store((f32x4{wv[0], wv[1], wv[2], wv[3]}), reinterpret_cast<f32x4*>(w));
+            __builtin_nontemporal_store((f32x4{wv[4], wv[5], wv[6], wv[7]}), reinterpret_cast<f32x4*>(w + 8));
+            __builtin_nontemporal_store(z, reinterpret_cast<f32x4*>(w + p.gplane));
+            __builtin_nontemporal_store(z, reinterpret_cast<f32x4*>(w + p.gplane + 8));
+          } else {  // two planes: ds = 0, G
+            __builtin_nontemporal_store(z, reinterpret_cast<f32x4*>(w));
+            __builtin_nontemporal_store(z, reinterpret_cast<f32x4*>(w + 8));
+            if constexpr (!DENSE) {
+              __builtin_nontemporal_store((f32x4{gv[0], gv[1], gv[2], gv[3]}), reinterpret_cast<f32x4*>(w + p.gplane));
+              __builtin_nontemporal_store((f32x4{gv[4], gv[5], gv[6], gv[7]}),
+                                          reinterpret_cast<f32x4*>(w + p.gplane + 8));
+            }
+          }
+        }
+        if constexpr (MB4) {
+#pragma unroll
+          for (int rr = 0; rr < 8; ++rr)
+            dtt[0] = mfma4b(lds_f1(lds, SH::KH + narrow_elem(crow(8 * half + rr, h), c & 15, KPN)), gv[rr], dtt[0]);
+        } else if constexpr (!DENSE) {
+#pragma unroll
+          for (int at = 0; at < KTA; ++at)
+#pragma unroll
+            for (int rr = 0; rr < 8; ++rr) {
+              const int r = 8 * half + rr;
+              const float v = lds_f1(lds, SH::KH + narrow_elem(crow(r, h), imin(32 * at + c, KP - 1), KPN));
+              dtt[at] = mfma((KP >= 32 || c < KP) ? v : 0.f, gv[rr], dtt[at]);
+            }
+        }
+      }
+      if (qb + 1 < p.NQB) {  // the Qh image read out: the next block's
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if constexpr (!DENSE) dma_narrow(Hl, hr_, i0 + 32, KPN);
+      }
+    }
+  }
+  for (int qb = 0; qb < (dead ? 0 : p.NQB); ++qb) {
     int ln = threadIdx.x;  // opaque per iteration: keeps the per-row LDS addresses out of the prologue
     asm volatile("" : "+v"(ln));
     const int c = ln & 31, h = (ln >> 5) & 1;
@@ -1900,8 +2150,38 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
     asm volatile("" : "+v"(mvl), "+v"(dsl));
     const float kbias = (jv && mvl == 0.f) ? 0.f : NEG_INF;  // this lane's key (sbm_attn.py:61)
     const float csp = dsl / ((float)p.B * (float)p.N * (float)p.M);
-    // W1: does a row of this query block have rho != 0 (its query side then needs P as well)?
-    const bool rho_any = W1 && __builtin_amdgcn_ballot_w64(lds_f1(lds, SH::KS + 16 * c + 12) != 0.f) != 0;
+    // FG: this block's X rows are loaded here, behind the wait (their latency hides under the S chain), and the row
+    // constants formed after it (form_rec), before the elementwise reads them
+    load_x(i0);
+    bool rho_any = false;  // W1: does a row of this query block have rho != 0 (its query side then needs P as well)?
+    auto form_rec = [&]() {
+      if constexpr (FG) {
+        // gamma of query i0 + c = rowsum(dX * X): this lane's half from the dX image row and its X registers, then
+        // the two halves added; the row constants as k_attn_rowprep forms them
+        const int xb0 = SWZ ? row_base64(c, h, SW_BOTH) : 4 * (c * DP + NS * h);
+        float gp = 0.f;
+#pragma unroll
+        for (int s4 = 0; s4 < NS / 4; ++s4) {
+          const f32x4 dx4 = lds_f4(lds, SH::KX + (SWZ ? (xb0 ^ (16 * s4)) : xb0 + 16 * s4));
+          gp = fmaf(dx4[0], xv4[s4][0], fmaf(dx4[1], xv4[s4][1], fmaf(dx4[2], xv4[s4][2], fmaf(dx4[3], xv4[s4][3], gp))));
+        }
+        const float gamma = xhalf_sum(gp);
+        const bool iv = i0 + c < p.N;
+        const f32x4 st = lds_f4(lds, SH::KS + 16 * c);  // lse, 1 / max(n, eps), [n >= eps] (finite data past N)
+        f32x4 rec;
+        rec[0] = iv ? -st[0] * LOG2E : NEG_INF;
+        rec[1] = iv ? dscale * st[1] : 0.f;
+        rec[2] = (iv && st[2] != 0.f) ? -gamma * st[1] : 0.f;
+        rec[3] = (iv && st[2] == 0.f) ? gamma : 0.f;
+        if (h == 0) {
+          *reinterpret_cast<f32x4*>(lds + SH::KS / 4 + 4 * c) = rec;
+          if (kbi == 0) *reinterpret_cast<f32x4*>(p.brow + (((int64_t)bh * p.NQB + qb) * 32 + c) * 4) = rec;
+        }
+        rho_any = W1 && __builtin_amdgcn_ballot_w64(rec[3] != 0.f) != 0;
+      } else {
+        rho_any = W1 && __builtin_amdgcn_ballot_w64(lds_f1(lds, SH::KS + 16 * c + 12) != 0.f) != 0;
+      }
+    };
     // sampled / keep bits shifted so that register r's query is bit crow(r, 0); queries past N and keys past M
     // count as not sampled
     const uint32_t qvm = p.N - i0 >= 32 ? 0xffffffffu : (1u << (p.N - i0)) - 1u;
@@ -1922,6 +2202,7 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
         const f32x4 x1 = lds_f4(lds, SH::KX + (SWZ ? (qrb ^ (32 * j2 + 16)) : qrb + 32 * j2 + 16));
         dpacc = mfma_bf(pack8(x0, x1), pack8(&vr[8 * j2]), dpacc);
       }
+      form_rec();
     } else {
 #pragma unroll
       for (int s4 = 0; s4 < NS / 4; ++s4) {
@@ -1929,6 +2210,7 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
 #pragma unroll
         for (int e = 0; e < 4; ++e) sacc = mfma(qv[e], kr[4 * s4 + e], sacc);
       }
+      form_rec();  // (between the chains: the X registers die before dP's accumulator is live)
 #pragma unroll
       for (int s4 = 0; s4 < NS / 4; ++s4) {
         const f32x4 xv = lds_f4(lds, SH::KX + (SWZ ? (qrb ^ (16 * s4)) : qrb + 16 * s4));
@@ -3209,6 +3491,7 @@ KArgs make_kargs(const csa_sbm_fwd_args* a, const Layout& L) {
   p.Act = (a->flags & CSA_FLAG_FWD_ONLY) ? nullptr : (float*)((char*)st + L.Act);
   p.Abits = (uint32_t*)((char*)st + L.Abits); p.Rbits = (uint32_t*)((char*)st + L.Rbits);
   p.cnt = (unsigned long long*)((char*)st + L.cnt);
+  p.tdead = (unsigned long long*)((char*)st + L.tdead);
   p.U = a->uniforms;
   p.seed_lo = (uint32_t)a->seed; p.seed_hi = (uint32_t)(a->seed >> 32); p.off = (uint32_t)a->offset;
   p.attn_p = a->attn_dropout; p.proj_p = a->proj_dropout;
@@ -3358,7 +3641,7 @@ csa_status launch_fwd(const csa_sbm_fwd_args* a, const Layout& L, hipStream_t st
 template <int D, int KPH, bool DENSE, bool DROP, bool DG, bool BF, typename MID>
 void launch_attn_bwd_v(const KArgs& p, int BH, const Layout& L, const csa_prof* pf, hipStream_t st, MID mid) {
   using SH = AttnBwdShape<D, KPH>;
-  {
+  if constexpr (DG) {  // (otherwise k_attn_bwd_kv forms the row constants itself)
     Stage sg(pf, CSA_STAGE_ATTN_ROWPREP, st);
     constexpr int RPW = 4 * (64 / (D / 4 <= 16 ? 16 : 32));  // rows per wave (k_attn_rowprep)
     const int64_t rows = (int64_t)BH * L.NQB * 32, per_block = 4LL * RPW;

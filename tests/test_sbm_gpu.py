@@ -505,3 +505,128 @@ def test_broadcast_upstream_gradient_is_materialised():
         outs.append([x.grad.cpu() for x in t])
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+def _dead_tile_masks(B, N):
+    """Key masks with whole 32-key tiles masked (padded ASTs): suffix padding at 1, 31, 64 and N valid keys, the
+    first tile masked, a masked middle tile between live ones, and every key masked."""
+    mask = torch.zeros(B, N)
+    lens = [1, 31, 64, N]
+    for b in range(min(B, 4)):
+        mask[b, lens[b]:] = 1.0
+    if B > 4:
+        mask[4, :32] = 1.0  # the first key tile dead (the kernels still run it as live)
+    if B > 5:
+        mask[5, 32:64] = 1.0  # a dead tile between live ones
+    if B > 6:
+        mask[6, :] = 1.0  # every key masked: X rows of uniform attention over nothing (0/0 as the reference)
+    return mask
+
+
+@pytest.mark.skipif(not has_gpu(), reason="needs GPU")
+@pytest.mark.parametrize("shape", [(6, 2, 150, 64, 10), (6, 2, 100, 96, 16), (6, 1, 300, 64, 64)])
+def test_sbm_dead_key_tiles_match_oracle(shape):
+    """Key tiles whose every key is masked run the light paths (forward: expA, sampling and bit words only;
+    k_attn_bwd_kv: a whole masked key block carries only the STE term into dT and its w tiles; k_attn_bwd_qg: no dQ
+    products for a dead tile). The sampled graph (padded positions included, sbm_attn.py:64), the sparsity, X, dQ /
+    dK / dV and every parameter gradient -- dC and the MLP weights take the STE term of the dead tiles' edges --
+    against the fp64 closed form; two runs bitwise identical."""
+    B, H, N, d, k = shape
+    Q, K, V, _, u, dX, dsp, params = _rand_case(B, H, N, d, k, seed=97 + N)
+    mask = _dead_tile_masks(B, N)
+    r1 = _run_module(Q, K, V, mask, u, dX, dsp, params, k)
+    r2 = _run_module(Q, K, V, mask, u, dX, dsp, params, k)
+    for a, b in zip(r1[:6], r2[:6]):
+        assert torch.equal(a, b)
+    X, sp, graph, dQ, dK, dV, grads = r1
+    ref, rg = closed_form.sbm_fwd_bwd(Q, K, V, mask, params, u, k, dX, dsp, graph_override=graph)
+    near = (torch.abs(u - ref["expA"].clamp(0.01, 0.99)) < 1e-6)
+    assert bool(torch.all(near[graph != ref["graph"].float()])), "graph flips away from fp32 ties"
+    assert float(graph[:, :, :, 64:].sum()) > 0  # sampled edges at padded keys are kept (and counted)
+    np.testing.assert_allclose(sp.numpy(), ref["sparsity"].numpy(), rtol=1e-6)
+    live = mask.sum(1) < N  # rows with no valid key are 0/0 in the reference (NaN) -- compared where finite
+    np.testing.assert_allclose(X[live].numpy(), ref["X"][live].numpy(), rtol=RTOL, atol=ATOL)
+    for name, t, key in (("dQ", dQ, "Q"), ("dK", dK, "K"), ("dV", dV, "V")):
+        np.testing.assert_allclose(t[live].numpy(), rg[key][live].numpy(), rtol=RTOL, atol=ATOL, err_msg=name)
+    assert torch.all(dK[~live] == 0) and torch.all(dV[~live] == 0)
+    if bool(live.all()):
+        for pn, gv in grads.items():
+            np.testing.assert_allclose(gv.numpy(), rg[pn].numpy(), rtol=RTOL, atol=ATOL, err_msg=pn)
+
+
+@pytest.mark.skipif(not has_gpu(), reason="needs GPU")
+def test_sbm_dead_key_tiles_parameter_gradients_match_oracle():
+    """The STE-only gradient of fully masked key tiles into the cluster weights and the projection MLP (dC, dW, db)
+    over a batch where most tiles are dead, against the fp64 closed form."""
+    B, H, N, d, k = 6, 8, 150, 64, 10
+    Q, K, V, _, u, dX, dsp, params = _rand_case(B, H, N, d, k, seed=1234)
+    mask = _dead_tile_masks(B, N)
+    X, sp, graph, dQ, dK, dV, grads = _run_module(Q, K, V, mask, u, dX, dsp, params, k)
+    _, rg = closed_form.sbm_fwd_bwd(Q, K, V, mask, params, u, k, dX, dsp, graph_override=graph)
+    for pn, gv in grads.items():
+        np.testing.assert_allclose(gv.numpy(), rg[pn].numpy(), rtol=RTOL, atol=ATOL * max(1.0, float(rg[pn].abs().max())),
+                                   err_msg=pn)
+
+
+@pytest.mark.skipif(not has_gpu(), reason="needs GPU")
+def test_train_mode_dead_key_tiles_match_oracle_with_regenerated_masks():
+    """Train mode (in-kernel Philox draws) over dead key tiles: the light forward still draws the STE uniforms and
+    the keep bits of every tile, so the graph equals the regenerated u16 < clamp(expA) 65536 and every gradient
+    matches the closed form under the regenerated masks."""
+    from oracle import philox
+    B, H, N, d, k = 6, 2, 150, 64, 10
+    Q, K, V, _, _, dX, dsp, params = _rand_case(B, H, N, d, k, seed=4321)
+    mask = _dead_tile_masks(B, N)
+    seed, offset, attn_p, proj_p = (0x2468ACE << 32) | 0x1357BDF, 5, 0.2, 0.1
+    cw = params["layer.weight"].cuda()
+    pw = [params[f"proj.{i}.weight"].cuda() for i in (0, 3, 6)]
+    pb = [params[f"proj.{i}.bias"].cuda() for i in (0, 3, 6)]
+    q, kk, v, mk = Q.cuda(), K.cuda(), V.cuda(), mask.cuda()
+    X, sp, state = torch.ops.csa.sbm_fwd(q, kk, v, mk, cw, pw, pb, None, k, seed, offset, attn_p, proj_p, False)
+    graph, _ = torch.ops.csa.sbm_maps(q, kk, v, mk, state, k, False)
+    g = torch.ops.csa.sbm_bwd(q, kk, v, mk, cw, pw, pb, k, attn_p, proj_p, seed, offset, False, state, X,
+                              dX.cuda(), dsp.cuda(), None)
+    torch.cuda.synchronize()
+    graph = graph.cpu()
+    keep = philox.attn_keep(B, H, N, N, seed, offset, attn_p)
+    ks = 1.0 / (1.0 - np.float32(proj_p))
+    pk = {f"{s}{l}": torch.from_numpy(philox.proj_keep(B, H, N, d, seed, offset, proj_p, l, int(s == "k")) * ks)
+          for s in "qk" for l in (0, 1)}
+    ref, rg = closed_form.sbm_fwd_bwd(Q, K, V, mask, params, None, k, dX, dsp,
+                                     attn_keep=torch.from_numpy(keep / (1.0 - np.float32(attn_p))), proj_keep=pk,
+                                     graph_override=graph)
+    u16 = philox.attn_uniforms(B, H, N, N, seed, offset, philox.RNG_STE)
+    want = philox.ste_graph(ref["expA"].numpy(), u16)
+    thr = np.clip(ref["expA"].numpy(), 0.01, 0.99) * 65536.0
+    diff = want != graph.numpy().astype(bool)
+    assert np.all(np.abs(u16[diff] - thr[diff]) < 0.5), f"{int(diff.sum())} graph flips away from ties"
+    assert float(graph[:, :, :, 64:].sum()) > 0  # dead tiles sample too
+    np.testing.assert_allclose(X.cpu().numpy(), ref["X"].numpy(), rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(sp.cpu().numpy(), ref["sparsity"].numpy(), rtol=1e-6)
+    names = ["Q", "K", "V", "layer.weight", "proj.0.weight", "proj.0.bias", "proj.3.weight", "proj.3.bias",
+             "proj.6.weight", "proj.6.bias"]
+    for name, t in zip(names, g):
+        np.testing.assert_allclose(t.cpu().numpy(), rg[name].numpy(), rtol=RTOL, atol=ATOL, err_msg=name)
+
+
+@pytest.mark.skipif(not has_gpu(), reason="needs GPU")
+def test_full_attention_dead_key_tiles_match_oracle():
+    """FullAttention (config 4) over dead key tiles: the same light paths without clusters -- X and dQ / dK / dV
+    against the oracle's autograd (eval mode)."""
+    from csa_amd.module.sbm_attn import FullAttention
+    from oracle import sbm_ref
+    B, H, N, d = 6, 2, 150, 64
+    g = torch.Generator().manual_seed(55)
+    Q, K, V, dX = (torch.randn(B, H, N, d, generator=g) for _ in range(4))
+    mask = _dead_tile_masks(B, N)
+    m = FullAttention({"attention_dropout": 0.2, "head_dim": d, "num_head": H}, 0).cuda().eval()
+    q, kk, v = (t.cuda().requires_grad_(True) for t in (Q, K, V))
+    X = m(q, kk, v, mask.cuda())[0]
+    X.backward(dX.cuda())
+    qr, kr, vr = (t.clone().double().requires_grad_(True) for t in (Q, K, V))
+    Xr = sbm_ref.full_attention(qr, kr, vr, mask.double())
+    Xr = Xr[0] if isinstance(Xr, tuple) else Xr
+    Xr.backward(dX.double())
+    np.testing.assert_allclose(X.detach().cpu().numpy(), Xr.detach().numpy(), rtol=RTOL, atol=ATOL)
+    for name, a, r in (("dQ", q, qr), ("dK", kk, kr), ("dV", v, vr)):
+        np.testing.assert_allclose(a.grad.cpu().numpy(), r.grad.numpy(), rtol=RTOL, atol=ATOL, err_msg=name)

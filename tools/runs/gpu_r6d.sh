@@ -1,0 +1,18 @@
+#!/bin/bash
+# Round 6: padded-batch dead key tiles (light forward / bwd_kv / bwd_qg paths) + the forward's sampling inside the S
+# chain's scheduling region: GPU tests (new dead-tile tests first), then a same-box A/B (base = round start, fwdv = the
+# fused row constants + pinned forward scalars, hip = this tree) of the headline and of the padded-mask leg
+set -o pipefail
+export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/r6d; mkdir -p $O
+L=$R/code-structure-aware-transformer_amd/csa_amd/lib
+cd $R
+timeout -k 10 300 python -u -m pytest tests/test_sbm_gpu.py -x -q --timeout 120 --timeout-method thread -k "dead" > $O/pytest_dead.txt 2>&1; rc=$?; tail -2 $O/pytest_dead.txt; [ $rc -eq 0 ] || { grep -E "Error|FAILED|Mismatch|assert|Max" $O/pytest_dead.txt | head -40; exit $rc; }
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.txt 2>&1; rc=$?; tail -2 $O/pytest.txt; [ $rc -eq 0 ] || { grep -E "Error|FAILED|Mismatch|assert|Max" $O/pytest.txt | head -40; exit $rc; }
+for i in 1 2 3; do
+  for lib in libcsa_base.so libcsa_fwdv.so libcsa_hip.so; do
+    out=$(CSA_HIP_LIB=$L/$lib timeout -k 10 120 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-train --no-bf16-leg --no-side-legs --no-cpu-config1) || exit 1
+    python3 -c "import json,sys; d=json.loads(sys.argv[1]); print(sys.argv[2], d['ms_per_step'], 'pad', d['padded_mask']['ms_per_step'], {k: round(v, 4) for k, v in d['stage_ms'].items()})" "$out" "$lib"
+  done
+done 2>&1 | grep -v amdgpu.ids | tee $O/ab.txt
