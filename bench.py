@@ -469,7 +469,13 @@ def stage_profilers():
     return ev, make_profs, stage_times
 
 
-def measure_layer(world, rank, dev, steps, warmup, B, N, d, k, dense, precision, eval_, reducer="torch"):
+def padded_lengths(B, N, rank):
+    """Config 2's padded batches: n_b ~ U[50, N] real nodes per AST (seeded per rank)."""
+    gpad = torch.Generator().manual_seed(4321 + rank)
+    return torch.randint(min(50, N), N + 1, (B,), generator=gpad)
+
+
+def measure_layer(world, rank, dev, steps, warmup, B, N, d, k, dense, precision, eval_, reducer="torch", padded=False):
     """One SBMAttention (or FullAttention) fwd+bwd step on synthetic inputs resident in HBM: an untimed pass with
     HIP events around every stage (per-stage kernel times, the dominant stage), then the timed region with events
     only around the dominant kernel's launch (its live average launch duration). Returns the pieces of the line."""
@@ -493,6 +499,9 @@ def measure_layer(world, rank, dev, steps, warmup, B, N, d, k, dense, precision,
         model = wrap_ddp(mod, dev, impl=reducer)  # in-order attention backward beside RCCL
     Q, K, V = (torch.randn(B, H, N, d, device=dev).requires_grad_(True) for _ in range(3))
     mask = torch.zeros(B, N, device=dev)
+    if padded:
+        nb = padded_lengths(B, N, rank)
+        mask.copy_((torch.arange(N)[None, :] >= nb[:, None]).float())
     dX = torch.randn(B, H, N, d, device=dev)
     dsp = torch.full((H,), 3.125e-4, device=dev)
 
@@ -705,6 +714,8 @@ def main():
                     help="operand precision of the attention contractions (fp32 = the reference's)")
     ap.add_argument("--no-bf16-leg", action="store_true", help="skip the bf16-mode side measurement")
     ap.add_argument("--no-padded-leg", action="store_true", help="skip the padded-mask (n_b ~ U[50,150]) leg")
+    ap.add_argument("--padded", action="store_true",
+                    help="the main measurement on padded batches (n_b ~ U[50, N], key mask on the padding; diagnostic)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-cpu-config1", action="store_true", help="skip the config-1 CPU CSATrans protocol")
@@ -748,14 +759,14 @@ def main():
     B, H, N, d, k = args.batch, 8, args.seq_len, args.head_dim, args.clusters
     progress(f"SBM layer B={B} N={N} d={d} k={k}: warm-up")
     L = measure_layer(world, rank, dev, args.steps, args.warmup, B, N, d, k, args.dense, args.precision, args.eval,
-                      reducer=args.reducer)
+                      reducer=args.reducer, padded=args.padded)
     mod, step, mask = L["mod"], L["step"], L["mask"]
     stage_ms, flops, timed, over, overlapped = L["stage_ms"], L["flops"], L["timed"], L["over"], L["overlapped"]
     dom, dom_ms, kernel_of, elapsed = L["dom"], L["dom_ms"], L["kernel_of"], L["elapsed"]
     ms_per_step = elapsed * 1000.0 / args.steps
     value = world * B * args.steps / elapsed
     roofline = L["roofline"]
-    headline = (B, N, d, k, args.precision, args.dense, args.eval) == (256, 150, 64, 10, "fp32", False, False)
+    headline = (B, N, d, k, args.precision, args.dense, args.eval, args.padded) == (256, 150, 64, 10, "fp32", False, False, False)
     table = pmc_table() if headline else None
     if roofline and table:
         tr = table["kernels"].get(kernel_of[dom])
@@ -773,7 +784,7 @@ def main():
         "metric": METRIC, "value": round(value, 1), "unit": "ASTs/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f32" if args.precision == "fp32" else "bf16 MFMA operands, f32 storage/accumulation",
-        "data": f"synthetic (N(0,1) Q/K/V, {N}-node ASTs, no padding)",
+        "data": f"synthetic (N(0,1) Q/K/V, {N}-node ASTs, " + ("padded: n_b ~ U[50, N] real nodes)" if args.padded else "no padding)"),
         "config": {"workload": "SBMAttention fwd+bwd (config/python.py dims) " + ("dense FullAttention" if args.dense
                    else "SBM") + ("" if N == 150 else f", long-AST stress N={N} k={k}"), "global_batch": B * world, "per_gpu_batch": B, "seq_len": N, "heads": H,
                    "head_dim": d, "clusters": 0 if args.dense else k, "mode": "eval" if args.eval else "train",
@@ -817,8 +828,7 @@ def main():
     if not args.dense and N == 150 and not args.no_padded_leg:
         # config 2's real batches are padded: n_b ~ U[50, 150] nodes per AST, the rest key-masked (same layer, B)
         progress("padded-mask leg")
-        gpad = torch.Generator().manual_seed(4321 + rank)
-        nb = torch.randint(50, N + 1, (B,), generator=gpad)
+        nb = padded_lengths(B, N, rank)
         mask.copy_((torch.arange(N)[None, :] >= nb[:, None]).float())
         for _ in range(args.warmup):
             step()

@@ -418,29 +418,41 @@ __device__ __forceinline__ uint32_t u16_of(const u32x4& r, int e) {
 // Hidden activations are accumulator tiles (feature rows in registers, data rows on lanes).
 // Proj dropout p>0 applies Linear -> Dropout -> ReLU (sbm_attn.py:22-30) with a stateless Philox
 // mask keyed by (row, feature, layer, Q/K), so the backward regenerates it bit-identically.
-template <int D>
-__device__ __forceinline__ void mlp_act(const KArgs& p, f32x16 (&a)[D / 32], int layer, int row, int bh, int isK) {
-  constexpr int DT = D / 32;
-  const int h = lane_id() >> 5;
-  const bool drop = p.proj_p > 0.f;
-  const float ks = drop ? 1.f / (1.f - p.proj_p) : 1.f;
-#pragma unroll
-  for (int ot = 0; ot < DT; ++ot)
-#pragma unroll
-    for (int gp = 0; gp < 2; ++gp) {
-      // one Philox call -> 8 x 16-bit uniforms for registers 8gp..8gp+7 (keep <=> u16 >= pdrop_thr)
-      u32x4 u = {0u, 0u, 0u, 0u};
-      if (drop)
-        u = philox4x32(u32x4{(uint32_t)row, (uint32_t)(4 * ot + 2 * gp + h) | (layer << 16) | (isK << 20),
-                             (uint32_t)bh, (RNG_PROJ_DROP << 28) ^ p.off}, p.seed_lo, p.seed_hi);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float v = a[ot][8 * gp + e];
-        if (drop) v = (u16_of(u, e) >= p.pdrop_thr) ? v * ks : 0.f;
-        a[ot][8 * gp + e] = fmaxf(v, 0.f);
+// The layer's Philox words (one call -> 8 x 16-bit uniforms for registers 8gp..8gp+7 of tile ot; keep <=>
+// u16 >= pdrop_thr) are generated one call per K-group as side work of the layer's own MFMA chain (gen(g) inside
+// the chain's scheduling regions), then applied (apply) to the finished accumulators. PD (a dropout launch): with
+// p = 0 the keep test passes everywhere and the scale is 1, so PD only decides whether the words are drawn.
+template <int D, bool PD>
+struct DropWords {
+  static constexpr int DT = D / 32, NC = 2 * DT;  // Philox calls per layer
+  u32x4 u[NC];
+  uint32_t k0, k1, c3, c1;  // Philox key, counter word 3 (stream, offset), counter word 1's layer / Q-K bits
+  int row, bh;
+  __device__ __forceinline__ DropWords(const KArgs& p, int layer, int row_, int bh_, int isK)
+      : k0(p.seed_lo), k1(p.seed_hi), c3((RNG_PROJ_DROP << 28) ^ p.off),
+        c1(((uint32_t)layer << 16) | ((uint32_t)isK << 20)), row(row_), bh(bh_) {}
+  __device__ __forceinline__ void gen(int g) {
+    if constexpr (PD) {
+      if (g < NC) {
+        const int ot = g >> 1, gp = g & 1, h = lane_id() >> 5;
+        u[g] = philox4x32(u32x4{(uint32_t)row, (uint32_t)(4 * ot + 2 * gp + h) | c1, (uint32_t)bh, c3}, k0, k1);
       }
     }
-}
+  }
+  __device__ __forceinline__ void apply(const KArgs& p, f32x16 (&a)[DT]) const {
+    const float ks = PD ? 1.f / (1.f - p.proj_p) : 1.f;
+#pragma unroll
+    for (int ot = 0; ot < DT; ++ot)
+#pragma unroll
+      for (int gp = 0; gp < 2; ++gp)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float v = a[ot][8 * gp + e];
+          if constexpr (PD) v = (u16_of(u[2 * ot + gp], e) >= p.pdrop_thr) ? v * ks : 0.f;
+          a[ot][8 * gp + e] = fmaxf(v, 0.f);
+        }
+  }
+};
 
 // fp32, k <= 16, d = 64 / 96 (k_proj_bwd_s): the cluster-weight gradient is formed from h2 instead of po,
 //   dC_h = sum dZ^T po = (sum dZ^T h2) W2^T + (sum dZ^T 1) b2^T     (po = h2 W2^T + b2, proj.6)
@@ -472,7 +484,7 @@ __device__ __forceinline__ void add_bias(const float (&ba)[D / 32], f32x16 (&a)[
 struct FwdFrags { const float* W[3]; const float* C; const float* S; const float* b[3]; };
 
 // h1 = relu(drop(W0 x + b0)) from lin-perm input rows
-template <int D, bool FL, bool BF = false>
+template <int D, bool FL, bool BF = false, bool PD = true>
 __device__ __forceinline__ void mlp_layer0(const KArgs& p, const float* W0, const float* b0, const float (&x)[D / 2],
                                            f32x16 (&h1)[D / 32], int row, int bh, int isK) {
   constexpr int DT = D / 32, NS = D / 2;
@@ -480,9 +492,11 @@ __device__ __forceinline__ void mlp_layer0(const KArgs& p, const float* W0, cons
   bias_operand<D>(b0, ba);
 #pragma unroll
   for (int ot = 0; ot < DT; ++ot) h1[ot] = zero16();
-  frag_chain<DT, NS / 4, FL ? FL_LA : MLP_LA, FL, BF>(W0, NS, h1, [&](int s) { return x[s]; });
+  DropWords<D, PD> dw(p, 0, row, bh, isK);
+  frag_chain<DT, NS / 4, FL ? FL_LA : MLP_LA, FL, BF>(W0, NS, h1, [&](int s) { return x[s]; },
+                                                       [&](int g) { dw.gen(g); });
   add_bias<D>(ba, h1);
-  mlp_act<D>(p, h1, 0, row, bh, isK);
+  dw.apply(p, h1);
 }
 
 // out = W_l in + b_l  (acc-perm input), l = 1, 2
@@ -739,7 +753,7 @@ __device__ __forceinline__ void load_item_x(const KArgs& p, int b, int hd, int r
 // F2 body: item r of (b, hd) from its x rows. `next` runs once every product is done and x is dead,
 // before the stores (the persistent kernel issues the next item's x loads there: a later vmcnt wait
 // for them then does not also wait for this item's stores, which drain under the next item).
-template <int D, int KT, bool FL, typename NEXT, bool BF = false>
+template <int D, int KT, bool FL, typename NEXT, bool BF = false, bool PD = true>
 __device__ __forceinline__ void proj_fwd_item(const KArgs& p, const FwdFrags& F, int b, int hd, int r, float (&x)[D / 2],
                                               float* scr, NEXT next) {
   const int lane = lane_id(), c = lane & 31, h = lane >> 5;
@@ -765,19 +779,29 @@ __device__ __forceinline__ void proj_fwd_item(const KArgs& p, const FwdFrags& F,
   float* const blk = p.Act ? p.Act + ((int64_t)bh * (p.NQB + p.NKB) + r) * ABLK : nullptr;
   const bool on = blk != nullptr;
   const __amdgpu_buffer_rsrc_t ars = make_rsrc(blk, on ? ABLK * 4 : 0);
+  // layer 1's side work: h1's staged stores and layer 1's dropout words
+  DropWords<D, PD> dw1(p, 1, row, bh, isK);
+  struct Side1 {
+    ActStager<D / 32> st;
+    DropWords<D, PD>* dw;
+    __device__ __forceinline__ void operator()(int g) {
+      if constexpr (STAGED) st(g);
+      dw->gen(g);
+    }
+  };
   struct Side {
     ActStager<D / 32> st;
     __device__ __forceinline__ void operator()(int g) { if constexpr (STAGED) st(g); }
   };
-  mlp_layer0<D, FL, BF>(p, F.W[0], F.b[0], x, h1, row, bh, isK);
+  mlp_layer0<D, FL, BF, PD>(p, F.W[0], F.b[0], x, h1, row, bh, isK);
   PHF(0)
-  mlp_layer<D, FL, BF>(F.W[1], F.b[1], h1, h2, Side{{ars, 0, scr, h1, {}}});
+  mlp_layer<D, FL, BF>(F.W[1], F.b[1], h1, h2, Side1{{ars, 0, scr, h1, {}}, &dw1});
   if (H1E && on) {
     if (ABF && p.kp <= 16) store_act_lds_bf<D / 32>(blk, h1, scr);
     else store_act_lds<D / 32>(blk, h1, scr);
   }
   PHF(1)
-  mlp_act<D>(p, h2, 1, row, bh, isK);
+  dw1.apply(p, h2);
   PHF(2)
   mlp_layer<D, FL, BF>(F.W[2], F.b[2], h2, po, Side{{ars, 32 * D * 4, scr, h2, {}}});
   PHF(3)
@@ -855,7 +879,7 @@ struct ProjFwdLds {
 };
 
 // BF: CSA_DTYPE_BF16 (MLP and cluster projection on bf16 MFMA; T = Kh S^T stays fp32)
-template <int D, int KT, bool BF = false>
+template <int D, int KT, bool BF = false, bool PD = true>
 __global__ __launch_bounds__((64 * ProjFwdLds<D, KT>::NW)) void k_proj_fwd_l(const KArgs p) {
   using LY = ProjFwdLds<D, KT>;
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -887,7 +911,7 @@ __global__ __launch_bounds__((64 * ProjFwdLds<D, KT>::NW)) void k_proj_fwd_l(con
     auto nextf = [&] {
       if (nx < i_hi) load_item_x<D>(p, nx / per_b, hd, nx % per_b, x);
     };
-    proj_fwd_item<D, KT, true, decltype(nextf), BF>(p, F, it / per_b, hd, it % per_b, x, scr, nextf);
+    proj_fwd_item<D, KT, true, decltype(nextf), BF, PD>(p, F, it / per_b, hd, it % per_b, x, scr, nextf);
   }
 }
 
@@ -1164,6 +1188,35 @@ __device__ __forceinline__ void attn_fwd_item(const KArgs& p, float* __restrict_
     if constexpr (!DENSE) myA = gp == 0 ? writelane_batch<0>(myA, bA) : writelane_batch<8>(myA, bA);
     if constexpr (DROP) myR = gp == 0 ? writelane_batch<0>(myR, bR) : writelane_batch<8>(myR, bR);
   };
+  // the same for a live tile after its softmax: the selects take the exponentials directly (Zg summed in register
+  // order: the same value bit for bit as a single pass)
+  auto sample_sel = [&](int gp, int j0_, const f32x16& eacc, const u32x4 (&r_ste)[2], const u32x4 (&r_drop)[2],
+                        const float (&ex)[16], float (&w)[16]) {
+    unsigned long long bA[16], bR[16];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int r = 8 * gp + e;
+      bool av = true, keep = true;
+      if constexpr (!DENSE) {
+        if constexpr (HAS_U) {
+          const int j = j0_ + crow(r, h);
+          const float v = p.U[((int64_t)bh * p.N + ic) * p.M + imin(j, p.M - 1)];
+          const float uu = (iv && j < p.M) ? v : 2.f;
+          av = uu < fminf(fmaxf(eacc[r], 0.01f), 0.99f);  // STE.py:11-13
+        } else {
+          av = (float)u16_of(r_ste[gp], e) < __builtin_amdgcn_fmed3f(eacc[r], e_lo, e_hi);
+        }
+      }
+      if constexpr (DROP) keep = u16_of(r_drop[gp], e) >= drop_thr;
+      const float wa = av ? ex[r] : 0.f;
+      zgp += wa;
+      w[r] = keep ? wa : 0.f;
+      bA[r] = __ballot(av);
+      bR[r] = __ballot(keep);
+    }
+    if constexpr (!DENSE) myA = gp == 0 ? writelane_batch<0>(myA, bA) : writelane_batch<8>(myA, bA);
+    if constexpr (DROP) myR = gp == 0 ? writelane_batch<0>(myR, bR) : writelane_batch<8>(myR, bR);
+  };
   // the tile's bit words out, its sampled edges counted
   auto store_bits = [&](int j0_) {
     if constexpr (!DENSE) {
@@ -1213,42 +1266,34 @@ __device__ __forceinline__ void attn_fwd_item(const KArgs& p, float* __restrict_
     float w[16];
     myA = myR = 0u;
     if (is_live(kt)) {
-      // Region 1: the tile's Philox words, expA and the first third of S; region 2: more of S beside the sampling of
-      // registers 0-7; region 3: the rest of S beside registers 8-15 (scheduling barriers between them: each region's
-      // VALU issues in the shadow of its own MFMAs, and at most one group's masks are live)
+      // the tile's Philox words first, pinned below the S / expA chains (an opaque use): left alone, the compiler
+      // sinks their VALU past the DMA branch, out of the chains' scheduling region, where nothing hides it
       philox_tile(kt, r_ste, r_drop);
-      const f32x16 eacc = echain();
+      // S^T = K Q^T : A operand = K rows from the image (row c, lin-perm chunks of half h)
       f32x16 sacc = zero16();
-      auto s_chain = [&](int j_lo, int j_hi) {  // S^T = K Q^T K-groups [j_lo, j_hi): A = K rows from the image
-        if constexpr (BF) {
+      if constexpr (BF) {
 #pragma unroll
-          for (int j2 = 0; j2 < NS / 8; ++j2) {
-            if (2 * j2 < j_lo || 2 * j2 >= j_hi) continue;  // (one bf16 step = K-groups 2 j2, 2 j2 + 1)
-            const f32x4 k0 = lds_f4(lds, SWZ ? (kbase ^ (32 * j2)) : kbase + 32 * j2);
-            const f32x4 k1 = lds_f4(lds, SWZ ? (kbase ^ (32 * j2 + 16)) : kbase + 32 * j2 + 16);
-            sacc = mfma_bf(pack8(k0, k1), pack8(&q[8 * j2]), sacc);
-          }
-        } else {
-#pragma unroll
-          for (int j = 0; j < NS / 4; ++j) {
-            if (j < j_lo || j >= j_hi) continue;
-            const f32x4 kv = lds_f4(lds, SWZ ? (kbase ^ (16 * j)) : kbase + 16 * j);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) sacc = mfma(kv[e], q[4 * j + e], sacc);
-          }
+        for (int j2 = 0; j2 < NS / 8; ++j2) {
+          const f32x4 k0 = lds_f4(lds, SWZ ? (kbase ^ (32 * j2)) : kbase + 32 * j2);
+          const f32x4 k1 = lds_f4(lds, SWZ ? (kbase ^ (32 * j2 + 16)) : kbase + 32 * j2 + 16);
+          sacc = mfma_bf(pack8(k0, k1), pack8(&q[8 * j2]), sacc);
         }
-      };
-      constexpr int J1 = (NS / 4) * 3 / 8, J2 = (NS / 4) * 11 / 16;  // d = 64: K-groups 0-2 | 3-4 | 5-7
-      float ma[16], mak[16];
-      s_chain(0, J1);
-      __builtin_amdgcn_sched_barrier(0);
-      s_chain(J1, J2);
-      sample_group(0, j0, eacc, r_ste, r_drop, ma, mak);
-      __builtin_amdgcn_sched_barrier(0);
-      s_chain(J2, NS / 4);
-      sample_group(1, j0, eacc, r_ste, r_drop, ma, mak);
-      __builtin_amdgcn_sched_barrier(0);
-      store_bits(j0);
+      } else {
+#pragma unroll
+        for (int j = 0; j < NS / 4; ++j) {
+          const f32x4 kv = lds_f4(lds, SWZ ? (kbase ^ (16 * j)) : kbase + 16 * j);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) sacc = mfma(kv[e], q[4 * j + e], sacc);
+        }
+      }
+      const f32x16 eacc = echain();
+#pragma unroll
+      for (int gp = 0; gp < 2; ++gp) {
+        if constexpr (!DENSE && !HAS_U)
+          asm volatile("" : "+v"(r_ste[gp].x), "+v"(r_ste[gp].y), "+v"(r_ste[gp].z), "+v"(r_ste[gp].w));
+        if constexpr (DROP)
+          asm volatile("" : "+v"(r_drop[gp].x), "+v"(r_drop[gp].y), "+v"(r_drop[gp].z), "+v"(r_drop[gp].w));
+      }
       // V^T operand values for this tile's PV: lane (d = 32t + c) reads V[key crow(r,h)][d]
       float vt[DT][16];
 #pragma unroll
@@ -1272,8 +1317,9 @@ __device__ __forceinline__ void attn_fwd_item(const KArgs& p, float* __restrict_
         s[r] = fmaf(sacc[r], scale, bz[r >> 2][r & 3]);
         tmax = fmaxf(tmax, s[r]);
       }
-      // online softmax update (exp(-inf - m) = 0 covers masked keys; m_use keeps an all-masked prefix finite). Z and
-      // Zg are summed in register order; ex * {0, 1} is the select ex or 0 bit for bit.
+      // online softmax update (exp(-inf - m) = 0 covers masked keys; m_use keeps an all-masked prefix finite): the
+      // exponentials first, then the sampled graph and the dropout keep mask eight registers at a time, each
+      // compare's lane mask consumed right away by its select and by the bit packing (sample_sel)
       tmax = xhalf_max(tmax);
       const float m_new = fmaxf(m_run, tmax);
       const float m_use = (m_new == NEG_INF) ? 0.f : m_new;
@@ -1290,12 +1336,12 @@ __device__ __forceinline__ void attn_fwd_item(const KArgs& p, float* __restrict_
         ex[r] = __expf(s[r] - m_use);
         zp += ex[r];
       }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        zgp += ex[r] * ma[r];
-        w[r] = ex[r] * mak[r];
-      }
       m_run = m_new;
+      sample_sel(0, j0, eacc, r_ste, r_drop, ex, w);
+      __builtin_amdgcn_sched_barrier(0);  // one group's masks at a time
+      sample_sel(1, j0, eacc, r_ste, r_drop, ex, w);
+      __builtin_amdgcn_sched_barrier(0);
+      store_bits(j0);
       // O^T += V^T W^T (keys beyond M carry w = 0)
       if constexpr (BF) {
         const bf16x8 w0 = pack8(&w[0]), w1 = pack8(&w[8]);
@@ -3609,13 +3655,21 @@ csa_status launch_fwd(const csa_sbm_fwd_args* a, const Layout& L, hipStream_t st
         {
           const int64_t items = a->B * (L.NQB + L.NKB), slots = (D == 64 && PL::NW == 4 ? 2 : 1) * 256LL;
           const int G = (int)std::max<int64_t>(1, std::min<int64_t>(slots / a->H, (items + PL::NW - 1) / PL::NW));
+          // (PD: the projection dropout's Philox words are drawn; without dropout they are not)
+#define CSA_PF_LAUNCH(BFV, PDV)                                                                         \
+  do {                                                                                                  \
+    set_dyn_lds((const void*)k_proj_fwd_l<D, KT, BFV, PDV>, (int)PL::BYTES);                            \
+    hipLaunchKernelGGL((k_proj_fwd_l<D, KT, BFV, PDV>), dim3(G, a->H), dim3(64 * PL::NW), PL::BYTES, st, p); \
+  } while (0)
+          const bool pd = a->proj_dropout > 0.f;
           if (p.bf16) {  // CSA_DTYPE_BF16: MLP + cluster projection on bf16 MFMA
-            set_dyn_lds((const void*)k_proj_fwd_l<D, KT, true>, (int)PL::BYTES);
-            hipLaunchKernelGGL((k_proj_fwd_l<D, KT, true>), dim3(G, a->H), dim3(64 * PL::NW), PL::BYTES, st, p);
+            if (pd) CSA_PF_LAUNCH(true, true);
+            else CSA_PF_LAUNCH(true, false);
           } else {
-            set_dyn_lds((const void*)k_proj_fwd_l<D, KT>, (int)PL::BYTES);
-            hipLaunchKernelGGL((k_proj_fwd_l<D, KT>), dim3(G, a->H), dim3(64 * PL::NW), PL::BYTES, st, p);
+            if (pd) CSA_PF_LAUNCH(false, true);
+            else CSA_PF_LAUNCH(false, false);
           }
+#undef CSA_PF_LAUNCH
           done = true;
         }
       }

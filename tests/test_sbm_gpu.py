@@ -532,7 +532,10 @@ def test_sbm_dead_key_tiles_match_oracle(shape):
     dK / dV and every parameter gradient -- dC and the MLP weights take the STE term of the dead tiles' edges --
     against the fp64 closed form; two runs bitwise identical."""
     B, H, N, d, k = shape
-    Q, K, V, _, u, dX, dsp, params = _rand_case(B, H, N, d, k, seed=97 + N)
+    # (seed 97 + N at d = 96, k = 16 put one projection-MLP activation of an unpadded AST within fp32 rounding of
+    # the ReLU kink: its K row's dK differs from the fp64 oracle by 1e-3 relative in every build, the round-start one
+    # included -- a tie like the sampling ties above, not a dead-tile effect; profiles/r06_dead_tile_diag.txt)
+    Q, K, V, _, u, dX, dsp, params = _rand_case(B, H, N, d, k, seed=101 + N)
     mask = _dead_tile_masks(B, N)
     r1 = _run_module(Q, K, V, mask, u, dX, dsp, params, k)
     r2 = _run_module(Q, K, V, mask, u, dX, dsp, params, k)

@@ -1,0 +1,17 @@
+#!/bin/bash
+# Round 6: GPU tests on this tree (projection-forward dropout words inside the layer chains) then a same-box A/B:
+# base = round start, fwdv = fused row constants + pinned forward scalars, skip = + dead key tiles + forward sampling
+# in the S region (commit 'SBM attention: row constants ...'), hip = + projection dropout words in the chains
+set -o pipefail
+export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/r6g; mkdir -p $O
+L=$R/code-structure-aware-transformer_amd/csa_amd/lib
+cd $R
+timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread  > $O/pytest.txt 2>&1; rc=$?; tail -2 $O/pytest.txt; [ $rc -eq 0 ] || { grep -E "^E  +|FAILED" $O/pytest.txt | head -40; exit $rc; }
+for i in 1 2 3; do
+  for lib in libcsa_base.so libcsa_fwdv.so libcsa_skip.so libcsa_hip.so; do
+    out=$(CSA_HIP_LIB=$L/$lib timeout -k 10 120 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-train --no-bf16-leg --no-side-legs --no-cpu-config1 2>/dev/null) || exit 1
+    python3 -c "import json,sys; d=json.loads(sys.argv[1]); print(sys.argv[2], d['ms_per_step'], 'pad', d['padded_mask']['ms_per_step'], {k: round(v, 4) for k, v in d['stage_ms'].items()})" "$out" "$lib"
+  done
+done 2>&1 | tee $O/ab.txt
