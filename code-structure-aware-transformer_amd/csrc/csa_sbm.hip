@@ -997,6 +997,16 @@ __device__ __forceinline__ uint32_t writelane_batch(uint32_t dst, const unsigned
   return dst;
 }
 
+// 16 ballots -> the bit word of each key lane (lanes 0..31: key c of the tile, bit = query row)
+__device__ __forceinline__ uint32_t pack_bits(const bool (&v)[16]) {
+  unsigned long long b[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) b[r] = __ballot(v[r]);
+  uint32_t w = 0;
+  w = writelane_batch<0>(w, b);
+  return writelane_batch<8>(w, b);
+}
+
 template <int D, int KPH>
 struct AttnFwdLds {
   static constexpr bool SWZ = (D == 64);                        // x4 DMA into swizzled unpadded tiles
@@ -1156,66 +1166,29 @@ __device__ __forceinline__ void attn_fwd_item(const KArgs& p, float* __restrict_
     }
     return eacc;
   };
-  // The sampled graph and the dropout keep mask of one group of eight registers: each compare's lane mask is consumed
-  // right away, by the bit packing (ballot -> v_writelane into the key's lane) and by the 0 / 1 multipliers the
-  // softmax applies later (ma: sampled, mak: sampled and kept), so at most 8 masks (16 SGPRs) are live. Independent
-  // of S: a live tile runs it between the S chain's MFMAs.
   uint32_t myA = 0u, myR = 0u;
-  auto sample_group = [&](int gp, int j0_, const f32x16& eacc, const u32x4 (&r_ste)[2], const u32x4 (&r_drop)[2],
-                          float (&ma)[16], float (&mak)[16]) {
-    unsigned long long bA[16], bR[16];
+  // the sampled graph and the dropout keep mask of a tile (16 + 16 compares; pack_bits makes the bit words)
+  auto sample_all = [&](int j0_, const f32x16& eacc, const u32x4 (&r_ste)[2], const u32x4 (&r_drop)[2],
+                        bool (&av)[16], bool (&keep)[16]) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int r = 8 * gp + e;
-      bool av = true, keep = true;
-      if constexpr (!DENSE) {
-        if constexpr (HAS_U) {
+    for (int r = 0; r < 16; ++r) { av[r] = true; keep[r] = true; }
+    if constexpr (!DENSE) {
+      if constexpr (HAS_U) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
           const int j = j0_ + crow(r, h);
           const float v = p.U[((int64_t)bh * p.N + ic) * p.M + imin(j, p.M - 1)];
           const float uu = (iv && j < p.M) ? v : 2.f;
-          av = uu < fminf(fmaxf(eacc[r], 0.01f), 0.99f);  // STE.py:11-13
-        } else {
-          av = (float)u16_of(r_ste[gp], e) < __builtin_amdgcn_fmed3f(eacc[r], e_lo, e_hi);
+          av[r] = uu < fminf(fmaxf(eacc[r], 0.01f), 0.99f);  // STE.py:11-13
         }
-      }
-      if constexpr (DROP) keep = u16_of(r_drop[gp], e) >= drop_thr;
-      ma[r] = av ? 1.f : 0.f;
-      mak[r] = (av && keep) ? 1.f : 0.f;
-      bA[r] = __ballot(av);
-      bR[r] = __ballot(keep);
-    }
-    // bit-pack: word [qb][key] holds 32 query bits (lanes 0..31); this group's 8 ballots into their key lanes
-    if constexpr (!DENSE) myA = gp == 0 ? writelane_batch<0>(myA, bA) : writelane_batch<8>(myA, bA);
-    if constexpr (DROP) myR = gp == 0 ? writelane_batch<0>(myR, bR) : writelane_batch<8>(myR, bR);
-  };
-  // the same for a live tile after its softmax: the selects take the exponentials directly (Zg summed in register
-  // order: the same value bit for bit as a single pass)
-  auto sample_sel = [&](int gp, int j0_, const f32x16& eacc, const u32x4 (&r_ste)[2], const u32x4 (&r_drop)[2],
-                        const float (&ex)[16], float (&w)[16]) {
-    unsigned long long bA[16], bR[16];
+      } else {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int r = 8 * gp + e;
-      bool av = true, keep = true;
-      if constexpr (!DENSE) {
-        if constexpr (HAS_U) {
-          const int j = j0_ + crow(r, h);
-          const float v = p.U[((int64_t)bh * p.N + ic) * p.M + imin(j, p.M - 1)];
-          const float uu = (iv && j < p.M) ? v : 2.f;
-          av = uu < fminf(fmaxf(eacc[r], 0.01f), 0.99f);  // STE.py:11-13
-        } else {
-          av = (float)u16_of(r_ste[gp], e) < __builtin_amdgcn_fmed3f(eacc[r], e_lo, e_hi);
-        }
+        for (int r = 0; r < 16; ++r) av[r] = (float)u16_of(r_ste[r >> 3], r & 7) < __builtin_amdgcn_fmed3f(eacc[r], e_lo, e_hi);
       }
-      if constexpr (DROP) keep = u16_of(r_drop[gp], e) >= drop_thr;
-      const float wa = av ? ex[r] : 0.f;
-      zgp += wa;
-      w[r] = keep ? wa : 0.f;
-      bA[r] = __ballot(av);
-      bR[r] = __ballot(keep);
     }
-    if constexpr (!DENSE) myA = gp == 0 ? writelane_batch<0>(myA, bA) : writelane_batch<8>(myA, bA);
-    if constexpr (DROP) myR = gp == 0 ? writelane_batch<0>(myR, bR) : writelane_batch<8>(myR, bR);
+    if constexpr (DROP)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) keep[r] = u16_of(r_drop[r >> 3], r & 7) >= drop_thr;
   };
   // the tile's bit words out, its sampled edges counted
   auto store_bits = [&](int j0_) {
@@ -1266,8 +1239,8 @@ __device__ __forceinline__ void attn_fwd_item(const KArgs& p, float* __restrict_
     float w[16];
     myA = myR = 0u;
     if (is_live(kt)) {
-      // the tile's Philox words first, pinned below the S / expA chains (an opaque use): left alone, the compiler
-      // sinks their VALU past the DMA branch, out of the chains' scheduling region, where nothing hides it
+      // the tile's Philox words depend only on (query, tile, head): computed first, so their VALU work can
+      // interleave with the S / expA MFMA chains below instead of waiting behind them
       philox_tile(kt, r_ste, r_drop);
       // S^T = K Q^T : A operand = K rows from the image (row c, lin-perm chunks of half h)
       f32x16 sacc = zero16();
@@ -1287,13 +1260,6 @@ __device__ __forceinline__ void attn_fwd_item(const KArgs& p, float* __restrict_
         }
       }
       const f32x16 eacc = echain();
-#pragma unroll
-      for (int gp = 0; gp < 2; ++gp) {
-        if constexpr (!DENSE && !HAS_U)
-          asm volatile("" : "+v"(r_ste[gp].x), "+v"(r_ste[gp].y), "+v"(r_ste[gp].z), "+v"(r_ste[gp].w));
-        if constexpr (DROP)
-          asm volatile("" : "+v"(r_drop[gp].x), "+v"(r_drop[gp].y), "+v"(r_drop[gp].z), "+v"(r_drop[gp].w));
-      }
       // V^T operand values for this tile's PV: lane (d = 32t + c) reads V[key crow(r,h)][d]
       float vt[DT][16];
 #pragma unroll
@@ -1317,9 +1283,12 @@ __device__ __forceinline__ void attn_fwd_item(const KArgs& p, float* __restrict_
         s[r] = fmaf(sacc[r], scale, bz[r >> 2][r & 3]);
         tmax = fmaxf(tmax, s[r]);
       }
-      // online softmax update (exp(-inf - m) = 0 covers masked keys; m_use keeps an all-masked prefix finite): the
-      // exponentials first, then the sampled graph and the dropout keep mask eight registers at a time, each
-      // compare's lane mask consumed right away by its select and by the bit packing (sample_sel)
+      bool av[16], keep[16];
+      sample_all(j0, eacc, r_ste, r_drop, av, keep);
+      if constexpr (!DENSE) myA = pack_bits(av);
+      if constexpr (DROP) myR = pack_bits(keep);
+      store_bits(j0);
+      // online softmax update (exp(-inf - m) = 0 covers masked keys; m_use keeps an all-masked prefix finite)
       tmax = xhalf_max(tmax);
       const float m_new = fmaxf(m_run, tmax);
       const float m_use = (m_new == NEG_INF) ? 0.f : m_new;
@@ -1330,18 +1299,15 @@ __device__ __forceinline__ void attn_fwd_item(const KArgs& p, float* __restrict_
       for (int t = 0; t < DT; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
-      float ex[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        ex[r] = __expf(s[r] - m_use);
-        zp += ex[r];
+        const float e = __expf(s[r] - m_use);
+        zp += e;
+        const float wa = av[r] ? e : 0.f;
+        zgp += wa;
+        w[r] = keep[r] ? wa : 0.f;
       }
       m_run = m_new;
-      sample_sel(0, j0, eacc, r_ste, r_drop, ex, w);
-      __builtin_amdgcn_sched_barrier(0);  // one group's masks at a time
-      sample_sel(1, j0, eacc, r_ste, r_drop, ex, w);
-      __builtin_amdgcn_sched_barrier(0);
-      store_bits(j0);
       // O^T += V^T W^T (keys beyond M carry w = 0)
       if constexpr (BF) {
         const bf16x8 w0 = pack8(&w[0]), w1 = pack8(&w[8]);
@@ -1364,9 +1330,10 @@ __device__ __forceinline__ void attn_fwd_item(const KArgs& p, float* __restrict_
       const int nx = pop_next(kt);  // (a dead tile: the ones after it are dead too)
       if constexpr (!DENSE)
         if (nx >= 0) dma_narrow(Tl, tr, nx * 32, KPN);
-      float ma[16], mak[16];
-      sample_group(0, j0, eacc, r_ste, r_drop, ma, mak);
-      sample_group(1, j0, eacc, r_ste, r_drop, ma, mak);
+      bool av[16], keep[16];
+      sample_all(j0, eacc, r_ste, r_drop, av, keep);
+      if constexpr (!DENSE) myA = pack_bits(av);
+      if constexpr (DROP) myR = pack_bits(keep);
       store_bits(j0);
       kt = nx;
     }
