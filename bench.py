@@ -838,7 +838,8 @@ def main():
                               "ms_per_step": round(el_pad * 1000.0 / args.steps, 4),
                               "mean_nodes": round(float(nb.float().mean()), 2),
                               "note": "config 2 padded batches: n_b ~ U[50,150] real nodes per AST (seeded), key mask "
-                                      "1 on the padding; every kernel still runs the full 150-node tiles"}
+                                      "1 on the padding; fully masked 32-key tiles take the attention kernels' light "
+                                      "paths (STE term only), the projection runs every row"}
     if world == 1 and headline and not args.no_side_legs:
         # BASELINE's other kernel configurations beside the headline, each with its dominant kernel's live roofline
         progress("CSE leg (java relation attention, B=64)")

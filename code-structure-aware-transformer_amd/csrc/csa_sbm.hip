@@ -1193,8 +1193,9 @@ __device__ __forceinline__ void attn_fwd_item(const KArgs& p, float* __restrict_
   // the tile's bit words out, its sampled edges counted
   auto store_bits = [&](int j0_) {
     if constexpr (!DENSE) {
-      if (h == 0) abp[j0_] = myA;
-      if (j0_ + c < p.M) cntl += __popc(myA & qmask);  // sampled edges inside [0,N) x [0,M)
+      const uint32_t aw = j0_ + c < p.M ? myA : 0u;  // keys past M: no sampled edge (k_attn_bwd_qg reads dead tiles' words)
+      if (h == 0) abp[j0_] = aw;
+      cntl += __popc(aw & qmask);  // sampled edges inside [0,N) x [0,M)
     }
     if constexpr (DROP) if (h == 0) rbp[j0_] = myR;
   };
@@ -1831,6 +1832,19 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 8) ? 4 : 2) void k_attn_bwd_
       if constexpr (!DENSE && !W1) gv[r] = tb[p.gplane + kt * 1024 + 32 * crow(r, h)];
     }
   };
+  // W1, a fully masked key tile: k_attn_bwd_kv stores no w tile for it (w = dM P = 0 on every element), so the
+  // sampled bits come from the forward's bit words instead (word of key crow(r, h), bit = this lane's query: the
+  // words of registers 4g .. 4g + 3 are keys 8g + 4h + 0..3, one 16-B broadcast load per half-wave), parked in dsv
+  // until the top of the tile's iteration
+  const uint32_t* abw = p.Abits + ((int64_t)bh * p.NQB + qb) * p.Mpad + 4 * h;
+  auto load_bits = [&](int kt) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(abw + kt * 32 + 8 * g);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dsv[4 * g + e] = v[e];
+    }
+  };
   // W1: this lane's rho (k_attn_rowprep) and the STE term; ds is summed unscaled and dQ scaled at the end
   const float rho = W1 ? p.brow[(((int64_t)bh * p.NQB + qb) * 32 + c) * 4 + 3] : 0.f;
   const float csp = (W1 && p.dsp) ? p.dsp[hd] / ((float)p.B * (float)p.N * (float)p.M) : 0.f;
@@ -1852,18 +1866,27 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 8) ? 4 : 2) void k_attn_bwd_
       asm volatile("" : "+v"(ln));
       const int c = ln & 31, h = (ln >> 5) & 1;
       const bool more = kt + 1 < p.NKB;
-      wait_vm_all();  // tile kt's K / T images and ds / G values have landed
+      wait_vm_all();  // tile kt's K / T images and ds / G values (dead: bit words) have landed
       if constexpr (W1) {  // k_attn_bwd_kv's expressions (W_NO_EDGE)
+        if ((tdead >> kt) & 1ull) {  // STE term only: G = A ? hardtanh(csp) : 0
   #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const bool a = __float_as_uint(dsv[r]) != W_NO_EDGE;
-          const float w = a ? dsv[r] : 0.f;
-          gv[r] = a ? __builtin_amdgcn_fmed3f(w + csp, -1.f, 1.f) : 0.f;
-          dsv[r] = w;
-        }
-        if (rho != 0.f) {  // rare: a degenerate row (n < eps) also takes -rho P from the second plane
+          for (int r = 0; r < 16; ++r) {
+            const bool a = (__float_as_uint(dsv[r]) >> c) & 1u;  // (the forward stores no bit for keys past M)
+            gv[r] = a ? __builtin_amdgcn_fmed3f(0.f + csp, -1.f, 1.f) : 0.f;
+            dsv[r] = 0.f;
+          }
+        } else {
   #pragma unroll
-          for (int r = 0; r < 16; ++r) dsv[r] = fmaf(-rho, tb[p.gplane + kt * 1024 + 32 * crow(r, h)], dsv[r]);
+          for (int r = 0; r < 16; ++r) {
+            const bool a = __float_as_uint(dsv[r]) != W_NO_EDGE;
+            const float w = a ? dsv[r] : 0.f;
+            gv[r] = a ? __builtin_amdgcn_fmed3f(w + csp, -1.f, 1.f) : 0.f;
+            dsv[r] = w;
+          }
+          if (rho != 0.f) {  // rare: a degenerate row (n < eps) also takes -rho P from the second plane
+  #pragma unroll
+            for (int r = 0; r < 16; ++r) dsv[r] = fmaf(-rho, tb[p.gplane + kt * 1024 + 32 * crow(r, h)], dsv[r]);
+          }
         }
       }
       // dQ^T += K^T ds^T (lane d holds K[key crow(r,h)][d], read from the SW_COL / padded image per K-step)
@@ -1905,10 +1928,12 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 8) ? 4 : 2) void k_attn_bwd_
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if ((tdead >> (kt + 1)) & 1ull) {
           if constexpr (!DENSE) dma_narrow(Tl, tr, kt * 32 + 32, KPN);
+          if constexpr (W1) load_bits(kt + 1);
+          else load_tile(kt + 1);
         } else {
           CSA_ISSUE_BQ(kt * 32 + 32);
+          load_tile(kt + 1);
         }
-        load_tile(kt + 1);
       }
     }
   } else {
@@ -1918,18 +1943,27 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 8) ? 4 : 2) void k_attn_bwd_
       asm volatile("" : "+v"(ln));
       const int c = ln & 31, h = (ln >> 5) & 1;
       const bool more = kt + 1 < p.NKB;
-      wait_vm_all();  // tile kt's K / T images and ds / G values have landed
+      wait_vm_all();  // tile kt's K / T images and ds / G values (dead: bit words) have landed
       if constexpr (W1) {  // k_attn_bwd_kv's expressions (W_NO_EDGE)
+        if ((tdead >> kt) & 1ull) {  // STE term only: G = A ? hardtanh(csp) : 0
   #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const bool a = __float_as_uint(dsv[r]) != W_NO_EDGE;
-          const float w = a ? dsv[r] : 0.f;
-          gv[r] = a ? __builtin_amdgcn_fmed3f(w + csp, -1.f, 1.f) : 0.f;
-          dsv[r] = w;
-        }
-        if (rho != 0.f) {  // rare: a degenerate row (n < eps) also takes -rho P from the second plane
+          for (int r = 0; r < 16; ++r) {
+            const bool a = (__float_as_uint(dsv[r]) >> c) & 1u;  // (the forward stores no bit for keys past M)
+            gv[r] = a ? __builtin_amdgcn_fmed3f(0.f + csp, -1.f, 1.f) : 0.f;
+            dsv[r] = 0.f;
+          }
+        } else {
   #pragma unroll
-          for (int r = 0; r < 16; ++r) dsv[r] = fmaf(-rho, tb[p.gplane + kt * 1024 + 32 * crow(r, h)], dsv[r]);
+          for (int r = 0; r < 16; ++r) {
+            const bool a = __float_as_uint(dsv[r]) != W_NO_EDGE;
+            const float w = a ? dsv[r] : 0.f;
+            gv[r] = a ? __builtin_amdgcn_fmed3f(w + csp, -1.f, 1.f) : 0.f;
+            dsv[r] = w;
+          }
+          if (rho != 0.f) {  // rare: a degenerate row (n < eps) also takes -rho P from the second plane
+  #pragma unroll
+            for (int r = 0; r < 16; ++r) dsv[r] = fmaf(-rho, tb[p.gplane + kt * 1024 + 32 * crow(r, h)], dsv[r]);
+          }
         }
       }
       // dQ^T += K^T ds^T (lane d holds K[key crow(r,h)][d], read from the SW_COL / padded image per K-step)
@@ -1971,10 +2005,12 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 8) ? 4 : 2) void k_attn_bwd_
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if ((tdead >> (kt + 1)) & 1ull) {
           if constexpr (!DENSE) dma_narrow(Tl, tr, kt * 32 + 32, KPN);
+          if constexpr (W1) load_bits(kt + 1);
+          else load_tile(kt + 1);
         } else {
           CSA_ISSUE_BQ(kt * 32 + 32);
+          load_tile(kt + 1);
         }
-        load_tile(kt + 1);
       }
     }
   }
@@ -2079,76 +2115,88 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
 #pragma unroll
   for (int t = 0; t < KTA; ++t) dtt[t] = zero16();
   // A key block whose every key is masked (padded ASTs, sbm_attn.py:61): P = 0 on all its elements, so dK = dV = 0
-  // and its only gradient is the STE term G = A ? hardtanh(csp (+ dgraph)) : 0 (STE.py:17-19), into dT here and, via
-  // its w tiles (w = 0 on every edge), into the query side's dQh. Key block 0 always runs the full loop (with FG it
-  // forms the row constants the query side reads).
+  // and its only gradient is the STE term G = A ? hardtanh(csp (+ dgraph)) : 0 (STE.py:17-19), into dT here and into
+  // the query side's dQh, which in the one-plane format reads the tile's A bits from the forward's bit words (no w
+  // tile is stored: those stores, a partial line per lane, cost more than the full loop, profiles/r06_dead_kv.txt).
+  // Key block 0 always runs the full loop (with FG it forms the row constants the query side reads).
   bool dead = false;
-  if (mk && kbi > 0) {
+  if (mk && kbi > 0 && p.NKB <= 64) {  // (the forward's dead-tile record, which k_attn_bwd_qg reads, spans 64 tiles)
     wait_vm_all();
     dead = __builtin_amdgcn_ballot_w64(jv && mval == 0.f) == 0;
   }
   if (dead) {
-    for (int qb = 0; qb < p.NQB; ++qb) {
-      const int i0 = qb * 32;
-      wait_vm_all();  // query block qb's Qh image and bit words have landed
-      const float csp = dspv / ((float)p.B * (float)p.N * (float)p.M);
-      const uint32_t qvm = p.N - i0 >= 32 ? 0xffffffffu : (1u << (p.N - i0)) - 1u;
-      const uint32_t wAs = (wAn & qvm & kvm) >> (4 * h);
-      if (qb + 1 < p.NQB) {
-        if constexpr (!DENSE) wAn = p.Abits[wcol + (int64_t)(qb + 1) * p.Mpad];
-      }
+    // Latency-bound otherwise (a round trip per query block, nothing to hide it under): the Qh images and bit words
+    // of up to CH query blocks are fetched together into the free Q / dX / Qh image space, then processed with no
+    // wait in between (the prologue's loads have landed: the wait above).
+    constexpr int CH0 = (int)((SH::KS) / SH::NIMG), CH = CH0 < 8 ? CH0 : 8;
+    const float csp = dspv / ((float)p.B * (float)p.N * (float)p.M);
+    for (int q0 = 0; q0 < p.NQB; q0 += CH) {
+      const int nq = imin(CH, p.NQB - q0);
+      uint32_t wA[CH];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the previous chunk's images read out
 #pragma unroll
-      for (int half = 0; half < 2; ++half) {
-        float gv[8], wv[8];
-#pragma unroll
-        for (int rr = 0; rr < 8; ++rr) {
-          const int r = 8 * half + rr;
-          const bool a = !DENSE && ((wAs >> crow(r, 0)) & 1u);
-          float cg = csp;
-          if constexpr (DG) {
-            const int ii = i0 + crow(r, h);
-            const int64_t me = ((int64_t)bh * p.N + imin(ii, p.N - 1)) * p.M + jc;
-            if (p.dgraph) cg += ldz(p.dgraph, me, INT64_MAX, (ii < p.N) && jv);
-          }
-          gv[rr] = a ? __builtin_amdgcn_fmed3f(0.f + cg, -1.f, 1.f) : 0.f;  // w = dM P = 0
-          wv[rr] = __uint_as_float(a ? 0u : W_NO_EDGE);
-        }
-        if constexpr (HO) {
-          float* const w = dsw + (int64_t)qb * p.NKB * 1024 + 16 * half;
-          const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-          if constexpr (W1) {  // w tiles, and P = 0 in the second plane (read for rows with rho != 0)
-            __builtin_nontemporal_store((f32x4{wv[0], wv[1], wv[2], wv[3]}), reinterpret_cast<f32x4*>(w));
-            __builtin_nontemporal_store((f32x4{wv[4], wv[5], wv[6], wv[7]}), reinterpret_cast<f32x4*>(w + 8));
-            __builtin_nontemporal_store(z, reinterpret_cast<f32x4*>(w + p.gplane));
-            __builtin_nontemporal_store(z, reinterpret_cast<f32x4*>(w + p.gplane + 8));
-          } else {  // two planes: ds = 0, G
-            __builtin_nontemporal_store(z, reinterpret_cast<f32x4*>(w));
-            __builtin_nontemporal_store(z, reinterpret_cast<f32x4*>(w + 8));
-            if constexpr (!DENSE) {
-              __builtin_nontemporal_store((f32x4{gv[0], gv[1], gv[2], gv[3]}), reinterpret_cast<f32x4*>(w + p.gplane));
-              __builtin_nontemporal_store((f32x4{gv[4], gv[5], gv[6], gv[7]}),
-                                          reinterpret_cast<f32x4*>(w + p.gplane + 8));
-            }
+      for (int u = 0; u < CH; ++u)
+        if (u < nq) {
+          if constexpr (!DENSE) {
+            dma_narrow(L0 + u * SH::NIMG, hr_, (q0 + u) * 32, KPN);
+            wA[u] = p.Abits[wcol + (int64_t)(q0 + u) * p.Mpad];
+          } else {
+            wA[u] = 0u;
           }
         }
-        if constexpr (MB4) {
+      wait_vm_all();
 #pragma unroll
-          for (int rr = 0; rr < 8; ++rr)
-            dtt[0] = mfma4b(lds_f1(lds, SH::KH + narrow_elem(crow(8 * half + rr, h), c & 15, KPN)), gv[rr], dtt[0]);
-        } else if constexpr (!DENSE) {
+      for (int u = 0; u < CH; ++u) {
+        if (u >= nq) break;
+        const int qb = q0 + u, i0 = qb * 32;
+        const int hb = u * SH::NIMG;  // this block's Qh image
+        const uint32_t qvm = p.N - i0 >= 32 ? 0xffffffffu : (1u << (p.N - i0)) - 1u;
+        const uint32_t wAs = (wA[u] & qvm & kvm) >> (4 * h);
 #pragma unroll
-          for (int at = 0; at < KTA; ++at)
+        for (int half = 0; half < 2; ++half) {
+          float gv[8];
 #pragma unroll
-            for (int rr = 0; rr < 8; ++rr) {
-              const int r = 8 * half + rr;
-              const float v = lds_f1(lds, SH::KH + narrow_elem(crow(r, h), imin(32 * at + c, KP - 1), KPN));
-              dtt[at] = mfma((KP >= 32 || c < KP) ? v : 0.f, gv[rr], dtt[at]);
+          for (int rr = 0; rr < 8; ++rr) {
+            const int r = 8 * half + rr;
+            const bool a = !DENSE && ((wAs >> crow(r, 0)) & 1u);
+            float cg = csp;
+            if constexpr (DG) {
+              const int ii = i0 + crow(r, h);
+              const int64_t me = ((int64_t)bh * p.N + imin(ii, p.N - 1)) * p.M + jc;
+              if (p.dgraph) cg += ldz(p.dgraph, me, INT64_MAX, (ii < p.N) && jv);
             }
+            gv[rr] = a ? __builtin_amdgcn_fmed3f(0.f + cg, -1.f, 1.f) : 0.f;  // w = dM P = 0
+          }
+          // one-plane format (W1): no w tile at all, k_attn_bwd_qg reads the tile's bits from the forward's words
+          // (its tdead record); two planes: ds = 0 and G
+          if constexpr (HO && !W1) {
+            float* const w = dsw + (int64_t)qb * p.NKB * 1024 + 16 * half;
+            const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+            {
+              __builtin_nontemporal_store(z, reinterpret_cast<f32x4*>(w));
+              __builtin_nontemporal_store(z, reinterpret_cast<f32x4*>(w + 8));
+              if constexpr (!DENSE) {
+                __builtin_nontemporal_store((f32x4{gv[0], gv[1], gv[2], gv[3]}), reinterpret_cast<f32x4*>(w + p.gplane));
+                __builtin_nontemporal_store((f32x4{gv[4], gv[5], gv[6], gv[7]}),
+                                            reinterpret_cast<f32x4*>(w + p.gplane + 8));
+              }
+            }
+          }
+          if constexpr (MB4) {
+#pragma unroll
+            for (int rr = 0; rr < 8; ++rr)
+              dtt[0] = mfma4b(lds_f1(lds, hb + narrow_elem(crow(8 * half + rr, h), c & 15, KPN)), gv[rr], dtt[0]);
+          } else if constexpr (!DENSE) {
+#pragma unroll
+            for (int at = 0; at < KTA; ++at)
+#pragma unroll
+              for (int rr = 0; rr < 8; ++rr) {
+                const int r = 8 * half + rr;
+                const float v = lds_f1(lds, hb + narrow_elem(crow(r, h), imin(32 * at + c, KP - 1), KPN));
+                dtt[at] = mfma((KP >= 32 || c < KP) ? v : 0.f, gv[rr], dtt[at]);
+              }
+          }
         }
-      }
-      if (qb + 1 < p.NQB) {  // the Qh image read out: the next block's
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if constexpr (!DENSE) dma_narrow(Hl, hr_, i0 + 32, KPN);
       }
     }
   }

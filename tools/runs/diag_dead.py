@@ -10,7 +10,7 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 
 dev = torch.device("cuda", 0)
-for n in (150, 128, 96, 64, 150, 128, 96, 64):
+for n in [int(x) for x in os.environ.get("DIAG_NS", "150,128,96,64,150,128,96,64").split(",")]:
     bench.padded_lengths = lambda B, N, rank, n=n: torch.full((B,), n, dtype=torch.long)
     L = bench.measure_layer(1, 0, dev, 10, 3, 256, 150, 64, 10, False, "fp32", False, "torch", padded=True)
     print(n, {k: round(v, 4) for k, v in L["stage_ms"].items()}, flush=True)
