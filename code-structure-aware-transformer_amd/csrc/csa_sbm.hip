@@ -1142,7 +1142,7 @@ __device__ __forceinline__ void attn_fwd_item(const KArgs& p, float* __restrict_
   const bool tmask = p.NKB <= 64;
   int kt = 0;
   // Philox words of tile kt (they depend only on (query, tile, head))
-  auto philox_tile = [&](int kt_, u32x4 (&r_ste)[2], u32x4 (&r_drop)[2]) {
+  auto philox_tile = [&](int kt_, u32x4 (&r_ste)[2], u32x4 (&r_drop)[2], bool with_drop = true) {
     uint32_t sk0 = p.seed_lo, sk1 = p.seed_hi;  // opaque per tile: round keys are not held across the loop
     asm volatile("" : "+s"(sk0), "+s"(sk1));
 #pragma unroll
@@ -1150,16 +1150,17 @@ __device__ __forceinline__ void attn_fwd_item(const KArgs& p, float* __restrict_
       if constexpr (!DENSE && !HAS_U)
         r_ste[gp] = philox4x32(u32x4{(uint32_t)i, (uint32_t)(8 * kt_ + 4 * gp + h), ctr_bh, ctr_ste}, sk0, sk1);
       if constexpr (DROP)
-        r_drop[gp] = philox4x32(u32x4{(uint32_t)i, (uint32_t)(8 * kt_ + 4 * gp + h), ctr_bh, ctr_drop}, sk0, sk1);
+        if (with_drop)
+          r_drop[gp] = philox4x32(u32x4{(uint32_t)i, (uint32_t)(8 * kt_ + 4 * gp + h), ctr_bh, ctr_drop}, sk0, sk1);
     }
   };
   // expA^T = T Qh^T (sbm_attn.py:55) of the tile in the T image
-  auto echain = [&]() {
+  auto echain = [&](int toff) {  // toff: the T image's offset from LY::TOFF (a dead-tile slot)
     f32x16 eacc = zero16();
     if constexpr (!DENSE) {
 #pragma unroll
       for (int j = 0; j < KPH / 4; ++j) {
-        const f32x4 tv = lds_f4(lds, tbase ^ (16 * j));
+        const f32x4 tv = lds_f4(lds, (tbase + toff) ^ (16 * j));
 #pragma unroll
         for (int e = 0; e < 4; ++e) eacc = mfma(tv[e], qh[4 * j + e], eacc);
       }
@@ -1191,30 +1192,27 @@ __device__ __forceinline__ void attn_fwd_item(const KArgs& p, float* __restrict_
       for (int r = 0; r < 16; ++r) keep[r] = u16_of(r_drop[r >> 3], r & 7) >= drop_thr;
   };
   // the tile's bit words out, its sampled edges counted
-  auto store_bits = [&](int j0_) {
+  auto store_abits = [&](int j0_) {
     if constexpr (!DENSE) {
       const uint32_t aw = j0_ + c < p.M ? myA : 0u;  // keys past M: no sampled edge (k_attn_bwd_qg reads dead tiles' words)
       if (h == 0) abp[j0_] = aw;
       cntl += __popc(aw & qmask);  // sampled edges inside [0,N) x [0,M)
     }
+  };
+  auto store_bits = [&](int j0_) {
+    store_abits(j0_);
     if constexpr (DROP) if (h == 0) rbp[j0_] = myR;
   };
-  // the tile after the current one in processing order (-1: none), taken off the remaining sets
-  auto pop_next = [&](int kt_) {
+  // the live tile after the current one (-1: none), taken off the remaining set
+  auto next_live = [&](int kt_) {
     if (!tmask) return kt_ + 1 < p.NKB ? kt_ + 1 : -1;
     if (rem_live) {
       const int nx = __builtin_ctzll(rem_live);
       rem_live &= rem_live - 1;
       return nx;
     }
-    if (rem_dead) {
-      const int nx = __builtin_ctzll(rem_dead);
-      rem_dead &= rem_dead - 1;
-      return nx;
-    }
     return -1;
   };
-  auto is_live = [&](int kt_) { return !tmask || !((dead >> kt_) & 1ull); };
   for (int idx = 0; idx < p.NKB; ++idx) {
     wait_vm_all();  // tile kt's K/V/T images (at idx = 0 also the query operands) have landed
     if (idx == 0) {
@@ -1238,8 +1236,7 @@ __device__ __forceinline__ void attn_fwd_item(const KArgs& p, float* __restrict_
     const int j0 = kt * 32;
     u32x4 r_ste[2], r_drop[2];
     float w[16];
-    myA = myR = 0u;
-    if (is_live(kt)) {
+    {
       // the tile's Philox words depend only on (query, tile, head): computed first, so their VALU work can
       // interleave with the S / expA MFMA chains below instead of waiting behind them
       philox_tile(kt, r_ste, r_drop);
@@ -1260,7 +1257,7 @@ __device__ __forceinline__ void attn_fwd_item(const KArgs& p, float* __restrict_
           for (int e = 0; e < 4; ++e) sacc = mfma(kv[e], q[4 * j + e], sacc);
         }
       }
-      const f32x16 eacc = echain();
+      const f32x16 eacc = echain(0);
       // V^T operand values for this tile's PV: lane (d = 32t + c) reads V[key crow(r,h)][d]
       float vt[DT][16];
 #pragma unroll
@@ -1272,11 +1269,8 @@ __device__ __forceinline__ void attn_fwd_item(const KArgs& p, float* __restrict_
       for (int g = 0; g < 4; ++g) bz[g] = lds_f4(lds, LY::BOFF + 4 * (j0 + 8 * g + 4 * h));
       // all of tile kt is in registers: start the next tile's DMA (overlaps the softmax and PV below)
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      const int nx = pop_next(kt);
-      if (nx >= 0) {
-        if (is_live(nx)) CSA_ISSUE_FWD(nx * 32);
-        else if constexpr (!DENSE) dma_narrow(Tl, tr, nx * 32, KPN);
-      }
+      const int nx = next_live(kt);
+      if (nx >= 0) CSA_ISSUE_FWD(nx * 32);
       float s[16];
       float tmax = NEG_INF;
 #pragma unroll
@@ -1323,20 +1317,42 @@ __device__ __forceinline__ void attn_fwd_item(const KArgs& p, float* __restrict_
 #pragma unroll
           for (int r = 0; r < 16; ++r) o[t] = mfma(vt[t][r], w[r], o[t]);
       }
+      if (nx < 0) break;
       kt = nx;
-    } else {  // every key of the tile masked: P = 0, so no softmax / PV work; sampling and bit words only
-      philox_tile(kt, r_ste, r_drop);
-      const f32x16 eacc = echain();
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      const int nx = pop_next(kt);  // (a dead tile: the ones after it are dead too)
-      if constexpr (!DENSE)
-        if (nx >= 0) dma_narrow(Tl, tr, nx * 32, KPN);
-      bool av[16], keep[16];
-      sample_all(j0, eacc, r_ste, r_drop, av, keep);
-      if constexpr (!DENSE) myA = pack_bits(av);
-      if constexpr (DROP) myR = pack_bits(keep);
-      store_bits(j0);
-      kt = nx;
+    }
+  }
+  // Dead tiles (every key masked, after the live ones): P = 0, so no softmax / PV work, and no dropout bits (nothing
+  // reads the keep bits of a masked key); expA, the STE draws and the graph's bit words only. Their T images come in
+  // chunks of up to DCH into the free K / V / T image space, with one wait per chunk: one tile at a time, each tile
+  // would wait out a memory round trip for a few hundred cycles of work.
+  if constexpr (!DENSE) {
+    constexpr int DCH0 = (LY::TOFF + LY::T_BYTES - LY::KOFF) / LY::T_BYTES, DCH = DCH0 < 8 ? DCH0 : 8;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    while (rem_dead) {
+      int kts[DCH];
+#pragma unroll
+      for (int u = 0; u < DCH; ++u) {
+        kts[u] = -1;
+        if (rem_dead) {
+          kts[u] = __builtin_ctzll(rem_dead);
+          rem_dead &= rem_dead - 1;
+          dma_narrow(Kl + u * LY::T_BYTES, tr, kts[u] * 32, KPN);
+        }
+      }
+      wait_vm_all();
+#pragma unroll
+      for (int u = 0; u < DCH; ++u) {
+        if (kts[u] < 0) break;
+        const int j0 = kts[u] * 32;
+        u32x4 r_ste[2], r_drop[2];
+        philox_tile(kts[u], r_ste, r_drop, false);
+        const f32x16 eacc = echain(u * LY::T_BYTES - LY::TOFF);
+        bool av[16], keep[16];
+        sample_all(j0, eacc, r_ste, r_drop, av, keep);
+        myA = pack_bits(av);
+        store_abits(j0);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the chunk's images read out before the next one lands
     }
   }
   const float Z = xhalf_sum(zp), Zg = xhalf_sum(zgp);
