@@ -131,7 +131,7 @@ Layout make_layout(int64_t B, int64_t H, int64_t N, int64_t M, int64_t D, int64_
   L.stats = take(sizeof(float) * B * H * N * 4);
   L.Abits = take(sizeof(uint32_t) * B * H * L.NQB * L.Mpad);
   L.Rbits = take(sizeof(uint32_t) * B * H * L.NQB * L.Mpad);
-  L.cnt = take(sizeof(unsigned long long) * H);
+  L.cnt = take(sizeof(uint32_t) * B * H * L.NQB);  // per (b,h, query block): sampled edges (k_attn_fwd)
   L.tdead = take(sizeof(unsigned long long) * B);  // per AST: key tiles whose every key is masked (bit kt)
   for (int l = 0; l < 3; ++l) L.Wf[l] = take(sizeof(float) * (dense ? 0 : D * D));
   for (int l = 0; l < 3; ++l) L.WfT[l] = take(sizeof(float) * (dense ? 0 : D * D));
@@ -300,7 +300,7 @@ __device__ __forceinline__ void frag_elem(const FragJob& J, int64_t e) {
 // [nS, n), which do not depend on S, grid-stride.
 template <int MAXE>
 __global__ __launch_bounds__(256) void k_prep(const float* __restrict__ C, float* __restrict__ S, int k, int D, int KP32,
-                                              unsigned long long* __restrict__ cnt, int H, const FragJobs jobs, int nS) {
+                                              int H, const FragJobs jobs, int nS) {
   if ((int)blockIdx.x >= H) {
     const int64_t t0 = (int64_t)(blockIdx.x - H) * 256 + threadIdx.x, stride = (int64_t)(gridDim.x - H) * 256;
     for (int j = nS; j < jobs.n; ++j) {
@@ -313,7 +313,6 @@ __global__ __launch_bounds__(256) void k_prep(const float* __restrict__ C, float
   // C_h (k x D <= 128 x 96) staged in LDS; each thread keeps its (up to MAXE) logits in registers
   // across the max / sum / normalise passes (one dot product per entry instead of three).
   const int hd = blockIdx.x, tid = threadIdx.x;
-  if (hd == 0 && tid < H) cnt[tid] = 0ull;  // this call's edge counters (k_attn_fwd) start at zero
   // rows padded to D + 1 floats: consecutive threads read consecutive rows b, which then sit in
   // different banks (an unpadded stride of D = 64 put every thread of a wave on one bank)
   __shared__ float Cs[128 * 97];
@@ -386,7 +385,7 @@ struct KArgs {
   const float *Wf[3], *WfT[3], *Cf, *CfT, *Sf, *SfT, *S;
   float *Qh, *Kh, *T, *stats, *Act;  // Act NULL for CSA_FLAG_FWD_ONLY (no activation blocks saved)
   uint32_t *Abits, *Rbits;
-  unsigned long long* cnt;
+  uint32_t* cnt;  // per (b,h, query block) sampled-edge counts, summed per head by k_sparsity_finish
   unsigned long long* tdead;  // per AST: fully masked key tiles (k_attn_fwd; bit 0 never set), NKB <= 64
   const float* U;
   uint32_t seed_lo, seed_hi, off;
@@ -1384,7 +1383,10 @@ __device__ __forceinline__ void attn_fwd_item(const KArgs& p, float* __restrict_
     cntl = (h == 0) ? cntl : 0u;
 #pragma unroll
     for (int o2 = 32; o2 >= 1; o2 >>= 1) cntl += __shfl_xor(cntl, o2, 64);
-    if (lane == 0 && cntl) atomicAdd(p.cnt + hd, (unsigned long long)cntl);
+    // one plain store per wave, summed by k_sparsity_finish (10240 atomic adds on the 8 counters of one cache line
+    // serialised in that L2 channel: 11 us of the headline forward, 64 us with 4 of 5 key tiles masked,
+    // profiles/r06_ab_sparsity_atomic.txt)
+    if (lane == 0) p.cnt[(int64_t)bh * p.NQB + qb] = cntl;
   }
 }
 
@@ -1396,9 +1398,18 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_fwd
   attn_fwd_item<D, KPH, DENSE, HAS_U, DROP, BF>(p, lds, xb.bh, xb.blk, true);
 }
 
-__global__ void k_sparsity_finish(const unsigned long long* __restrict__ cnt, float* __restrict__ sp, int H, float bnm) {
-  const int t = threadIdx.x;
-  if (t < H) sp[t] = (float)cnt[t] / bnm;  // torch.sum(graph)/(b*n*m), exact integer count (sbm_attn.py:64)
+// one workgroup per head: the head's B * NQB per-wave counts summed exactly (integers: any order gives the same total)
+__global__ __launch_bounds__(256) void k_sparsity_finish(const uint32_t* __restrict__ cnt, float* __restrict__ sp,
+                                                         int H, int B, int NQB, float bnm) {
+  __shared__ unsigned long long red[4];
+  const int hd = blockIdx.x, t = threadIdx.x;
+  unsigned long long s = 0;
+  for (int e = t; e < B * NQB; e += 256) s += cnt[((int64_t)(e / NQB) * H + hd) * NQB + e % NQB];
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+  if ((t & 63) == 0) red[t >> 6] = s;
+  __syncthreads();
+  if (t == 0) sp[hd] = (float)((red[0] + red[1]) + (red[2] + red[3])) / bnm;  // torch.sum(graph)/(b*n*m), sbm_attn.py:64
 }
 
 // ------------------------------------------------------------------------------------
@@ -3567,7 +3578,7 @@ KArgs make_kargs(const csa_sbm_fwd_args* a, const Layout& L) {
   p.stats = (float*)((char*)st + L.stats);
   p.Act = (a->flags & CSA_FLAG_FWD_ONLY) ? nullptr : (float*)((char*)st + L.Act);
   p.Abits = (uint32_t*)((char*)st + L.Abits); p.Rbits = (uint32_t*)((char*)st + L.Rbits);
-  p.cnt = (unsigned long long*)((char*)st + L.cnt);
+  p.cnt = (uint32_t*)((char*)st + L.cnt);
   p.tdead = (unsigned long long*)((char*)st + L.tdead);
   p.U = a->uniforms;
   p.seed_lo = (uint32_t)a->seed; p.seed_hi = (uint32_t)(a->seed >> 32); p.off = (uint32_t)a->offset;
@@ -3675,7 +3686,7 @@ csa_status launch_fwd(const csa_sbm_fwd_args* a, const Layout& L, hipStream_t st
     J.n = n;
     const int kk = (int)(a->k * a->k);
     auto prep = kk <= 256 ? k_prep<1> : kk <= 1024 ? k_prep<4> : kk <= 4096 ? k_prep<16> : k_prep<64>;
-    hipLaunchKernelGGL(prep, dim3((unsigned)a->H + 128), dim3(256), 0, st, a->cluster_w, S, (int)a->k, D, KP32, p.cnt,
+    hipLaunchKernelGGL(prep, dim3((unsigned)a->H + 128), dim3(256), 0, st, a->cluster_w, S, (int)a->k, D, KP32,
                        (int)a->H, J, nS);
     }
     {
@@ -3710,8 +3721,8 @@ csa_status launch_fwd(const csa_sbm_fwd_args* a, const Layout& L, hipStream_t st
       Stage sg(a->prof, CSA_STAGE_ATTN_FWD, st);
       launch_attn_fwd_any<D, KPH, false>(p, BH, L, a->uniforms != nullptr, a->attn_dropout > 0.f, st);
     }
-    hipLaunchKernelGGL(k_sparsity_finish, dim3(1), dim3(64), 0, st, (const unsigned long long*)p.cnt, a->sparsity,
-                       (int)a->H, (float)a->B * (float)a->N * (float)a->M);
+    hipLaunchKernelGGL(k_sparsity_finish, dim3((unsigned)a->H), dim3(256), 0, st, (const uint32_t*)p.cnt, a->sparsity,
+                       (int)a->H, (int)a->B, (int)L.NQB, (float)a->B * (float)a->N * (float)a->M);
   } else {
     Stage sg(a->prof, CSA_STAGE_ATTN_FWD, st);
     launch_attn_fwd_any<D, 0, true>(p, BH, L, false, a->attn_dropout > 0.f, st);
