@@ -2350,15 +2350,18 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
           gv[rr] = a ? __builtin_amdgcn_fmed3f(fmaf(dM, P, cg), -1.f, 1.f) : 0.f;  // STE.py:19 hardtanh(A * grad)
         }
         awv[rr] = (a && kp) ? P * rec[1] : 0.f;  // dropout(attn) weight for dV
-        if constexpr (W1) {  // stored as soon as four are ready (fewer live registers); non-temporal, see below
+        if constexpr (W1) {  // stored as soon as four are ready (fewer live registers); plain stores, see below
           if ((rr & 3) == 3)
-            __builtin_nontemporal_store((f32x4{wv[0], wv[1], wv[2], wv[3]}), reinterpret_cast<f32x4*>(wst + 2 * (rr & 4)));
+            *reinterpret_cast<f32x4*>(wst + 2 * (rr & 4)) = f32x4{wv[0], wv[1], wv[2], wv[3]};
         }
       }
       if constexpr (HO) {  // queries 16 half + 4 h + (0..3) and + 8: two f32x4 per tile, for ds and for G
         float* const w = wst;
-        // non-temporal: the tiles are read once, by the next kernel (same-box A/B: k_attn_bwd_qg 157 -> 134 us)
-#define CSA_ST4(ptr, val) __builtin_nontemporal_store((val), reinterpret_cast<f32x4*>(ptr))
+        // Plain (write-back) stores: a lane writes 16 B of its key's 128-B tile row per instruction, so a row is
+        // completed by four instructions; non-temporal stores sent each 32-B piece on its own (round 6, same box:
+        // k_attn_bwd_kv 356 -> 345 us, k_attn_bwd_qg unchanged, profiles/r06_ab_wtile_store.txt; round 4 had measured
+        // non-temporal stores faster for the two-plane tiles, k_attn_bwd_qg 157 -> 134 us, before the one-plane format)
+#define CSA_ST4(ptr, val) (*reinterpret_cast<f32x4*>(ptr) = (val))
         if constexpr (W1) {  // (the w values are stored in the elementwise loop)
           if (rho_any) {  // rare (a degenerate row): P of the half's elements, recomputed, into the second plane
             float pv[8];
