@@ -524,13 +524,14 @@ def _dead_tile_masks(B, N):
 
 
 @pytest.mark.skipif(not has_gpu(), reason="needs GPU")
-@pytest.mark.parametrize("shape", [(6, 2, 150, 64, 10), (6, 2, 100, 96, 16), (6, 1, 300, 64, 64)])
+@pytest.mark.parametrize("shape", [(6, 2, 150, 64, 10), (6, 2, 100, 96, 16), (6, 1, 300, 64, 64), (2, 1, 2080, 64, 10)])
 def test_sbm_dead_key_tiles_match_oracle(shape):
-    """Key tiles whose every key is masked run the light paths (forward: expA, sampling and bit words only;
-    k_attn_bwd_kv: a whole masked key block carries only the STE term into dT and its w tiles; k_attn_bwd_qg: no dQ
-    products for a dead tile). The sampled graph (padded positions included, sbm_attn.py:64), the sparsity, X, dQ /
-    dK / dV and every parameter gradient -- dC and the MLP weights take the STE term of the dead tiles' edges --
-    against the fp64 closed form; two runs bitwise identical."""
+    """Key tiles whose every key is masked run the light paths (forward: after the live tiles, expA, sampling and
+    the graph's bit words only; k_attn_bwd_kv: a whole masked key block carries only the STE term into dT and stores
+    no w tiles; k_attn_bwd_qg: no dQ products for a dead tile, its A bits from the forward's words). N = 2080 has 65
+    key tiles, past the 64-tile dead-tile record: every tile runs the full path there. The sampled graph (padded
+    positions included, sbm_attn.py:64), the sparsity, X, dQ / dK / dV and every parameter gradient -- dC and the MLP
+    weights take the STE term of the dead tiles' edges -- against the fp64 closed form; two runs bitwise identical."""
     B, H, N, d, k = shape
     # (seed 97 + N at d = 96, k = 16 put one projection-MLP activation of an unpadded AST within fp32 rounding of
     # the ReLU kink: its K row's dK differs from the fp64 oracle by 1e-3 relative in every build, the round-start one
