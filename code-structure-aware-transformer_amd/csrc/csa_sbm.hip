@@ -2200,12 +2200,11 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
             float* const w = dsw + (int64_t)qb * p.NKB * 1024 + 16 * half;
             const f32x4 z = {0.f, 0.f, 0.f, 0.f};
             {
-              __builtin_nontemporal_store(z, reinterpret_cast<f32x4*>(w));
-              __builtin_nontemporal_store(z, reinterpret_cast<f32x4*>(w + 8));
+              *reinterpret_cast<f32x4*>(w) = z;  // plain stores, as the live tiles' (partial rows per lane)
+              *reinterpret_cast<f32x4*>(w + 8) = z;
               if constexpr (!DENSE) {
-                __builtin_nontemporal_store((f32x4{gv[0], gv[1], gv[2], gv[3]}), reinterpret_cast<f32x4*>(w + p.gplane));
-                __builtin_nontemporal_store((f32x4{gv[4], gv[5], gv[6], gv[7]}),
-                                            reinterpret_cast<f32x4*>(w + p.gplane + 8));
+                *reinterpret_cast<f32x4*>(w + p.gplane) = f32x4{gv[0], gv[1], gv[2], gv[3]};
+                *reinterpret_cast<f32x4*>(w + p.gplane + 8) = f32x4{gv[4], gv[5], gv[6], gv[7]};
               }
             }
           }
