@@ -574,9 +574,9 @@ def test_sbm_dead_key_tiles_parameter_gradients_match_oracle():
 
 @pytest.mark.skipif(not has_gpu(), reason="needs GPU")
 def test_train_mode_dead_key_tiles_match_oracle_with_regenerated_masks():
-    """Train mode (in-kernel Philox draws) over dead key tiles: the light forward still draws the STE uniforms and
-    the keep bits of every tile, so the graph equals the regenerated u16 < clamp(expA) 65536 and every gradient
-    matches the closed form under the regenerated masks."""
+    """Train mode (in-kernel Philox draws) over dead key tiles: the light forward still draws the STE uniforms of
+    every tile (not the keep bits of a dead tile, which nothing reads: its P is 0), so the graph equals the
+    regenerated u16 < clamp(expA) 65536 and every gradient matches the closed form under the regenerated masks."""
     from oracle import philox
     B, H, N, d, k = 6, 2, 150, 64, 10
     Q, K, V, _, _, dX, dsp, params = _rand_case(B, H, N, d, k, seed=4321)
@@ -611,6 +611,35 @@ def test_train_mode_dead_key_tiles_match_oracle_with_regenerated_masks():
              "proj.6.weight", "proj.6.bias"]
     for name, t in zip(names, g):
         np.testing.assert_allclose(t.cpu().numpy(), rg[name].numpy(), rtol=RTOL, atol=ATOL, err_msg=name)
+
+
+@pytest.mark.skipif(not has_gpu(), reason="needs GPU")
+def test_map_gradient_path_over_dead_key_tiles_matches_training_path():
+    """Upstream map gradients select the two-plane ds | G handoff with k_attn_rowprep's row constants; there a dead
+    key block stores ds = 0 and its G tiles for the query side, where the training path stores no tile for it.
+    Zero dgraph / dattn must give the training path's gradients (train mode, dropout, dead tiles)."""
+    B, H, N, d, k = 6, 2, 150, 64, 10
+    Q, K, V, _, _, dX, dsp, params = _rand_case(B, H, N, d, k, seed=777)
+    mask = _dead_tile_masks(B, N)
+    cw = params["layer.weight"].cuda()
+    pw = [params[f"proj.{i}.weight"].cuda() for i in (0, 3, 6)]
+    pb = [params[f"proj.{i}.bias"].cuda() for i in (0, 3, 6)]
+    q, kk, v, mk = Q.cuda(), K.cuda(), V.cuda(), mask.cuda()
+    seed, offset = 0xDEAD5EED, 3
+    X, sp, state = torch.ops.csa.sbm_fwd(q, kk, v, mk, cw, pw, pb, None, k, seed, offset, 0.2, 0.1, False)
+    g0 = torch.ops.csa.sbm_bwd(q, kk, v, mk, cw, pw, pb, k, 0.2, 0.1, seed, offset, False, state, X,
+                               dX.cuda(), dsp.cuda(), None)
+    zeros = torch.zeros(B, H, N, N, device="cuda")
+    g1 = torch.ops.csa.sbm_bwd(q, kk, v, mk, cw, pw, pb, k, 0.2, 0.1, seed, offset, False, state, X,
+                               dX.cuda(), dsp.cuda(), zeros, dattn=zeros)
+    torch.cuda.synchronize()
+    a = [t.cpu() for t in g0 if isinstance(t, torch.Tensor)]
+    b = [t.cpu() for t in g1 if isinstance(t, torch.Tensor)]
+    assert len(a) == len(b) > 0
+    for i, (x, y) in enumerate(zip(a, b)):
+        # the two paths sum gamma = rowsum(dX * X) in different orders: fp32 rounding apart
+        np.testing.assert_allclose(y.numpy(), x.numpy(), rtol=1e-4, atol=1e-5 * max(1.0, float(x.abs().max())),
+                                   err_msg=f"output {i}")
 
 
 @pytest.mark.skipif(not has_gpu(), reason="needs GPU")
