@@ -485,45 +485,55 @@ __host__ __device__ constexpr int tile_pos(int j) { return 16 * ((j >> 2) & 1) +
 // so does RT, whose row y of this block reads the staged column y.
 // Dynamic LDS: rel_prep_lds_bytes(N) = two staged 32 x N byte blocks (64 KB at N = 1024).
 inline size_t rel_prep_lds_bytes(int64_t N) { return 2 * (size_t)((32 * N + 15) / 16 * 16); }
-__global__ __launch_bounds__(256) void k_rel_prep(const RelArgs p, uint16_t* __restrict__ RM, uint16_t* __restrict__ RT) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t srel[];
+// One (32-row block at, plane bp) item on NTH threads (tid < NTH): k_rel_prep runs it on 256, k_rel_logits' extra
+// one-wave workgroups on 64 (the same stores, so the planes are identical either way).
+template <int NTH>
+__device__ __forceinline__ void rel_prep_item(const RelArgs& p, uint16_t* __restrict__ RM, uint16_t* __restrict__ RT,
+                                              uint8_t* srel, int at, int bp, int tid) {
   uint8_t* const smask = srel + (32 * p.N + 15) / 16 * 16;
-  const int NT = p.NP / 32, at = (int)blockIdx.x;
-  const int bp = blockIdx.y, b = bp / p.P_, pl = bp % p.P_;
+  const int NT = p.NP / 32;
+  const int b = bp / p.P_, pl = bp % p.P_;
   const int hd = p.group > 0 ? (pl == 0 ? 0 : p.group) : pl;  // a head that reads plane pl
   const int a0 = at * 32, nrow = imin(32, p.N - a0);
   const uint8_t* rp = p.rel + plane_off(p, b, hd, p.rel_sb, p.rel_sh) + (int64_t)a0 * p.N;
   const uint8_t* mp = p.mask + plane_off(p, b, hd, p.mask_sb, p.mask_sh) + (int64_t)a0 * p.N;
-  const int nbytes = nrow * p.N, t = (int)threadIdx.x;
+  const int nbytes = nrow * p.N;
   if ((((uintptr_t)rp | (uintptr_t)mp | (uintptr_t)nbytes) & 3) == 0) {
-    for (int e = t; e < nbytes / 4; e += 256) {
+    for (int e = tid; e < nbytes / 4; e += NTH) {
       reinterpret_cast<uint32_t*>(srel)[e] = reinterpret_cast<const uint32_t*>(rp)[e];
       reinterpret_cast<uint32_t*>(smask)[e] = reinterpret_cast<const uint32_t*>(mp)[e];
     }
   } else {
-    for (int e = t; e < nbytes; e += 256) { srel[e] = rp[e]; smask[e] = mp[e]; }
+    for (int e = tid; e < nbytes; e += NTH) { srel[e] = rp[e]; smask[e] = mp[e]; }
   }
   __syncthreads();
   uint16_t* rm = RM + (size_t)bp * p.NP * p.NP;
   uint16_t* rt = RT + (size_t)bp * p.NP * p.NP;
-  const int rl = t >> 3, k = t & 7, pos = 16 * (k & 1) + 4 * (k >> 1);
-  const int a = a0 + rl;
   auto code = [&](int row, int col) -> uint32_t {  // staged (row, col) of this block; 0x0100 outside [0,N)^2
     if (row >= nrow || col >= p.N) return 0x0100u;
     int r = srel[row * p.N + col];
     r = r < p.L ? r : p.L - 1;  // memory safety; the reference requires rel < L
     return (uint32_t)r | (smask[row * p.N + col] ? 0x100u : 0u);
   };
-  for (int bt = 0; bt < NT; ++bt) {
-    const int c0 = bt * 32 + 4 * k;
-    // RM row a, columns c0 .. c0 + 3: rel[a][c] | mask[a][c] << 8
-    *reinterpret_cast<uint2*>(rm + (size_t)a * p.NP + bt * 32 + pos) =
-        uint2{code(rl, c0) | (code(rl, c0 + 1) << 16), code(rl, c0 + 2) | (code(rl, c0 + 3) << 16)};
-    // RT row y = bt * 32 + rl, columns a0 + 4 k .. + 3: rel[x][y] of the staged rows x
-    const int y = bt * 32 + rl, x0 = 4 * k;
-    *reinterpret_cast<uint2*>(rt + (size_t)y * p.NP + a0 + pos) =
-        uint2{code(x0, y) | (code(x0 + 1, y) << 16), code(x0 + 2, y) | (code(x0 + 3, y) << 16)};
+  for (int t = tid; t < 256; t += NTH) {  // 32 rows x 8 column groups
+    const int rl = t >> 3, k = t & 7, pos = 16 * (k & 1) + 4 * (k >> 1);
+    const int a = a0 + rl;
+    for (int bt = 0; bt < NT; ++bt) {
+      const int c0 = bt * 32 + 4 * k;
+      // RM row a, columns c0 .. c0 + 3: rel[a][c] | mask[a][c] << 8
+      *reinterpret_cast<uint2*>(rm + (size_t)a * p.NP + bt * 32 + pos) =
+          uint2{code(rl, c0) | (code(rl, c0 + 1) << 16), code(rl, c0 + 2) | (code(rl, c0 + 3) << 16)};
+      // RT row y = bt * 32 + rl, columns a0 + 4 k .. + 3: rel[x][y] of the staged rows x
+      const int y = bt * 32 + rl, x0 = 4 * k;
+      *reinterpret_cast<uint2*>(rt + (size_t)y * p.NP + a0 + pos) =
+          uint2{code(x0, y) | (code(x0 + 1, y) << 16), code(x0 + 2, y) | (code(x0 + 3, y) << 16)};
+    }
   }
+}
+
+__global__ __launch_bounds__(256) void k_rel_prep(const RelArgs p, uint16_t* __restrict__ RM, uint16_t* __restrict__ RT) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t srel[];
+  rel_prep_item<256>(p, RM, RT, srel, (int)blockIdx.x, (int)blockIdx.y, (int)threadIdx.x);
 }
 
 // k_rel_prep for N > 1024 (its staged rows would exceed 64 KB of LDS): one 32 x 32 tile of one plane per workgroup; a thread codes 4 consecutive columns of one row, which
@@ -702,10 +712,16 @@ __device__ __forceinline__ void logits_tile(const RelArgs& p, const float* lds, 
 // other waves of the SIMD (<= 20 per CU by LDS, ~100 VGPRs) cover it, so the grid (2 x ceil(NQB / 2) x B x H
 // waves) runs in one round. Stores are coalesced along the relation index.
 template <int D>
-__global__ __launch_bounds__(64, 4) void k_rel_logits(const RelArgs p, float* __restrict__ c2p, float* __restrict__ p2ct) {
+__global__ __launch_bounds__(64, 4) void k_rel_logits(const RelArgs p, float* __restrict__ c2p, float* __restrict__ p2ct,
+                                                     uint16_t* __restrict__ RM, uint16_t* __restrict__ RT, int nlog) {
   constexpr int NS = D / 2;
   static_assert(D == 64, "fused CSE path is d_k = 64");
   extern __shared__ __attribute__((aligned(16))) float lds[];
+  if ((int)blockIdx.x >= nlog) {  // the relation-plane prep (k_rel_prep's items), one wave each, beside the logits
+    const int it = (int)blockIdx.x - nlog, NT = p.NP / 32;
+    rel_prep_item<64>(p, RM, RT, reinterpret_cast<uint8_t*>(lds), it % NT, it / NT, lane_id());
+    return;
+  }
   const uint32_t L0 = lds_offset(lds);
   const int lane = lane_id(), c = lane & 31, h = lane >> 5;
   const int NRP = (p.NQB + 1) / 2;  // pairs of row blocks
@@ -1864,10 +1880,18 @@ csa_status csa_rel_attn_fwd(const csa_rel_attn_args* a, void* stream) {
   if (R.fused) {
     {
     const RelStage sg(a->prof, CSA_REL_STAGE_LOGITS, st);
-    hipLaunchKernelGGL(k_rel_logits<64>, dim3(xcd_grid(2 * (int)((p.NQB + 1) / 2), (int)(a->B * a->H))), dim3(64),
-                       32 * 64 * 4, st, p, (float*)p.c2p, (float*)p.p2ct);
     const int NT = (int)(R.NP / 32);
-    if (rel_prep_lds_bytes(a->N) <= 65536) {
+    const unsigned nlog = xcd_grid(2 * (int)((p.NQB + 1) / 2), (int)(a->B * a->H));
+    const size_t prep_lds = rel_prep_lds_bytes(a->N);
+    // N <= 256: the prep items ride in the logits launch as extra one-wave workgroups (its LDS then grows to the
+    // staged rows, <= 16 KB, and the logits grid still fits one round); larger N keeps the separate launch
+    const bool merged = prep_lds <= 16384;
+    const size_t logits_lds = merged ? std::max<size_t>(32 * 64 * 4, prep_lds) : 32 * 64 * 4;
+    const unsigned nprep = merged ? (unsigned)(NT * a->B * p.P_) : 0u;
+    hipLaunchKernelGGL(k_rel_logits<64>, dim3(nlog + nprep), dim3(64), logits_lds, st, p, (float*)p.c2p, (float*)p.p2ct,
+                       (uint16_t*)p.RM, (uint16_t*)p.RT, (int)nlog);
+    if (merged) {
+    } else if (prep_lds <= 65536) {
       set_dyn_lds((const void*)k_rel_prep, (int)rel_prep_lds_bytes(a->N));
       hipLaunchKernelGGL(k_rel_prep, dim3((unsigned)NT, (unsigned)(a->B * p.P_)), dim3(256), rel_prep_lds_bytes(a->N),
                          st, p, (uint16_t*)p.RM, (uint16_t*)p.RT);
