@@ -149,13 +149,15 @@ def test_rel_attn_full_size_rows_match_oracle_and_deterministic():
 
 
 @pytest.mark.skipif(not has_gpu(), reason="needs GPU")
-def test_rel_attn_long_ast_tile_prep_matches_oracle():
-    """N = 1040 > 1024: the relation planes are prepared one 32 x 32 tile per workgroup (k_rel_prep_t; at
-    N <= 1024 k_rel_prep stages whole 32-row blocks in LDS, covered by every other test here: dword staging at
-    N = 150, byte staging at N = 37 and 23). Random relation codes and masks in the compact (B,2,N,N) layout;
-    outputs and gradients vs the fp64 oracle."""
+@pytest.mark.parametrize("N", [300, 1040])
+def test_rel_attn_long_ast_tile_prep_matches_oracle(N):
+    """The three relation-plane prep paths: N = 1040 > 1024 prepares one 32 x 32 tile per workgroup
+    (k_rel_prep_t); N = 300 stages whole 32-row blocks in LDS in k_rel_prep's own launch (staged rows > 16 KB); at
+    N <= 256 the same 32-row items run as one-wave workgroups of the logits launch, covered by every other test here
+    (dword staging at N = 150, byte staging at N = 37 and 23). Random relation codes and masks in the compact
+    (B,2,N,N) layout; outputs and gradients vs the fp64 oracle."""
     from oracle import cse_ref
-    B, H, N, dk, L = 1, 8, 1040, 64, 150
+    B, H, dk, L = 1, 8, 64, 150
     g = torch.Generator().manual_seed(21)
     Lr, Tr = (torch.randint(0, L, (B, N, N), generator=g, dtype=torch.int64) for _ in range(2))
     Lm, Tm = ((torch.rand(B, N, N, generator=g) < 0.3) for _ in range(2))
