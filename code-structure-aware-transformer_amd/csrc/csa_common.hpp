@@ -348,6 +348,17 @@ __device__ __forceinline__ BhBlock xcd_block(int nb, int BH) {
   return r;
 }
 inline unsigned xcd_grid(int nb, int BH) { return (unsigned)(8 * ((BH + 7) / 8) * nb); }
+// The same blocks on the same XCDs, walked in the reverse order inside each XCD: a consumer of the previous kernel's
+// per-(b,h) output starts with the (b,h)s that kernel wrote last, still in the XCD's L2 (k_attn_bwd_kv after the
+// forward, which k_attn_bwd_qg then walks against: profiles/r06_ab_xcd_order.txt).
+__device__ __forceinline__ BhBlock xcd_block_rev(int nb, int BH) {
+  const int id = blockIdx.x, x = id & 7, slot = (int)(gridDim.x >> 3) - 1 - (id >> 3);
+  BhBlock r;
+  r.bh = 8 * (slot / nb) + x;
+  r.blk = slot % nb;
+  r.valid = r.bh < BH;
+  return r;
+}
 
 // ---------------------------------------------------------------------------------------
 // Host-side launch plumbing. Every entry point runs on the device of the stream it is given, not

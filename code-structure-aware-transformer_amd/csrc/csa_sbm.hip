@@ -2082,7 +2082,7 @@ __global__ __launch_bounds__(64, (D <= 64 && KPH <= 16) ? 2 : 1) void k_attn_bwd
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const uint32_t L0 = lds_offset(lds), Ql = L0 + SH::KQ, Xl = L0 + SH::KX, Hl = L0 + SH::KH, Sl = L0 + SH::KS;
   const int lane = lane_id(), c = lane & 31, h = lane >> 5;
-  const BhBlock xb = xcd_block(p.NKB, p.B * p.H);
+  const BhBlock xb = xcd_block_rev(p.NKB, p.B * p.H);  // reverse of the forward's walk (L2 reuse of X, bit words)
   if (!xb.valid) return;
   const int kbi = xb.blk, bh = xb.bh, b = bh / p.H, hd = bh % p.H;
   const int j = kbi * 32 + c;
