@@ -338,7 +338,22 @@ def train_step_bench(world, rank, dev, steps, warmup, config="java", per_gpu_bat
     for i in range(warmup):
         step(*batches[i % nbatches])
     losses = []
-    el = timed_region(world, dev, steps, lambda i: losses.append(step(*batches[i % nbatches])))
+    # an event after every step (no host sync) for the per-step median beside the contract's mean: the legs' means
+    # swing by several ms from run to run on a few long steps (profiles/r06_train_step_distribution.txt)
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)] if dev.type == "cuda" else None
+
+    def timed(i):
+        if evs is not None and i == 0:
+            evs[0].record()
+        losses.append(step(*batches[i % nbatches]))
+        if evs is not None:
+            evs[i + 1].record()
+
+    el = timed_region(world, dev, steps, timed)
+    med = None
+    if evs is not None:
+        per = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(steps))
+        med = round(per[steps // 2], 3)
     mean_loss = float(torch.stack(losses).mean())
     nparam = sum(p.numel() for p in model.parameters())
     wrapped = world > 1 or force_ddp
@@ -347,7 +362,8 @@ def train_step_bench(world, rank, dev, steps, warmup, config="java", per_gpu_bat
                                                                            " (one GPU, no data-parallel wrapper)"),
             "per_gpu_batch": per_gpu_batch,
             "global_batch": per_gpu_batch * world, "steps": steps, "warmup": warmup,
-            "ms_per_step": round(el * 1000 / steps, 3), "samples_per_s": round(world * per_gpu_batch * steps / el, 1),
+            "ms_per_step": round(el * 1000 / steps, 3), "median_step_ms": med,
+            "samples_per_s": round(world * per_gpu_batch * steps / el, 1),
             "params": nparam, "mean_loss": round(mean_loss, 4), "n_ranks": world,
             "exchange": (f"{reducer} gradient all-reduce over RCCL ({16 if impl == 'bucketed' else 64} MB buckets)"
                          if world > 1 else
